@@ -1,0 +1,94 @@
+"""ctypes / numpy mirrors of the C-ABI types declared in include/fbr.h.
+
+The layouts follow the reference's data model: ``POINT_XYZIRT`` is the PointXYZIRT payload of
+/root/reference/src/imageProjection.cpp:8-21, ``POINT_XYZI`` is pcl::PointXYZI
+(/root/reference/include/utility.h:55), ``FbrParams`` carries config/params.yaml plus the constants
+mapOptmization.h hard-codes, ``FbrRegStats`` reports what registration() decided.
+"""
+import ctypes
+
+import numpy as np
+
+POINT_XYZIRT = np.dtype(
+    [("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("intensity", "<f4"), ("ring", "<u2"),
+     ("pad_", "<u2"), ("time", "<f4")], align=True)
+assert POINT_XYZIRT.itemsize == 24
+
+POINT_XYZI = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("intensity", "<f4")])
+assert POINT_XYZI.itemsize == 16
+
+REG_STATS_FIELDS = ["status", "iterations", "converged", "degenerate", "n_sel", "n_corner_ds",
+                    "n_surf_ds", "n_corner_map", "n_surf_map", "n_points", "n_corner", "n_surf"]
+REG_STATS = np.dtype([(f, "<i4") for f in REG_STATS_FIELDS])
+
+FBR_OK = 0
+FBR_REG_OK = 0
+FBR_REG_NOT_ENOUGH_FEATURES = 1
+FBR_REG_SKIPPED_INTERVAL = 2
+
+
+class FbrParams(ctypes.Structure):
+    _fields_ = [
+        ("n_scan", ctypes.c_int32),
+        ("horizon_scan", ctypes.c_int32),
+        ("edge_threshold", ctypes.c_float),
+        ("surf_threshold", ctypes.c_float),
+        ("edge_feature_min_valid_num", ctypes.c_int32),
+        ("surf_feature_min_valid_num", ctypes.c_int32),
+        ("odometry_surf_leaf_size", ctypes.c_float),
+        ("mapping_corner_leaf_size", ctypes.c_float),
+        ("mapping_surf_leaf_size", ctypes.c_float),
+        ("z_tollerance", ctypes.c_float),
+        ("rotation_tollerance", ctypes.c_float),
+        ("number_of_cores", ctypes.c_int32),
+        ("mapping_process_interval", ctypes.c_double),
+        ("crop_half", ctypes.c_float * 3),
+        ("max_iterations", ctypes.c_int32),
+        ("max_points_per_scan", ctypes.c_int32),
+        ("max_batch", ctypes.c_int32),
+        ("reserved_", ctypes.c_int32 * 4),
+    ]
+
+
+class FbrRegStats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_int32) for f in REG_STATS_FIELDS]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f in REG_STATS_FIELDS}
+
+
+def default_params(n_scan=16, horizon_scan=1800, **overrides):
+    """fbr_params_default(): params.yaml values + the reference's hard-coded constants."""
+    p = FbrParams()
+    p.n_scan = n_scan
+    p.horizon_scan = horizon_scan
+    p.edge_threshold = 1.0
+    p.surf_threshold = 0.1
+    p.edge_feature_min_valid_num = 10
+    p.surf_feature_min_valid_num = 100
+    p.odometry_surf_leaf_size = 0.4
+    p.mapping_corner_leaf_size = 0.2
+    p.mapping_surf_leaf_size = 0.4
+    p.z_tollerance = 1000.0
+    p.rotation_tollerance = 1000.0
+    p.number_of_cores = 4
+    p.mapping_process_interval = 0.15
+    p.crop_half[0], p.crop_half[1], p.crop_half[2] = 30.0, 30.0, 10.0
+    p.max_iterations = 30
+    p.max_points_per_scan = n_scan * horizon_scan
+    p.max_batch = 1
+    for k, v in overrides.items():
+        if k == "crop_half":
+            for i in range(3):
+                p.crop_half[i] = v[i]
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def ptr(a, ctype=ctypes.c_void_p):
+    """Raw pointer of a contiguous numpy array (None -> NULL)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return ctypes.cast(a.ctypes.data, ctype)

@@ -1,0 +1,98 @@
+"""Synthetic scans, maps and registration jobs (ctypes front-end of csrc/fbr_synth.cpp).
+
+Implements the input spec of SURVEY.md §8d / BASELINE.md: beam tables for VLP-16 (16 rows),
+HDL-64 (64 rows, kitti2bag.py:242-243 elevation range), Ouster-128 and a dense 512-row sensor;
+firing-order emission with azimuth jitter, 1 cm range noise, 5 % dropouts, 0.5 % sub-1 m returns;
+ground-truth viewpoints near the origin of a procedural plaza and guesses perturbed by
+U(+-0.3 m) / U(+-2 deg).  Everything is seeded and deterministic.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .fbr_types import POINT_XYZI, POINT_XYZIRT, ptr
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "libfbr_synth.so")
+        if not os.path.exists(path):
+            raise RuntimeError("libfbr_synth.so missing: run __graft_entry__.build()")
+        L = ctypes.CDLL(path)
+        L.fbr_synth_scan.restype = ctypes.c_int64
+        L.fbr_synth_scan.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_double), ctypes.c_uint64,
+                                     ctypes.c_void_p, ctypes.c_void_p]
+        L.fbr_synth_map.restype = ctypes.c_int
+        L.fbr_synth_map.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
+                                    ctypes.c_double, ctypes.c_double, ctypes.c_void_p,
+                                    ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p,
+                                    ctypes.POINTER(ctypes.c_int64)]
+        _LIB = L
+    return _LIB
+
+
+SCENE_SEED = 7
+
+# Config -> (N_SCAN, Horizon_SCAN, map radius, surf density /m^2, corner density /m)
+CONFIGS = {
+    "C1": (16, 1800, 45.0, 12.0, 12.0),
+    "C2": (64, 1800, 45.0, 12.0, 12.0),
+    "C3": (128, 2048, 60.0, 12.0, 12.0),
+}
+
+
+def scan(pose_world, n_scan, horizon_scan, seed, scene_seed=SCENE_SEED):
+    """Ray-cast one scan at world pose [roll,pitch,yaw,x,y,z]; returns POINT_XYZIRT array."""
+    out = np.zeros(n_scan * horizon_scan, dtype=POINT_XYZIRT)
+    pose = (ctypes.c_double * 6)(*[float(v) for v in pose_world])
+    n = lib().fbr_synth_scan(scene_seed, n_scan, horizon_scan, pose, seed, None, ptr(out))
+    return out[:n].copy()
+
+
+def prior_map(radius=45.0, surf_density=5.0, corner_density=5.0, seed=11,
+              scene_seed=SCENE_SEED):
+    """World-frame prior (corner, surf) feature maps of the scene (POINT_XYZI arrays)."""
+    L = lib()
+    nc, ns = ctypes.c_int64(), ctypes.c_int64()
+    L.fbr_synth_map(scene_seed, seed, radius, surf_density, corner_density, None,
+                    ctypes.byref(nc), None, ctypes.byref(ns))
+    corner = np.zeros(nc.value, dtype=POINT_XYZI)
+    surf = np.zeros(ns.value, dtype=POINT_XYZI)
+    L.fbr_synth_map(scene_seed, seed, radius, surf_density, corner_density, ptr(corner),
+                    ctypes.byref(nc), ptr(surf), ctypes.byref(ns))
+    return corner, surf
+
+
+def job(seed, max_offset=6.0):
+    """(ground-truth pose, perturbed guess) for job `seed`, poses as [roll,pitch,yaw,x,y,z]."""
+    rng = np.random.default_rng(seed)
+    r = rng.uniform(0.0, max_offset)
+    a = rng.uniform(-np.pi, np.pi)
+    gt = np.array([rng.uniform(-0.01, 0.01), rng.uniform(-0.01, 0.01), rng.uniform(-np.pi, np.pi),
+                   r * np.cos(a), r * np.sin(a), 1.8], dtype=np.float64)
+    guess = gt.copy()
+    guess[:3] += rng.uniform(-np.deg2rad(2.0), np.deg2rad(2.0), 3)
+    guess[3:] += rng.uniform(-0.3, 0.3, 3)
+    return gt, guess.astype(np.float32)
+
+
+def make_jobs(config, n_jobs, base_seed=1000):
+    """n_jobs independent (scan, guess, gt) registration jobs of a config (C4: seed 1000+j)."""
+    n_scan, w, *_ = CONFIGS[config]
+    jobs = []
+    for j in range(n_jobs):
+        gt, guess = job(base_seed + j)
+        pts = scan(gt, n_scan, w, seed=base_seed + j)
+        jobs.append((pts, guess, gt))
+    return jobs
+
+
+def config_map(config, seed=11):
+    _, _, radius, sd, cd = CONFIGS[config]
+    return prior_map(radius, sd, cd, seed=seed)

@@ -1,0 +1,188 @@
+/* fbr.h — C-ABI of the MI355X-native feature-based scan-to-map registration path.
+ *
+ * Drop-in boundary for the per-scan hot loop of qpc001/Feature_Base_Pointcloud_Registration
+ * (a LIO-SAM-derived localiser).  The reference's "operator API" for this path is in-process C++:
+ *
+ *   ImageProjection::cloudHandler()            src/imageProjection.cpp:182-226
+ *     projectPointCloud() / cloudExtraction()  src/imageProjection.cpp:583-670
+ *   FeatureExtraction::featureExtra()          src/featureExtraction.h:79-103
+ *   mapOptimization::registration()            src/mapOptmization.h:263-343
+ *   mapOptimization::allocateMemory() (map)    src/mapOptmization.h:245-260
+ *
+ * Each entry point below names the reference function it replaces.  Conventions:
+ *   - plain C types only; host buffers are caller-owned; device memory is owned by the ctx;
+ *   - every function returns an int status: 0 = FBR_OK, < 0 = error (fbr_strerror());
+ *   - a ctx is bound to one HIP device and one HIP stream and is not thread-safe
+ *     (one ctx per host thread and device, as the reference runs one scan at a time);
+ *   - poses are the reference's transformTobeMapped layout [roll, pitch, yaw, x, y, z]
+ *     (mapOptmization.h:131); fbr_affine_from_pose / fbr_pose_from_affine convert to and from the
+ *     Eigen::Affine3f the reference's registration() takes, with PCL's exact formulas.
+ */
+#ifndef FBR_H_
+#define FBR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FBR_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------------------- */
+#define FBR_OK 0
+#define FBR_ERR_INVALID_ARG (-1)  /* null pointer, negative size, bad parameter            */
+#define FBR_ERR_HIP (-2)          /* a HIP runtime call failed                              */
+#define FBR_ERR_NO_MAP (-3)       /* registration requested before fbr_set_map()           */
+#define FBR_ERR_CAPACITY (-4)     /* input larger than the ctx was created for              */
+#define FBR_ERR_UNSUPPORTED (-5)  /* configuration outside what the kernels handle          */
+#define FBR_ERR_NO_DEVICE (-6)    /* no HIP device / extension not usable                   */
+#define FBR_ERR_STATE (-7)        /* call order violated (e.g. features before projection)  */
+
+/* ---- registration outcome (fbr_reg_stats.status) -------------------------------------------- */
+#define FBR_REG_OK 0                    /* scan2MapOptimization ran                           */
+#define FBR_REG_NOT_ENOUGH_FEATURES 1   /* mapOptmization.h:1410/1440 gate: pose left at guess */
+#define FBR_REG_SKIPPED_INTERVAL 2      /* mapOptmization.h:279 mappingProcessInterval gate    */
+
+/* Raw lidar point: the PointXYZIRT payload of imageProjection.cpp:8-21 (x,y,z,intensity f32,
+ * ring u16, time f32), laid out with natural alignment (24 bytes). */
+typedef struct fbr_point_xyzirt {
+  float x, y, z, intensity;
+  uint16_t ring;
+  uint16_t pad_;
+  float time;
+} fbr_point_xyzirt;
+
+/* Work point: pcl::PointXYZI payload (include/utility.h:55). */
+typedef struct fbr_point_xyzi {
+  float x, y, z, intensity;
+} fbr_point_xyzi;
+
+/* Tunables.  Defaults (fbr_params_default) are config/params.yaml plus the constants the
+ * reference hard-codes (SURVEY §5 "Config / flags"). */
+typedef struct fbr_params {
+  int32_t n_scan;                    /* N_SCAN                       params.yaml:19        */
+  int32_t horizon_scan;              /* Horizon_SCAN                 params.yaml:20        */
+  float edge_threshold;              /* edgeThreshold 1.0            params.yaml:45        */
+  float surf_threshold;              /* surfThreshold 0.1            params.yaml:46        */
+  int32_t edge_feature_min_valid_num;/* 10                           params.yaml:47        */
+  int32_t surf_feature_min_valid_num;/* 100                          params.yaml:48        */
+  float odometry_surf_leaf_size;     /* 0.4 per-ring surf VoxelGrid  params.yaml:51        */
+  float mapping_corner_leaf_size;    /* 0.2                          params.yaml:52        */
+  float mapping_surf_leaf_size;      /* 0.4                          params.yaml:53        */
+  float z_tollerance;                /* 1000                         params.yaml:56        */
+  float rotation_tollerance;         /* 1000                         params.yaml:57        */
+  int32_t number_of_cores;           /* 4 (CPU paths only)           params.yaml:60        */
+  double mapping_process_interval;   /* 0.15 s                       params.yaml:61        */
+  float crop_half[3];                /* 30, 30, 10 m local-map box   mapOptmization.h:286  */
+  int32_t max_iterations;            /* 30 Gauss-Newton iterations   mapOptmization.h:1417 */
+  int32_t max_points_per_scan;       /* device capacity: raw points per scan               */
+  int32_t max_batch;                 /* device capacity: scans per device batch            */
+  int32_t reserved_[4];
+} fbr_params;
+
+/* Per-scan registration statistics. */
+typedef struct fbr_reg_stats {
+  int32_t status;       /* FBR_REG_*                                                       */
+  int32_t iterations;   /* LMOptimization calls made (<= max_iterations)                   */
+  int32_t converged;    /* 1 if the loop ended on the 0.05 deg / 0.05 cm test               */
+  int32_t degenerate;   /* isDegenerate after the last LMOptimization call                  */
+  int32_t n_sel;        /* correspondences in the last LMOptimization call                  */
+  int32_t n_corner_ds;  /* laserCloudCornerLastDSNum                                        */
+  int32_t n_surf_ds;    /* laserCloudSurfLastDSNum                                          */
+  int32_t n_corner_map; /* laserCloudCornerFromMapDSNum (cropped local map)                 */
+  int32_t n_surf_map;   /* laserCloudSurfFromMapDSNum                                       */
+  int32_t n_points;     /* valid projected points (cloud_deskewed size)                     */
+  int32_t n_corner;     /* corner features before DS                                        */
+  int32_t n_surf;       /* surface features before DS                                       */
+} fbr_reg_stats;
+
+typedef struct fbr_ctx fbr_ctx;
+
+void fbr_params_default(fbr_params* p);
+const char* fbr_strerror(int status);
+int fbr_abi_version(void);
+int fbr_device_count(int* count);
+
+/* Create / destroy a context on HIP device `hip_device` (ParamServer + member construction,
+ * utility.h:146-212, featureExtraction.h:48-77, mapOptmization.h:153-196). */
+int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device);
+int fbr_destroy(fbr_ctx* ctx);
+
+/* Load the prior global feature map (already read from cloudCorner.pcd / cloudSurf.pcd) and
+ * apply the start-up VoxelGrid (corner leaf mapping_corner_leaf_size, surf leaf
+ * mapping_surf_leaf_size), replacing mapOptmization.h:245-260.  Builds the device search grid. */
+int fbr_set_map(fbr_ctx* ctx, const fbr_point_xyzi* corner, int64_t n_corner,
+                const fbr_point_xyzi* surf, int64_t n_surf);
+/* Down-sampled global map actually used (sizes, then optional copies; pass NULL to skip). */
+int fbr_get_map(fbr_ctx* ctx, int64_t* n_corner, int64_t* n_surf, fbr_point_xyzi* corner,
+                fbr_point_xyzi* surf);
+
+/* A2+A4: projectPointCloud() + cloudExtraction() (imageProjection.cpp:583-670).
+ * Fills the cloud_info fields (msg/cloud_info.msg:5-9,32): start_ring/end_ring [n_scan],
+ * col_ind/range/cloud [n_out] (size the buffers for n_in points). */
+int fbr_project(fbr_ctx* ctx, const fbr_point_xyzirt* points, int64_t n_in, int32_t* start_ring,
+                int32_t* end_ring, int32_t* col_ind, float* range, fbr_point_xyzi* cloud,
+                int64_t* n_out);
+
+/* A6-A9: FeatureExtraction::featureExtra() on the ctx's last projection
+ * (featureExtraction.h:79-294).  label[n_out] gets cloudLabel (1 corner, -1 picked surf, 0);
+ * corner/surf get cloud_corner / cloud_surface (size corner for 20*6*n_scan points and surf for
+ * n_out points).  Any output pointer may be NULL. */
+int fbr_extract_features(fbr_ctx* ctx, int8_t* label, fbr_point_xyzi* corner, int64_t* n_corner,
+                         fbr_point_xyzi* surf, int64_t* n_surf);
+
+/* A10-A18: mapOptimization::registration() (mapOptmization.h:263-343) on given feature clouds,
+ * ignoring the time gate.  pose_inout: [roll,pitch,yaw,x,y,z] guess in, registered pose out. */
+int fbr_register(fbr_ctx* ctx, const fbr_point_xyzi* corner, int64_t n_corner,
+                 const fbr_point_xyzi* surf, int64_t n_surf, float pose_inout[6],
+                 fbr_reg_stats* stats);
+/* Same, also returning the pose after every Gauss-Newton iteration (trace [max_iterations][6]). */
+int fbr_register_trace(fbr_ctx* ctx, const fbr_point_xyzi* corner, int64_t n_corner,
+                       const fbr_point_xyzi* surf, int64_t n_surf, float pose_inout[6],
+                       fbr_reg_stats* stats, float* trace);
+
+/* One scan through the whole path in stream mode (cloudHandler after the cache queue,
+ * imageProjection.cpp:197-225): the FeatureExtraction scratch state carries over between calls
+ * as in the reference; `stamp` feeds the mappingProcessInterval gate (mapOptmization.h:279). */
+int fbr_process_scan(fbr_ctx* ctx, const fbr_point_xyzirt* points, int64_t n_in, double stamp,
+                     float pose_inout[6], fbr_reg_stats* stats);
+/* Forget the carried FeatureExtraction / time-gate state (as a freshly constructed node). */
+int fbr_reset_stream(fbr_ctx* ctx);
+
+/* Independent jobs (config C4): each job is one scan registered from its own guess against the
+ * shared map, with fresh FeatureExtraction state.  Processed in device batches of max_batch. */
+int fbr_process_batch(fbr_ctx* ctx, const fbr_point_xyzirt* const* scans, const int64_t* n_in,
+                      int n_jobs, float* poses_inout /* [n_jobs][6] */,
+                      fbr_reg_stats* stats /* [n_jobs] or NULL */);
+
+/* Device-resident batch (throughput measurement): stage copies the scans and guesses to HBM;
+ * launch enqueues the whole path for the staged batch on the ctx stream (asynchronous, inputs
+ * are not modified so it may be re-launched); wait blocks; results copies poses/stats out. */
+int fbr_batch_stage(fbr_ctx* ctx, const fbr_point_xyzirt* const* scans, const int64_t* n_in,
+                    int n_jobs, const float* poses_in /* [n_jobs][6] */);
+int fbr_batch_launch(fbr_ctx* ctx);
+int fbr_batch_wait(fbr_ctx* ctx);
+int fbr_batch_results(fbr_ctx* ctx, float* poses_out /* [n_jobs][6] */,
+                      fbr_reg_stats* stats /* [n_jobs] or NULL */);
+/* Sum of the per-scan algorithmic byte counts of the last completed batch (roofline input). */
+int fbr_batch_bytes(fbr_ctx* ctx, double* bytes_total, double* bytes_gn);
+
+/* Kernel timing with HIP events recorded on the ctx stream around every launch of the named
+ * kernel ("gn_residual", "project", ...). */
+int fbr_set_profiling(fbr_ctx* ctx, int enable);
+int fbr_kernel_time(fbr_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches);
+void* fbr_stream(fbr_ctx* ctx);
+
+/* VoxelGrid<PointXYZI>::filter on the device (the kernel every DS in the path uses). */
+int fbr_voxel_grid(fbr_ctx* ctx, const fbr_point_xyzi* in, int64_t n, float leaf,
+                   fbr_point_xyzi* out, int64_t* n_out);
+
+/* pcl::getTransformation / pcl::getTranslationAndEulerAngles (row-major 4x4 float). */
+void fbr_affine_from_pose(const float pose[6], float m[16]);
+void fbr_pose_from_affine(const float m[16], float pose[6]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FBR_H_ */

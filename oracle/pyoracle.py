@@ -1,0 +1,179 @@
+"""ctypes front-end of the CPU oracle (oracle/fbr_oracle.cpp).  TEST INFRASTRUCTURE ONLY.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg — never by the
+product package.  See fbr_oracle.cpp's header for what the oracle restates and its parity status
+("parity unpinned": the reference is unbuildable here and ships no golden vectors).
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+_REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _REPO not in sys.path:
+    sys.path.insert(0, _REPO)
+
+from feature_base_pointcloud_registration_amd.fbr_types import (  # noqa: E402
+    POINT_XYZI, FbrRegStats, ptr)
+
+_LIB = None
+_VP = ctypes.c_void_p
+_I64 = ctypes.c_int64
+
+
+def lib_path():
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "libfbr_oracle.so")
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", os.path.dirname(os.path.abspath(__file__))])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(lib_path()):
+            build()
+        L = ctypes.CDLL(lib_path())
+        L.orc_project.restype = _I64
+        L.orc_project.argtypes = [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _VP]
+        L.orc_voxel_grid.restype = _I64
+        L.orc_voxel_grid.argtypes = [_VP, _I64, ctypes.c_float, _VP]
+        L.orc_stream_create.restype = _VP
+        L.orc_stream_create.argtypes = [_VP]
+        L.orc_stream_destroy.argtypes = [_VP]
+        L.orc_stream_reset.argtypes = [_VP]
+        L.orc_features.argtypes = [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _VP, _VP]
+        L.orc_map_create.restype = _VP
+        L.orc_map_create.argtypes = [_VP, _VP, _I64, _VP, _I64]
+        L.orc_map_destroy.argtypes = [_VP]
+        L.orc_map_get.argtypes = [_VP, _VP, _VP, _VP, _VP]
+        L.orc_register.argtypes = [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP, ctypes.c_int]
+        L.orc_process_scan.argtypes = [_VP, _VP, _VP, _I64, ctypes.c_double, _VP, _VP, ctypes.c_int]
+        L.orc_affine_from_pose.argtypes = [_VP, _VP]
+        L.orc_pose_from_affine.argtypes = [_VP, _VP]
+        L.orc_jacobi.argtypes = [_VP, ctypes.c_int, _VP, _VP]
+        L.orc_qr_solve.argtypes = [_VP, ctypes.c_int, _VP]
+        L.orc_colpiv_solve.argtypes = [_VP, _VP, _VP]
+        L.orc_knn5.argtypes = [_VP, _I64, _VP, _I64, _VP, _VP]
+        L.orc_sort_smoothness.argtypes = [_VP, _I64, _VP]
+        _LIB = L
+    return _LIB
+
+
+def project(params, pts):
+    """projectPointCloud + cloudExtraction -> dict of cloud_info fields."""
+    L = lib()
+    n_in = len(pts)
+    H = params.n_scan
+    start = np.zeros(H, np.int32)
+    end = np.zeros(H, np.int32)
+    col = np.zeros(max(n_in, 1), np.int32)
+    rng = np.zeros(max(n_in, 1), np.float32)
+    cloud = np.zeros(max(n_in, 1), POINT_XYZI)
+    n = L.orc_project(ctypes.byref(params), ptr(pts), n_in, ptr(start), ptr(end), ptr(col),
+                      ptr(rng), ptr(cloud))
+    return dict(start_ring=start, end_ring=end, col_ind=col[:n].copy(), range=rng[:n].copy(),
+                cloud=cloud[:n].copy())
+
+
+def voxel_grid(points, leaf):
+    out = np.zeros(max(len(points), 1), POINT_XYZI)
+    n = lib().orc_voxel_grid(ptr(points), len(points), ctypes.c_float(leaf), ptr(out))
+    return out[:n].copy()
+
+
+class Stream:
+    """A FeatureExtraction instance with its persistent scratch (stream mode)."""
+
+    def __init__(self, params):
+        self.params = params
+        self.h = lib().orc_stream_create(ctypes.byref(params))
+
+    def reset(self):
+        lib().orc_stream_reset(self.h)
+
+    def features(self, pts):
+        n_in = len(pts)
+        label = np.zeros(max(n_in, 1), np.int8)
+        corner = np.zeros(max(20 * 6 * self.params.n_scan, 1), POINT_XYZI)
+        surf = np.zeros(max(n_in, 1), POINT_XYZI)
+        nc, ns, npnt = _I64(), _I64(), _I64()
+        lib().orc_features(self.h, ptr(pts), n_in, ptr(label), ptr(corner), ctypes.byref(nc),
+                           ptr(surf), ctypes.byref(ns), ctypes.byref(npnt))
+        return dict(label=label[:npnt.value].copy(), corner=corner[:nc.value].copy(),
+                    surf=surf[:ns.value].copy(), n_points=npnt.value)
+
+    def process_scan(self, omap, pts, stamp, pose, n_threads=4):
+        pose = np.ascontiguousarray(pose, dtype=np.float32).copy()
+        st = FbrRegStats()
+        lib().orc_process_scan(self.h, omap.h, ptr(pts), len(pts), ctypes.c_double(stamp),
+                               ptr(pose), ctypes.byref(st), n_threads)
+        return pose, st.as_dict()
+
+    def __del__(self):
+        try:
+            lib().orc_stream_destroy(self.h)
+        except Exception:
+            pass
+
+
+class Map:
+    """Global prior map after the start-up VoxelGrid (mapOptmization.h:245-260)."""
+
+    def __init__(self, params, corner, surf):
+        self.params = params
+        self.h = lib().orc_map_create(ctypes.byref(params), ptr(corner), len(corner), ptr(surf),
+                                      len(surf))
+
+    def arrays(self):
+        nc, ns = _I64(), _I64()
+        lib().orc_map_get(self.h, ctypes.byref(nc), ctypes.byref(ns), None, None)
+        c = np.zeros(max(nc.value, 1), POINT_XYZI)
+        s = np.zeros(max(ns.value, 1), POINT_XYZI)
+        lib().orc_map_get(self.h, None, None, ptr(c), ptr(s))
+        return c[:nc.value].copy(), s[:ns.value].copy()
+
+    def register(self, corner, surf, pose, n_threads=4):
+        """registration() core: returns (pose, stats dict, per-iteration pose trace)."""
+        pose = np.ascontiguousarray(pose, dtype=np.float32).copy()
+        st = FbrRegStats()
+        trace = np.zeros((self.params.max_iterations, 6), np.float32)
+        lib().orc_register(ctypes.byref(self.params), self.h, ptr(corner), len(corner), ptr(surf),
+                           len(surf), ptr(pose), ctypes.byref(st), ptr(trace), n_threads)
+        d = st.as_dict()
+        return pose, d, trace[:d["iterations"]].copy()
+
+    def __del__(self):
+        try:
+            lib().orc_map_destroy(self.h)
+        except Exception:
+            pass
+
+
+def affine_from_pose(pose):
+    m = np.zeros(16, np.float32)
+    lib().orc_affine_from_pose(ptr(np.ascontiguousarray(pose, np.float32)), ptr(m))
+    return m.reshape(4, 4)
+
+
+def pose_from_affine(m):
+    p = np.zeros(6, np.float32)
+    lib().orc_pose_from_affine(ptr(np.ascontiguousarray(m, np.float32).reshape(16)), ptr(p))
+    return p
+
+
+def sort_smoothness(values):
+    v = np.ascontiguousarray(values, np.float32)
+    out = np.zeros(len(v), np.int64)
+    lib().orc_sort_smoothness(ptr(v), len(v), ptr(out))
+    return out
+
+
+def knn5(map_pts, queries):
+    idx = np.zeros((len(queries), 5), np.int32)
+    d2 = np.zeros((len(queries), 5), np.float32)
+    lib().orc_knn5(ptr(map_pts), len(map_pts), ptr(queries), len(queries), ptr(idx), ptr(d2))
+    return idx, d2
