@@ -1,0 +1,294 @@
+"""Python front-end of libfbr_hip.so (the extern "C" boundary of include/fbr.h).
+
+The classes mirror the reference's per-scan operator interface so that tests read like the
+reference's own call sites:
+
+  ImageProjection.projectPointCloud/cloudExtraction  -> Context.project()      imageProjection.cpp:583-670
+  FeatureExtraction.featureExtra                     -> Context.extract_features() featureExtraction.h:79
+  mapOptimization.registration                       -> Context.register()     mapOptmization.h:263
+  cloudHandler (projection -> features -> registration) -> Context.process_scan()  imageProjection.cpp:182
+
+There is no CPU fallback: if the HIP library or a GPU is missing every call raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .fbr_types import (POINT_XYZI, POINT_XYZIRT, REG_STATS, FbrParams, FbrRegStats,
+                        default_params, ptr)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+_VP = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+
+EXPORTED_SYMBOLS = [
+    "fbr_params_default", "fbr_strerror", "fbr_abi_version", "fbr_device_count", "fbr_create",
+    "fbr_destroy", "fbr_set_map", "fbr_get_map", "fbr_project", "fbr_extract_features",
+    "fbr_register", "fbr_register_trace", "fbr_process_scan", "fbr_reset_stream",
+    "fbr_process_batch", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
+    "fbr_batch_results", "fbr_batch_bytes", "fbr_set_profiling", "fbr_kernel_time", "fbr_stream",
+    "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math",
+]
+
+
+class FbrError(RuntimeError):
+    def __init__(self, status, where=""):
+        self.status = status
+        super().__init__(f"{where}: {strerror(status)} ({status})")
+
+
+def lib_path():
+    return os.path.join(_HERE, "libfbr_hip.so")
+
+
+def lib():
+    """Load the HIP library (raises if it was not built: no silent fallback)."""
+    global _LIB
+    if _LIB is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: the HIP extension is not built "
+                               "(run __graft_entry__.build())")
+        L = ctypes.CDLL(path)
+        sig = {
+            "fbr_params_default": (None, [_VP]),
+            "fbr_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+            "fbr_abi_version": (ctypes.c_int, []),
+            "fbr_device_count": (ctypes.c_int, [_VP]),
+            "fbr_create": (ctypes.c_int, [_VP, _VP, ctypes.c_int]),
+            "fbr_destroy": (ctypes.c_int, [_VP]),
+            "fbr_set_map": (ctypes.c_int, [_VP, _VP, _I64, _VP, _I64]),
+            "fbr_get_map": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
+            "fbr_project": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _VP, _VP]),
+            "fbr_extract_features": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
+            "fbr_register": (ctypes.c_int, [_VP, _VP, _I64, _VP, _I64, _VP, _VP]),
+            "fbr_register_trace": (ctypes.c_int, [_VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP]),
+            "fbr_process_scan": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_double, _VP, _VP]),
+            "fbr_reset_stream": (ctypes.c_int, [_VP]),
+            "fbr_process_batch": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, _VP, _VP]),
+            "fbr_batch_stage": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, _VP]),
+            "fbr_batch_launch": (ctypes.c_int, [_VP]),
+            "fbr_batch_wait": (ctypes.c_int, [_VP]),
+            "fbr_batch_results": (ctypes.c_int, [_VP, _VP, _VP]),
+            "fbr_batch_bytes": (ctypes.c_int, [_VP, _VP, _VP]),
+            "fbr_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
+            "fbr_kernel_time": (ctypes.c_int, [_VP, ctypes.c_char_p, _VP, _VP]),
+            "fbr_stream": (_VP, [_VP]),
+            "fbr_voxel_grid": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_float, _VP, _VP]),
+            "fbr_affine_from_pose": (None, [_VP, _VP]),
+            "fbr_pose_from_affine": (None, [_VP, _VP]),
+            "fbr_selftest_math": (ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def strerror(status):
+    return lib().fbr_strerror(status).decode()
+
+
+def _check(status, where):
+    if status != 0:
+        raise FbrError(status, where)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    _check(lib().fbr_device_count(ctypes.byref(n)), "fbr_device_count")
+    return n.value
+
+
+def selftest_math(a, b):
+    """Device sqrt(|a|), a/b, atan2f(a,b), a*b+b*a-a (see fbr_selftest_math)."""
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    out = np.zeros((len(a), 4), np.float32)
+    _check(lib().fbr_selftest_math(len(a), ptr(a), ptr(b), ptr(out)), "fbr_selftest_math")
+    return out
+
+
+def affine_from_pose(pose):
+    m = np.zeros(16, np.float32)
+    lib().fbr_affine_from_pose(ptr(np.ascontiguousarray(pose, np.float32)), ptr(m))
+    return m.reshape(4, 4)
+
+
+def pose_from_affine(m):
+    p = np.zeros(6, np.float32)
+    lib().fbr_pose_from_affine(ptr(np.ascontiguousarray(m, np.float32).reshape(16)), ptr(p))
+    return p
+
+
+def _as_points(a, dtype):
+    a = np.ascontiguousarray(a)
+    if a.dtype != dtype:
+        raise TypeError(f"expected dtype {dtype}, got {a.dtype}")
+    return a
+
+
+class Context:
+    """One fbr_ctx: a HIP device, a stream, HBM buffers for `max_batch` scans."""
+
+    def __init__(self, params=None, device=0, **kw):
+        self.params = params if params is not None else default_params(**kw)
+        self._h = ctypes.c_void_p()
+        _check(lib().fbr_create(ctypes.byref(self._h), ctypes.byref(self.params), device), "fbr_create")
+
+    def close(self):
+        if self._h:
+            lib().fbr_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- map (mapOptmization.h:245-260) ----
+    def set_map(self, corner, surf):
+        corner = _as_points(corner, POINT_XYZI)
+        surf = _as_points(surf, POINT_XYZI)
+        _check(lib().fbr_set_map(self._h, ptr(corner), len(corner), ptr(surf), len(surf)), "fbr_set_map")
+
+    def get_map(self):
+        nc, ns = _I64(), _I64()
+        _check(lib().fbr_get_map(self._h, ctypes.byref(nc), ctypes.byref(ns), None, None), "fbr_get_map")
+        c = np.zeros(max(nc.value, 1), POINT_XYZI)
+        s = np.zeros(max(ns.value, 1), POINT_XYZI)
+        _check(lib().fbr_get_map(self._h, None, None, ptr(c), ptr(s)), "fbr_get_map")
+        return c[:nc.value].copy(), s[:ns.value].copy()
+
+    # ---- A2+A4 ----
+    def project(self, pts):
+        pts = _as_points(pts, POINT_XYZIRT)
+        n_in, H = len(pts), self.params.n_scan
+        start = np.zeros(H, np.int32)
+        end = np.zeros(H, np.int32)
+        cap = max(n_in, 1)
+        col = np.zeros(cap, np.int32)
+        rng = np.zeros(cap, np.float32)
+        cloud = np.zeros(cap, POINT_XYZI)
+        n = _I64()
+        _check(lib().fbr_project(self._h, ptr(pts), n_in, ptr(start), ptr(end), ptr(col), ptr(rng),
+                                 ptr(cloud), ctypes.byref(n)), "fbr_project")
+        k = n.value
+        return dict(start_ring=start, end_ring=end, col_ind=col[:k].copy(), range=rng[:k].copy(),
+                    cloud=cloud[:k].copy())
+
+    # ---- A6-A9 ----
+    def extract_features(self, n_points):
+        H, W = self.params.n_scan, self.params.horizon_scan
+        label = np.zeros(max(n_points, 1), np.int8)
+        corner = np.zeros(120 * H, POINT_XYZI)
+        surf = np.zeros(max(H * W, 1), POINT_XYZI)
+        nc, ns = _I64(), _I64()
+        _check(lib().fbr_extract_features(self._h, ptr(label), ptr(corner), ctypes.byref(nc), ptr(surf),
+                                          ctypes.byref(ns)), "fbr_extract_features")
+        return dict(label=label[:n_points].copy(), corner=corner[:nc.value].copy(),
+                    surf=surf[:ns.value].copy())
+
+    def features(self, pts):
+        pr = self.project(pts)
+        f = self.extract_features(len(pr["col_ind"]))
+        f["n_points"] = len(pr["col_ind"])
+        return f
+
+    # ---- A10-A18 ----
+    def register(self, corner, surf, pose, trace=False):
+        corner = _as_points(corner, POINT_XYZI)
+        surf = _as_points(surf, POINT_XYZI)
+        pose = np.ascontiguousarray(pose, dtype=np.float32).copy()
+        st = FbrRegStats()
+        if trace:
+            tr = np.zeros((self.params.max_iterations, 6), np.float32)
+            _check(lib().fbr_register_trace(self._h, ptr(corner), len(corner), ptr(surf), len(surf),
+                                            ptr(pose), ctypes.byref(st), ptr(tr)), "fbr_register_trace")
+            d = st.as_dict()
+            return pose, d, tr[:d["iterations"]].copy()
+        _check(lib().fbr_register(self._h, ptr(corner), len(corner), ptr(surf), len(surf), ptr(pose),
+                                  ctypes.byref(st)), "fbr_register")
+        return pose, st.as_dict()
+
+    def process_scan(self, pts, stamp, pose):
+        pts = _as_points(pts, POINT_XYZIRT)
+        pose = np.ascontiguousarray(pose, dtype=np.float32).copy()
+        st = FbrRegStats()
+        _check(lib().fbr_process_scan(self._h, ptr(pts), len(pts), ctypes.c_double(stamp), ptr(pose),
+                                      ctypes.byref(st)), "fbr_process_scan")
+        return pose, st.as_dict()
+
+    def reset_stream(self):
+        _check(lib().fbr_reset_stream(self._h), "fbr_reset_stream")
+
+    # ---- batches of independent jobs ----
+    def _scan_ptrs(self, scans):
+        scans = [_as_points(s, POINT_XYZIRT) for s in scans]
+        arr = (ctypes.c_void_p * len(scans))(*[s.ctypes.data for s in scans])
+        n_in = np.array([len(s) for s in scans], np.int64)
+        return scans, arr, n_in
+
+    def process_batch(self, scans, guesses):
+        keep, arr, n_in = self._scan_ptrs(scans)
+        poses = np.ascontiguousarray(np.asarray(guesses, np.float32).reshape(-1, 6)).copy()
+        stats = np.zeros(len(keep), REG_STATS)
+        _check(lib().fbr_process_batch(self._h, arr, ptr(n_in), len(keep), ptr(poses), ptr(stats)),
+               "fbr_process_batch")
+        return poses, stats
+
+    def batch_stage(self, scans, guesses):
+        keep, arr, n_in = self._scan_ptrs(scans)
+        g = np.ascontiguousarray(np.asarray(guesses, np.float32).reshape(-1, 6))
+        _check(lib().fbr_batch_stage(self._h, arr, ptr(n_in), len(keep), ptr(g)), "fbr_batch_stage")
+        self._staged = len(keep)
+
+    def batch_launch(self):
+        _check(lib().fbr_batch_launch(self._h), "fbr_batch_launch")
+
+    def batch_wait(self):
+        _check(lib().fbr_batch_wait(self._h), "fbr_batch_wait")
+
+    def batch_results(self):
+        poses = np.zeros((self._staged, 6), np.float32)
+        stats = np.zeros(self._staged, REG_STATS)
+        _check(lib().fbr_batch_results(self._h, ptr(poses), ptr(stats)), "fbr_batch_results")
+        return poses, stats
+
+    def batch_bytes(self):
+        t, g = ctypes.c_double(), ctypes.c_double()
+        _check(lib().fbr_batch_bytes(self._h, ctypes.byref(t), ctypes.byref(g)), "fbr_batch_bytes")
+        return t.value, g.value
+
+    def set_profiling(self, on=True):
+        _check(lib().fbr_set_profiling(self._h, 1 if on else 0), "fbr_set_profiling")
+
+    def kernel_time(self, name):
+        ms, n = ctypes.c_double(), _I64()
+        _check(lib().fbr_kernel_time(self._h, name.encode(), ctypes.byref(ms), ctypes.byref(n)),
+               "fbr_kernel_time")
+        return ms.value, n.value
+
+    def voxel_grid(self, pts, leaf):
+        pts = _as_points(pts, POINT_XYZI)
+        out = np.zeros(max(len(pts), 1), POINT_XYZI)
+        n = _I64()
+        _check(lib().fbr_voxel_grid(self._h, ptr(pts), len(pts), ctypes.c_float(leaf), ptr(out),
+                                    ctypes.byref(n)), "fbr_voxel_grid")
+        return out[:n.value].copy()
+
+
+__all__ = ["Context", "FbrError", "FbrParams", "default_params", "lib", "device_count",
+           "affine_from_pose", "pose_from_affine", "EXPORTED_SYMBOLS"]

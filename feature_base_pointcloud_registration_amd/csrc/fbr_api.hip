@@ -1,0 +1,866 @@
+// fbr_api.hip — the extern "C" boundary (include/fbr.h) and the device pipeline orchestration.
+//
+// One fbr_ctx = one HIP device + one stream + the HBM buffers for a batch of up to max_batch
+// scans.  A batch runs entirely on the device:
+//   memset owners -> k_project -> k_rowcount/k_compact        (imageProjection.cpp:583-670)
+//   -> k_features (per ring) -> k_voxel_grid (per ring surf)  (featureExtraction.h:109-294)
+//   -> k_concat -> k_voxel_grid x2 (downsampleCurrentScan)    (mapOptmization.h:981-993)
+//   -> k_gn_init -> [k_gn_residual -> k_gn_solve] x max_iter  (mapOptmization.h:1403-1442)
+//   -> k_gn_finalize                                          (transformUpdate, :1444-1479)
+// with no host round trip between stages (converged jobs drop out on the device).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "fbr_common.h"
+#include "fbr_kernels.h"
+
+using namespace fbr;
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "fbr: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      return FBR_ERR_HIP;                                                            \
+    }                                                                                \
+  } while (0)
+
+namespace {
+
+struct KernelTimer {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+  double total_ms = 0.0;
+  int64_t launches = 0;
+};
+
+template <typename T>
+int dalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  CK(hipMalloc((void**)p, sizeof(T) * count));
+  return FBR_OK;
+}
+
+}  // namespace
+
+struct fbr_ctx {
+  fbr_params P;
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  int H = 0, W = 0, Bcap = 0;
+  int64_t HW = 0, NMAX = 0;
+  // inputs
+  fbr_point_xyzirt* d_pts = nullptr;
+  int64_t* d_nin = nullptr;
+  float* d_guess = nullptr;
+  // projection
+  int32_t *d_owner = nullptr, *d_rowcnt = nullptr, *d_col = nullptr, *d_start = nullptr, *d_end = nullptr,
+          *d_nvalid = nullptr;
+  float4* d_cloud = nullptr;
+  float* d_range = nullptr;
+  // features
+  StreamState* d_sstate = nullptr;    // [Bcap] batch (zeroed per batch)
+  StreamState* d_sstream = nullptr;   // [1]   stream mode (persistent)
+  int8_t* d_label = nullptr;          // [Bcap][HW]
+  int8_t* d_label_stream = nullptr;   // [HW]   stream mode (persistent)
+  float4* d_corner_slot = nullptr;
+  int32_t* d_corner_cnt = nullptr;
+  float4* d_cand = nullptr;
+  int32_t* d_cand_cnt = nullptr;
+  float4* d_surf_ring = nullptr;
+  int32_t* d_surf_ring_cnt = nullptr;
+  int32_t* d_err = nullptr;
+  float4 *d_corner_all = nullptr, *d_surf_all = nullptr, *d_cornerDS = nullptr, *d_surfDS = nullptr;
+  int32_t *d_ncorner = nullptr, *d_nsurf = nullptr, *d_ncds = nullptr, *d_nsds = nullptr;
+  uint32_t *d_vg_scratch = nullptr, *d_vg_hist = nullptr;
+  int64_t vg_scratch_elems = 0, vg_hist_elems = 0;
+  // registration
+  GnState* d_gn = nullptr;
+  int4* d_items = nullptr;
+  int32_t *d_nitems = nullptr, *d_item_range = nullptr, *d_cropcnt = nullptr;
+  double* d_partial = nullptr;
+  int max_items = 0;
+  float* d_pose_out = nullptr;
+  fbr_reg_stats* d_stats = nullptr;
+  float* d_trace = nullptr;
+  // map
+  bool has_map = false;
+  float4 *d_map_c = nullptr, *d_map_s = nullptr;
+  int32_t *d_cs_c = nullptr, *d_cs_s = nullptr;
+  GridDesc gc{}, gs{};
+  std::vector<fbr_point_xyzi> map_c_host, map_s_host;
+  // state
+  bool have_projection = false;
+  int staged_B = 0;
+  std::vector<int64_t> staged_nin;
+  double time_last = -1.0;
+  bool profiling = false;
+  std::map<std::string, KernelTimer> timers;
+  std::vector<int32_t> last_iters, last_q, last_n, last_m;
+};
+
+namespace {
+
+void timer_begin(fbr_ctx* c, const char* name, hipEvent_t* ev_end) {
+  *ev_end = nullptr;
+  if (!c->profiling) return;
+  KernelTimer& t = c->timers[name];
+  std::pair<hipEvent_t, hipEvent_t> pr;
+  if (!t.pool.empty()) {
+    pr = t.pool.back();
+    t.pool.pop_back();
+  } else {
+    (void)hipEventCreate(&pr.first);
+    (void)hipEventCreate(&pr.second);
+  }
+  (void)hipEventRecord(pr.first, c->stream);
+  t.pending.push_back(pr);
+  *ev_end = pr.second;
+}
+void timer_end(fbr_ctx* c, hipEvent_t ev_end) {
+  if (ev_end) (void)hipEventRecord(ev_end, c->stream);
+}
+
+#define TIMED(ctx, name, launch)      \
+  do {                                \
+    hipEvent_t ev_;                   \
+    timer_begin(ctx, name, &ev_);     \
+    launch;                           \
+    timer_end(ctx, ev_);              \
+  } while (0)
+
+int64_t seg_cap(int W) { return W / 6 + 8; }
+
+int check_params(const fbr_params* p) {
+  if (!p) return FBR_ERR_INVALID_ARG;
+  if (p->n_scan <= 0 || p->horizon_scan <= 0 || p->horizon_scan > kMaxW) return FBR_ERR_UNSUPPORTED;
+  if (p->max_points_per_scan <= 0 || p->max_batch <= 0 || p->max_iterations <= 0) return FBR_ERR_INVALID_ARG;
+  if (!(p->odometry_surf_leaf_size > 0 && p->mapping_corner_leaf_size > 0 && p->mapping_surf_leaf_size > 0))
+    return FBR_ERR_INVALID_ARG;
+  return FBR_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// map grid (built once per fbr_set_map; see k_register.hip for why this replaces the KD-trees)
+// ---------------------------------------------------------------------------------------------
+int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pts, int32_t** d_cs, GridDesc* g) {
+  if (*d_pts) (void)hipFree(*d_pts);
+  if (*d_cs) (void)hipFree(*d_cs);
+  *d_pts = nullptr;
+  *d_cs = nullptr;
+  const int64_t n = (int64_t)pts.size();
+  float inv = 1.0f;  // power-of-two cell >= 1 m: floor(p * inv) is exact
+  int64_t lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0}, dims[3] = {1, 1, 1};
+  for (int attempt = 0; attempt < 12; ++attempt) {
+    for (int d = 0; d < 3; ++d) {
+      lo[d] = INT64_MAX;
+      hi[d] = INT64_MIN;
+    }
+    for (const auto& p : pts) {
+      const float v[3] = {p.x, p.y, p.z};
+      for (int d = 0; d < 3; ++d) {
+        const int64_t cidx = (int64_t)std::floor(v[d] * inv);
+        lo[d] = std::min(lo[d], cidx);
+        hi[d] = std::max(hi[d], cidx);
+      }
+    }
+    if (n == 0)
+      for (int d = 0; d < 3; ++d) lo[d] = hi[d] = 0;
+    for (int d = 0; d < 3; ++d) dims[d] = hi[d] - lo[d] + 1;
+    if (dims[0] * dims[1] * dims[2] <= (int64_t)1 << 26) break;
+    inv *= 0.5f;
+  }
+  const int64_t ncell = dims[0] * dims[1] * dims[2];
+  std::vector<int32_t> cell(n), start(ncell + 1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    const fbr_point_xyzi& p = pts[i];
+    const int64_t cx = (int64_t)std::floor(p.x * inv) - lo[0], cy = (int64_t)std::floor(p.y * inv) - lo[1],
+                  cz = (int64_t)std::floor(p.z * inv) - lo[2];
+    cell[i] = (int32_t)((cz * dims[1] + cy) * dims[0] + cx);
+    start[cell[i] + 1]++;
+  }
+  for (int64_t k = 0; k < ncell; ++k) start[k + 1] += start[k];
+  std::vector<float4> sorted(std::max<int64_t>(n, 1));
+  std::vector<int32_t> fill(start.begin(), start.end() - 1);
+  for (int64_t i = 0; i < n; ++i) {  // counting sort, index order kept inside a cell
+    const fbr_point_xyzi& p = pts[i];
+    float w;
+    int32_t ii = (int32_t)i;
+    std::memcpy(&w, &ii, 4);
+    sorted[fill[cell[i]]++] = make_float4(p.x, p.y, p.z, w);
+  }
+  if (dalloc(d_pts, std::max<int64_t>(n, 1)) || dalloc(d_cs, ncell + 1)) return FBR_ERR_HIP;
+  if (n) CK(hipMemcpy(*d_pts, sorted.data(), sizeof(float4) * n, hipMemcpyHostToDevice));
+  CK(hipMemcpy(*d_cs, start.data(), sizeof(int32_t) * (ncell + 1), hipMemcpyHostToDevice));
+  g->inv_cell = inv;
+  for (int d = 0; d < 3; ++d) {
+    g->origin[d] = (float)lo[d];
+    g->dims[d] = (int32_t)dims[d];
+  }
+  g->n_cells = (int32_t)ncell;
+  g->n_points = n;
+  return FBR_OK;
+}
+
+// One-segment device VoxelGrid with temporary buffers (map start-up filter, fbr_voxel_grid).
+int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf, std::vector<fbr_point_xyzi>& out) {
+  out.clear();
+  if (n <= 0) return FBR_OK;
+  if (n > INT32_MAX / 4) return FBR_ERR_CAPACITY;
+  float4 *d_in = nullptr, *d_out = nullptr;
+  int32_t* d_cnt = nullptr;
+  uint32_t *d_sc = nullptr, *d_h = nullptr;
+  const int64_t hs = ((n + 255) / 256) * 256;
+  int rc = FBR_OK;
+  if (dalloc(&d_in, n) || dalloc(&d_out, n) || dalloc(&d_cnt, 2) || dalloc(&d_sc, 4 * n) || dalloc(&d_h, hs)) {
+    rc = FBR_ERR_HIP;
+  } else {
+    int32_t nn = (int32_t)n;
+    if (hipMemcpyAsync(d_in, in, sizeof(float4) * n, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(d_cnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+      rc = FBR_ERR_HIP;
+    } else {
+      VgArgs a{};
+      a.in = d_in;
+      a.stride_in = n;
+      a.cnt_in = d_cnt;
+      a.out = d_out;
+      a.stride_out = n;
+      a.cnt_out = d_cnt + 1;
+      a.scratch = d_sc;
+      a.hist = d_h;
+      a.hist_stride = hs;
+      a.leaf = leaf;
+      a.nseg = 1;
+      launch_voxel_grid(c->stream, a);
+      int32_t nout = 0;
+      if (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+          hipStreamSynchronize(c->stream) != hipSuccess) {
+        rc = FBR_ERR_HIP;
+      } else {
+        out.resize(nout);
+        if (nout && hipMemcpy(out.data(), d_out, sizeof(float4) * nout, hipMemcpyDeviceToHost) != hipSuccess)
+          rc = FBR_ERR_HIP;
+      }
+    }
+  }
+  (void)hipFree(d_in);
+  (void)hipFree(d_out);
+  (void)hipFree(d_cnt);
+  (void)hipFree(d_sc);
+  (void)hipFree(d_h);
+  return rc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// pipeline stages
+// ---------------------------------------------------------------------------------------------
+int stage_project(fbr_ctx* c, int B) {
+  CK(hipMemsetAsync(c->d_owner, 0x7F, sizeof(int32_t) * B * c->HW, c->stream));
+  TIMED(c, "project", launch_project(c->stream, c->d_pts, c->d_nin, c->NMAX, B, c->H, c->W, c->d_owner));
+  TIMED(c, "extract", launch_extract(c->stream, c->d_pts, c->NMAX, c->d_owner, B, c->H, c->W, c->d_rowcnt,
+                                     c->d_cloud, c->d_col, c->d_range, c->d_start, c->d_end, c->d_nvalid));
+  return FBR_OK;
+}
+
+int stage_features(fbr_ctx* c, int B, bool stream_mode) {
+  FeatArgs a{};
+  a.B = B;
+  a.H = c->H;
+  a.W = c->W;
+  a.cloud = c->d_cloud;
+  a.col = c->d_col;
+  a.range = c->d_range;
+  a.start_ring = c->d_start;
+  a.end_ring = c->d_end;
+  a.nvalid = c->d_nvalid;
+  a.edge_thr = c->P.edge_threshold;
+  a.surf_thr = c->P.surf_threshold;
+  if (stream_mode) {
+    a.stream = c->d_sstream;
+    a.label = c->d_label_stream;
+  } else {
+    CK(hipMemsetAsync(c->d_sstate, 0, sizeof(StreamState) * B, c->stream));
+    CK(hipMemsetAsync(c->d_label, 0, (size_t)B * c->HW, c->stream));
+    a.stream = c->d_sstate;
+    a.label = c->d_label;
+  }
+  a.corner_slot = c->d_corner_slot;
+  a.corner_cnt = c->d_corner_cnt;
+  a.cand = c->d_cand;
+  a.cand_cnt = c->d_cand_cnt;
+  a.err = c->d_err;
+  a.lcap = c->W + 16;
+  a.segcap = (int)seg_cap(c->W);
+  CK(hipMemsetAsync(c->d_err, 0, sizeof(int32_t) * B, c->stream));
+  TIMED(c, "features", launch_features(c->stream, a));
+  VgArgs v{};
+  v.in = c->d_cand;
+  v.stride_in = c->W;
+  v.cnt_in = c->d_cand_cnt;
+  v.out = c->d_surf_ring;
+  v.stride_out = c->W;
+  v.cnt_out = c->d_surf_ring_cnt;
+  v.scratch = c->d_vg_scratch;
+  v.hist = c->d_vg_hist;
+  v.hist_stride = ((c->W + 255) / 256) * 256;
+  v.leaf = c->P.odometry_surf_leaf_size;
+  v.nseg = B * c->H;
+  TIMED(c, "voxel_ring", launch_voxel_grid(c->stream, v));
+  TIMED(c, "concat", launch_concat(c->stream, B, c->H, c->W, c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring,
+                                   c->d_surf_ring_cnt, c->d_corner_all, c->HW, c->d_ncorner, c->d_surf_all, c->HW,
+                                   c->d_nsurf));
+  return FBR_OK;
+}
+
+GnArgs gn_args(fbr_ctx* c, int B, bool trace) {
+  GnArgs a{};
+  a.B = B;
+  a.max_iter = c->P.max_iterations;
+  a.cornerDS = c->d_cornerDS;
+  a.capc = c->HW;
+  a.ncds = c->d_ncds;
+  a.surfDS = c->d_surfDS;
+  a.caps = c->HW;
+  a.nsds = c->d_nsds;
+  a.mc = MapGrid{c->d_map_c, c->d_cs_c, c->gc};
+  a.ms = MapGrid{c->d_map_s, c->d_cs_s, c->gs};
+  a.gn = c->d_gn;
+  a.guess = c->d_guess;
+  a.items = c->d_items;
+  a.nitems = c->d_nitems;
+  a.item_range = c->d_item_range;
+  a.partial = c->d_partial;
+  a.max_items = c->max_items;
+  a.edge_min = c->P.edge_feature_min_valid_num;
+  a.surf_min = c->P.surf_feature_min_valid_num;
+  for (int k = 0; k < 3; ++k) a.crop_half[k] = c->P.crop_half[k];
+  a.rot_tol = c->P.rotation_tollerance;
+  a.z_tol = c->P.z_tollerance;
+  a.pose_out = c->d_pose_out;
+  a.stats = c->d_stats;
+  a.trace = trace ? c->d_trace : nullptr;
+  return a;
+}
+
+// Registration of the clouds in d_corner_all / d_surf_all (counts d_ncorner / d_nsurf) from d_guess.
+int stage_register(fbr_ctx* c, int B, bool trace) {
+  if (!c->has_map) return FBR_ERR_NO_MAP;
+  VgArgs v{};
+  v.scratch = c->d_vg_scratch;
+  v.hist = c->d_vg_hist;
+  v.hist_stride = ((c->HW + 255) / 256) * 256;
+  v.nseg = B;
+  v.in = c->d_corner_all;
+  v.stride_in = c->HW;
+  v.cnt_in = c->d_ncorner;
+  v.out = c->d_cornerDS;
+  v.stride_out = c->HW;
+  v.cnt_out = c->d_ncds;
+  v.leaf = c->P.mapping_corner_leaf_size;
+  TIMED(c, "voxel_scan", launch_voxel_grid(c->stream, v));
+  v.in = c->d_surf_all;
+  v.cnt_in = c->d_nsurf;
+  v.out = c->d_surfDS;
+  v.cnt_out = c->d_nsds;
+  v.leaf = c->P.mapping_surf_leaf_size;
+  TIMED(c, "voxel_scan", launch_voxel_grid(c->stream, v));
+  GnArgs a = gn_args(c, B, trace);
+  if (trace) CK(hipMemsetAsync(c->d_trace, 0, sizeof(float) * B * c->P.max_iterations * 6, c->stream));
+  TIMED(c, "gn_init", launch_gn_init(c->stream, a));
+  CK(hipMemsetAsync(c->d_cropcnt, 0, sizeof(int32_t) * 2 * B, c->stream));
+  TIMED(c, "crop", launch_crop_count(c->stream, a, c->d_map_c, c->gc.n_points, 0, c->d_cropcnt));
+  TIMED(c, "crop", launch_crop_count(c->stream, a, c->d_map_s, c->gs.n_points, 1, c->d_cropcnt));
+  const int grid = std::max(1, std::min(c->max_items, 2048));
+  for (int it = 0; it < c->P.max_iterations; ++it) {
+    TIMED(c, "gn_residual", launch_gn_residual(c->stream, a, grid));
+    TIMED(c, "gn_solve", launch_gn_solve(c->stream, a));
+  }
+  TIMED(c, "gn_finalize", launch_gn_finalize(c->stream, a));
+  return FBR_OK;
+}
+
+int copy_stats(fbr_ctx* c, int B, fbr_reg_stats* stats) {
+  std::vector<fbr_reg_stats> st(B);
+  std::vector<int32_t> crop(2 * B), nv(B), nc(B), ns(B);
+  CK(hipMemcpyAsync(st.data(), c->d_stats, sizeof(fbr_reg_stats) * B, hipMemcpyDeviceToHost, c->stream));
+  CK(hipMemcpyAsync(crop.data(), c->d_cropcnt, sizeof(int32_t) * 2 * B, hipMemcpyDeviceToHost, c->stream));
+  CK(hipMemcpyAsync(nv.data(), c->d_nvalid, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
+  CK(hipMemcpyAsync(nc.data(), c->d_ncorner, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
+  CK(hipMemcpyAsync(ns.data(), c->d_nsurf, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
+  CK(hipStreamSynchronize(c->stream));
+  c->last_iters.resize(B);
+  c->last_q.resize(B);
+  c->last_n.resize(B);
+  c->last_m.resize(B);
+  for (int j = 0; j < B; ++j) {
+    st[j].n_corner_map = crop[2 * j];
+    st[j].n_surf_map = crop[2 * j + 1];
+    st[j].n_points = nv[j];
+    st[j].n_corner = nc[j];
+    st[j].n_surf = ns[j];
+    c->last_iters[j] = st[j].iterations;
+    c->last_q[j] = st[j].n_corner_ds + st[j].n_surf_ds;
+    c->last_n[j] = nv[j];
+    c->last_m[j] = crop[2 * j] + crop[2 * j + 1];
+    if (stats) stats[j] = st[j];
+  }
+  return FBR_OK;
+}
+
+int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n) {
+  if (n < 0 || n > c->NMAX) return FBR_ERR_CAPACITY;
+  if (n) CK(hipMemcpyAsync(c->d_pts + job * c->NMAX, pts, sizeof(fbr_point_xyzirt) * n, hipMemcpyHostToDevice, c->stream));
+  CK(hipMemcpyAsync(c->d_nin + job, &n, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+  CK(hipStreamSynchronize(c->stream));  // n lives on the caller's stack
+  return FBR_OK;
+}
+
+int check_err(fbr_ctx* c, int B) {
+  std::vector<int32_t> e(B);
+  CK(hipMemcpyAsync(e.data(), c->d_err, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
+  CK(hipStreamSynchronize(c->stream));
+  for (int j = 0; j < B; ++j)
+    if (e[j]) return FBR_ERR_UNSUPPORTED;
+  return FBR_OK;
+}
+
+int upload_cloud(fbr_ctx* c, float4* dst, int32_t* dcnt, const fbr_point_xyzi* src, int64_t n) {
+  if (n < 0 || n > c->HW) return FBR_ERR_CAPACITY;
+  if (n && !src) return FBR_ERR_INVALID_ARG;
+  if (n) CK(hipMemcpyAsync(dst, src, sizeof(float4) * n, hipMemcpyHostToDevice, c->stream));
+  int32_t nn = (int32_t)n;
+  CK(hipMemcpyAsync(dcnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  CK(hipStreamSynchronize(c->stream));
+  return FBR_OK;
+}
+
+}  // namespace
+
+// =============================================================================================
+extern "C" {
+
+void fbr_params_default(fbr_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->n_scan = 16;
+  p->horizon_scan = 1800;
+  p->edge_threshold = 1.0f;
+  p->surf_threshold = 0.1f;
+  p->edge_feature_min_valid_num = 10;
+  p->surf_feature_min_valid_num = 100;
+  p->odometry_surf_leaf_size = 0.4f;
+  p->mapping_corner_leaf_size = 0.2f;
+  p->mapping_surf_leaf_size = 0.4f;
+  p->z_tollerance = 1000.0f;
+  p->rotation_tollerance = 1000.0f;
+  p->number_of_cores = 4;
+  p->mapping_process_interval = 0.15;
+  p->crop_half[0] = 30.0f;
+  p->crop_half[1] = 30.0f;
+  p->crop_half[2] = 10.0f;
+  p->max_iterations = 30;
+  p->max_points_per_scan = p->n_scan * p->horizon_scan;
+  p->max_batch = 1;
+}
+
+const char* fbr_strerror(int s) {
+  switch (s) {
+    case FBR_OK: return "ok";
+    case FBR_ERR_INVALID_ARG: return "invalid argument";
+    case FBR_ERR_HIP: return "HIP runtime error";
+    case FBR_ERR_NO_MAP: return "no map set (call fbr_set_map first)";
+    case FBR_ERR_CAPACITY: return "input exceeds the context capacity";
+    case FBR_ERR_UNSUPPORTED: return "configuration not supported by the device kernels";
+    case FBR_ERR_NO_DEVICE: return "no HIP device available";
+    case FBR_ERR_STATE: return "call order violated";
+    default: return "unknown status";
+  }
+}
+
+int fbr_abi_version(void) { return FBR_ABI_VERSION; }
+
+int fbr_device_count(int* count) {
+  if (!count) return FBR_ERR_INVALID_ARG;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return FBR_OK;
+}
+
+int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
+  if (!out) return FBR_ERR_INVALID_ARG;
+  *out = nullptr;
+  int rc = check_params(p);
+  if (rc) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return FBR_ERR_NO_DEVICE;
+  if (hip_device < 0 || hip_device >= ndev) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(hip_device));
+  fbr_ctx* c = new fbr_ctx();
+  c->P = *p;
+  c->dev = hip_device;
+  c->H = p->n_scan;
+  c->W = p->horizon_scan;
+  c->HW = (int64_t)c->H * c->W;
+  c->Bcap = p->max_batch;
+  c->NMAX = p->max_points_per_scan;
+  const int64_t B = c->Bcap, HW = c->HW, H = c->H;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return FBR_ERR_HIP;
+  }
+  c->max_items = (int)(B * 2 * ((HW + 255) / 256 + 1));
+  c->vg_scratch_elems = 4 * B * HW;
+  c->vg_hist_elems = B * std::max<int64_t>(((HW + 255) / 256) * 256, H * (((c->W + 255) / 256) * 256));
+  bool fail = dalloc(&c->d_pts, B * c->NMAX) || dalloc(&c->d_nin, B) || dalloc(&c->d_guess, B * 6) ||
+              dalloc(&c->d_owner, B * HW) || dalloc(&c->d_rowcnt, B * H) || dalloc(&c->d_col, B * HW) ||
+              dalloc(&c->d_start, B * H) || dalloc(&c->d_end, B * H) || dalloc(&c->d_nvalid, B) ||
+              dalloc(&c->d_cloud, B * HW) || dalloc(&c->d_range, B * HW) || dalloc(&c->d_sstate, B) ||
+              dalloc(&c->d_sstream, 1) || dalloc(&c->d_label, B * HW) || dalloc(&c->d_label_stream, HW) ||
+              dalloc(&c->d_corner_slot, B * H * kCornerPerRing) || dalloc(&c->d_corner_cnt, B * H) ||
+              dalloc(&c->d_cand, B * HW) || dalloc(&c->d_cand_cnt, B * H) || dalloc(&c->d_surf_ring, B * HW) ||
+              dalloc(&c->d_surf_ring_cnt, B * H) || dalloc(&c->d_err, B) || dalloc(&c->d_corner_all, B * HW) ||
+              dalloc(&c->d_surf_all, B * HW) || dalloc(&c->d_cornerDS, B * HW) || dalloc(&c->d_surfDS, B * HW) ||
+              dalloc(&c->d_ncorner, B) || dalloc(&c->d_nsurf, B) || dalloc(&c->d_ncds, B) || dalloc(&c->d_nsds, B) ||
+              dalloc(&c->d_vg_scratch, c->vg_scratch_elems) || dalloc(&c->d_vg_hist, c->vg_hist_elems) ||
+              dalloc(&c->d_gn, B) || dalloc(&c->d_items, c->max_items) || dalloc(&c->d_nitems, 1) ||
+              dalloc(&c->d_item_range, 2 * B) || dalloc(&c->d_cropcnt, 2 * B) ||
+              dalloc(&c->d_partial, (int64_t)c->max_items * 32) || dalloc(&c->d_pose_out, B * 6) ||
+              dalloc(&c->d_stats, B) || dalloc(&c->d_trace, B * p->max_iterations * 6);
+  if (fail) {
+    fbr_destroy(c);
+    return FBR_ERR_HIP;
+  }
+  if (hipMemset(c->d_sstream, 0, sizeof(StreamState)) != hipSuccess ||
+      hipMemset(c->d_label_stream, 0, HW) != hipSuccess || hipMemset(c->d_col, 0, sizeof(int32_t) * B * HW) != hipSuccess ||
+      hipMemset(c->d_range, 0, sizeof(float) * B * HW) != hipSuccess) {
+    fbr_destroy(c);
+    return FBR_ERR_HIP;
+  }
+  *out = c;
+  return FBR_OK;
+}
+
+int fbr_destroy(fbr_ctx* c) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  (void)hipSetDevice(c->dev);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* ptrs[] = {c->d_pts, c->d_nin, c->d_guess, c->d_owner, c->d_rowcnt, c->d_col, c->d_start, c->d_end,
+                  c->d_nvalid, c->d_cloud, c->d_range, c->d_sstate, c->d_sstream, c->d_label, c->d_label_stream,
+                  c->d_corner_slot, c->d_corner_cnt, c->d_cand, c->d_cand_cnt, c->d_surf_ring, c->d_surf_ring_cnt,
+                  c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
+                  c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_vg_hist, c->d_gn, c->d_items, c->d_nitems,
+                  c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_map_c,
+                  c->d_map_s, c->d_cs_c, c->d_cs_s};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  for (auto& kv : c->timers) {
+    for (auto& pr : kv.second.pending) {
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+    for (auto& pr : kv.second.pool) {
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+  }
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return FBR_OK;
+}
+
+int fbr_set_map(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corner, const fbr_point_xyzi* surf,
+                int64_t n_surf) {
+  if (!c || n_corner < 0 || n_surf < 0 || (n_corner && !corner) || (n_surf && !surf)) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  int rc = voxel_grid_once(c, corner, n_corner, c->P.mapping_corner_leaf_size, c->map_c_host);
+  if (!rc) rc = voxel_grid_once(c, surf, n_surf, c->P.mapping_surf_leaf_size, c->map_s_host);
+  if (!rc) rc = build_grid(c, c->map_c_host, &c->d_map_c, &c->d_cs_c, &c->gc);
+  if (!rc) rc = build_grid(c, c->map_s_host, &c->d_map_s, &c->d_cs_s, &c->gs);
+  c->has_map = rc == FBR_OK;
+  return rc;
+}
+
+int fbr_get_map(fbr_ctx* c, int64_t* n_corner, int64_t* n_surf, fbr_point_xyzi* corner, fbr_point_xyzi* surf) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  if (!c->has_map) return FBR_ERR_NO_MAP;
+  if (n_corner) *n_corner = (int64_t)c->map_c_host.size();
+  if (n_surf) *n_surf = (int64_t)c->map_s_host.size();
+  if (corner) std::memcpy(corner, c->map_c_host.data(), sizeof(fbr_point_xyzi) * c->map_c_host.size());
+  if (surf) std::memcpy(surf, c->map_s_host.data(), sizeof(fbr_point_xyzi) * c->map_s_host.size());
+  return FBR_OK;
+}
+
+int fbr_project(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, int32_t* start_ring, int32_t* end_ring,
+                int32_t* col_ind, float* range, fbr_point_xyzi* cloud, int64_t* n_out) {
+  if (!c || (n_in && !points)) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  int rc = upload_scan(c, 0, points, n_in);
+  if (rc) return rc;
+  rc = stage_project(c, 1);
+  if (rc) return rc;
+  int32_t n = 0;
+  CK(hipMemcpyAsync(&n, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  CK(hipStreamSynchronize(c->stream));
+  if (start_ring) CK(hipMemcpy(start_ring, c->d_start, sizeof(int32_t) * c->H, hipMemcpyDeviceToHost));
+  if (end_ring) CK(hipMemcpy(end_ring, c->d_end, sizeof(int32_t) * c->H, hipMemcpyDeviceToHost));
+  if (col_ind && n) CK(hipMemcpy(col_ind, c->d_col, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  if (range && n) CK(hipMemcpy(range, c->d_range, sizeof(float) * n, hipMemcpyDeviceToHost));
+  if (cloud && n) CK(hipMemcpy(cloud, c->d_cloud, sizeof(float4) * n, hipMemcpyDeviceToHost));
+  if (n_out) *n_out = n;
+  c->have_projection = true;
+  return FBR_OK;
+}
+
+int fbr_extract_features(fbr_ctx* c, int8_t* label, fbr_point_xyzi* corner, int64_t* n_corner, fbr_point_xyzi* surf,
+                         int64_t* n_surf) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  if (!c->have_projection) return FBR_ERR_STATE;
+  CK(hipSetDevice(c->dev));
+  int rc = stage_features(c, 1, true);
+  if (rc) return rc;
+  rc = check_err(c, 1);
+  if (rc) return rc;
+  int32_t n = 0, nc = 0, ns = 0;
+  CK(hipMemcpy(&n, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost));
+  CK(hipMemcpy(&nc, c->d_ncorner, sizeof(int32_t), hipMemcpyDeviceToHost));
+  CK(hipMemcpy(&ns, c->d_nsurf, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (label && n) CK(hipMemcpy(label, c->d_label_stream, (size_t)n, hipMemcpyDeviceToHost));
+  if (corner && nc) CK(hipMemcpy(corner, c->d_corner_all, sizeof(float4) * nc, hipMemcpyDeviceToHost));
+  if (surf && ns) CK(hipMemcpy(surf, c->d_surf_all, sizeof(float4) * ns, hipMemcpyDeviceToHost));
+  if (n_corner) *n_corner = nc;
+  if (n_surf) *n_surf = ns;
+  return FBR_OK;
+}
+
+int fbr_register_trace(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corner, const fbr_point_xyzi* surf,
+                       int64_t n_surf, float pose_inout[6], fbr_reg_stats* stats, float* trace) {
+  if (!c || !pose_inout) return FBR_ERR_INVALID_ARG;
+  if (!c->has_map) return FBR_ERR_NO_MAP;
+  CK(hipSetDevice(c->dev));
+  int rc = upload_cloud(c, c->d_corner_all, c->d_ncorner, corner, n_corner);
+  if (!rc) rc = upload_cloud(c, c->d_surf_all, c->d_nsurf, surf, n_surf);
+  if (rc) return rc;
+  CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->stream));
+  CK(hipMemsetAsync(c->d_nvalid, 0, sizeof(int32_t), c->stream));
+  rc = stage_register(c, 1, trace != nullptr);
+  if (rc) return rc;
+  CK(hipMemcpyAsync(pose_inout, c->d_pose_out, sizeof(float) * 6, hipMemcpyDeviceToHost, c->stream));
+  if (trace)
+    CK(hipMemcpyAsync(trace, c->d_trace, sizeof(float) * 6 * c->P.max_iterations, hipMemcpyDeviceToHost, c->stream));
+  fbr_reg_stats st;
+  rc = copy_stats(c, 1, &st);
+  if (rc) return rc;
+  st.n_points = 0;
+  st.n_corner = (int32_t)n_corner;
+  st.n_surf = (int32_t)n_surf;
+  if (stats) *stats = st;
+  return FBR_OK;
+}
+
+int fbr_register(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corner, const fbr_point_xyzi* surf,
+                 int64_t n_surf, float pose_inout[6], fbr_reg_stats* stats) {
+  return fbr_register_trace(c, corner, n_corner, surf, n_surf, pose_inout, stats, nullptr);
+}
+
+int fbr_process_scan(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, double stamp, float pose_inout[6],
+                     fbr_reg_stats* stats) {
+  if (!c || !pose_inout || (n_in && !points)) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  int rc = upload_scan(c, 0, points, n_in);
+  if (!rc) rc = stage_project(c, 1);
+  if (!rc) rc = stage_features(c, 1, true);
+  if (!rc) rc = check_err(c, 1);
+  if (rc) return rc;
+  c->have_projection = true;
+  fbr_reg_stats st;
+  std::memset(&st, 0, sizeof(st));
+  if (stamp - c->time_last >= c->P.mapping_process_interval) {  // mapOptmization.h:279
+    if (!c->has_map) return FBR_ERR_NO_MAP;
+    c->time_last = stamp;
+    CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->stream));
+    rc = stage_register(c, 1, false);
+    if (rc) return rc;
+    CK(hipMemcpyAsync(pose_inout, c->d_pose_out, sizeof(float) * 6, hipMemcpyDeviceToHost, c->stream));
+    rc = copy_stats(c, 1, &st);
+    if (rc) return rc;
+  } else {
+    int32_t nv = 0, nc = 0, ns = 0;
+    CK(hipMemcpy(&nv, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(&nc, c->d_ncorner, sizeof(int32_t), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(&ns, c->d_nsurf, sizeof(int32_t), hipMemcpyDeviceToHost));
+    st.status = FBR_REG_SKIPPED_INTERVAL;
+    st.n_points = nv;
+    st.n_corner = nc;
+    st.n_surf = ns;
+  }
+  if (stats) *stats = st;
+  return FBR_OK;
+}
+
+int fbr_reset_stream(fbr_ctx* c) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  CK(hipMemsetAsync(c->d_sstream, 0, sizeof(StreamState), c->stream));
+  CK(hipMemsetAsync(c->d_label_stream, 0, c->HW, c->stream));
+  CK(hipMemsetAsync(c->d_col, 0, sizeof(int32_t) * c->HW, c->stream));
+  CK(hipMemsetAsync(c->d_range, 0, sizeof(float) * c->HW, c->stream));
+  CK(hipStreamSynchronize(c->stream));
+  c->time_last = -1.0;
+  c->have_projection = false;
+  return FBR_OK;
+}
+
+int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int64_t* n_in, int n_jobs,
+                    const float* poses_in) {
+  if (!c || !scans || !n_in || !poses_in || n_jobs <= 0) return FBR_ERR_INVALID_ARG;
+  if (n_jobs > c->Bcap) return FBR_ERR_CAPACITY;
+  CK(hipSetDevice(c->dev));
+  for (int j = 0; j < n_jobs; ++j) {
+    if (n_in[j] < 0 || n_in[j] > c->NMAX) return FBR_ERR_CAPACITY;
+    if (n_in[j] && !scans[j]) return FBR_ERR_INVALID_ARG;
+    if (n_in[j])
+      CK(hipMemcpyAsync(c->d_pts + j * c->NMAX, scans[j], sizeof(fbr_point_xyzirt) * n_in[j], hipMemcpyHostToDevice,
+                        c->stream));
+  }
+  CK(hipMemcpyAsync(c->d_nin, n_in, sizeof(int64_t) * n_jobs, hipMemcpyHostToDevice, c->stream));
+  CK(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * n_jobs, hipMemcpyHostToDevice, c->stream));
+  CK(hipStreamSynchronize(c->stream));
+  c->staged_B = n_jobs;
+  c->staged_nin.assign(n_in, n_in + n_jobs);
+  return FBR_OK;
+}
+
+int fbr_batch_launch(fbr_ctx* c) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  if (c->staged_B <= 0) return FBR_ERR_STATE;
+  if (!c->has_map) return FBR_ERR_NO_MAP;
+  CK(hipSetDevice(c->dev));
+  int rc = stage_project(c, c->staged_B);
+  if (!rc) rc = stage_features(c, c->staged_B, false);
+  if (!rc) rc = stage_register(c, c->staged_B, false);
+  return rc;
+}
+
+int fbr_batch_wait(fbr_ctx* c) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  CK(hipStreamSynchronize(c->stream));
+  return FBR_OK;
+}
+
+int fbr_batch_results(fbr_ctx* c, float* poses_out, fbr_reg_stats* stats) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  if (c->staged_B <= 0) return FBR_ERR_STATE;
+  CK(hipSetDevice(c->dev));
+  const int B = c->staged_B;
+  int rc = check_err(c, B);
+  if (rc) return rc;
+  if (poses_out) CK(hipMemcpyAsync(poses_out, c->d_pose_out, sizeof(float) * 6 * B, hipMemcpyDeviceToHost, c->stream));
+  return copy_stats(c, B, stats);
+}
+
+int fbr_batch_bytes(fbr_ctx* c, double* bytes_total, double* bytes_gn) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  if (c->last_iters.empty()) return FBR_ERR_STATE;
+  double tot = 0.0, gn = 0.0;
+  for (size_t j = 0; j < c->last_iters.size(); ++j) {
+    const double nin = j < c->staged_nin.size() ? (double)c->staged_nin[j] : 0.0;
+    const double n = c->last_n[j], M = c->last_m[j], Q = c->last_q[j], I = c->last_iters[j];
+    const double g = I * 96.0 * Q;  // query 16 B + 5 neighbours x 16 B per iteration
+    tot += 22.0 * nin + 80.0 * n + 16.0 * M + 16.0 * Q + g;
+    gn += g;
+  }
+  if (bytes_total) *bytes_total = tot;
+  if (bytes_gn) *bytes_gn = gn;
+  return FBR_OK;
+}
+
+int fbr_process_batch(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int64_t* n_in, int n_jobs,
+                      float* poses_inout, fbr_reg_stats* stats) {
+  if (!c || !scans || !n_in || !poses_inout || n_jobs < 0) return FBR_ERR_INVALID_ARG;
+  for (int j0 = 0; j0 < n_jobs; j0 += c->Bcap) {
+    const int B = std::min(c->Bcap, n_jobs - j0);
+    int rc = fbr_batch_stage(c, scans + j0, n_in + j0, B, poses_inout + 6 * j0);
+    if (!rc) rc = fbr_batch_launch(c);
+    if (!rc) rc = fbr_batch_wait(c);
+    if (!rc) rc = fbr_batch_results(c, poses_inout + 6 * j0, stats ? stats + j0 : nullptr);
+    if (rc) return rc;
+  }
+  return FBR_OK;
+}
+
+int fbr_voxel_grid(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf, fbr_point_xyzi* out, int64_t* n_out) {
+  if (!c || n < 0 || (n && !in) || !(leaf > 0)) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  std::vector<fbr_point_xyzi> o;
+  int rc = voxel_grid_once(c, in, n, leaf, o);
+  if (rc) return rc;
+  if (out) std::memcpy(out, o.data(), sizeof(fbr_point_xyzi) * o.size());
+  if (n_out) *n_out = (int64_t)o.size();
+  return FBR_OK;
+}
+
+int fbr_set_profiling(fbr_ctx* c, int enable) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  c->profiling = enable != 0;
+  return FBR_OK;
+}
+
+int fbr_kernel_time(fbr_ctx* c, const char* kernel, double* total_ms, int64_t* launches) {
+  if (!c || !kernel) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  auto itr = c->timers.find(kernel);
+  if (itr == c->timers.end()) {
+    if (total_ms) *total_ms = 0.0;
+    if (launches) *launches = 0;
+    return FBR_OK;
+  }
+  KernelTimer& t = itr->second;
+  for (auto& pr : t.pending) {
+    CK(hipEventSynchronize(pr.second));
+    float ms = 0.0f;
+    CK(hipEventElapsedTime(&ms, pr.first, pr.second));
+    t.total_ms += ms;
+    t.launches += 1;
+    t.pool.push_back(pr);
+  }
+  t.pending.clear();
+  if (total_ms) *total_ms = t.total_ms;
+  if (launches) *launches = t.launches;
+  return FBR_OK;
+}
+
+void* fbr_stream(fbr_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+// pcl::getTransformation(x, y, z, roll, pitch, yaw) (pcl/common/impl/eigen.hpp), float.
+void fbr_affine_from_pose(const float pose[6], float m[16]) {
+  const float roll = pose[0], pitch = pose[1], yaw = pose[2];
+  const float A = std::cos(yaw), B = std::sin(yaw), C = std::cos(pitch), D = std::sin(pitch), E = std::cos(roll),
+              F = std::sin(roll), DE = D * E, DF = D * F;
+  m[0] = A * C; m[1] = A * DF - B * E; m[2] = B * F + A * DE; m[3] = pose[3];
+  m[4] = B * C; m[5] = A * E + B * DF; m[6] = B * DE - A * F; m[7] = pose[4];
+  m[8] = -D;    m[9] = C * F;          m[10] = C * E;         m[11] = pose[5];
+  m[12] = 0.0f; m[13] = 0.0f; m[14] = 0.0f; m[15] = 1.0f;
+}
+
+// pcl::getTranslationAndEulerAngles (pcl/common/impl/eigen.hpp), float.
+void fbr_pose_from_affine(const float m[16], float pose[6]) {
+  pose[3] = m[3];
+  pose[4] = m[7];
+  pose[5] = m[11];
+  pose[0] = std::atan2(m[9], m[10]);
+  pose[1] = std::asin(-m[8]);
+  pose[2] = std::atan2(m[4], m[0]);
+}
+
+}  // extern "C"

@@ -1,0 +1,78 @@
+// fbr_common.h — shared device-side definitions of the MI355X registration path.
+//
+// HBM layout (per device batch of B jobs, each job = one scan registered from its own guess):
+//   raw points   fbr_point_xyzirt [B][NMAX]           (24 B AoS, the PointXYZIRT payload)
+//   cell owner   int32            [B][H*W]            first-wins claim (atomicMin of input index)
+//   cloud        float4           [B][H*W]            ring-major compacted xyzi (cloud_deskewed)
+//   col / range  int32 / float    [B][H*W]            cloud_info.pointColInd / pointRange
+//   ring index   int32            [B][H] x2           cloud_info.startRingIndex / endRingIndex
+//   label        int8             [B][H*W]            cloudLabel (the feature mask)
+//   corner slot  float4           [B][H][120]         per-ring corner picks in visit order
+//   surf cand    float4           [B][H][W]           per-ring surf candidates (label <= 0)
+//   surf ring DS float4           [B][H][W]           per-ring VoxelGrid output
+//   corner/surf  float4           [B][CAPC] / [B][H*W] concatenated feature clouds
+//   cornerDS/surfDS float4        [B][CAPC] / [B][H*W] registration down-sampled queries
+// Map (shared by all jobs, read-only, built once by fbr_set_map):
+//   pts          float4 [M] sorted by 1 m grid cell (w = bit pattern of the global map index)
+//   cell start   int32 [ncells+1]
+#pragma once
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <limits.h>
+#include <stdint.h>
+
+#include "../../include/fbr.h"
+
+namespace fbr {
+
+constexpr int kEmptyOwner = 0x7F7F7F7F;   // byte-memset sentinel: larger than any point index
+constexpr int kCornerPerSeg = 20;         // featureExtraction.h:217
+constexpr int kCornerPerRing = 20 * 6;
+constexpr int kMaxSegment = 512;          // per-ring segment length capacity (W <= 3000)
+constexpr int kMaxW = 4096;               // Horizon_SCAN capacity of the per-ring kernels
+constexpr float kGridCell = 1.0f;         // kNN search grid cell (>= sqrt of the d2 < 1.0 gate)
+
+// Correctly rounded f32 sqrt (glibc sqrtf / SSE sqrtss semantics).  gfx950's f32 sqrt lowering
+// (including __fsqrt_rn) is off by one ulp on ~15 % of inputs; the double sqrt is correctly rounded
+// and rounding it to float is innocuous for sqrt (53 >= 2*24+2 bits).
+__host__ __device__ inline float sqrt_rn(float x) { return (float)sqrt((double)x); }
+
+// x86-64 cvttsd2si: NaN / out-of-range -> INT_MIN (imageProjection.cpp:611 conversion).
+__host__ __device__ inline int x86_cvt(double v) {
+  if (!(v > -2147483649.0 && v < 2147483648.0)) return (int)0x80000000;
+  return (int)v;
+}
+
+// Stream-mode FeatureExtraction state that survives between scans (featureExtraction.h:39-42):
+// the never-recomputed smoothness slot 4 and cloudNeighborPicked[0..4].
+struct StreamState {
+  float smooth4_value;
+  int32_t smooth4_ind;
+  int8_t picked04[8];
+};
+
+// Per-job Gauss-Newton state (mapOptmization.h transformTobeMapped / isDegenerate / loop).
+struct GnState {
+  float pose[6];      // transformTobeMapped
+  float T[12];        // trans2Affine3f(pose), row-major 3x4
+  float trig[6];      // srx, crx, sry, cry, srz, crz for LMOptimization
+  int32_t active;     // 1 while iterating
+  int32_t iter;       // LMOptimization calls made
+  int32_t converged;
+  int32_t degenerate;
+  int32_t n_sel;
+  int32_t status;     // FBR_REG_*
+  float matP[36];     // iteration-0 degeneracy projection (zero afterwards: local cv::Mat)
+  float crop_min[3], crop_max[3];
+  int32_t pad[2];
+};
+
+struct GridDesc {        // dense 3D grid over a map
+  float origin[3];       // world coordinate of cell (0,0,0) corner
+  float inv_cell;
+  int32_t dims[3];
+  int32_t n_cells;
+  int64_t n_points;
+};
+
+}  // namespace fbr

@@ -1,0 +1,98 @@
+// fbr_kernels.h — argument blocks and host launchers of the device kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fbr_common.h"
+
+namespace fbr {
+
+// ---- A2+A4 (k_project.hip) ----
+void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
+                    int W, int32_t* owner);
+void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,
+                    int W, int32_t* rowcnt, float4* cloud, int32_t* col, float* range, int32_t* start_ring,
+                    int32_t* end_ring, int32_t* nvalid);
+
+// ---- A6-A8 (k_features.hip) ----
+struct FeatArgs {
+  int B, H, W;
+  const float4* cloud;
+  const int32_t* col;
+  const float* range;
+  const int32_t* start_ring;
+  const int32_t* end_ring;
+  const int32_t* nvalid;
+  float edge_thr, surf_thr;
+  StreamState* stream;   // [B]
+  int8_t* label;         // [B][H*W]
+  float4* corner_slot;   // [B][H][120]
+  int32_t* corner_cnt;   // [B][H]
+  float4* cand;          // [B][H][W]
+  int32_t* cand_cnt;     // [B][H]
+  int32_t* err;          // [B]
+  int lcap, segcap;      // LDS capacities (window length, segment length)
+};
+void launch_features(hipStream_t s, const FeatArgs& a);
+
+// ---- A9 VoxelGrid over segments (k_voxel.hip) ----
+struct VgArgs {
+  const float4* in;
+  int64_t stride_in;
+  const int32_t* cnt_in;  // per-segment input counts
+  float4* out;
+  int64_t stride_out;
+  int32_t* cnt_out;
+  uint32_t* scratch;      // [nseg][4][stride_in]
+  uint32_t* hist;         // [nseg][hist_stride]
+  int64_t hist_stride;    // >= ceil(stride_in/256)*256
+  float leaf;
+  int nseg;
+};
+void launch_voxel_grid(hipStream_t s, const VgArgs& a);
+
+// Concatenate per-ring corner slots / per-ring surf DS outputs into per-job clouds (the
+// cornerCloud / surfaceCloud push_back order of featureExtraction.h:219,292).
+void launch_concat(hipStream_t s, int B, int H, int W, const float4* corner_slot, const int32_t* corner_cnt,
+                   const float4* surf_ring, const int32_t* surf_ring_cnt, float4* corner_all, int64_t capc,
+                   int32_t* n_corner, float4* surf_all, int64_t caps, int32_t* n_surf);
+
+// ---- A10-A18 (k_register.hip) ----
+struct MapGrid {
+  const float4* pts;          // sorted by cell; w = bit pattern of the map index
+  const int32_t* cell_start;  // [n_cells+1]
+  GridDesc g;
+};
+
+struct GnArgs {
+  int B, max_iter;
+  const float4* cornerDS;
+  int64_t capc;
+  const int32_t* ncds;
+  const float4* surfDS;
+  int64_t caps;
+  const int32_t* nsds;
+  MapGrid mc, ms;
+  GnState* gn;               // [B]
+  const float* guess;        // [B][6]
+  int4* items;               // work items {job, type, start, count}
+  int32_t* nitems;           // [1]
+  int32_t* item_range;       // [B][2] first / end item of each job
+  double* partial;           // [max_items][32]
+  int max_items;
+  int edge_min, surf_min;
+  float crop_half[3];
+  float rot_tol, z_tol;
+  float* pose_out;           // [B][6]
+  fbr_reg_stats* stats;      // [B]
+  float* trace;              // [B][max_iter][6] or null
+};
+void launch_gn_init(hipStream_t s, const GnArgs& a);
+void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid);
+void launch_gn_solve(hipStream_t s, const GnArgs& a);
+void launch_gn_finalize(hipStream_t s, const GnArgs& a);
+// laserCloud{Corner,Surf}FromMapDSNum: CropBox counts of the global map per job.
+void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* map_pts, int64_t n, int which,
+                       int32_t* counts /* [B][2] */);
+
+}  // namespace fbr

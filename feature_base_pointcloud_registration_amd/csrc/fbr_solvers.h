@@ -1,0 +1,345 @@
+// fbr_solvers.h — single-lane float small dense solvers used inside the registration kernels.
+//
+// The reference calls third-party solvers inside its hot loop; each is restated here in float
+// with the published algorithm's operation order (no FMA: the library is built with
+// -ffp-contract=off) so the device residuals and normal-equation solves follow the reference:
+//   cv::eigen on the 3x3 corner covariance   mapOptmization.h:1060  -> jacobi_eigen<3>
+//   cv::eigen on the 6x6 AtA (degeneracy)    mapOptmization.h:1353  -> jacobi_eigen<6>
+//   cv::solve(AtA, AtB, X, DECOMP_QR)        mapOptmization.h:1343  -> qr_solve6
+//   matV.inv() (LU)                          mapOptmization.h:1370  -> lu_inv6
+//   Eigen colPivHouseholderQr().solve        mapOptmization.h:1169  -> colpiv_solve53
+//   OpenCV CV_32F gemm (double accumulate)   mapOptmization.h:1338-1340,1370,1376
+#pragma once
+#include <hip/hip_runtime.h>
+#include <float.h>
+
+#include "fbr_common.h"
+
+namespace fbr {
+
+__device__ __forceinline__ float cvhypot(float a, float b) {
+  a = fabsf(a);
+  b = fabsf(b);
+  if (a > b) {
+    b /= a;
+    return a * sqrt_rn(1.0f + b * b);
+  }
+  if (b > 0.0f) {
+    a /= b;
+    return b * sqrt_rn(1.0f + a * a);
+  }
+  return 0.0f;
+}
+
+// OpenCV JacobiImpl_<float>: A (N x N row-major, destroyed), W eigenvalues (descending),
+// V rows = eigenvectors.
+template <int N>
+__device__ void jacobi_eigen(float* A, float* W, float* V) {
+  const float eps = FLT_EPSILON;
+  int indR[N], indC[N];
+  for (int i = 0; i < N; i++)
+    for (int j = 0; j < N; j++) V[i * N + j] = (i == j) ? 1.0f : 0.0f;
+  float mv;
+  for (int k = 0; k < N; k++) {
+    W[k] = A[(N + 1) * k];
+    if (k < N - 1) {
+      int m = k + 1;
+      mv = fabsf(A[N * k + m]);
+      for (int i = k + 2; i < N; i++) {
+        float val = fabsf(A[N * k + i]);
+        if (mv < val) mv = val, m = i;
+      }
+      indR[k] = m;
+    }
+    if (k > 0) {
+      int m = 0;
+      mv = fabsf(A[k]);
+      for (int i = 1; i < k; i++) {
+        float val = fabsf(A[N * i + k]);
+        if (mv < val) mv = val, m = i;
+      }
+      indC[k] = m;
+    }
+  }
+  const int maxIters = N * N * 30;
+  for (int iters = 0; iters < maxIters; iters++) {
+    int k = 0;
+    mv = fabsf(A[indR[0]]);
+    for (int i = 1; i < N - 1; i++) {
+      float val = fabsf(A[N * i + indR[i]]);
+      if (mv < val) mv = val, k = i;
+    }
+    int l = indR[k];
+    for (int i = 1; i < N; i++) {
+      float val = fabsf(A[N * indC[i] + i]);
+      if (mv < val) mv = val, k = indC[i], l = i;
+    }
+    float p = A[N * k + l];
+    if (fabsf(p) <= eps) break;
+    float y = (float)((double)(W[l] - W[k]) * 0.5);
+    float t = fabsf(y) + cvhypot(p, y);
+    float s = cvhypot(p, t);
+    float c = t / s;
+    s = p / s;
+    t = (p / t) * p;
+    if (y < 0.0f) s = -s, t = -t;
+    A[N * k + l] = 0.0f;
+    W[k] -= t;
+    W[l] += t;
+    float a0, b0;
+#define FBR_ROT(v0, v1) a0 = v0, b0 = v1, v0 = a0 * c - b0 * s, v1 = a0 * s + b0 * c
+    for (int i = 0; i < k; i++) FBR_ROT(A[N * i + k], A[N * i + l]);
+    for (int i = k + 1; i < l; i++) FBR_ROT(A[N * k + i], A[N * i + l]);
+    for (int i = l + 1; i < N; i++) FBR_ROT(A[N * k + i], A[N * l + i]);
+    for (int i = 0; i < N; i++) FBR_ROT(V[N * k + i], V[N * l + i]);
+#undef FBR_ROT
+    for (int j = 0; j < 2; j++) {
+      int idx = j == 0 ? k : l;
+      if (idx < N - 1) {
+        int m = idx + 1;
+        mv = fabsf(A[N * idx + m]);
+        for (int i = idx + 2; i < N; i++) {
+          float val = fabsf(A[N * idx + i]);
+          if (mv < val) mv = val, m = i;
+        }
+        indR[idx] = m;
+      }
+      if (idx > 0) {
+        int m = 0;
+        mv = fabsf(A[idx]);
+        for (int i = 1; i < idx; i++) {
+          float val = fabsf(A[N * i + idx]);
+          if (mv < val) mv = val, m = i;
+        }
+        indC[idx] = m;
+      }
+    }
+  }
+  for (int k = 0; k < N - 1; k++) {
+    int m = k;
+    for (int i = k + 1; i < N; i++)
+      if (W[m] < W[i]) m = i;
+    if (k != m) {
+      float t = W[m];
+      W[m] = W[k];
+      W[k] = t;
+      for (int i = 0; i < N; i++) {
+        float u = V[N * m + i];
+        V[N * m + i] = V[N * k + i];
+        V[N * k + i] = u;
+      }
+    }
+  }
+}
+
+// OpenCV QRImpl (Householder) for a 6x6 system, eps = FLT_EPSILON*10; returns 0 if singular.
+__device__ int qr_solve6(float* A, float* b) {
+  const int n = 6, m = 6;
+  const float eps = FLT_EPSILON * 10.0f;
+  float vl[6], hF[6];
+  for (int l = 0; l < n; l++) {
+    const int vlSize = m - l;
+    float vlNorm = 0.0f;
+    for (int i = 0; i < vlSize; i++) {
+      vl[i] = A[(l + i) * n + l];
+      vlNorm += vl[i] * vl[i];
+    }
+    float tmpV = vl[0];
+    vl[0] = vl[0] + (vl[0] >= 0.0f ? 1.0f : -1.0f) * sqrt_rn(vlNorm);
+    vlNorm = sqrt_rn(vlNorm + vl[0] * vl[0] - tmpV * tmpV);
+    for (int i = 0; i < vlSize; i++) vl[i] /= vlNorm;
+    for (int j = l; j < n; j++) {
+      float v_lA = 0.0f;
+      for (int i = l; i < m; i++) v_lA += vl[i - l] * A[i * n + j];
+      for (int i = l; i < m; i++) A[i * n + j] -= 2.0f * vl[i - l] * v_lA;
+    }
+    hF[l] = vl[0] * vl[0];
+    for (int i = 1; i < vlSize; i++) A[(l + i) * n + l] = vl[i] / vl[0];
+  }
+  for (int l = 0; l < n; l++) {
+    vl[0] = 1.0f;
+    for (int j = 1; j < m - l; j++) vl[j] = A[(j + l) * n + l];
+    float v_lB = 0.0f;
+    for (int i = l; i < m; i++) v_lB += vl[i - l] * b[i];
+    for (int i = l; i < m; i++) b[i] -= 2.0f * vl[i - l] * v_lB * hF[l];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    for (int j = n - 1; j > i; j--) b[i] -= b[j] * A[i * n + j];
+    if (fabsf(A[i * n + i]) < eps) return 0;
+    b[i] /= A[i * n + i];
+  }
+  return 1;
+}
+
+// OpenCV LUImpl with an identity right-hand side (Mat::inv, DECOMP_LU), 6x6, eps FLT_EPSILON*10.
+__device__ int lu_inv6(const float* Ain, float* Bi) {
+  const int n = 6;
+  const float eps = FLT_EPSILON * 10.0f;
+  float A[36];
+  for (int i = 0; i < 36; ++i) A[i] = Ain[i];
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < n; j++) Bi[i * n + j] = (i == j) ? 1.0f : 0.0f;
+  for (int i = 0; i < n; i++) {
+    int k = i;
+    for (int j = i + 1; j < n; j++)
+      if (fabsf(A[j * n + i]) > fabsf(A[k * n + i])) k = j;
+    if (fabsf(A[k * n + i]) < eps) return 0;
+    if (k != i) {
+      for (int j = i; j < n; j++) {
+        float t = A[i * n + j];
+        A[i * n + j] = A[k * n + j];
+        A[k * n + j] = t;
+      }
+      for (int j = 0; j < n; j++) {
+        float t = Bi[i * n + j];
+        Bi[i * n + j] = Bi[k * n + j];
+        Bi[k * n + j] = t;
+      }
+    }
+    float d = -1.0f / A[i * n + i];
+    for (int j = i + 1; j < n; j++) {
+      float alpha = A[j * n + i] * d;
+      for (int c = i + 1; c < n; c++) A[j * n + c] += alpha * A[i * n + c];
+      for (int c = 0; c < n; c++) Bi[j * n + c] += alpha * Bi[i * n + c];
+    }
+  }
+  for (int i = n - 1; i >= 0; i--)
+    for (int j = 0; j < n; j++) {
+      float s = Bi[i * n + j];
+      for (int c = i + 1; c < n; c++) s -= A[i * n + c] * Bi[c * n + j];
+      Bi[i * n + j] = s / A[i * n + i];
+    }
+  return 1;
+}
+
+// OpenCV gemm for CV_32F: double accumulation, float store.  C[M][N] = A[M][K] B[K][N].
+__device__ void gemm_f32_acc64(const float* A, const float* B, float* C, int M, int K, int N) {
+  for (int i = 0; i < M; i++)
+    for (int j = 0; j < N; j++) {
+      double s = 0.0;
+      for (int k = 0; k < K; k++) s += (double)A[i * K + k] * (double)B[k * N + j];
+      C[i * N + j] = (float)s;
+    }
+}
+
+// Eigen 3.3 ColPivHouseholderQR<Matrix<float,5,3>>::compute(A).solve(b), sequential sums.
+__device__ void colpiv_solve53(const float (&Ain)[5][3], const float (&bin)[5], float (&x)[3]) {
+  const int rows = 5, cols = 3, size = 3;
+  float qr[5][3];
+  for (int i = 0; i < 5; ++i)
+    for (int j = 0; j < 3; ++j) qr[i][j] = Ain[i][j];
+  float hc[3], nUpd[3], nDir[3];
+  int transp[3];
+  for (int k = 0; k < cols; ++k) {
+    float s = 0.0f;
+    for (int i = 0; i < rows; i++) s += qr[i][k] * qr[i][k];
+    nDir[k] = sqrt_rn(s);
+    nUpd[k] = nDir[k];
+  }
+  const float eps = FLT_EPSILON;
+  float mxn = nUpd[0];
+  for (int k = 1; k < cols; ++k)
+    if (nUpd[k] > mxn) mxn = nUpd[k];
+  const float th = (mxn * eps) * (mxn * eps) / (float)rows;
+  const float ndt = sqrt_rn(eps);
+  int nz = size;
+  for (int k = 0; k < size; ++k) {
+    int big = k;
+    float bv = nUpd[k];
+    for (int j = k + 1; j < cols; ++j)
+      if (nUpd[j] > bv) bv = nUpd[j], big = j;
+    const float bsq = bv * bv;
+    if (nz == size && bsq < th * (float)(rows - k)) nz = k;
+    transp[k] = big;
+    if (k != big) {
+      for (int i = 0; i < rows; ++i) {
+        float t = qr[i][k];
+        qr[i][k] = qr[i][big];
+        qr[i][big] = t;
+      }
+      float t = nUpd[k];
+      nUpd[k] = nUpd[big];
+      nUpd[big] = t;
+      t = nDir[k];
+      nDir[k] = nDir[big];
+      nDir[big] = t;
+    }
+    float tailSq = 0.0f;
+    for (int i = k + 1; i < rows; ++i) tailSq += qr[i][k] * qr[i][k];
+    const float c0 = qr[k][k];
+    float beta, tau;
+    if (tailSq <= FLT_MIN) {
+      tau = 0.0f;
+      beta = c0;
+      for (int i = k + 1; i < rows; ++i) qr[i][k] = 0.0f;
+    } else {
+      beta = sqrt_rn(c0 * c0 + tailSq);
+      if (c0 >= 0.0f) beta = -beta;
+      const float den = c0 - beta;
+      for (int i = k + 1; i < rows; ++i) qr[i][k] = qr[i][k] / den;
+      tau = (beta - c0) / beta;
+    }
+    hc[k] = tau;
+    qr[k][k] = beta;
+    if (k + 1 < cols && tau != 0.0f) {
+      for (int j = k + 1; j < cols; ++j) {
+        float tmp = 0.0f;
+        for (int i = k + 1; i < rows; ++i) tmp += qr[i][k] * qr[i][j];
+        tmp += qr[k][j];
+        qr[k][j] -= tau * tmp;
+        for (int i = k + 1; i < rows; ++i) qr[i][j] -= tmp * (tau * qr[i][k]);
+      }
+    }
+    for (int j = k + 1; j < cols; ++j) {
+      if (nUpd[j] != 0.0f) {
+        float temp = fabsf(qr[k][j]) / nUpd[j];
+        temp = (1.0f + temp) * (1.0f - temp);
+        temp = temp < 0.0f ? 0.0f : temp;
+        const float q = nUpd[j] / nDir[j];
+        const float temp2 = temp * (q * q);
+        if (temp2 <= ndt) {
+          float s = 0.0f;
+          for (int i = k + 1; i < rows; i++) s += qr[i][j] * qr[i][j];
+          nDir[j] = sqrt_rn(s);
+          nUpd[j] = nDir[j];
+        } else {
+          nUpd[j] *= sqrt_rn(temp);
+        }
+      }
+    }
+  }
+  int perm[3] = {0, 1, 2};
+  for (int k = 0; k < size; ++k) {
+    int t = perm[k];
+    perm[k] = perm[transp[k]];
+    perm[transp[k]] = t;
+  }
+  if (nz == 0) {
+    x[0] = x[1] = x[2] = 0.0f;
+    return;
+  }
+  float c[5];
+  for (int i = 0; i < 5; ++i) c[i] = bin[i];
+  for (int k = 0; k < nz; ++k) {
+    const float tau = hc[k];
+    if (rows - k == 1) {
+      c[k] *= 1.0f - tau;
+    } else if (tau != 0.0f) {
+      float tmp = 0.0f;
+      for (int i = k + 1; i < rows; ++i) tmp += qr[i][k] * c[i];
+      tmp += c[k];
+      c[k] -= tau * tmp;
+      for (int i = k + 1; i < rows; ++i) c[i] -= tmp * (tau * qr[i][k]);
+    }
+  }
+  for (int i = nz - 1; i >= 0; --i) {
+    if (c[i] != 0.0f) {
+      c[i] /= qr[i][i];
+      for (int t = 0; t < i; ++t) c[t] -= c[i] * qr[t][i];
+    }
+  }
+  for (int i = 0; i < 3; ++i) x[i] = 0.0f;
+  for (int i = 0; i < nz; ++i) x[perm[i]] = c[i];
+}
+
+}  // namespace fbr

@@ -1,0 +1,114 @@
+// k_project.hip — A2 projectPointCloud + A4 cloudExtraction on the device.
+//
+// Reference: /root/reference/src/imageProjection.cpp:583-640 (projection, first point wins a
+// range-image cell) and :642-670 (ring-major compaction, start/endRingIndex).
+//
+// K1 k_project:   one lane per raw point.  Column/range arithmetic is bit-for-bit the
+//                 reference's (fdlibm atan2f, float *180, double /M_PI, double round, x86 int
+//                 conversion, float sqrt without FMA).  A passing point claims its cell with
+//                 atomicMin(owner, input index): the minimum index is exactly the reference's
+//                 "first point wins" (rangeMat != FLT_MAX test, :623).
+// K2 k_rowcount / k_compact: one wave per (job, ring row); ballot + popcount compaction keeps the
+//                 row-major (ring, column) order of cloudExtraction.  Range is recomputed from the
+//                 owning point (same expression, same bits) instead of storing a range image.
+// Roofline: HBM-bound.  Algorithmic bytes: 24 B per raw point read (K1), 4 B/cell owner
+// write+read, 24 B per valid point written (xyzi 16 + col 4 + range 4).
+#include "fbr_common.h"
+#include "fbr_fdlibm.h"
+#include "fbr_kernels.h"
+
+namespace fbr {
+
+__device__ __forceinline__ bool project_point(const fbr_point_xyzirt& q, int H, int W, int& cell) {
+  int rowIdn = q.ring;
+  if (rowIdn < 0 || rowIdn >= H) return false;
+  float horizonAngle = (float)((double)(fd_atan2f(q.x, q.y) * 180.0f) / M_PI);
+  float ang_res_x = (float)(360.0 / (double)(float)W);
+  int columnIdn = x86_cvt(-round(((double)horizonAngle - 90.0) / (double)ang_res_x) + (double)(W / 2));
+  if (columnIdn >= W) columnIdn -= W;
+  if (columnIdn < 0 || columnIdn >= W) return false;
+  float range = sqrt_rn(q.x * q.x + q.y * q.y + q.z * q.z);
+  if (range < 1.0f) return false;
+  cell = rowIdn * W + columnIdn;
+  return true;
+}
+
+__global__ void k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ nin,
+                          int64_t nmax, int H, int W, int32_t* __restrict__ owner) {
+  const int job = blockIdx.y;
+  const int64_t n = nin[job];
+  const fbr_point_xyzirt* P = pts + (int64_t)job * nmax;
+  int32_t* O = owner + (int64_t)job * H * W;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    fbr_point_xyzirt q = P[i];
+    int cell;
+    if (project_point(q, H, W, cell)) atomicMin(&O[cell], (int32_t)i);
+  }
+}
+
+// One wave per (job,row): number of claimed cells in the row.
+__global__ void k_rowcount(const int32_t* __restrict__ owner, int H, int W, int32_t* __restrict__ rowcnt) {
+  const int row = blockIdx.x, job = blockIdx.y, lane = threadIdx.x;
+  const int32_t* O = owner + ((int64_t)job * H + row) * W;
+  int cnt = 0;
+  for (int c = lane; c < W; c += 64) cnt += (O[c] != kEmptyOwner);
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if (lane == 0) rowcnt[job * H + row] = cnt;
+}
+
+__global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, const int32_t* __restrict__ owner,
+                          const int32_t* __restrict__ rowcnt, int H, int W, float4* __restrict__ cloud,
+                          int32_t* __restrict__ col, float* __restrict__ range, int32_t* __restrict__ start_ring,
+                          int32_t* __restrict__ end_ring, int32_t* __restrict__ nvalid) {
+  const int row = blockIdx.x, job = blockIdx.y, lane = threadIdx.x;
+  const int64_t HW = (int64_t)H * W;
+  const int32_t* RC = rowcnt + job * H;
+  int off = 0;
+  for (int r = lane; r < row; r += 64) off += RC[r];
+  for (int s = 32; s > 0; s >>= 1) off += __shfl_xor(off, s);
+  const int cnt = RC[row];
+  if (lane == 0) {
+    start_ring[job * H + row] = off - 1 + 5;        // imageProjection.cpp:650
+    end_ring[job * H + row] = off + cnt - 1 - 5;    // :668
+    if (row == H - 1) nvalid[job] = off + cnt;
+  }
+  const int32_t* O = owner + job * HW + (int64_t)row * W;
+  const fbr_point_xyzirt* P = pts + (int64_t)job * nmax;
+  float4* C = cloud + job * HW;
+  int32_t* CI = col + job * HW;
+  float* R = range + job * HW;
+  int base = off;
+  for (int c0 = 0; c0 < W; c0 += 64) {
+    const int c = c0 + lane;
+    const int32_t o = c < W ? O[c] : kEmptyOwner;
+    const bool v = o != kEmptyOwner;
+    const uint64_t m = __ballot(v);
+    if (v) {
+      const int dst = base + __popcll(m & ((1ull << lane) - 1ull));
+      const fbr_point_xyzirt q = P[o];
+      C[dst] = make_float4(q.x, q.y, q.z, q.intensity);
+      CI[dst] = c;
+      R[dst] = sqrt_rn(q.x * q.x + q.y * q.y + q.z * q.z);
+    }
+    base += __popcll(m);
+  }
+}
+
+void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
+                    int W, int32_t* owner) {
+  int blocks = (int)((nmax + 255) / 256);
+  if (blocks > 512) blocks = 512;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_project, dim3(blocks, B), dim3(256), 0, s, pts, nin, nmax, H, W, owner);
+}
+
+void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,
+                    int W, int32_t* rowcnt, float4* cloud, int32_t* col, float* range, int32_t* start_ring,
+                    int32_t* end_ring, int32_t* nvalid) {
+  hipLaunchKernelGGL(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, rowcnt);
+  hipLaunchKernelGGL(k_compact, dim3(H, B), dim3(64), 0, s, pts, nmax, owner, rowcnt, H, W, cloud, col, range,
+                     start_ring, end_ring, nvalid);
+}
+
+}  // namespace fbr

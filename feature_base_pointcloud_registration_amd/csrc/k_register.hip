@@ -1,0 +1,428 @@
+// k_register.hip — A10-A18: scan2MapOptimization on the device.
+//
+// Reference: /root/reference/src/mapOptmization.h
+//   registration()            :263-343  crop box (:284-304), pose <-> transformTobeMapped (:309,:326)
+//   cornerOptimization()      :1002-1124 point-to-line residual, kNN-5, 3x3 cv::eigen
+//   surfOptimization()        :1126-1215 point-to-plane residual, kNN-5, 5x3 colPivHouseholderQr
+//   combineOptimizationCoeffs :1218-1243 corner rows (index order) then surf rows
+//   LMOptimization()          :1246-1401 camera-frame Jacobian rows, AtA/AtB, QR solve,
+//                                        iteration-0 degeneracy (eigen < 100), update, 0.05/0.05 stop
+//   scan2MapOptimization()    :1403-1442 feature gate, <= 30 iterations
+//   transformUpdate()         :1444-1489 tolerance clamps (imuAvailable == 0)
+//
+// Design (MI355X-first, results identical to the reference's KD-tree path):
+//   * The reference rebuilds two FLANN KD-trees on the cropped local map every scan.  Here the
+//     global map is bucketed ONCE into a dense grid with power-of-two cells >= 1 m (exact
+//     integer cell coordinates); the per-scan CropBox becomes a per-candidate box test.  Because
+//     a correspondence is kept only if the 5th neighbour has d2 < 1.0 (:1027, :1154), scanning the
+//     27 cells around the query and keeping the 5 smallest (d2, index) with d2 < 1.0 selects
+//     exactly the same neighbours as exact kNN-5 on the cropped cloud.
+//   * k_gn_residual: one lane per query (corner and surf queries of every active job of the batch
+//     are packed into 256-query work items); transform, kNN, residual and Jacobian row in float
+//     with the reference's operation order; the 21+6 normal-equation products are reduced in fp64
+//     (OpenCV's CV_32F gemm accumulates in double) by wave shuffles into one partial per item.
+//   * k_gn_solve: one lane per job sums its items in order (corner items, then surf items: the
+//     combineOptimizationCoeffs row order), rounds AtA/AtB to float and runs the reference's float
+//     QR solve / Jacobi / LU; the Gauss-Newton state never leaves the device.
+// Roofline: HBM/L2 gather-bound.  Algorithmic bytes per query per iteration: 16 (query) +
+// 5 x 16 (neighbours) = 96 B.
+#include "fbr_common.h"
+#include "fbr_kernels.h"
+#include "fbr_solvers.h"
+
+namespace fbr {
+
+namespace {
+constexpr int kResThreads = 256;
+constexpr int kPartial = 32;  // doubles per item partial: 21 AtA upper + 6 AtB + count
+}
+
+// pcl::getTransformation (x,y,z,roll,pitch,yaw) in float, sin/cos rounded from double.
+__device__ void pose_to_T(const float* tr, float* T, float* trig) {
+  const float roll = tr[0], pitch = tr[1], yaw = tr[2];
+  const float A = (float)cos((double)yaw), B = (float)sin((double)yaw), C = (float)cos((double)pitch),
+              D = (float)sin((double)pitch), E = (float)cos((double)roll), F = (float)sin((double)roll);
+  const float DE = D * E, DF = D * F;
+  T[0] = A * C; T[1] = A * DF - B * E; T[2] = B * F + A * DE; T[3] = tr[3];
+  T[4] = B * C; T[5] = A * E + B * DF; T[6] = B * DE - A * F; T[7] = tr[4];
+  T[8] = -D;    T[9] = C * F;          T[10] = C * E;         T[11] = tr[5];
+  // LMOptimization (:1259-1264): srx, crx (pitch), sry, cry (yaw), srz, crz (roll)
+  trig[0] = D; trig[1] = C; trig[2] = B; trig[3] = A; trig[4] = F; trig[5] = E;
+}
+
+struct Knn5 {
+  float d[5];
+  int idx[5];
+  float x[5], y[5], z[5];
+  int cnt;
+};
+
+__device__ __forceinline__ bool knn_less(float d, int i, float d2, int i2) { return d < d2 || (d == d2 && i < i2); }
+
+// Insert by compare-swap down a sorted 5-slot list (compile-time indices: stays in registers).
+__device__ __forceinline__ void knn_insert(Knn5& r, float d, int idx, float px, float py, float pz) {
+  if (!knn_less(d, idx, r.d[4], r.idx[4])) return;
+  r.cnt = min(r.cnt + 1, 5);
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    if (knn_less(d, idx, r.d[t], r.idx[t])) {
+      const float td = r.d[t], tx = r.x[t], ty = r.y[t], tz = r.z[t];
+      const int ti = r.idx[t];
+      r.d[t] = d; r.idx[t] = idx; r.x[t] = px; r.y[t] = py; r.z[t] = pz;
+      d = td; idx = ti; px = tx; py = ty; pz = tz;
+    }
+  }
+}
+
+// All map points with d2 < 1.0 inside the crop box, 5 smallest by (d2, map index).
+__device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
+                          Knn5& r) {
+  r.cnt = 0;
+#pragma unroll
+  for (int t = 0; t < 5; ++t) { r.d[t] = __int_as_float(0x7f800000); r.idx[t] = 0x7fffffff; r.x[t] = r.y[t] = r.z[t] = 0.0f; }
+  const float inv = m.g.inv_cell;
+  const float fx = floorf(qx * inv), fy = floorf(qy * inv), fz = floorf(qz * inv);
+  if (!(fabsf(fx) < 1e9f && fabsf(fy) < 1e9f && fabsf(fz) < 1e9f)) return;
+  const int cx = (int)fx - (int)m.g.origin[0], cy = (int)fy - (int)m.g.origin[1], cz = (int)fz - (int)m.g.origin[2];
+  const int X = m.g.dims[0], Y = m.g.dims[1], Z = m.g.dims[2];
+  if (cx < -1 || cy < -1 || cz < -1 || cx > X || cy > Y || cz > Z) return;
+  const int x0 = max(cx - 1, 0), x1 = min(cx + 1, X - 1);
+  if (x0 > x1) return;
+  for (int z = max(cz - 1, 0); z <= min(cz + 1, Z - 1); ++z)
+    for (int y = max(cy - 1, 0); y <= min(cy + 1, Y - 1); ++y) {
+      const int rowbase = (z * Y + y) * X;
+      const int b = m.cell_start[rowbase + x0], e = m.cell_start[rowbase + x1 + 1];
+      for (int i = b; i < e; ++i) {
+        const float4 p = m.pts[i];
+        if (p.x < bmin[0] || p.y < bmin[1] || p.z < bmin[2]) continue;  // pcl::CropBox, inclusive
+        if (p.x > bmax[0] || p.y > bmax[1] || p.z > bmax[2]) continue;
+        float dist = 0.0f, diff;
+        diff = qx - p.x; dist += diff * diff;                            // flann::L2_Simple
+        diff = qy - p.y; dist += diff * diff;
+        diff = qz - p.z; dist += diff * diff;
+        if (dist < 1.0f) knn_insert(r, dist, __float_as_int(p.w), p.x, p.y, p.z);
+      }
+    }
+}
+
+// cornerOptimization body (:1016-1121): coefficient row for one corner query, false if rejected.
+__device__ bool corner_residual(const Knn5& nn, float x0, float y0, float z0, float4& coeff) {
+  if (nn.cnt < 5 || !(nn.d[4] < 1.0f)) return false;
+  float cx = 0, cy = 0, cz = 0;
+  for (int j = 0; j < 5; j++) { cx += nn.x[j]; cy += nn.y[j]; cz += nn.z[j]; }
+  cx /= 5.0f; cy /= 5.0f; cz /= 5.0f;
+  float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+  for (int j = 0; j < 5; j++) {
+    const float ax = nn.x[j] - cx, ay = nn.y[j] - cy, az = nn.z[j] - cz;
+    a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
+    a22 += ay * ay; a23 += ay * az;
+    a33 += az * az;
+  }
+  a11 /= 5.0f; a12 /= 5.0f; a13 /= 5.0f; a22 /= 5.0f; a23 /= 5.0f; a33 /= 5.0f;
+  float A1[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33};
+  float D1[3], V1[9];
+  jacobi_eigen<3>(A1, D1, V1);
+  if (!(D1[0] > 3.0f * D1[1])) return false;
+  const float x1 = (float)((double)cx + 0.1 * (double)V1[0]), y1 = (float)((double)cy + 0.1 * (double)V1[1]),
+              z1 = (float)((double)cz + 0.1 * (double)V1[2]);
+  const float x2 = (float)((double)cx - 0.1 * (double)V1[0]), y2 = (float)((double)cy - 0.1 * (double)V1[1]),
+              z2 = (float)((double)cz - 0.1 * (double)V1[2]);
+  const float a012 = sqrt_rn(((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) +
+                                ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) +
+                                ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1)) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1)));
+  const float l12 = sqrt_rn((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
+  const float la = ((y1 - y2) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) +
+                    (z1 - z2) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1))) / a012 / l12;
+  const float lb = -((x1 - x2) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) -
+                     (z1 - z2) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1))) / a012 / l12;
+  const float lc = -((x1 - x2) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) +
+                     (y1 - y2) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1))) / a012 / l12;
+  const float ld2 = a012 / l12;
+  const float s = (float)(1.0 - 0.9 * (double)fabsf(ld2));
+  coeff = make_float4(s * la, s * lb, s * lc, s * ld2);
+  return (double)s > 0.1;
+}
+
+// surfOptimization body (:1145-1211).
+__device__ bool surf_residual(const Knn5& nn, float x0, float y0, float z0, float4& coeff) {
+  if (nn.cnt < 5 || !(nn.d[4] < 1.0f)) return false;
+  float A0[5][3], B0[5], X0[3];
+  for (int j = 0; j < 5; j++) { A0[j][0] = nn.x[j]; A0[j][1] = nn.y[j]; A0[j][2] = nn.z[j]; B0[j] = -1.0f; }
+  colpiv_solve53(A0, B0, X0);
+  float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1.0f;
+  const float ps = sqrt_rn(pa * pa + pb * pb + pc * pc);
+  pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+  for (int j = 0; j < 5; j++)
+    if ((double)fabsf(pa * nn.x[j] + pb * nn.y[j] + pc * nn.z[j] + pd) > 0.2) return false;
+  const float pd2 = pa * x0 + pb * y0 + pc * z0 + pd;
+  const float s = (float)(1.0 - 0.9 * (double)fabsf(pd2) /
+                                    (double)sqrt_rn(sqrt_rn(x0 * x0 + y0 * y0 + z0 * z0)));
+  coeff = make_float4(s * pa, s * pb, s * pc, s * pd2);
+  return (double)s > 0.1;
+}
+
+__global__ void k_gn_init(GnArgs a) {
+  __shared__ int32_t scan[1024];
+  const int tid = threadIdx.x;
+  int base = 0;
+  for (int j0 = 0; j0 < a.B; j0 += 1024) {
+    const int job = j0 + tid;
+    int nc_items = 0, ns_items = 0;
+    if (job < a.B) {
+      GnState& g = a.gn[job];
+      for (int k = 0; k < 6; ++k) g.pose[k] = a.guess[job * 6 + k];
+      pose_to_T(g.pose, g.T, g.trig);
+      for (int k = 0; k < 3; ++k) {  // edge = size + origin (float), :289-292
+        g.crop_min[k] = -a.crop_half[k] + g.pose[3 + k];
+        g.crop_max[k] = a.crop_half[k] + g.pose[3 + k];
+      }
+      for (int k = 0; k < 36; ++k) g.matP[k] = 0.0f;
+      const int nc = a.ncds[job], ns = a.nsds[job];
+      g.iter = 0; g.converged = 0; g.degenerate = 0; g.n_sel = 0;
+      if (nc > a.edge_min && ns > a.surf_min) {
+        g.status = FBR_REG_OK;
+        g.active = 1;
+        nc_items = (nc + kResThreads - 1) / kResThreads;
+        ns_items = (ns + kResThreads - 1) / kResThreads;
+      } else {
+        g.status = FBR_REG_NOT_ENOUGH_FEATURES;
+        g.active = 0;
+      }
+    }
+    scan[tid] = nc_items + ns_items;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const int v = tid >= off ? scan[tid - off] : 0;
+      __syncthreads();
+      scan[tid] += v;
+      __syncthreads();
+    }
+    const int incl = scan[tid];
+    const int excl = base + incl - (nc_items + ns_items);
+    if (job < a.B) {
+      a.item_range[2 * job] = excl;
+      a.item_range[2 * job + 1] = excl + nc_items + ns_items;
+      const int nc = a.ncds[job], ns = a.nsds[job];
+      int it = excl;
+      for (int t = 0; t < nc_items; ++t, ++it)
+        if (it < a.max_items) a.items[it] = make_int4(job, 0, t * kResThreads, min(kResThreads, nc - t * kResThreads));
+      for (int t = 0; t < ns_items; ++t, ++it)
+        if (it < a.max_items) a.items[it] = make_int4(job, 1, t * kResThreads, min(kResThreads, ns - t * kResThreads));
+    }
+    base += scan[1023];
+    __syncthreads();
+  }
+  if (tid == 0) a.nitems[0] = min(base, a.max_items);
+}
+
+__global__ void __launch_bounds__(kResThreads)
+k_gn_residual(GnArgs a) {
+  __shared__ double red[kResThreads / 64][28];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nitems = a.nitems[0];
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int4 item = a.items[it];
+    const int job = item.x;
+    const GnState& g = a.gn[job];
+    if (!g.active) continue;  // block-uniform
+    float row[6] = {0, 0, 0, 0, 0, 0}, b = 0.0f;
+    bool ok = false;
+    if (tid < item.w) {
+      const bool corner = item.y == 0;
+      const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
+      const float* T = g.T;
+      // pointAssociateToMap (:397-403)
+      const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
+      const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
+      const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
+      Knn5 nn;
+      knn5_grid(corner ? a.mc : a.ms, x0, y0, z0, g.crop_min, g.crop_max, nn);
+      float4 c;
+      ok = corner ? corner_residual(nn, x0, y0, z0, c) : surf_residual(nn, x0, y0, z0, c);
+      if (ok) {
+        // LMOptimization row (:1286-1332), camera-frame swap
+        const float srx = g.trig[0], crx = g.trig[1], sry = g.trig[2], cry = g.trig[3], srz = g.trig[4],
+                    crz = g.trig[5];
+        const float pox = p.y, poy = p.z, poz = p.x;
+        const float cox = c.y, coy = c.z, coz = c.x;
+        const float arx = (crx * sry * srz * pox + crx * crz * sry * poy - srx * sry * poz) * cox +
+                          (-srx * srz * pox - crz * srx * poy - crx * poz) * coy +
+                          (crx * cry * srz * pox + crx * cry * crz * poy - cry * srx * poz) * coz;
+        const float ary = ((cry * srx * srz - crz * sry) * pox + (sry * srz + cry * crz * srx) * poy + crx * cry * poz) * cox +
+                          ((-cry * crz - srx * sry * srz) * pox + (cry * srz - crz * srx * sry) * poy - crx * sry * poz) * coz;
+        const float arz = ((crz * srx * sry - cry * srz) * pox + (-cry * crz - srx * sry * srz) * poy) * cox +
+                          (crx * crz * pox - crx * srz * poy) * coy +
+                          ((sry * srz + cry * crz * srx) * pox + (crz * sry - cry * srx * srz) * poy) * coz;
+        row[0] = arz; row[1] = arx; row[2] = ary; row[3] = coz; row[4] = cox; row[5] = coy;
+        b = -c.w;
+      }
+    }
+    // fp64 products: 21 upper AtA entries, 6 AtB, count
+    double v[28];
+    int q = 0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int c2 = r; c2 < 6; ++c2) v[q++] = (double)row[r] * (double)row[c2];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) v[q++] = (double)row[r] * (double)b;
+    v[27] = ok ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < 28; ++k) {
+      double x = v[k];
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+      v[k] = x;
+    }
+    if (lane == 0)
+      for (int k = 0; k < 28; ++k) red[wave][k] = v[k];
+    __syncthreads();
+    if (tid < 28) {
+      double s = 0.0;
+      for (int w = 0; w < kResThreads / 64; ++w) s += red[w][tid];
+      a.partial[(int64_t)it * kPartial + tid] = s;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_gn_solve(GnArgs a) {
+  const int job = blockIdx.x * blockDim.x + threadIdx.x;
+  if (job >= a.B) return;
+  GnState& g = a.gn[job];
+  if (!g.active) return;
+  double acc[28];
+  for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+  const int i0 = a.item_range[2 * job], i1 = a.item_range[2 * job + 1];
+  for (int it = i0; it < i1; ++it)
+    for (int k = 0; k < 28; ++k) acc[k] += a.partial[(int64_t)it * kPartial + k];
+  const int iterCount = g.iter;
+  g.iter = iterCount + 1;
+  const int sel = (int)acc[27];
+  g.n_sel = sel;
+  if (a.trace) {
+    // filled below after the update; pre-fill with the current pose for the early-return case
+    for (int k = 0; k < 6; ++k) a.trace[((int64_t)job * a.max_iter + iterCount) * 6 + k] = g.pose[k];
+  }
+  if (sel < 50) {  // :1268 return false
+    if (g.iter >= a.max_iter) g.active = 0;
+    return;
+  }
+  float AtA[36], X[6], tmp[36];
+  {
+    int q = 0;
+    for (int r = 0; r < 6; ++r)
+      for (int c = r; c < 6; ++c) {
+        AtA[r * 6 + c] = (float)acc[q];
+        AtA[c * 6 + r] = (float)acc[q];
+        ++q;
+      }
+    for (int r = 0; r < 6; ++r) X[r] = (float)acc[21 + r];
+  }
+  for (int k = 0; k < 36; ++k) tmp[k] = AtA[k];
+  if (!qr_solve6(tmp, X))
+    for (int k = 0; k < 6; ++k) X[k] = 0.0f;
+  float matP[36];
+  for (int k = 0; k < 36; ++k) matP[k] = 0.0f;  // local cv::Mat matP (:1278)
+  if (iterCount == 0) {
+    float E[6], V[36], V2[36], Vi[36];
+    for (int k = 0; k < 36; ++k) tmp[k] = AtA[k];
+    jacobi_eigen<6>(tmp, E, V);
+    for (int k = 0; k < 36; ++k) V2[k] = V[k];
+    int deg = 0;
+    for (int i = 5; i >= 0; i--) {
+      if (E[i] < 100.0f) {
+        for (int j = 0; j < 6; j++) V2[i * 6 + j] = 0.0f;
+        deg = 1;
+      } else {
+        break;
+      }
+    }
+    g.degenerate = deg;
+    if (!lu_inv6(V, Vi))
+      for (int k = 0; k < 36; ++k) Vi[k] = 0.0f;
+    gemm_f32_acc64(Vi, V2, matP, 6, 6, 6);
+  }
+  if (g.degenerate) {
+    float X2[6];
+    for (int k = 0; k < 6; ++k) X2[k] = X[k];
+    gemm_f32_acc64(matP, X2, X, 6, 6, 1);
+  }
+  for (int k = 0; k < 6; ++k) g.pose[k] += X[k];
+  if (a.trace)
+    for (int k = 0; k < 6; ++k) a.trace[((int64_t)job * a.max_iter + iterCount) * 6 + k] = g.pose[k];
+  const double r0 = (double)(X[0] * 57.29578f), r1 = (double)(X[1] * 57.29578f), r2 = (double)(X[2] * 57.29578f);
+  const float deltaR = (float)sqrt(r0 * r0 + r1 * r1 + r2 * r2);
+  const double t0 = (double)(X[3] * 100.0f), t1 = (double)(X[4] * 100.0f), t2 = (double)(X[5] * 100.0f);
+  const float deltaT = (float)sqrt(t0 * t0 + t1 * t1 + t2 * t2);
+  if ((double)deltaR < 0.05 && (double)deltaT < 0.05) {
+    g.converged = 1;
+    g.active = 0;
+  } else if (g.iter >= a.max_iter) {
+    g.active = 0;
+  }
+  pose_to_T(g.pose, g.T, g.trig);
+}
+
+__global__ void k_gn_finalize(GnArgs a) {
+  const int job = blockIdx.x * blockDim.x + threadIdx.x;
+  if (job >= a.B) return;
+  GnState& g = a.gn[job];
+  float p[6];
+  for (int k = 0; k < 6; ++k) p[k] = g.pose[k];
+  if (g.status == FBR_REG_OK) {  // transformUpdate clamps (:1476-1478)
+    auto clampf = [](float v, float lim) {
+      if (v < -lim) v = -lim;
+      if (v > lim) v = lim;
+      return v;
+    };
+    p[0] = clampf(p[0], a.rot_tol);
+    p[1] = clampf(p[1], a.rot_tol);
+    p[5] = clampf(p[5], a.z_tol);
+  }
+  for (int k = 0; k < 6; ++k) a.pose_out[job * 6 + k] = p[k];
+  fbr_reg_stats& s = a.stats[job];
+  s.status = g.status;
+  s.iterations = g.iter;
+  s.converged = g.converged;
+  s.degenerate = g.degenerate;
+  s.n_sel = g.n_sel;
+  s.n_corner_ds = a.ncds[job];
+  s.n_surf_ds = a.nsds[job];
+}
+
+// CropBox counts of the global map for every job's box (statistics only).
+__global__ void k_crop_count(GnArgs a, const float4* pts, int64_t n, int which, int32_t* counts) {
+  extern __shared__ int32_t c[];
+  for (int j = threadIdx.x; j < a.B; j += blockDim.x) c[j] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 p = pts[i];
+    for (int j = 0; j < a.B; ++j) {
+      const GnState& g = a.gn[j];
+      if (p.x < g.crop_min[0] || p.y < g.crop_min[1] || p.z < g.crop_min[2]) continue;
+      if (p.x > g.crop_max[0] || p.y > g.crop_max[1] || p.z > g.crop_max[2]) continue;
+      atomicAdd(&c[j], 1);
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < a.B; j += blockDim.x)
+    if (c[j]) atomicAdd(&counts[2 * j + which], c[j]);
+}
+
+void launch_gn_init(hipStream_t s, const GnArgs& a) { hipLaunchKernelGGL(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
+void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
+  hipLaunchKernelGGL(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);
+}
+void launch_gn_solve(hipStream_t s, const GnArgs& a) {
+  hipLaunchKernelGGL(k_gn_solve, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
+}
+void launch_gn_finalize(hipStream_t s, const GnArgs& a) {
+  hipLaunchKernelGGL(k_gn_finalize, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
+}
+void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* pts, int64_t n, int which, int32_t* counts) {
+  if (n <= 0) return;
+  int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_crop_count, dim3(grid), dim3(256), sizeof(int32_t) * a.B, s, a, pts, n, which, counts);
+}
+
+}  // namespace fbr

@@ -178,6 +178,11 @@ void* fbr_stream(fbr_ctx* ctx);
 int fbr_voxel_grid(fbr_ctx* ctx, const fbr_point_xyzi* in, int64_t n, float leaf,
                    fbr_point_xyzi* out, int64_t* n_out);
 
+/* Diagnostic: device numerics probe.  For i < n writes out[4i..4i+3] = {sqrtf(|a|), a/b,
+ * atan2f(a,b), a*b+b*a-a} computed by the device kernels' primitives (tests compare the bits with
+ * the host libm the reference uses). */
+int fbr_selftest_math(int n, const float* a, const float* b, float* out);
+
 /* pcl::getTransformation / pcl::getTranslationAndEulerAngles (row-major 4x4 float). */
 void fbr_affine_from_pose(const float pose[6], float m[16]);
 void fbr_pose_from_affine(const float m[16], float pose[6]);
