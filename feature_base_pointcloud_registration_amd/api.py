@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = [
     "fbr_destroy", "fbr_set_map", "fbr_get_map", "fbr_project", "fbr_extract_features",
     "fbr_register", "fbr_register_trace", "fbr_process_scan", "fbr_reset_stream",
     "fbr_process_batch", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
-    "fbr_batch_results", "fbr_batch_bytes", "fbr_set_profiling", "fbr_kernel_time", "fbr_stream",
+    "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_kernel_time", "fbr_stream",
     "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math",
 ]
 
@@ -73,6 +73,7 @@ def lib():
             "fbr_batch_launch": (ctypes.c_int, [_VP]),
             "fbr_batch_wait": (ctypes.c_int, [_VP]),
             "fbr_batch_results": (ctypes.c_int, [_VP, _VP, _VP]),
+            "fbr_batch_export": (ctypes.c_int, [_VP, _VP]),
             "fbr_batch_bytes": (ctypes.c_int, [_VP, _VP, _VP]),
             "fbr_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
             "fbr_kernel_time": (ctypes.c_int, [_VP, ctypes.c_char_p, _VP, _VP]),
@@ -266,6 +267,10 @@ class Context:
         stats = np.zeros(self._staged, REG_STATS)
         _check(lib().fbr_batch_results(self._h, ptr(poses), ptr(stats)), "fbr_batch_results")
         return poses, stats
+
+    def batch_export(self, device_ptr):
+        """Enqueue the 32 B/job pose records into device memory at `device_ptr` (int address)."""
+        _check(lib().fbr_batch_export(self._h, ctypes.c_void_p(device_ptr)), "fbr_batch_export")
 
     def batch_bytes(self):
         t, g = ctypes.c_double(), ctypes.c_double()

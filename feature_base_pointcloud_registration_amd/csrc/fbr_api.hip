@@ -769,6 +769,15 @@ int fbr_batch_results(fbr_ctx* c, float* poses_out, fbr_reg_stats* stats) {
   return copy_stats(c, B, stats);
 }
 
+int fbr_batch_export(fbr_ctx* c, void* device_dst) {
+  if (!c || !device_dst) return FBR_ERR_INVALID_ARG;
+  if (c->staged_B <= 0) return FBR_ERR_STATE;
+  CK(hipSetDevice(c->dev));
+  launch_export_records(c->stream, c->staged_B, c->d_pose_out, c->d_stats, (float*)device_dst);
+  CK(hipGetLastError());
+  return FBR_OK;
+}
+
 int fbr_batch_bytes(fbr_ctx* c, double* bytes_total, double* bytes_gn) {
   if (!c) return FBR_ERR_INVALID_ARG;
   if (c->last_iters.empty()) return FBR_ERR_STATE;

@@ -92,6 +92,7 @@ void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid);
 void launch_gn_solve(hipStream_t s, const GnArgs& a);
 void launch_gn_finalize(hipStream_t s, const GnArgs& a);
 // laserCloud{Corner,Surf}FromMapDSNum: CropBox counts of the global map per job.
+void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, float* dst);
 void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* map_pts, int64_t n, int which,
                        int32_t* counts /* [B][2] */);
 

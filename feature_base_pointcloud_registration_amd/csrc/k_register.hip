@@ -409,6 +409,19 @@ __global__ void k_crop_count(GnArgs a, const float4* pts, int64_t n, int which, 
     if (c[j]) atomicAdd(&counts[2 * j + which], c[j]);
 }
 
+// 32-byte pose record per job {pose[6], iterations, status} for the cross-GPU gather.
+__global__ void k_export_records(int B, const float* pose_out, const fbr_reg_stats* stats, float* dst) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= B) return;
+  for (int k = 0; k < 6; ++k) dst[8 * j + k] = pose_out[6 * j + k];
+  dst[8 * j + 6] = __int_as_float(stats[j].iterations);
+  dst[8 * j + 7] = __int_as_float(stats[j].status);
+}
+
+void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, float* dst) {
+  hipLaunchKernelGGL(k_export_records, dim3((B + 63) / 64), dim3(64), 0, s, B, pose_out, stats, dst);
+}
+
 void launch_gn_init(hipStream_t s, const GnArgs& a) { hipLaunchKernelGGL(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
   hipLaunchKernelGGL(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);

@@ -165,6 +165,10 @@ int fbr_batch_launch(fbr_ctx* ctx);
 int fbr_batch_wait(fbr_ctx* ctx);
 int fbr_batch_results(fbr_ctx* ctx, float* poses_out /* [n_jobs][6] */,
                       fbr_reg_stats* stats /* [n_jobs] or NULL */);
+/* Enqueue (on the ctx stream, after the launched batch) a copy of the per-job pose records
+ * {pose[6] f32, iterations i32, status i32} = 32 B/job into `device_dst` (device memory of the
+ * ctx's device, [n_jobs][8] x 4 B) — the payload of the cross-GPU pose all-gather. */
+int fbr_batch_export(fbr_ctx* ctx, void* device_dst);
 /* Sum of the per-scan algorithmic byte counts of the last completed batch (roofline input). */
 int fbr_batch_bytes(fbr_ctx* ctx, double* bytes_total, double* bytes_gn);
 
