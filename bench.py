@@ -69,7 +69,7 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group(backend="nccl", init_method="env://")
 
-    from feature_base_pointcloud_registration_amd import api, synth
+    from feature_base_pointcloud_registration_amd import api, shard, synth
     from feature_base_pointcloud_registration_amd.fbr_types import default_params
 
     cfg = args.config
@@ -86,18 +86,17 @@ def main():
     ctx.set_map(corner_map, surf_map)
     ctx.batch_stage(scans, guesses)
 
-    gather_buf = gather_all = None
+    gather_buf = None
     if dist is not None:
         import torch
         gather_buf = torch.zeros(B * 8, dtype=torch.float32, device=f"cuda:{local_rank}")
-        gather_all = torch.zeros(world * B * 8, dtype=torch.float32, device=f"cuda:{local_rank}")
 
     def step():
         ctx.batch_launch()
         if dist is not None:
             ctx.batch_export(gather_buf.data_ptr())
             ctx.batch_wait()
-            dist.all_gather_into_tensor(gather_all, gather_buf)
+            shard.gather_records(dist, gather_buf, world)
 
     for _ in range(args.warmup):
         step()
