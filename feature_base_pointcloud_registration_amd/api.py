@@ -41,7 +41,8 @@ class FbrError(RuntimeError):
 
 
 def lib_path():
-    return os.path.join(_HERE, "libfbr_hip.so")
+    # FBR_LIB selects a diagnostic build (tools/); the default is the shipped library
+    return os.environ.get("FBR_LIB") or os.path.join(_HERE, "libfbr_hip.so")
 
 
 def lib():

@@ -41,16 +41,18 @@ def _headers():
     return hs
 
 
-def build_hip(verbose=False, force=False):
-    os.makedirs(OBJ, exist_ok=True)
-    out = os.path.join(HERE, "libfbr_hip.so")
+def build_hip(verbose=False, force=False, defines=(), name="libfbr_hip.so"):
+    obj_dir = OBJ if not defines else OBJ + "_diag"
+    os.makedirs(obj_dir, exist_ok=True)
+    out = os.path.join(HERE, name)
     hdrs = _headers()
     flags = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
-             "-I", CSRC, "-I", os.path.join(REPO, "include"), "-Wno-unused-result"]
+             "-I", CSRC, "-I", os.path.join(REPO, "include"), "-Wno-unused-result",
+             *[f"-D{d}" for d in defines]]
     objs, jobs = [], []
     for src in HIP_SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(OBJ, src.replace(".hip", ".o"))
+        o = os.path.join(obj_dir, src.replace(".hip", ".o"))
         objs.append(o)
         if force or _newer(o, [s] + hdrs):
             jobs.append([hipcc(), *flags, "-c", s, "-o", o])

@@ -105,6 +105,7 @@ struct fbr_ctx {
   bool profiling = false;
   std::map<std::string, KernelTimer> timers;
   std::vector<int32_t> last_iters, last_q, last_n, last_m;
+  unsigned long long* d_feat_stamps = nullptr;  // diagnostic builds (FBR_FEAT_STAMPS) only
 };
 
 namespace {
@@ -300,6 +301,12 @@ int stage_features(fbr_ctx* c, int B, bool stream_mode) {
   a.err = c->d_err;
   a.lcap = c->W + 16;
   a.segcap = (int)seg_cap(c->W);
+  a.kseg = 1;
+  while (a.kseg < a.segcap - 1) a.kseg <<= 1;
+  a.nwcap = (a.lcap + 63) / 64 + 1;
+  a.region_a = (int)std::max<int64_t>((int64_t)6 * a.lcap, (int64_t)8 * a.kseg + (int64_t)16 * a.segcap + 16 + 8 * 12);
+  a.region_a = (a.region_a + 15) & ~15;
+  a.stamps = c->d_feat_stamps;
   CK(hipMemsetAsync(c->d_err, 0, sizeof(int32_t) * B, c->stream));
   TIMED(c, "features", launch_features(c->stream, a));
   VgArgs v{};
@@ -816,6 +823,20 @@ int fbr_voxel_grid(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf, 
   if (rc) return rc;
   if (out) std::memcpy(out, o.data(), sizeof(fbr_point_xyzi) * o.size());
   if (n_out) *n_out = (int64_t)o.size();
+  return FBR_OK;
+}
+
+// Diagnostic: per-ring phase cycle sums of k_features (only filled by a -DFBR_FEAT_STAMPS build).
+extern "C" int fbr_diag_feature_stamps(fbr_ctx* c, unsigned long long* out /* [max_batch*n_scan][12] */) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  const size_t n = (size_t)c->Bcap * c->H * 12;
+  if (!c->d_feat_stamps) {
+    CK(hipMalloc(&c->d_feat_stamps, sizeof(unsigned long long) * n));
+    CK(hipMemset(c->d_feat_stamps, 0, sizeof(unsigned long long) * n));
+    return FBR_OK;
+  }
+  if (out) CK(hipMemcpy(out, c->d_feat_stamps, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
   return FBR_OK;
 }
 

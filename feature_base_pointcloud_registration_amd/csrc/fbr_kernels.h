@@ -32,7 +32,12 @@ struct FeatArgs {
   int32_t* cand_cnt;     // [B][H]
   int32_t* err;          // [B]
   int lcap, segcap;      // LDS capacities (window length, segment length)
+  int kseg;              // segment sort capacity: next power of two >= segcap - 1 (<= 1024)
+  int nwcap;             // 64-bit words per window bit array
+  int region_a;          // bytes of the phase-aliased LDS region
+  unsigned long long* stamps;  // diagnostic builds only: [B*H][12] phase cycle sums
 };
+size_t features_lds_bytes(const FeatArgs& a);
 void launch_features(hipStream_t s, const FeatArgs& a);
 
 // ---- A9 VoxelGrid over segments (k_voxel.hip) ----

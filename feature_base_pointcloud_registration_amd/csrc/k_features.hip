@@ -9,14 +9,25 @@
 // flattened arrays in LDS.  The only cross-ring object is the stale
 // cloudSmoothness[4] slot (never recomputed, :113) and cloudNeighborPicked[0..4]; they live in
 // StreamState and are carried only in stream mode.
-//   - curvature: the reference's left-to-right f32 sum, no FMA;
-//   - occlusion: the sequential loop only ever writes 1s, so each cell's final value is the OR of
-//     the marks that cover it — computed in parallel;
-//   - sort: parallel stable rank sort (equal to std::sort when no two curvatures tie and none is
-//     NaN); segments with ties fall back to the exact libstdc++ introsort emulation (fbr_sort.h);
-//   - picks: the greedy corner/surf walks are inherently ordered; lane 0 walks the sorted segment
-//     with early exit once the sorted curvature crosses the threshold (exact: the remaining
-//     entries fail the same test).
+//
+// Every per-index flag (occlusion marks, column gaps > 10, cloudNeighborPicked, cloudLabel,
+// curvature above/below the thresholds) is a bit in 64-bit words over the window, produced by wave
+// ballots; marks and suppression become shifted ORs.
+//   * curvature: the reference's left-to-right f32 sum, no FMA.
+//   * occlusion: the sequential loop only ever writes 1s, so cloudNeighborPicked is the OR of the
+//     marks covering each index: picked = C | OR_{d=0..5} A>>d | OR_{d=1..6} B<<d.
+//   * sort: per segment, an LDS bitonic sort of (curvature bits, position) keys — std::sort's order
+//     whenever the segment has no tied (or NaN) curvature; a segment with ties runs the exact
+//     libstdc++ introsort emulation (fbr_sort.h) on one lane instead.
+//   * picks: the corner walk (descending, ep first, 20 per segment) and the surf walk (ascending,
+//     ep last) are greedy: a candidate is taken iff no earlier-visited taken candidate suppresses
+//     it.  Suppression reach (+-5 indices, stopped by a column gap > 10) depends only on
+//     pointColInd and is symmetric, so the walk is a greedy independent set in visit-priority
+//     order.  The wave resolves it in rounds on wave-uniform bitmasks: a candidate becomes "taken"
+//     once every higher-priority conflicting candidate is "not taken", and "not taken" once one of
+//     them is taken — final decisions, identical to the sequential walk.  The corner cap keeps the
+//     first 20 taken in visit order.  The segment holding the stale slot keeps the sequential walk
+//     (its stale index may duplicate a member).
 // Outputs: label (the feature mask), per-ring corner slots in visit order, per-ring surf
 // candidates (label <= 0, index order) for the per-ring VoxelGrid (k_voxel.hip).
 #include "fbr_common.h"
@@ -26,48 +37,168 @@
 namespace fbr {
 
 namespace {
-constexpr uint8_t kPicked = 1;
-constexpr uint8_t kLabPos = 2;   // label == 1
-constexpr uint8_t kLabNeg = 4;   // label == -1
-constexpr uint8_t kOccA = 8;     // depth1 - depth2 > 0.3 at j (marks j-5..j)
-constexpr uint8_t kOccB = 16;    // depth2 - depth1 > 0.3 at j (marks j+1..j+6)
-constexpr uint8_t kOccC = 32;    // parallel beam at j
-constexpr int kColM2 = 1 << 30;  // pointColInd[-2]: glibc chunk-size word (large)
+constexpr uint64_t kPadKey = ~0ull;
 }  // namespace
 
-struct FeatLds {
-  int wlo, L;
-  float* r;        // ranges, later reused by nothing
-  int16_t* col;    // column index
-  float* curv;
-  uint8_t* fl;     // picked / label / occlusion bits
-  SmoothEntry* seg;
-  SmoothEntry* srt;
+// Window bit-words (index i of the window <-> bit i&63 of word i>>6).
+struct Bits {
+  uint64_t* w;
+  __device__ __forceinline__ bool get(int i) const { return (w[i >> 6] >> (i & 63)) & 1ull; }
+  __device__ __forceinline__ void set_serial(int i) const { w[i >> 6] |= 1ull << (i & 63); }
 };
 
-__device__ __forceinline__ int col_at(const FeatLds& S, int k) {
-  if (k == -1) return 0;
-  if (k == -2) return kColM2;
-  return S.col[k - S.wlo];
+struct FeatLds {
+  int wlo, L, nw;
+  float* curv;        // [Lcap]
+  Bits gap;           // |col[i+1]-col[i]| > 10
+  Bits picked, labpos, labneg, edgec, surfc;
+  Bits occa, occb, occc;
+  // region A, phase 1
+  float* r;           // [Lcap]
+  int16_t* col;       // [Lcap]
+  // region A, phase 2 (per segment)
+  uint64_t* keys;     // [kseg]
+  uint16_t* sorder;   // [segcap] member index at each sorted position
+  uint16_t* rankc;    // [segcap] corner visit rank of each member
+  uint32_t* cm;       // [segcap] conflict masks
+  SmoothEntry* seg;   // [segcap] serial-path entries
+  uint64_t* tmask;    // [WMAX] taken mask copy for the cap scan
+};
+
+// Forward / backward suppression reach of window index li (<= 5 each).
+__device__ __forceinline__ int reach_fwd(const FeatLds& S, int li) {
+  int f = 0;
+  while (f < 5 && !S.gap.get(li + f)) ++f;
+  return f;
+}
+__device__ __forceinline__ int reach_bwd(const FeatLds& S, int li) {
+  int b = 0;
+  while (b < 5 && li - 1 - b >= 0 && !S.gap.get(li - 1 - b)) ++b;
+  return b;
 }
 
-// Neighbour suppression after a pick (featureExtraction.h:227-240 / 259-274).
-__device__ __forceinline__ void suppress(const FeatLds& S, int ind) {
-  for (int l = 1; l <= 5; l++) {
-    int cd = abs(col_at(S, ind + l) - col_at(S, ind + l - 1));
-    if (cd > 10) break;
-    S.fl[ind + l - S.wlo] |= kPicked;
-  }
-  for (int l = -1; l >= -5; l--) {
-    int cd = abs(col_at(S, ind + l) - col_at(S, ind + l + 1));
-    if (cd > 10) break;
-    int k = ind + l;
-    if (k >= 0) S.fl[k - S.wlo] |= kPicked;  // k == -1: write lands outside the array (scratch)
+// Mark cloudNeighborPicked over [li-bwd, li+fwd] (the suppression loops :227-240 / :259-274).
+__device__ __forceinline__ void or_range(const Bits& b, int lo, int hi) {
+  const int w0 = lo >> 6, w1 = hi >> 6;
+  const uint64_t m0 = ~0ull << (lo & 63);
+  const uint64_t m1 = (hi & 63) == 63 ? ~0ull : ((1ull << ((hi & 63) + 1)) - 1ull);
+  if (w0 == w1) {
+    atomicOr((unsigned long long*)&b.w[w0], (unsigned long long)(m0 & m1));
+  } else {
+    atomicOr((unsigned long long*)&b.w[w0], (unsigned long long)m0);
+    atomicOr((unsigned long long*)&b.w[w1], (unsigned long long)m1);
   }
 }
 
+// Sequential walks (the reference loops verbatim) over S.seg[0..m] (seg[m] = the unsorted ep entry).
+__device__ void serial_walks(const FeatLds& S, const FeatArgs& a, int job, int m, const float4* CL,
+                             float4* corner_out, int& corner_cnt) {
+  int largestPickedNum = 0;
+  for (int k = m; k >= 0; k--) {  // corners, k = ep .. sp (:208-242)
+    const int ind = S.seg[k].ind;
+    const int li = ind - S.wlo;
+    if (li < 0 || li + 5 >= S.L) { atomicOr(&a.err[job], 4); return; }
+    if (!S.picked.get(li) && S.curv[li] > a.edge_thr) {
+      largestPickedNum++;
+      if (largestPickedNum <= kCornerPerSeg) {
+        S.labpos.set_serial(li);
+        corner_out[corner_cnt++] = CL[ind];
+      } else {
+        break;
+      }
+      S.picked.set_serial(li);
+      const int f = reach_fwd(S, li), b = reach_bwd(S, li);  // index -1 (col[-1]) is scratch
+      for (int l = 1; l <= f; ++l) S.picked.set_serial(li + l);
+      for (int l = 1; l <= b; ++l) S.picked.set_serial(li - l);
+    }
+  }
+  for (int k = 0; k <= m; k++) {  // surf, k = sp .. ep (:245-276)
+    const int ind = S.seg[k].ind;
+    const int li = ind - S.wlo;
+    if (li < 0 || li + 5 >= S.L) { atomicOr(&a.err[job], 4); return; }
+    if (!S.picked.get(li) && S.curv[li] < a.surf_thr) {
+      S.labneg.set_serial(li);
+      S.picked.set_serial(li);
+      const int f = reach_fwd(S, li), b = reach_bwd(S, li);
+      for (int l = 1; l <= f; ++l) S.picked.set_serial(li + l);
+      for (int l = 1; l <= b; ++l) S.picked.set_serial(li - l);
+    }
+  }
+}
+
+// 10 neighbour bits of member (64*w + lane) from the wave-uniform masks of words w-1, w, w+1:
+// bit 5+d for d in [-5,-1], bit 4+d for d in [1,5] (the cm encoding).
+__device__ __forceinline__ uint32_t win10(uint64_t a, uint64_t b, uint64_t c, int lane) {
+  const int start = 59 + lane;  // bit (64 + lane - 5) of the 192-bit concatenation a | b<<64 | c<<128
+  uint64_t x;
+  if (start < 64) {
+    x = (a >> start) | (b << (64 - start));
+  } else {
+    const int s2 = start - 64;
+    x = (b >> s2) | (s2 ? (c << (64 - s2)) : 0ull);
+  }
+  const uint32_t w11 = (uint32_t)(x & 0x7FFull);
+  return (w11 & 0x1Fu) | ((w11 >> 6) << 5);
+}
+
+// Greedy rounds.  cmbits(u) = 10-bit mask of the higher-priority conflicting members of u.
+// und: candidate members on entry; on exit tak = the members the sequential walk takes.
+template <int WMAX, typename CmF>
+__device__ void greedy_rounds(int m, int lane, uint64_t (&und)[WMAX], uint64_t (&tak)[WMAX], CmF cmbits,
+                              const FeatArgs& a, int job) {
+  const int nwm = (m >> 6) + 1;
+  uint32_t cmr[WMAX];
+#pragma unroll
+  for (int w = 0; w < WMAX; ++w) cmr[w] = (w < nwm && 64 * w + lane <= m) ? cmbits(64 * w + lane) : 0u;
+  for (int round = 0;; ++round) {
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < WMAX; ++w) {
+      if (w < nwm) {
+        bool nt = false, tk = false;
+        if ((und[w] >> lane) & 1ull) {
+          const uint32_t wt = win10(w > 0 ? tak[w - 1] : 0ull, tak[w], w + 1 < WMAX ? tak[w + 1] : 0ull, lane);
+          const uint32_t wu = win10(w > 0 ? und[w - 1] : 0ull, und[w], w + 1 < WMAX ? und[w + 1] : 0ull, lane);
+          if (wt & cmr[w]) nt = true;
+          else if (!(wu & cmr[w])) tk = true;
+        }
+        const uint64_t bt = __ballot(tk), bn = __ballot(nt);
+        tak[w] |= bt;
+        und[w] &= ~(bt | bn);
+        any |= und[w] != 0ull;
+      }
+    }
+    if (!any) break;
+    if (round > 4 * (m + 2)) {  // unreachable: each round decides the best-ranked undecided
+      if (lane == 0) atomicOr(&a.err[job], 8);
+      break;
+    }
+  }
+}
+
+// Diagnostic build only (-DFBR_FEAT_STAMPS, tools/feat_stamps.py): per-phase s_memtime cycle sums
+// per ring into FeatArgs::stamps.  The shipped library is compiled without it.
+#ifdef FBR_FEAT_STAMPS
+#define FBR_STAMP(i)                                               \
+  do {                                                             \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+    stamp_acc[i] += t_ - stamp_last;                               \
+    stamp_last = t_;                                               \
+  } while (0)
+#else
+#define FBR_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
+// WMAX: 64-bit words of segment-member masks (members <= 64*WMAX); QP: bitonic pairs per lane
+// (segment sort <= 128*QP keys).  <6,4> covers Horizon_SCAN <= 2048, <12,8> up to 4096.
+template <int WMAX, int QP>
 __global__ void __launch_bounds__(64)
 k_features(FeatArgs a) {
+#ifdef FBR_FEAT_STAMPS
+  unsigned long long stamp_acc[12] = {0}, stamp_last = __builtin_amdgcn_s_memtime();
+#endif
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int H = a.H, W = a.W;
   const int job = blockIdx.x / H, ring = blockIdx.x % H, lane = threadIdx.x;
@@ -87,67 +218,117 @@ k_features(FeatArgs a) {
   S.wlo = max(s - 12, 0);
   const int whi = min(e + 11, n);
   S.L = whi - S.wlo;
-  const int Lcap = a.lcap;
-  unsigned char* p = smem;
-  S.r = (float*)p;                 p += sizeof(float) * Lcap;
-  S.curv = (float*)p;              p += sizeof(float) * Lcap;
-  S.seg = (SmoothEntry*)p;         p += sizeof(SmoothEntry) * a.segcap;
-  S.srt = (SmoothEntry*)p;         p += sizeof(SmoothEntry) * a.segcap;
-  S.col = (int16_t*)p;             p += sizeof(int16_t) * Lcap;
-  S.fl = (uint8_t*)p;
+  S.nw = (S.L + 63) >> 6;
+  const int Lcap = a.lcap, segcap = a.segcap, nwcap = a.nwcap, kseg = a.kseg;
   if (S.L > Lcap) {
     if (lane == 0) atomicOr(&a.err[job], 1);
     return;
   }
+  unsigned char* p = smem;
+  unsigned char* regionA = p;        p += a.region_a;
+  S.curv = (float*)p;                p += sizeof(float) * Lcap;
+  uint64_t* words = (uint64_t*)p;    // 9 bit arrays of nwcap words
+  S.gap.w = words;
+  S.picked.w = words + 1 * nwcap;
+  S.labpos.w = words + 2 * nwcap;
+  S.labneg.w = words + 3 * nwcap;
+  S.edgec.w = words + 4 * nwcap;
+  S.surfc.w = words + 5 * nwcap;
+  S.occa.w = words + 6 * nwcap;
+  S.occb.w = words + 7 * nwcap;
+  S.occc.w = words + 8 * nwcap;
+  S.r = (float*)regionA;
+  S.col = (int16_t*)(regionA + sizeof(float) * Lcap);
+  S.keys = (uint64_t*)regionA;
+  S.seg = (SmoothEntry*)(regionA + sizeof(uint64_t) * kseg);
+  S.cm = (uint32_t*)((unsigned char*)S.seg + sizeof(SmoothEntry) * segcap);
+  S.sorder = (uint16_t*)((unsigned char*)S.cm + sizeof(uint32_t) * segcap);
+  S.rankc = S.sorder + segcap;
+  S.tmask = (uint64_t*)(((uintptr_t)(S.rankc + segcap) + 15) & ~(uintptr_t)15);
+
   const float* R = a.range + job * HW;
   const int32_t* C = a.col + job * HW;
   const float4* CL = a.cloud + job * HW;
   StreamState* st = a.stream + job;
-  for (int i = lane; i < S.L; i += 64) {
-    S.r[i] = R[S.wlo + i];
-    S.col[i] = (int16_t)C[S.wlo + i];
-    S.fl[i] = 0;
-    S.curv[i] = 0.0f;
+  // ---- phase 1: stage the window ----
+  for (int i0 = 0; i0 < S.L; i0 += 256) {
+    float rv[4];
+    int cv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = i0 + 64 * q + lane;
+      rv[q] = i < S.L ? R[S.wlo + i] : 0.0f;
+      cv[q] = i < S.L ? C[S.wlo + i] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = i0 + 64 * q + lane;
+      if (i < S.L) {
+        S.r[i] = rv[q];
+        S.col[i] = (int16_t)cv[q];
+      }
+    }
   }
+  for (int w = lane; w < 9 * nwcap; w += 64) words[w] = 0ull;
   __syncthreads();
-  // ---- markOccludedPoints conditions per j in [5, n-6) (featureExtraction.h:140-175) ----
-  for (int i = lane; i < S.L; i += 64) {
+  FBR_STAMP(0);
+  // ---- phase 2: occlusion marks, column gaps, curvature, threshold bits (chunk c = 64 indices) ----
+  for (int c = 0; c < S.nw; ++c) {
+    const int i = 64 * c + lane;
     const int j = S.wlo + i;
-    if (j < 5 || j >= n - 6 || i == 0 || i + 1 >= S.L) continue;
-    uint8_t f = 0;
-    const float depth1 = S.r[i], depth2 = S.r[i + 1];
-    const int columnDiff = abs((int)S.col[i + 1] - (int)S.col[i]);
-    if (columnDiff < 10) {
-      if ((double)(depth1 - depth2) > 0.3) f |= kOccA;
-      else if ((double)(depth2 - depth1) > 0.3) f |= kOccB;
+    bool fa = false, fb = false, fc = false, gp = true;
+    float curv = 0.0f;
+    if (i < S.L) {
+      if (i + 1 < S.L) gp = abs((int)S.col[i + 1] - (int)S.col[i]) > 10;
+      if (j >= 5 && j < n - 6 && i >= 1 && i + 1 < S.L) {  // markOccludedPoints (:140-175)
+        const float depth1 = S.r[i], depth2 = S.r[i + 1];
+        const int columnDiff = abs((int)S.col[i + 1] - (int)S.col[i]);
+        if (columnDiff < 10) {
+          if ((double)(depth1 - depth2) > 0.3) fa = true;
+          else if ((double)(depth2 - depth1) > 0.3) fb = true;
+        }
+        const float diff1 = fabsf(S.r[i - 1] - S.r[i]);
+        const float diff2 = fabsf(S.r[i + 1] - S.r[i]);
+        fc = (double)diff1 > 0.02 * (double)S.r[i] && (double)diff2 > 0.02 * (double)S.r[i];
+      }
+      if (j >= 5 && j < n - 5 && i >= 5 && i + 5 < S.L) {  // calculateSmoothness (:113-122)
+        const float d = S.r[i - 5] + S.r[i - 4] + S.r[i - 3] + S.r[i - 2] + S.r[i - 1] - S.r[i] * 10.0f +
+                        S.r[i + 1] + S.r[i + 2] + S.r[i + 3] + S.r[i + 4] + S.r[i + 5];
+        curv = d * d;
+      }
+      S.curv[i] = curv;  // indices outside [5, n-5) keep the zero-initialised scratch value
     }
-    const float diff1 = fabsf(S.r[i - 1] - S.r[i]);
-    const float diff2 = fabsf(S.r[i + 1] - S.r[i]);
-    if ((double)diff1 > 0.02 * (double)S.r[i] && (double)diff2 > 0.02 * (double)S.r[i]) f |= kOccC;
-    S.fl[i] = f;
+    const uint64_t ba = __ballot(fa), bb = __ballot(fb), bc = __ballot(fc), bg = __ballot(gp);
+    const uint64_t be = __ballot(i < S.L && curv > a.edge_thr);
+    const uint64_t bs = __ballot(i < S.L && curv < a.surf_thr);
+    if (lane == 0) {
+      S.occa.w[c] = ba;
+      S.occb.w[c] = bb;
+      S.occc.w[c] = bc;
+      S.gap.w[c] = bg;
+      S.edgec.w[c] = be;
+      S.surfc.w[c] = bs;
+    }
   }
   __syncthreads();
-  // ---- cloudNeighborPicked after smoothness reset + occlusion marks; curvature ----
-  for (int i = lane; i < S.L; i += 64) {
-    const int k = S.wlo + i;
-    bool picked = (k < 5) && st->picked04[k] != 0;
-    for (int j = k; j <= k + 5 && !picked; ++j)
-      if (j - S.wlo < S.L && (S.fl[j - S.wlo] & kOccA)) picked = true;
-    for (int j = k - 6; j <= k - 1 && !picked; ++j)
-      if (j >= S.wlo && (S.fl[j - S.wlo] & kOccB)) picked = true;
-    if (S.fl[i] & kOccC) picked = true;
-    // Only this lane writes byte i and the occlusion bits other lanes read are left unchanged.
-    if (picked) S.fl[i] |= kPicked;
-    if (k >= 5 && k < n - 5 && i >= 5 && i + 5 < S.L) {  // calculateSmoothness (:113-122), f32 left-to-right
-      float d = S.r[i - 5] + S.r[i - 4] + S.r[i - 3] + S.r[i - 2] + S.r[i - 1] - S.r[i] * 10.0f + S.r[i + 1] +
-                S.r[i + 2] + S.r[i + 3] + S.r[i + 4] + S.r[i + 5];
-      S.curv[i] = d * d;
-    }
+  // cloudNeighborPicked: reset over [5, n-5) (:124) then the marks; indices < 5 keep stream state
+  for (int c = lane; c < S.nw; c += 64) {
+    const uint64_t A = S.occa.w[c], An = c + 1 < S.nw ? S.occa.w[c + 1] : 0ull;
+    const uint64_t B = S.occb.w[c], Bp = c > 0 ? S.occb.w[c - 1] : 0ull;
+    uint64_t mk = S.occc.w[c] | A;
+#pragma unroll
+    for (int d = 1; d <= 5; ++d) mk |= (A >> d) | (An << (64 - d));
+#pragma unroll
+    for (int d = 1; d <= 6; ++d) mk |= (B << d) | (Bp >> (64 - d));
+    if (c == 0 && S.wlo == 0)
+      for (int k = 0; k < 5 && k < S.L; ++k)
+        if (st->picked04[k]) mk |= 1ull << k;
+    S.picked.w[c] = mk;
   }
   __syncthreads();
+  FBR_STAMP(1);
 
   // ---- extractFeatures (:188-285) ----
-  const float edgeThr = a.edge_thr, surfThr = a.surf_thr;
   int corner_cnt = 0, cand_cnt = 0;
   float4* corner_out = a.corner_slot + (int64_t)slot * kCornerPerRing;
   float4* cand_out = a.cand + (int64_t)slot * W;
@@ -156,109 +337,234 @@ k_features(FeatArgs a) {
     const int ep = (s * (5 - j) + e * (j + 1)) / 6 - 1;
     if (sp >= ep) continue;
     const int m = ep - sp;
-    if (m + 1 > a.segcap) {
+    if (m + 1 > segcap || m > kseg) {
       if (lane == 0) atomicOr(&a.err[job], 2);
       return;
     }
     const bool has_stale = (sp <= 4 && 4 < ep);
-    for (int t = lane; t <= m; t += 64) {
-      const int pos = sp + t;
-      SmoothEntry en;
-      if (pos == 4) { en.v = st->smooth4_value; en.ind = st->smooth4_ind; }
-      else { en.v = S.curv[pos - S.wlo]; en.ind = pos; }
-      S.seg[t] = en;
+    // -- sort [sp, ep) by (curvature bits, position) --
+    int kpow = 1;
+    while (kpow < m) kpow <<= 1;
+    for (int t = lane; t < kpow; t += 64) {
+      uint64_t key = kPadKey;
+      if (t < m) {
+        const int pos = sp + t;
+        const float v = (pos == 4) ? st->smooth4_value : S.curv[pos - S.wlo];
+        key = ((uint64_t)__float_as_uint(v) << 16) | (uint64_t)t;
+      }
+      S.keys[t] = key;
     }
     __syncthreads();
-    // parallel stable rank sort of seg[0..m)
-    bool tie = false, nan = false;
-    for (int t = lane; t < m; t += 64) {
-      const float v = S.seg[t].v;
-      int rank = 0;
-      for (int u = 0; u < m; ++u) {
-        const float w = S.seg[u].v;
-        rank += (w < v) || (w == v && u < t);
-        tie |= (w == v) && (u != t);
-      }
-      nan |= (v != v);
-      S.srt[min(rank, m - 1)] = S.seg[t];
-    }
-    const bool any_tie = __any(tie || nan);
-    const bool any_nan = __any(nan);
-    __syncthreads();
-    if (lane == 0) {
-      if (any_tie) {
-        for (int t = 0; t < m; ++t) S.srt[t] = S.seg[t];
-        std_sort_emul(S.srt, m);
-      }
-      S.srt[m] = S.seg[m];  // cloudSmoothness[ep] is never sorted (:203)
-      if (has_stale) {      // the slot left at position 4 is the next scan's stale entry
-        st->smooth4_value = S.srt[4 - sp].v;
-        st->smooth4_ind = S.srt[4 - sp].ind;
-      }
-      const bool fast = !has_stale && !any_nan;
-      // corner picks, k = ep .. sp (:208-242)
-      int largestPickedNum = 0;
-      for (int k = m; k >= 0; k--) {
-        const SmoothEntry en = S.srt[k];
-        if (fast && k < m && !(en.v > edgeThr)) break;
-        const int ind = en.ind;
-        const int li = ind - S.wlo;
-        if (li < 0 || li + 5 >= S.L) { atomicOr(&a.err[job], 4); break; }
-        if ((S.fl[li] & kPicked) == 0 && S.curv[li] > edgeThr) {
-          largestPickedNum++;
-          if (largestPickedNum <= kCornerPerSeg) {
-            S.fl[li] |= kLabPos;
-            corner_out[corner_cnt++] = CL[ind];
-          } else {
-            break;
+    for (int k2 = 2; k2 <= kpow; k2 <<= 1) {
+      for (int j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
+        // pairs (t, t^j2) with t < t^j2: pair index q -> t = (q / j2) * 2 * j2 + q % j2
+        const int npairs = kpow >> 1;
+        uint64_t xs[QP], ys[QP];
+        int ts[QP];
+#pragma unroll
+        for (int q4 = 0; q4 < QP; ++q4) {
+          const int q = lane + 64 * q4;
+          ts[q4] = (q / j2) * 2 * j2 + (q % j2);
+          if (q < npairs) {
+            xs[q4] = S.keys[ts[q4]];
+            ys[q4] = S.keys[ts[q4] + j2];
           }
-          S.fl[li] |= kPicked;
-          suppress(S, ind);
         }
-      }
-      // surf picks, k = sp .. ep (:245-276); ep handled last
-      for (int k = 0; k <= m; k++) {
-        if (k < m && fast && !(S.srt[k].v < surfThr)) k = m;  // rest of the sorted part fails
-        const SmoothEntry en = S.srt[k];
-        const int ind = en.ind;
-        const int li = ind - S.wlo;
-        if (li < 0 || li + 5 >= S.L) { atomicOr(&a.err[job], 4); break; }
-        if ((S.fl[li] & kPicked) == 0 && S.curv[li] < surfThr) {
-          S.fl[li] = (uint8_t)((S.fl[li] & ~kLabPos) | kLabNeg | kPicked);
-          suppress(S, ind);
+#pragma unroll
+        for (int q4 = 0; q4 < QP; ++q4) {
+          const int q = lane + 64 * q4;
+          if (q < npairs) {
+            const int t = ts[q4];
+            const bool up = (t & k2) == 0;
+            if ((xs[q4] > ys[q4]) == up) {
+              S.keys[t] = ys[q4];
+              S.keys[t + j2] = xs[q4];
+            }
+          }
         }
+        __syncthreads();
       }
     }
-    __syncthreads();
+    bool bad = false;
+    for (int t = lane; t < m; t += 64) {
+      const uint32_t vb = (uint32_t)(S.keys[t] >> 16);
+      bad |= vb > 0x7f800000u;  // NaN
+      if (t + 1 < m) bad |= (uint32_t)(S.keys[t + 1] >> 16) == vb;
+    }
+    const bool tie = __any(bad);
+    FBR_STAMP(2);
+    if (has_stale || tie) {
+      // materialise the segment in the reference's sorted order on one lane
+      if (lane == 0) {
+        if (tie) {
+          for (int t = 0; t < m; ++t) {
+            const int pos = sp + t;
+            S.seg[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind}
+                                  : SmoothEntry{S.curv[pos - S.wlo], pos};
+          }
+          std_sort_emul(S.seg, m);
+        } else {
+          for (int t = 0; t < m; ++t) {
+            const int pos = sp + (int)(S.keys[t] & 0xFFFFu);
+            S.seg[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind}
+                                  : SmoothEntry{S.curv[pos - S.wlo], pos};
+          }
+        }
+        S.seg[m] = SmoothEntry{S.curv[ep - S.wlo], ep};  // cloudSmoothness[ep] is never sorted (:203)
+        if (has_stale) {  // the entry left at position 4 is the next scan's stale slot
+          st->smooth4_value = S.seg[4 - sp].v;
+          st->smooth4_ind = S.seg[4 - sp].ind;
+        }
+      }
+      __syncthreads();
+    }
+    if (has_stale) {
+      if (lane == 0) serial_walks(S, a, job, m, CL, corner_out, corner_cnt);
+      corner_cnt = __shfl(corner_cnt, 0);
+      __syncthreads();
+    } else {
+      // -- members u in [0, m] (index sp+u): sorted order, visit ranks, conflict masks --
+      for (int k = lane; k <= m; k += 64) {
+        const int u = (k == m) ? m : (tie ? S.seg[k].ind - sp : (int)(S.keys[k] & 0xFFFFu));
+        S.sorder[k] = (uint16_t)u;
+        S.rankc[u] = (uint16_t)(k == m ? 0 : m - k);  // corner visit order: ep, then descending
+      }
+      __syncthreads();
+      for (int u = lane; u <= m; u += 64) {
+        const int li = sp + u - S.wlo;
+        const int f = reach_fwd(S, li), b = reach_bwd(S, li);
+        const int ru = S.rankc[u];
+        uint32_t nb = 0, hc = 0;
+        for (int d = 1; d <= f && u + d <= m; ++d) {
+          nb |= 1u << (4 + d);
+          if (S.rankc[u + d] < ru) hc |= 1u << (4 + d);
+        }
+        for (int d = 1; d <= b && u - d >= 0; ++d) {
+          nb |= 1u << (5 - d);
+          if (S.rankc[u - d] < ru) hc |= 1u << (5 - d);
+        }
+        S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
+      }
+      __syncthreads();
+      FBR_STAMP(3);
+      // -- corner walk --
+      uint64_t und[WMAX], tak[WMAX];
+#pragma unroll
+      for (int w = 0; w < WMAX; ++w) {
+        const int u = 64 * w + lane;
+        bool cand = false;
+        if (u <= m) {
+          const int li = sp + u - S.wlo;
+          cand = !S.picked.get(li) && S.edgec.get(li);
+        }
+        und[w] = __ballot(cand);
+        tak[w] = 0ull;
+      }
+      greedy_rounds(m, lane, und, tak, [&](int u) { return S.cm[u] & 1023u; }, a, job);
+      FBR_STAMP(4);
+      if (lane < WMAX) {
+        uint64_t t = 0;
+#pragma unroll
+        for (int w = 0; w < WMAX; ++w)
+          if (w == lane) t = tak[w];
+        S.tmask[lane] = t;
+      }
+      __syncthreads();
+      int taken = 0, cutoff = m + 1;
+      for (int r0 = 0; r0 <= m && taken <= kCornerPerSeg; r0 += 64) {
+        const int rr = r0 + lane;
+        int u = -1;
+        if (rr <= m) u = S.sorder[rr == 0 ? m : m - rr];
+        const bool acc = u >= 0 && ((S.tmask[u >> 6] >> (u & 63)) & 1ull);
+        const uint64_t mk = __ballot(acc);
+        const int pos = taken + __popcll(mk & ((1ull << lane) - 1ull));
+        if (acc && pos < kCornerPerSeg) corner_out[corner_cnt + pos] = CL[sp + u];
+        int cut = (acc && pos == kCornerPerSeg) ? rr : (m + 1);
+        for (int o = 32; o > 0; o >>= 1) cut = min(cut, __shfl_xor(cut, o));
+        cutoff = min(cutoff, cut);
+        taken += __popcll(mk);
+      }
+      corner_cnt += min(taken, kCornerPerSeg);
+      for (int u = lane; u <= m; u += 64) {
+        if (((S.tmask[u >> 6] >> (u & 63)) & 1ull) && S.rankc[u] < cutoff) {
+          const int li = sp + u - S.wlo;
+          const uint32_t c = S.cm[u];
+          atomicOr((unsigned long long*)&S.labpos.w[li >> 6], 1ull << (li & 63));
+          or_range(S.picked, li - (int)((c >> 24) & 15u), li + (int)((c >> 20) & 15u));
+        }
+      }
+      __syncthreads();
+      FBR_STAMP(5);
+      // -- surf walk: ascending, ep last -> higher priority = not higher corner priority --
+#pragma unroll
+      for (int w = 0; w < WMAX; ++w) {
+        const int u = 64 * w + lane;
+        bool cand = false;
+        if (u <= m) {
+          const int li = sp + u - S.wlo;
+          cand = !S.picked.get(li) && S.surfc.get(li);
+        }
+        und[w] = __ballot(cand);
+        tak[w] = 0ull;
+      }
+      greedy_rounds(m, lane, und, tak, [&](int u) {
+        const uint32_t c = S.cm[u];
+        return ((c >> 10) & 1023u) & ~(c & 1023u);
+      }, a, job);
+      FBR_STAMP(6);
+#pragma unroll
+      for (int w = 0; w < WMAX; ++w) {
+        const int u = 64 * w + lane;
+        if (u <= m && ((tak[w] >> lane) & 1ull)) {
+          const int li = sp + u - S.wlo;
+          const uint32_t c = S.cm[u];
+          atomicOr((unsigned long long*)&S.labneg.w[li >> 6], 1ull << (li & 63));
+          or_range(S.picked, li - (int)((c >> 24) & 15u), li + (int)((c >> 20) & 15u));
+        }
+      }
+      __syncthreads();
+    }
+    FBR_STAMP(7);
     // surf candidates: label[k] <= 0 for k in [sp, ep] (:279-284), index order
     for (int t0 = 0; t0 <= m; t0 += 64) {
       const int t = t0 + lane;
-      const bool c = t <= m && !(S.fl[sp + t - S.wlo] & kLabPos);
+      const bool c = t <= m && !S.labpos.get(sp + t - S.wlo);
       const uint64_t mk = __ballot(c);
       if (c) cand_out[cand_cnt + __popcll(mk & ((1ull << lane) - 1ull))] = CL[sp + t];
       cand_cnt += __popcll(mk);
     }
     __syncthreads();
+    FBR_STAMP(8);
   }
-  corner_cnt = __shfl(corner_cnt, 0);
   // ---- outputs ----
   int8_t* LB = a.label + job * HW;
   for (int k = max(cb, 0) + lane; k < ca; k += 64) {
-    const uint8_t f = S.fl[k - S.wlo];
-    const int8_t lab = (f & kLabPos) ? 1 : ((f & kLabNeg) ? -1 : 0);
+    const int li = k - S.wlo;
+    const int8_t lab = S.labpos.get(li) ? 1 : (S.labneg.get(li) ? -1 : 0);
     if (k >= 5 && k < n - 5) LB[k] = lab;      // cloudLabel reset range (:126)
     else if (k < 5 && lab != 0) LB[k] = lab;   // stale slots keep earlier values
   }
-  if (cb <= 0 && lane < 5 && lane < S.L) st->picked04[lane] = (int8_t)(S.fl[lane - S.wlo] & kPicked);
+  if (cb <= 0 && lane < 5 && lane < S.L) st->picked04[lane] = S.picked.get(lane) ? 1 : 0;
   if (lane == 0) {
     a.corner_cnt[slot] = corner_cnt;
     a.cand_cnt[slot] = cand_cnt;
   }
+#ifdef FBR_FEAT_STAMPS
+  FBR_STAMP(9);
+  if (lane == 0 && a.stamps)
+    for (int i = 0; i < 12; ++i) a.stamps[(int64_t)slot * 12 + i] = stamp_acc[i];
+#endif
+}
+
+size_t features_lds_bytes(const FeatArgs& a) {
+  return (size_t)a.region_a + (size_t)a.lcap * sizeof(float) + (size_t)9 * a.nwcap * sizeof(uint64_t) + 64;
 }
 
 void launch_features(hipStream_t s, const FeatArgs& a) {
-  size_t lds = (size_t)a.lcap * (4 + 4 + 2 + 1) + (size_t)a.segcap * 2 * sizeof(SmoothEntry) + 64;
-  hipLaunchKernelGGL(k_features, dim3(a.B * a.H), dim3(64), lds, s, a);
+  if (a.segcap <= 6 * 64 && a.kseg <= 4 * 128)
+    hipLaunchKernelGGL((k_features<6, 4>), dim3(a.B * a.H), dim3(64), features_lds_bytes(a), s, a);
+  else
+    hipLaunchKernelGGL((k_features<12, 8>), dim3(a.B * a.H), dim3(64), features_lds_bytes(a), s, a);
 }
 
 }  // namespace fbr
