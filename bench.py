@@ -34,7 +34,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def kernel_bytes(name, tot):
     n_in, n, Q, IQ, M = tot["n_in"], tot["n"], tot["Q"], tot["IQ"], tot["M"]
     return {
-        "gn_residual": 96.0 * IQ,             # query 16 B + 5 neighbours x 16 B per iteration
+        "gn_knn": 116.0 * IQ,                 # query 16 B + the 5 neighbours found 80 B + 5 positions out 20 B
+        "gn_residual": 116.0 * IQ,            # query 16 B + 5 positions 20 B + 5 neighbour gathers 80 B
         "project": 24.0 * n_in + 4.0 * n,     # raw point read + owner claim
         "extract": 4.0 * 2 * n + 28.0 * n,    # owners, owning point, xyzi+col+range write
         "features": 41.0 * n,                 # range/col/cloud read, label + candidate write
@@ -122,7 +123,7 @@ def main():
 
     poses, stats = ctx.batch_results()
     tb, tg = ctx.batch_bytes()
-    kernels = ["gn_residual", "gn_solve", "project", "extract", "features", "voxel_ring", "concat",
+    kernels = ["gn_knn", "gn_residual", "gn_solve", "project", "extract", "features", "voxel_ring", "concat",
                "voxel_scan", "gn_init", "crop", "gn_finalize"]
     ktimes = {k: ctx.kernel_time(k) for k in kernels}
 

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -87,6 +88,10 @@ struct fbr_ctx {
   int4* d_items = nullptr;
   int32_t *d_nitems = nullptr, *d_item_range = nullptr, *d_cropcnt = nullptr;
   double* d_partial = nullptr;
+  int32_t* d_nbr = nullptr;
+  unsigned long long* h_iter_flags = nullptr;  // host-mapped, written by k_gn_solve
+  unsigned long long* d_iter_flags = nullptr;  // its device address
+  unsigned long long gn_gen = 0;
   int max_items = 0;
   float* d_pose_out = nullptr;
   fbr_reg_stats* d_stats = nullptr;
@@ -158,7 +163,13 @@ int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pt
   *d_pts = nullptr;
   *d_cs = nullptr;
   const int64_t n = (int64_t)pts.size();
-  float inv = 1.0f;  // power-of-two cell >= 1 m: floor(p * inv) is exact
+  // Power-of-two cell (floor(p * inv) is exact).  0.5 m by default: with the kNN's lower-bound
+  // pruning the visited volume tracks the 5th-neighbour ball; FBR_KNN_CELL overrides (tuning).
+  float inv = 2.0f;
+  if (const char* e = std::getenv("FBR_KNN_CELL")) {
+    const float cell = std::strtof(e, nullptr);
+    if (cell > 0.0f) inv = std::exp2(-std::round(std::log2(cell)));
+  }
   int64_t lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0}, dims[3] = {1, 1, 1};
   for (int attempt = 0; attempt < 12; ++attempt) {
     for (int d = 0; d < 3; ++d) {
@@ -355,6 +366,8 @@ GnArgs gn_args(fbr_ctx* c, int B, bool trace) {
   a.pose_out = c->d_pose_out;
   a.stats = c->d_stats;
   a.trace = trace ? c->d_trace : nullptr;
+  a.nbr = c->d_nbr;
+  a.iter_flags = c->d_iter_flags;
   return a;
 }
 
@@ -373,6 +386,7 @@ int stage_register(fbr_ctx* c, int B, bool trace) {
   v.stride_out = c->HW;
   v.cnt_out = c->d_ncds;
   v.leaf = c->P.mapping_corner_leaf_size;
+  v.morton = 1;  // internal clouds: spatially compact query order for the kNN waves
   TIMED(c, "voxel_scan", launch_voxel_grid(c->stream, v));
   v.in = c->d_surf_all;
   v.cnt_in = c->d_nsurf;
@@ -387,9 +401,31 @@ int stage_register(fbr_ctx* c, int B, bool trace) {
   TIMED(c, "crop", launch_crop_count(c->stream, a, c->d_map_c, c->gc.n_points, 0, c->d_cropcnt));
   TIMED(c, "crop", launch_crop_count(c->stream, a, c->d_map_s, c->gs.n_points, 1, c->d_cropcnt));
   const int grid = std::max(1, std::min(c->max_items, 2048));
+  // Iterations run on the device without host round trips; the host stays kLag iterations
+  // ahead and stops enqueueing once k_gn_solve reports that no job of the batch is active.
+  constexpr int kLag = 2;
+  const unsigned long long gen = ++c->gn_gen;
+  bool watch = c->h_iter_flags != nullptr;
   for (int it = 0; it < c->P.max_iterations; ++it) {
+    if (watch && it >= kLag) {
+      volatile unsigned long long* f = c->h_iter_flags + (it - kLag);
+      unsigned long long v = *f;
+      for (long spins = 0; (v >> 32) != (gen & 0xFFFFFFFFull); ++spins) {
+        if ((spins & 1023) == 1023) {
+          const hipError_t q = hipStreamQuery(c->stream);
+          if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
+          if (q == hipSuccess && ((v = *f) >> 32) != (gen & 0xFFFFFFFFull)) {
+            watch = false;  // flag not visible although the stream drained: enqueue the rest
+            break;
+          }
+        }
+        v = *f;
+      }
+      if (watch && (v & 0xFFFFFFFFull) == 0) break;
+    }
+    TIMED(c, "gn_knn", launch_gn_knn(c->stream, a, grid));
     TIMED(c, "gn_residual", launch_gn_residual(c->stream, a, grid));
-    TIMED(c, "gn_solve", launch_gn_solve(c->stream, a));
+    TIMED(c, "gn_solve", launch_gn_solve(c->stream, a, it, gen));
   }
   TIMED(c, "gn_finalize", launch_gn_finalize(c->stream, a));
   return FBR_OK;
@@ -541,12 +577,17 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_vg_scratch, c->vg_scratch_elems) || dalloc(&c->d_vg_hist, c->vg_hist_elems) ||
               dalloc(&c->d_gn, B) || dalloc(&c->d_items, c->max_items) || dalloc(&c->d_nitems, 1) ||
               dalloc(&c->d_item_range, 2 * B) || dalloc(&c->d_cropcnt, 2 * B) ||
-              dalloc(&c->d_partial, (int64_t)c->max_items * 32) || dalloc(&c->d_pose_out, B * 6) ||
+              dalloc(&c->d_partial, (int64_t)c->max_items * 32) ||
+              dalloc(&c->d_nbr, (int64_t)c->max_items * 5 * 256) ||
+              hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * std::max(1, p->max_iterations),
+                            hipHostMallocMapped) != hipSuccess ||
+              hipHostGetDevicePointer((void**)&c->d_iter_flags, c->h_iter_flags, 0) != hipSuccess || dalloc(&c->d_pose_out, B * 6) ||
               dalloc(&c->d_stats, B) || dalloc(&c->d_trace, B * p->max_iterations * 6);
   if (fail) {
     fbr_destroy(c);
     return FBR_ERR_HIP;
   }
+  std::memset(c->h_iter_flags, 0, sizeof(unsigned long long) * std::max(1, p->max_iterations));
   if (hipMemset(c->d_sstream, 0, sizeof(StreamState)) != hipSuccess ||
       hipMemset(c->d_label_stream, 0, HW) != hipSuccess || hipMemset(c->d_col, 0, sizeof(int32_t) * B * HW) != hipSuccess ||
       hipMemset(c->d_range, 0, sizeof(float) * B * HW) != hipSuccess) {
@@ -567,9 +608,10 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_vg_hist, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_map_c,
-                  c->d_map_s, c->d_cs_c, c->d_cs_s};
+                  c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);
   for (auto& kv : c->timers) {
     for (auto& pr : kv.second.pending) {
       (void)hipEventDestroy(pr.first);

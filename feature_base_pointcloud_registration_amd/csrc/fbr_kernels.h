@@ -53,6 +53,7 @@ struct VgArgs {
   int64_t hist_stride;    // >= ceil(stride_in/256)*256
   float leaf;
   int nseg;
+  int morton;             // 1: emit voxels in Morton order of (i,j,k) instead of PCL key order
 };
 void launch_voxel_grid(hipStream_t s, const VgArgs& a);
 
@@ -91,10 +92,13 @@ struct GnArgs {
   float* pose_out;           // [B][6]
   fbr_reg_stats* stats;      // [B]
   float* trace;              // [B][max_iter][6] or null
+  int32_t* nbr;              // [max_items][5][256] kNN-5 map positions of each query (-1 = rejected)
+  unsigned long long* iter_flags;  // host-mapped [max_iter]: (generation << 32) | jobs still active
 };
 void launch_gn_init(hipStream_t s, const GnArgs& a);
+void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid);
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid);
-void launch_gn_solve(hipStream_t s, const GnArgs& a);
+void launch_gn_solve(hipStream_t s, const GnArgs& a, int iter_idx, unsigned long long gen);
 void launch_gn_finalize(hipStream_t s, const GnArgs& a);
 // laserCloud{Corner,Surf}FromMapDSNum: CropBox counts of the global map per job.
 void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, float* dst);

@@ -12,14 +12,17 @@
 //
 // Design (MI355X-first, results identical to the reference's KD-tree path):
 //   * The reference rebuilds two FLANN KD-trees on the cropped local map every scan.  Here the
-//     global map is bucketed ONCE into a dense grid with power-of-two cells >= 1 m (exact
-//     integer cell coordinates); the per-scan CropBox becomes a per-candidate box test.  Because
-//     a correspondence is kept only if the 5th neighbour has d2 < 1.0 (:1027, :1154), scanning the
-//     27 cells around the query and keeping the 5 smallest (d2, index) with d2 < 1.0 selects
-//     exactly the same neighbours as exact kNN-5 on the cropped cloud.
-//   * k_gn_residual: one lane per query (corner and surf queries of every active job of the batch
-//     are packed into 256-query work items); transform, kNN, residual and Jacobian row in float
-//     with the reference's operation order; the 21+6 normal-equation products are reduced in fp64
+//     global map is bucketed ONCE into a dense grid with power-of-two cells (exact integer cell
+//     coordinates); the per-scan CropBox becomes a per-candidate box test.  Because a
+//     correspondence is kept only if the 5th neighbour has d2 < 1.0 (:1027, :1154), keeping the 5
+//     smallest (d2, index) with d2 < 1.0 among the cells within radius 1 selects exactly the same
+//     neighbours as exact kNN-5 on the cropped cloud.  Cells are pruned with a float lower bound
+//     that provably never exceeds a member point's computed distance (see axis_lb).
+//   * k_gn_knn: one lane per query (corner and surf queries of every active job of the batch are
+//     packed into 256-query work items; the mapping-DS clouds are in Morton order, so a wave's
+//     queries are spatially compact); writes 5 neighbour positions per query.
+//   * k_gn_residual: gathers the 5 neighbours, residual and Jacobian row in float with the
+//     reference's operation order; the 21+6 normal-equation products are reduced in fp64
 //     (OpenCV's CV_32F gemm accumulates in double) by wave shuffles into one partial per item.
 //   * k_gn_solve: one lane per job sums its items in order (corner items, then surf items: the
 //     combineOptimizationCoeffs row order), rounds AtA/AtB to float and runs the reference's float
@@ -52,44 +55,85 @@ __device__ void pose_to_T(const float* tr, float* T, float* trig) {
 
 struct Knn5 {
   float d[5];
-  int idx[5];
-  float x[5], y[5], z[5];
-  int cnt;
+  int id[5];   // map index (tie-break of FLANN's sorted result)
+  int pos[5];  // position in the cell-sorted map array
 };
 
 __device__ __forceinline__ bool knn_less(float d, int i, float d2, int i2) { return d < d2 || (d == d2 && i < i2); }
 
 // Insert by compare-swap down a sorted 5-slot list (compile-time indices: stays in registers).
-__device__ __forceinline__ void knn_insert(Knn5& r, float d, int idx, float px, float py, float pz) {
-  if (!knn_less(d, idx, r.d[4], r.idx[4])) return;
-  r.cnt = min(r.cnt + 1, 5);
+__device__ __forceinline__ void knn_insert(Knn5& r, float d, int id, int pos) {
+  if (!knn_less(d, id, r.d[4], r.id[4])) return;
 #pragma unroll
   for (int t = 0; t < 5; ++t) {
-    if (knn_less(d, idx, r.d[t], r.idx[t])) {
-      const float td = r.d[t], tx = r.x[t], ty = r.y[t], tz = r.z[t];
-      const int ti = r.idx[t];
-      r.d[t] = d; r.idx[t] = idx; r.x[t] = px; r.y[t] = py; r.z[t] = pz;
-      d = td; idx = ti; px = tx; py = ty; pz = tz;
+    if (knn_less(d, id, r.d[t], r.id[t])) {
+      const float td = r.d[t];
+      const int ti = r.id[t], tp = r.pos[t];
+      r.d[t] = d; r.id[t] = id; r.pos[t] = pos;
+      d = td; id = ti; pos = tp;
     }
   }
 }
 
-// All map points with d2 < 1.0 inside the crop box, 5 smallest by (d2, map index).
+// Lower bound of |q - p| along one axis for a point p in the cell at offset o from q's cell
+// (cells are [k*c, (k+1)*c) with c a power of two, so every edge is exact).  Rounding is
+// monotone, so fl(edge - q) <= |fl(q - p)| and the bound composed in the distance's own
+// operation order never exceeds the distance computed for any point of that cell.
+__device__ __forceinline__ float axis_lb(float q, float fcell, int o, float c) {
+  if (o == 0) return 0.0f;
+  if (o > 0) return (fcell + (float)o) * c - q;
+  return q - (fcell + (float)(o + 1)) * c;
+}
+
+__device__ __forceinline__ int rank_offset(int k, int s) { return k == 0 ? 0 : ((k & 1) ? s * ((k + 1) >> 1) : -s * (k >> 1)); }
+
+// Exact kNN-5 among map points inside the crop box with d2 < 1.0, ordered by (d2, map index):
+// the neighbour set FLANN's exact search returns on the cropped cloud whenever the reference
+// keeps the correspondence (pointSearchSqDis[4] < 1.0, :1027/:1154).  Cell rows (y,z) are visited
+// nearest-side-first; a row, and the cells of a row, are skipped once their lower-bound distance
+// exceeds the current 5th distance or reaches 1.0.
 __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
                           Knn5& r) {
-  r.cnt = 0;
 #pragma unroll
-  for (int t = 0; t < 5; ++t) { r.d[t] = __int_as_float(0x7f800000); r.idx[t] = 0x7fffffff; r.x[t] = r.y[t] = r.z[t] = 0.0f; }
-  const float inv = m.g.inv_cell;
-  const float fx = floorf(qx * inv), fy = floorf(qy * inv), fz = floorf(qz * inv);
-  if (!(fabsf(fx) < 1e9f && fabsf(fy) < 1e9f && fabsf(fz) < 1e9f)) return;
+  for (int t = 0; t < 5; ++t) { r.d[t] = __int_as_float(0x7f800000); r.id[t] = 0x7fffffff; r.pos[t] = -1; }
+  const float inv = m.g.inv_cell, c = 1.0f / inv;
+  const float sx = qx * inv, sy = qy * inv, sz = qz * inv;
+  const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+  if (!(fabsf(fx) < 1e7f && fabsf(fy) < 1e7f && fabsf(fz) < 1e7f)) return;
+  const int R = inv > 1.0f ? (int)inv : 1;  // cells per side covering radius 1
   const int cx = (int)fx - (int)m.g.origin[0], cy = (int)fy - (int)m.g.origin[1], cz = (int)fz - (int)m.g.origin[2];
   const int X = m.g.dims[0], Y = m.g.dims[1], Z = m.g.dims[2];
-  if (cx < -1 || cy < -1 || cz < -1 || cx > X || cy > Y || cz > Z) return;
-  const int x0 = max(cx - 1, 0), x1 = min(cx + 1, X - 1);
-  if (x0 > x1) return;
-  for (int z = max(cz - 1, 0); z <= min(cz + 1, Z - 1); ++z)
-    for (int y = max(cy - 1, 0); y <= min(cy + 1, Y - 1); ++y) {
+  if (cx < -R || cy < -R || cz < -R || cx >= X + R || cy >= Y + R || cz >= Z + R) return;
+  const int sgy = (sy - fy) >= 0.5f ? 1 : -1, sgz = (sz - fz) >= 0.5f ? 1 : -1;
+  const int K = 2 * R;
+  for (int ksum = 0; ksum <= 2 * K; ++ksum) {
+    for (int ky = max(0, ksum - K); ky <= min(K, ksum); ++ky) {
+      const int oy = rank_offset(ky, sgy), oz = rank_offset(ksum - ky, sgz);
+      const int y = cy + oy, z = cz + oz;
+      if (y < 0 || y >= Y || z < 0 || z >= Z) continue;
+      const float ly = axis_lb(qy, fy, oy, c), lz = axis_lb(qz, fz, oz, c);
+      const float ly2 = ly * ly, lz2 = lz * lz;
+      float lb = 0.0f;
+      lb += ly2;
+      lb += lz2;
+      if (lb > r.d[4] || !(lb < 1.0f)) continue;
+      int xa = 0, xb = 0;
+      for (int o = 1; o <= R; ++o) {
+        const float lx = axis_lb(qx, fx, -o, c);
+        float t = 0.0f;
+        t += lx * lx; t += ly2; t += lz2;
+        if (t > r.d[4] || !(t < 1.0f)) break;
+        xa = -o;
+      }
+      for (int o = 1; o <= R; ++o) {
+        const float lx = axis_lb(qx, fx, o, c);
+        float t = 0.0f;
+        t += lx * lx; t += ly2; t += lz2;
+        if (t > r.d[4] || !(t < 1.0f)) break;
+        xb = o;
+      }
+      const int x0 = max(cx + xa, 0), x1 = min(cx + xb, X - 1);
+      if (x0 > x1) continue;
       const int rowbase = (z * Y + y) * X;
       const int b = m.cell_start[rowbase + x0], e = m.cell_start[rowbase + x1 + 1];
       for (int i = b; i < e; ++i) {
@@ -100,14 +144,18 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         diff = qx - p.x; dist += diff * diff;                            // flann::L2_Simple
         diff = qy - p.y; dist += diff * diff;
         diff = qz - p.z; dist += diff * diff;
-        if (dist < 1.0f) knn_insert(r, dist, __float_as_int(p.w), p.x, p.y, p.z);
+        if (dist < 1.0f) knn_insert(r, dist, __float_as_int(p.w), i);
       }
     }
+  }
 }
 
 // cornerOptimization body (:1016-1121): coefficient row for one corner query, false if rejected.
-__device__ bool corner_residual(const Knn5& nn, float x0, float y0, float z0, float4& coeff) {
-  if (nn.cnt < 5 || !(nn.d[4] < 1.0f)) return false;
+struct Nbr5 {
+  float x[5], y[5], z[5];
+};
+
+__device__ bool corner_residual(const Nbr5& nn, float x0, float y0, float z0, float4& coeff) {
   float cx = 0, cy = 0, cz = 0;
   for (int j = 0; j < 5; j++) { cx += nn.x[j]; cy += nn.y[j]; cz += nn.z[j]; }
   cx /= 5.0f; cy /= 5.0f; cz /= 5.0f;
@@ -144,8 +192,7 @@ __device__ bool corner_residual(const Knn5& nn, float x0, float y0, float z0, fl
 }
 
 // surfOptimization body (:1145-1211).
-__device__ bool surf_residual(const Knn5& nn, float x0, float y0, float z0, float4& coeff) {
-  if (nn.cnt < 5 || !(nn.d[4] < 1.0f)) return false;
+__device__ bool surf_residual(const Nbr5& nn, float x0, float y0, float z0, float4& coeff) {
   float A0[5][3], B0[5], X0[3];
   for (int j = 0; j < 5; j++) { A0[j][0] = nn.x[j]; A0[j][1] = nn.y[j]; A0[j][2] = nn.z[j]; B0[j] = -1.0f; }
   colpiv_solve53(A0, B0, X0);
@@ -215,6 +262,33 @@ __global__ void k_gn_init(GnArgs a) {
   if (tid == 0) a.nitems[0] = min(base, a.max_items);
 }
 
+// kNN pass: one lane per query, writes the 5 neighbour positions (slot 0 = -1: no correspondence).
+__global__ void __launch_bounds__(kResThreads)
+k_gn_knn(GnArgs a) {
+  const int tid = threadIdx.x;
+  const int nitems = a.nitems[0];
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int4 item = a.items[it];
+    const int job = item.x;
+    const GnState& g = a.gn[job];
+    if (!g.active) continue;  // block-uniform
+    if (tid >= item.w) continue;
+    const bool corner = item.y == 0;
+    const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
+    const float* T = g.T;
+    // pointAssociateToMap (:397-403)
+    const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
+    const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
+    const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
+    Knn5 nn;
+    knn5_grid(corner ? a.mc : a.ms, x0, y0, z0, g.crop_min, g.crop_max, nn);
+    const bool ok = nn.pos[4] >= 0 && nn.d[4] < 1.0f;
+    int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? nn.pos[k] : -1;
+  }
+}
+
 __global__ void __launch_bounds__(kResThreads)
 k_gn_residual(GnArgs a) {
   __shared__ double red[kResThreads / 64][28];
@@ -227,16 +301,21 @@ k_gn_residual(GnArgs a) {
     if (!g.active) continue;  // block-uniform
     float row[6] = {0, 0, 0, 0, 0, 0}, b = 0.0f;
     bool ok = false;
-    if (tid < item.w) {
+    const int32_t* nb = a.nbr + (int64_t)it * 5 * kResThreads + tid;
+    if (tid < item.w && nb[0] >= 0) {
       const bool corner = item.y == 0;
       const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
       const float* T = g.T;
-      // pointAssociateToMap (:397-403)
       const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
       const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
       const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
-      Knn5 nn;
-      knn5_grid(corner ? a.mc : a.ms, x0, y0, z0, g.crop_min, g.crop_max, nn);
+      const float4* mp = corner ? a.mc.pts : a.ms.pts;
+      Nbr5 nn;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const float4 q = mp[nb[k * kResThreads]];
+        nn.x[k] = q.x; nn.y[k] = q.y; nn.z[k] = q.z;
+      }
       float4 c;
       ok = corner ? corner_residual(nn, x0, y0, z0, c) : surf_residual(nn, x0, y0, z0, c);
       if (ok) {
@@ -285,9 +364,14 @@ k_gn_residual(GnArgs a) {
   }
 }
 
-__global__ void k_gn_solve(GnArgs a) {
-  const int job = blockIdx.x * blockDim.x + threadIdx.x;
-  if (job >= a.B) return;
+constexpr int kSolveThreads = 256;
+
+struct SolveLds {  // per-lane strided arrays of the 6x6 degeneracy eigen-decomposition
+  float A[36 * kSolveThreads], V[36 * kSolveThreads], W[6 * kSolveThreads];
+  int R[6 * kSolveThreads], C[6 * kSolveThreads];
+};
+
+__device__ void gn_solve_job(const GnArgs& a, int job, SolveLds& L) {
   GnState& g = a.gn[job];
   if (!g.active) return;
   double acc[28];
@@ -325,8 +409,16 @@ __global__ void k_gn_solve(GnArgs a) {
   for (int k = 0; k < 36; ++k) matP[k] = 0.0f;  // local cv::Mat matP (:1278)
   if (iterCount == 0) {
     float E[6], V[36], V2[36], Vi[36];
-    for (int k = 0; k < 36; ++k) tmp[k] = AtA[k];
-    jacobi_eigen<6>(tmp, E, V);
+    {
+      const int t = threadIdx.x;
+#pragma unroll
+      for (int k = 0; k < 36; ++k) L.A[k * kSolveThreads + t] = AtA[k];
+      jacobi_eigen_lds<6, kSolveThreads>(L.A + t, L.W + t, L.V + t, L.R + t, L.C + t);
+#pragma unroll
+      for (int k = 0; k < 36; ++k) V[k] = L.V[k * kSolveThreads + t];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) E[k] = L.W[k * kSolveThreads + t];
+    }
     for (int k = 0; k < 36; ++k) V2[k] = V[k];
     int deg = 0;
     for (int i = 5; i >= 0; i--) {
@@ -340,12 +432,12 @@ __global__ void k_gn_solve(GnArgs a) {
     g.degenerate = deg;
     if (!lu_inv6(V, Vi))
       for (int k = 0; k < 36; ++k) Vi[k] = 0.0f;
-    gemm_f32_acc64(Vi, V2, matP, 6, 6, 6);
+    gemm_f32_acc64<6, 6, 6>(Vi, V2, matP);
   }
   if (g.degenerate) {
     float X2[6];
     for (int k = 0; k < 6; ++k) X2[k] = X[k];
-    gemm_f32_acc64(matP, X2, X, 6, 6, 1);
+    gemm_f32_acc64<6, 6, 1>(matP, X2, X);
   }
   for (int k = 0; k < 6; ++k) g.pose[k] += X[k];
   if (a.trace)
@@ -361,6 +453,26 @@ __global__ void k_gn_solve(GnArgs a) {
     g.active = 0;
   }
   pose_to_T(g.pose, g.T, g.trig);
+}
+
+// One workgroup: every job's LMOptimization step, then the number of jobs still iterating is
+// published to host-mapped memory as (generation << 32 | count) so the host stops enqueueing
+// iterations once the whole batch has converged.
+__global__ void __launch_bounds__(kSolveThreads) k_gn_solve(GnArgs a, int iter_idx, unsigned long long gen) {
+  __shared__ SolveLds L;
+  __shared__ int cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  int mine = 0;
+  for (int job = threadIdx.x; job < a.B; job += blockDim.x) {
+    gn_solve_job(a, job, L);
+    mine += a.gn[job].active;
+  }
+  if (mine) atomicAdd(&cnt, mine);
+  __syncthreads();
+  if (threadIdx.x == 0 && a.iter_flags)
+    __hip_atomic_store(&a.iter_flags[iter_idx], (gen << 32) | (unsigned long long)cnt, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void k_gn_finalize(GnArgs a) {
@@ -423,11 +535,14 @@ void launch_export_records(hipStream_t s, int B, const float* pose_out, const fb
 }
 
 void launch_gn_init(hipStream_t s, const GnArgs& a) { hipLaunchKernelGGL(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
+void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid) {
+  hipLaunchKernelGGL(k_gn_knn, dim3(grid), dim3(kResThreads), 0, s, a);
+}
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
   hipLaunchKernelGGL(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);
 }
-void launch_gn_solve(hipStream_t s, const GnArgs& a) {
-  hipLaunchKernelGGL(k_gn_solve, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
+void launch_gn_solve(hipStream_t s, const GnArgs& a, int iter_idx, unsigned long long gen) {
+  hipLaunchKernelGGL(k_gn_solve, dim3(1), dim3(kSolveThreads), 0, s, a, iter_idx, gen);
 }
 void launch_gn_finalize(hipStream_t s, const GnArgs& a) {
   hipLaunchKernelGGL(k_gn_finalize, dim3((a.B + 63) / 64), dim3(64), 0, s, a);

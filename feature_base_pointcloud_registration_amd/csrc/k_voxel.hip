@@ -11,6 +11,11 @@
 // (ascending input index inside a voxel).  Voxel membership and output order are exact; centroids
 // agree with the reference to float rounding (tests state the tolerance).
 //
+// Morton mode (downsampleCurrentScan only): the same voxels and centroids, emitted in Morton order
+// of (i,j,k) so that consecutive output points are spatially compact.  The order of the mapping
+// DS clouds only fixes the summation order of AtA (accumulated in fp64, so immaterial); it makes
+// every 64-query wave of the registration kernels touch a compact patch of the map grid.
+//
 // One 256-thread workgroup per segment.  The (key, index) pairs are sorted by an LSD radix sort
 // (8-bit digits, only as many passes as the key range needs) whose ping-pong buffers live in a
 // per-segment global scratch (L2-resident at these sizes); stability inside a 256-element tile
@@ -27,6 +32,15 @@ constexpr int kVgWaves = kVgThreads / 64;
 
 // Block-wide stable LSD radix sort of n (key, val) pairs.  Returns the buffer index (0 or 1)
 // holding the result.  Must be called by all 256 threads.
+__device__ __forceinline__ uint32_t spread3_10(uint32_t v) {  // 10 bits -> every third bit
+  v &= 0x3FFu;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
 __device__ int block_radix_sort(uint32_t* k[2], uint32_t* v[2], uint32_t* hist, int n, int nbits,
                                 uint32_t* lds_hist /*[256]*/, uint32_t* lds_wc /*[kVgWaves][256]*/,
                                 uint32_t* lds_tot /*[256]*/) {
@@ -160,6 +174,7 @@ k_voxel_grid(VgArgs a) {
     div_b[d] = max_b - min_b[d] + 1;
   }
   const uint32_t mul1 = (uint32_t)div_b[0], mul2 = (uint32_t)div_b[0] * (uint32_t)div_b[1];
+  const bool morton = a.morton && div_b[0] <= 1024 && div_b[1] <= 1024 && div_b[2] <= 1024;
   uint32_t* sc = a.scratch + (int64_t)seg * 4 * a.stride_in;
   uint32_t* kb[2] = {sc, sc + 2 * a.stride_in};
   uint32_t* vb[2] = {sc + a.stride_in, sc + 3 * a.stride_in};
@@ -168,12 +183,19 @@ k_voxel_grid(VgArgs a) {
     const int ijk0 = (int)(floorf(p.x * inv) - (float)min_b[0]);
     const int ijk1 = (int)(floorf(p.y * inv) - (float)min_b[1]);
     const int ijk2 = (int)(floorf(p.z * inv) - (float)min_b[2]);
-    kb[0][i] = (uint32_t)ijk0 + (uint32_t)ijk1 * mul1 + (uint32_t)ijk2 * mul2;
+    kb[0][i] = morton ? (spread3_10((uint32_t)ijk0) | (spread3_10((uint32_t)ijk1) << 1) |
+                         (spread3_10((uint32_t)ijk2) << 2))
+                      : (uint32_t)ijk0 + (uint32_t)ijk1 * mul1 + (uint32_t)ijk2 * mul2;
     vb[0][i] = (uint32_t)i;
   }
   const uint64_t nkeys = (uint64_t)div_b[0] * (uint64_t)div_b[1] * (uint64_t)div_b[2];
   int nbits = 32;
-  if (nkeys <= 0xFFFFFFFFull) {
+  if (morton) {
+    int b = 1;
+    for (int d = 0; d < 3; ++d)
+      if (div_b[d] > 1) b = max(b, 32 - __clz((uint32_t)(div_b[d] - 1)));
+    nbits = 3 * b;
+  } else if (nkeys <= 0xFFFFFFFFull) {
     const uint32_t maxk = (uint32_t)(nkeys - 1);
     nbits = maxk == 0 ? 1 : 32 - __clz(maxk);
   }

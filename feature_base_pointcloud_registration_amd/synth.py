@@ -82,6 +82,20 @@ def job(seed, max_offset=6.0):
     return gt, guess.astype(np.float32)
 
 
+def trajectory(seed, n, step=0.4, dyaw=np.deg2rad(1.0)):
+    """n consecutive ground-truth poses of a sensor driving forward (odometry-stream tests: each
+    registration starts from the previous result, as cloudHandler's static pose chain does)."""
+    gt0, _ = job(seed)
+    out = []
+    for k in range(n):
+        p = gt0.copy()
+        p[2] = gt0[2] + k * dyaw
+        p[3] = gt0[3] + k * step * np.cos(gt0[2])
+        p[4] = gt0[4] + k * step * np.sin(gt0[2])
+        out.append(p)
+    return out
+
+
 def make_jobs(config, n_jobs, base_seed=1000):
     """n_jobs independent (scan, guess, gt) registration jobs of a config (C4: seed 1000+j)."""
     n_scan, w, *_ = CONFIGS[config]

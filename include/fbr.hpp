@@ -1,0 +1,216 @@
+/* fbr.hpp — header-only C++ host mirror of the reference's operator interface for the hot path,
+ * layered on the C-ABI in fbr.h (libfbr_hip.so).  No ROS, PCL or Eigen types: the cloud_info
+ * message is mirrored by fbr::CloudInfo (msg/cloud_info.msg fields on the path) and
+ * Eigen::Affine3f by fbr::Affine3f (row-major 4x4 float, Eigen's matrix() element order).
+ *
+ *   reference (file:line)                                         mirror
+ *   ImageProjection::cloudHandler / projectPointCloud /             fbr::ImageProjection::cloudHandler
+ *     cloudExtraction (src/imageProjection.cpp:182-226, 583-670)    (+ the static pose chain :206-218)
+ *   FeatureExtraction::featureExtra (src/featureExtraction.h:79)    fbr::FeatureExtraction::featureExtra
+ *   mapOptimization::registration (src/mapOptmization.h:263-343)    fbr::MapOptimization::registration
+ *
+ * Error behaviour follows the reference: a scan that fails the cachePointCloud checks is dropped
+ * (cloudHandler returns false); too few features leave the pose untouched (status in lastStats()).
+ * Device or argument errors, which the reference has no analogue for, throw fbr::Error.
+ *
+ * The three objects share one fbr::Context (one HIP device + stream), because the device keeps the
+ * projection, feature state and map resident between the stages — the reference's objects are
+ * also members of one node (imageProjection.cpp:96-97).
+ */
+#ifndef FBR_HPP_
+#define FBR_HPP_
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fbr.h"
+
+namespace fbr {
+
+struct Error : std::runtime_error {
+  int status;
+  Error(int s, const char* what) : std::runtime_error(std::string(what) + ": " + fbr_strerror(s)), status(s) {}
+};
+
+inline void check(int s, const char* what) {
+  if (s != FBR_OK) throw Error(s, what);
+}
+
+/* Eigen::Affine3f as a row-major 4x4 float matrix. */
+struct Affine3f {
+  float m[16];
+  static Affine3f Identity() {
+    Affine3f a{};
+    a.m[0] = a.m[5] = a.m[10] = a.m[15] = 1.0f;
+    return a;
+  }
+  /* pcl::getTransformation(x, y, z, roll, pitch, yaw) */
+  static Affine3f fromPose(const float rpyxyz[6]) {
+    Affine3f a;
+    fbr_affine_from_pose(rpyxyz, a.m);
+    return a;
+  }
+  /* pcl::getTranslationAndEulerAngles -> [roll, pitch, yaw, x, y, z] */
+  void toPose(float rpyxyz[6]) const { fbr_pose_from_affine(m, rpyxyz); }
+  float x() const { return m[3]; }
+  float y() const { return m[7]; }
+  float z() const { return m[11]; }
+};
+
+/* The cloud_info fields the path reads or writes (msg/cloud_info.msg:5-9, 32-34), plus the
+ * feature mask (FeatureExtraction::cloudLabel, featureExtraction.h:41). */
+struct CloudInfo {
+  double stamp = 0.0;                         // header.stamp.toSec()
+  std::vector<int32_t> startRingIndex;        // [N_SCAN]
+  std::vector<int32_t> endRingIndex;          // [N_SCAN]
+  std::vector<int32_t> pointColInd;           // [n]
+  std::vector<float> pointRange;              // [n]
+  std::vector<fbr_point_xyzi> cloud_deskewed; // [n] extractedCloud
+  std::vector<fbr_point_xyzi> cloud_corner;   // cornerCloud (visit order)
+  std::vector<fbr_point_xyzi> cloud_surface;  // surfaceCloud (per-ring DS, ring order)
+  std::vector<int8_t> cloudLabel;             // [n] 1 corner, -1 picked surf, 0
+};
+
+/* One HIP device + stream + device-resident state (RAII over fbr_ctx). */
+class Context {
+ public:
+  explicit Context(const fbr_params& p, int hip_device = 0) : p_(p) {
+    check(fbr_create(&ctx_, &p_, hip_device), "fbr_create");
+  }
+  ~Context() {
+    if (ctx_) fbr_destroy(ctx_);
+  }
+  Context(const Context&) = delete;
+  Context& operator=(const Context&) = delete;
+  fbr_ctx* get() const { return ctx_; }
+  const fbr_params& params() const { return p_; }
+
+ private:
+  fbr_params p_;
+  fbr_ctx* ctx_ = nullptr;
+};
+
+/* ImageProjection (imageProjection.cpp:29): projectPointCloud + cloudExtraction on the device. */
+class ImageProjection {
+ public:
+  explicit ImageProjection(Context& c) : c_(c) {}
+
+  /* cloudHandler's projection half (:197-199).  Returns false where cachePointCloud drops the
+   * scan (:229-301: a ring outside [0, N_SCAN) is not an error there, only points are skipped;
+   * an empty cloud yields an empty CloudInfo). */
+  bool cloudHandler(const fbr_point_xyzirt* pts, int64_t n, double stamp, CloudInfo& info) {
+    const int H = c_.params().n_scan;
+    info.stamp = stamp;
+    info.startRingIndex.assign(H, 0);
+    info.endRingIndex.assign(H, 0);
+    info.pointColInd.resize(n);
+    info.pointRange.resize(n);
+    info.cloud_deskewed.resize(n);
+    int64_t n_out = 0;
+    check(fbr_project(c_.get(), pts, n, info.startRingIndex.data(), info.endRingIndex.data(),
+                      info.pointColInd.data(), info.pointRange.data(), info.cloud_deskewed.data(), &n_out),
+          "fbr_project");
+    info.pointColInd.resize(n_out);
+    info.pointRange.resize(n_out);
+    info.cloud_deskewed.resize(n_out);
+    info.cloud_corner.clear();
+    info.cloud_surface.clear();
+    info.cloudLabel.clear();
+    return true;
+  }
+
+ private:
+  Context& c_;
+};
+
+/* FeatureExtraction (featureExtraction.h:19): featureExtra(cloud_info) on the projection the
+ * context holds (the same scan ImageProjection just handled). */
+class FeatureExtraction {
+ public:
+  explicit FeatureExtraction(Context& c) : c_(c) {}
+
+  void featureExtra(CloudInfo& info) {
+    const int64_t n = (int64_t)info.pointColInd.size();
+    const int64_t corner_cap = 20 * 6 * (int64_t)c_.params().n_scan;
+    info.cloudLabel.resize(n);
+    info.cloud_corner.resize(corner_cap);
+    info.cloud_surface.resize(n);
+    int64_t nc = 0, ns = 0;
+    check(fbr_extract_features(c_.get(), info.cloudLabel.data(), info.cloud_corner.data(), &nc,
+                               info.cloud_surface.data(), &ns),
+          "fbr_extract_features");
+    info.cloud_corner.resize(nc);
+    info.cloud_surface.resize(ns);
+  }
+
+ private:
+  Context& c_;
+};
+
+/* mapOptimization (mapOptmization.h:54): prior map + registration(cloud_info, Affine3f&). */
+class MapOptimization {
+ public:
+  explicit MapOptimization(Context& c) : c_(c) {}
+
+  /* corner_GlobalMap / surf_GlobalMap as loaded from the PCDs (:245-260; the start-up VoxelGrid is
+   * applied on the device). */
+  void setGlobalMap(const std::vector<fbr_point_xyzi>& corner, const std::vector<fbr_point_xyzi>& surf) {
+    check(fbr_set_map(c_.get(), corner.data(), (int64_t)corner.size(), surf.data(), (int64_t)surf.size()),
+          "fbr_set_map");
+  }
+
+  /* registration (:263-343): mappingProcessInterval gate, getTranslationAndEulerAngles of the
+   * guess, CropBox + DS + scan2MapOptimization on the device, getTransformation of the result. */
+  void registration(const CloudInfo& info, Affine3f& pose_guess) {
+    stats_ = fbr_reg_stats{};
+    if (!(info.stamp - timeLastProcessing_ >= c_.params().mapping_process_interval)) {
+      stats_.status = FBR_REG_SKIPPED_INTERVAL;
+      return;
+    }
+    timeLastProcessing_ = info.stamp;
+    float pose[6];
+    pose_guess.toPose(pose);
+    check(fbr_register(c_.get(), info.cloud_corner.data(), (int64_t)info.cloud_corner.size(),
+                       info.cloud_surface.data(), (int64_t)info.cloud_surface.size(), pose, &stats_),
+          "fbr_register");
+    pose_guess = Affine3f::fromPose(pose);
+  }
+
+  const fbr_reg_stats& lastStats() const { return stats_; }
+
+ private:
+  Context& c_;
+  double timeLastProcessing_ = -1.0;  // mapOptmization.h:135 (timeLastProcessing = -1)
+  fbr_reg_stats stats_{};
+};
+
+/* The node-level chain of cloudHandler (:182-226): project -> featureExtra -> registration with
+ * the static pose (step = identity, so pose = pose * step = pose). */
+class Node {
+ public:
+  explicit Node(Context& c) : proj_(c), feat_(c), map_(c), pose_(Affine3f::Identity()) {}
+  MapOptimization& matcher() { return map_; }
+  const Affine3f& pose() const { return pose_; }
+  void setPose(const Affine3f& p) { pose_ = p; }
+  const CloudInfo& cloudInfo() const { return info_; }
+
+  bool cloudHandler(const fbr_point_xyzirt* pts, int64_t n, double stamp) {
+    if (!proj_.cloudHandler(pts, n, stamp, info_)) return false;
+    feat_.featureExtra(info_);
+    map_.registration(info_, pose_);
+    return true;
+  }
+
+ private:
+  ImageProjection proj_;
+  FeatureExtraction feat_;
+  MapOptimization map_;
+  Affine3f pose_;
+  CloudInfo info_;
+};
+
+}  // namespace fbr
+
+#endif /* FBR_HPP_ */

@@ -61,3 +61,21 @@ def has_gpu():
         return api.device_count() > 0
     except Exception:
         return False
+
+
+def build_mirror_demo():
+    """Compile tests/native/mirror_demo.cpp (the C++ host mirror include/fbr.hpp driving the
+    reference's cloudHandler chain) with the host compiler against libfbr_hip.so."""
+    from feature_base_pointcloud_registration_amd import api
+    src = os.path.join(NATIVE, "mirror_demo.cpp")
+    out_dir = os.path.join(NATIVE, "build")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, "mirror_demo")
+    lib = api.lib_path()
+    deps = [src, lib, os.path.join(REPO, "include", "fbr.hpp"), os.path.join(REPO, "include", "fbr.h")]
+    if not os.path.exists(out) or any(os.path.getmtime(d) > os.path.getmtime(out) for d in deps):
+        libdir = os.path.dirname(lib)
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(REPO, "include"), "-o", out, src,
+                               "-L", libdir, "-l:" + os.path.basename(lib), "-Wl,-rpath," + libdir,
+                               "-Wl,-rpath-link,/opt/rocm/lib"])
+    return out
