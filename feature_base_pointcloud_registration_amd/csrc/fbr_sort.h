@@ -127,13 +127,17 @@ __host__ __device__ inline int sm_lg(long n) {
   return r;
 }
 
-// std::sort(a, a + n, by_value())
-__host__ __device__ inline void std_sort_emul(SmoothEntry* a, int n) {
+struct SortFrame {
+  int first, last, depth;
+};
+constexpr int kSortStack = 32;  // >= 2*lg(n)+1 pending frames for n < 2^15
+
+// std::sort(a, a + n, by_value()); `stack` holds kSortStack frames (LDS on the device, so the
+// dynamically indexed stack does not live in scratch).  Partitions are disjoint, so handling the
+// right-hand parts from an explicit stack instead of recursion gives the same array.
+__host__ __device__ inline void std_sort_emul(SmoothEntry* a, int n, SortFrame* stack) {
   if (n <= 0) return;
-  struct Frame {
-    int first, last, depth;
-  };
-  Frame stack[64];
+  using Frame = SortFrame;
   int sp = 0;
   stack[sp++] = Frame{0, n, 2 * sm_lg(n)};
   while (sp > 0) {
@@ -148,7 +152,7 @@ __host__ __device__ inline void std_sort_emul(SmoothEntry* a, int n) {
       int mid = first + (last - first) / 2;
       sm_move_median_to_first(a, first, first + 1, mid, last - 1);
       int cut = sm_unguarded_partition(a, first + 1, last, first);
-      stack[sp++] = Frame{cut, last, depth};
+      if (sp < kSortStack) stack[sp++] = Frame{cut, last, depth};
       last = cut;
     }
   }
@@ -159,6 +163,11 @@ __host__ __device__ inline void std_sort_emul(SmoothEntry* a, int n) {
   } else {
     sm_insertion_sort(a, 0, n);
   }
+}
+
+inline void std_sort_emul(SmoothEntry* a, int n) {  // host convenience
+  SortFrame stack[kSortStack];
+  std_sort_emul(a, n, stack);
 }
 
 }  // namespace fbr

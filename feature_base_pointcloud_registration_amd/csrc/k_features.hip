@@ -63,18 +63,27 @@ struct FeatLds {
   uint32_t* cm;       // [segcap] conflict masks
   SmoothEntry* seg;   // [segcap] serial-path entries
   uint64_t* tmask;    // [WMAX] taken mask copy for the cap scan
+  SortFrame* sstack;  // [kSortStack] introsort emulation stack (tie segments, lane 0)
 };
 
-// Forward / backward suppression reach of window index li (<= 5 each).
+// 64 window bits [lo, lo+64) of a bit array; bits at negative window indices read as 1 (the
+// suppression loops stop there) and bits past the array as 0.
+__device__ __forceinline__ uint64_t bits64(const Bits& b, int lo, int nw) {
+  const int w = lo >> 6, sh = lo & 63;  // arithmetic shift: floor for negative lo
+  const uint64_t a = (w >= 0 && w < nw) ? b.w[w] : (w < 0 ? ~0ull : 0ull);
+  const uint64_t c = (w + 1 >= 0 && w + 1 < nw) ? b.w[w + 1] : (w + 1 < 0 ? ~0ull : 0ull);
+  return sh ? ((a >> sh) | (c << (64 - sh))) : a;
+}
+
+// Forward / backward suppression reach of window index li (<= 5 each): consecutive indices
+// without a column gap > 10 (:230-240 / :262-274), from the gap bit words.
 __device__ __forceinline__ int reach_fwd(const FeatLds& S, int li) {
-  int f = 0;
-  while (f < 5 && !S.gap.get(li + f)) ++f;
-  return f;
+  const uint64_t x = bits64(S.gap, li, S.nw);      // bit d = gap at li+d
+  return __builtin_ctzll(x | 0x20ull);              // zeros before the first gap, capped at 5
 }
 __device__ __forceinline__ int reach_bwd(const FeatLds& S, int li) {
-  int b = 0;
-  while (b < 5 && li - 1 - b >= 0 && !S.gap.get(li - 1 - b)) ++b;
-  return b;
+  const uint64_t x = bits64(S.gap, li - 64, S.nw);  // bit 63-d = gap at li-1-d
+  return __builtin_clzll(x | (1ull << 58));        // capped at 5
 }
 
 // Mark cloudNeighborPicked over [li-bwd, li+fwd] (the suppression loops :227-240 / :259-274).
@@ -176,6 +185,111 @@ __device__ void greedy_rounds(int m, int lane, uint64_t (&und)[WMAX], uint64_t (
   }
 }
 
+// libstdc++ 11 std::sort on a segment with tied curvatures, wave-parallel.  The final
+// __insertion_sort / __unguarded_insertion_sort pass is stable, so std::sort's result is the
+// stable sort of the array as the introsort partition phase leaves it.  That phase is reproduced
+// exactly: __unguarded_partition(lo, hi, pivot) swaps the k-th element (from the left) that is
+// not < pivot with the k-th element (from the right) that is not > pivot while the former lies
+// left of the latter, and returns min(g_K, r_{K-1}) for the first k = K where that fails
+// (swapped elements stop the scans).  Checked against std::sort on tie-heavy arrays
+// (tests/test_oracle_pinning.py).  Depth exhaustion falls back to the serial heap sort.
+__device__ int wave_partition(SmoothEntry* a, int lo, int hi, float p, int* posL, int* posR, int lane) {
+  int cntL = 0;
+  for (int b = lo; b < hi; b += 64) {
+    const int i = b + lane;
+    const bool isL = i < hi && !(a[i].v < p);
+    const uint64_t bl = __ballot(isL);
+    if (isL) posL[cntL + __popcll(bl & ((1ull << lane) - 1ull))] = i;
+    cntL += __popcll(bl);
+  }
+  int cntR = 0;
+  for (int t = hi - 1; t >= lo; t -= 64) {
+    const int i = t - lane;
+    const bool isR = i >= lo && !(p < a[i].v);
+    const uint64_t br = __ballot(isR);
+    if (isR) posR[cntR + __popcll(br & ((1ull << lane) - 1ull))] = i;
+    cntR += __popcll(br);
+  }
+  __syncthreads();
+  const int mn = min(cntL, cntR);
+  int K1 = 0;  // swaps performed = number of k with g_k < r_k (a prefix of k)
+  for (int k0 = 0; k0 < mn; k0 += 64) {
+    const int k = k0 + lane;
+    const uint64_t bo = __ballot(k < mn && posL[k] < posR[k]);
+    K1 += __popcll(bo);
+    if (bo != ~0ull) break;
+  }
+  for (int k = lane; k < K1; k += 64) {
+    const int x = posL[k], y = posR[k];
+    const SmoothEntry t = a[x];
+    a[x] = a[y];
+    a[y] = t;
+  }
+  int cut = K1 < cntL ? posL[K1] : INT_MAX;
+  if (K1 > 0) cut = min(cut, posR[K1 - 1]);
+  __syncthreads();
+  return min(cut, hi);
+}
+
+__device__ void wave_introsort_partitions(SmoothEntry* a, int n, SortFrame* stack, int* posL, int* posR,
+                                          int lane) {
+  int sp = 0;
+  stack[sp++] = SortFrame{0, n, 2 * sm_lg(n)};  // every lane writes / reads the same frames
+  while (sp > 0) {
+    const SortFrame f = stack[--sp];
+    int first = f.first, last = f.last, depth = f.depth;
+    while (last - first > 16) {
+      if (depth == 0) {  // std::partial_sort(first, last, last)
+        if (lane == 0) sm_heap_sort(a, first, last);
+        __syncthreads();
+        break;
+      }
+      --depth;
+      const int mid = first + (last - first) / 2;
+      if (lane == 0) sm_move_median_to_first(a, first, first + 1, mid, last - 1);
+      __syncthreads();
+      const int cut = wave_partition(a, first + 1, last, a[first].v, posL, posR, lane);
+      if (sp < kSortStack) stack[sp++] = SortFrame{cut, last, depth};
+      last = cut;
+    }
+  }
+  __syncthreads();
+}
+
+// In-LDS bitonic sort of kpow (power of two) 64-bit keys, QP compare-exchange pairs per lane.
+template <int QP>
+__device__ __forceinline__ void bitonic_sort_keys(uint64_t* keys, int kpow, int lane) {
+  for (int k2 = 2; k2 <= kpow; k2 <<= 1) {
+    for (int j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
+      const int npairs = kpow >> 1;
+      uint64_t xs[QP], ys[QP];
+      int ts[QP];
+#pragma unroll
+      for (int q4 = 0; q4 < QP; ++q4) {
+        const int q = lane + 64 * q4;
+        ts[q4] = ((q & ~(j2 - 1)) << 1) | (q & (j2 - 1));  // j2 is a power of two
+        if (q < npairs) {
+          xs[q4] = keys[ts[q4]];
+          ys[q4] = keys[ts[q4] + j2];
+        }
+      }
+#pragma unroll
+      for (int q4 = 0; q4 < QP; ++q4) {
+        const int q = lane + 64 * q4;
+        if (q < npairs) {
+          const int t = ts[q4];
+          const bool up = (t & k2) == 0;
+          if ((xs[q4] > ys[q4]) == up) {
+            keys[t] = ys[q4];
+            keys[t + j2] = xs[q4];
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // Diagnostic build only (-DFBR_FEAT_STAMPS, tools/feat_stamps.py): per-phase s_memtime cycle sums
 // per ring into FeatArgs::stamps.  The shipped library is compiled without it.
 #ifdef FBR_FEAT_STAMPS
@@ -245,6 +359,7 @@ k_features(FeatArgs a) {
   S.sorder = (uint16_t*)((unsigned char*)S.cm + sizeof(uint32_t) * segcap);
   S.rankc = S.sorder + segcap;
   S.tmask = (uint64_t*)(((uintptr_t)(S.rankc + segcap) + 15) & ~(uintptr_t)15);
+  S.sstack = (SortFrame*)(words + 9 * nwcap);
 
   const float* R = a.range + job * HW;
   const int32_t* C = a.col + job * HW;
@@ -355,66 +470,50 @@ k_features(FeatArgs a) {
       S.keys[t] = key;
     }
     __syncthreads();
-    for (int k2 = 2; k2 <= kpow; k2 <<= 1) {
-      for (int j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
-        // pairs (t, t^j2) with t < t^j2: pair index q -> t = (q / j2) * 2 * j2 + q % j2
-        const int npairs = kpow >> 1;
-        uint64_t xs[QP], ys[QP];
-        int ts[QP];
-#pragma unroll
-        for (int q4 = 0; q4 < QP; ++q4) {
-          const int q = lane + 64 * q4;
-          ts[q4] = (q / j2) * 2 * j2 + (q % j2);
-          if (q < npairs) {
-            xs[q4] = S.keys[ts[q4]];
-            ys[q4] = S.keys[ts[q4] + j2];
-          }
-        }
-#pragma unroll
-        for (int q4 = 0; q4 < QP; ++q4) {
-          const int q = lane + 64 * q4;
-          if (q < npairs) {
-            const int t = ts[q4];
-            const bool up = (t & k2) == 0;
-            if ((xs[q4] > ys[q4]) == up) {
-              S.keys[t] = ys[q4];
-              S.keys[t + j2] = xs[q4];
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-    bool bad = false;
+    bitonic_sort_keys<QP>(S.keys, kpow, lane);
+    bool tflag = false, nflag = false;
     for (int t = lane; t < m; t += 64) {
       const uint32_t vb = (uint32_t)(S.keys[t] >> 16);
-      bad |= vb > 0x7f800000u;  // NaN
-      if (t + 1 < m) bad |= (uint32_t)(S.keys[t + 1] >> 16) == vb;
+      nflag |= vb > 0x7f800000u;  // NaN
+      if (t + 1 < m) tflag |= (uint32_t)(S.keys[t + 1] >> 16) == vb;
     }
-    const bool tie = __any(bad);
+    const bool nan = __any(nflag);
+    const bool tie = __any(tflag) || nan;
     FBR_STAMP(2);
-    if (has_stale || tie) {
-      // materialise the segment in the reference's sorted order on one lane
+    if (tie) {
+      // equal curvatures: their order is introsort's; materialise std::sort's result in S.seg
+      for (int t = lane; t < m; t += 64) {
+        const int pos = sp + t;
+        S.seg[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.curv[pos - S.wlo], pos};
+      }
+      __syncthreads();
+      if (nan) {
+        if (lane == 0) std_sort_emul(S.seg, m, S.sstack);
+        __syncthreads();
+      } else {
+        wave_introsort_partitions(S.seg, m, S.sstack, (int*)S.cm, (int*)S.sorder, lane);
+        for (int t = lane; t < kpow; t += 64)
+          S.keys[t] = t < m ? (((uint64_t)__float_as_uint(S.seg[t].v) << 16) | (uint64_t)t) : kPadKey;
+        __syncthreads();
+        bitonic_sort_keys<QP>(S.keys, kpow, lane);  // stable sort of the partitioned array
+        SmoothEntry* tmp = (SmoothEntry*)S.cm;       // cm + sorder + rankc = 8 B per entry
+        for (int k = lane; k < m; k += 64) tmp[k] = S.seg[S.keys[k] & 0xFFFFu];
+        __syncthreads();
+        for (int k = lane; k < m; k += 64) S.seg[k] = tmp[k];
+        __syncthreads();
+      }
+    } else if (has_stale) {
+      for (int k = lane; k < m; k += 64) {
+        const int pos = sp + (int)(S.keys[k] & 0xFFFFu);
+        S.seg[k] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.curv[pos - S.wlo], pos};
+      }
+      __syncthreads();
+    }
+    if (has_stale) {
       if (lane == 0) {
-        if (tie) {
-          for (int t = 0; t < m; ++t) {
-            const int pos = sp + t;
-            S.seg[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind}
-                                  : SmoothEntry{S.curv[pos - S.wlo], pos};
-          }
-          std_sort_emul(S.seg, m);
-        } else {
-          for (int t = 0; t < m; ++t) {
-            const int pos = sp + (int)(S.keys[t] & 0xFFFFu);
-            S.seg[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind}
-                                  : SmoothEntry{S.curv[pos - S.wlo], pos};
-          }
-        }
         S.seg[m] = SmoothEntry{S.curv[ep - S.wlo], ep};  // cloudSmoothness[ep] is never sorted (:203)
-        if (has_stale) {  // the entry left at position 4 is the next scan's stale slot
-          st->smooth4_value = S.seg[4 - sp].v;
-          st->smooth4_ind = S.seg[4 - sp].ind;
-        }
+        st->smooth4_value = S.seg[4 - sp].v;            // the entry left at position 4 is the next
+        st->smooth4_ind = S.seg[4 - sp].ind;            // scan's stale slot
       }
       __syncthreads();
     }
@@ -435,13 +534,18 @@ k_features(FeatArgs a) {
         const int f = reach_fwd(S, li), b = reach_bwd(S, li);
         const int ru = S.rankc[u];
         uint32_t nb = 0, hc = 0;
-        for (int d = 1; d <= f && u + d <= m; ++d) {
-          nb |= 1u << (4 + d);
-          if (S.rankc[u + d] < ru) hc |= 1u << (4 + d);
+        int rn[10];
+#pragma unroll
+        for (int d = 1; d <= 5; ++d) {  // independent LDS reads, then the masks
+          rn[4 + d] = (d <= f && u + d <= m) ? (int)S.rankc[u + d] : INT_MAX;
+          rn[5 - d] = (d <= b && u - d >= 0) ? (int)S.rankc[u - d] : INT_MAX;
         }
-        for (int d = 1; d <= b && u - d >= 0; ++d) {
-          nb |= 1u << (5 - d);
-          if (S.rankc[u - d] < ru) hc |= 1u << (5 - d);
+#pragma unroll
+        for (int d = 1; d <= 5; ++d) {
+          if (d <= f && u + d <= m) nb |= 1u << (4 + d);
+          if (d <= b && u - d >= 0) nb |= 1u << (5 - d);
+          if (rn[4 + d] < ru) hc |= 1u << (4 + d);
+          if (rn[5 - d] < ru) hc |= 1u << (5 - d);
         }
         S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
       }
@@ -557,7 +661,8 @@ k_features(FeatArgs a) {
 }
 
 size_t features_lds_bytes(const FeatArgs& a) {
-  return (size_t)a.region_a + (size_t)a.lcap * sizeof(float) + (size_t)9 * a.nwcap * sizeof(uint64_t) + 64;
+  return (size_t)a.region_a + (size_t)a.lcap * sizeof(float) + (size_t)9 * a.nwcap * sizeof(uint64_t) +
+         sizeof(SortFrame) * kSortStack + 64;
 }
 
 void launch_features(hipStream_t s, const FeatArgs& a) {

@@ -73,3 +73,74 @@ def test_oracle_projection_rejects_nonfinite_like_x86():
     pts["ring"] = [0, 1, 2, 3]
     pr = O.project(P, pts)
     assert len(pr["col_ind"]) == 2  # the finite point and the inf-range point (range < 1 is false)
+
+
+# ---- the wave-parallel std::sort used by k_features.hip for segments with tied curvatures ----
+def _lg(n):
+    r = -1
+    while n:
+        n >>= 1
+        r += 1
+    return r
+
+
+def _move_median_to_first(a, res, x, y, z):  # libstdc++ __move_median_to_first
+    v = lambda i: a[i][0]  # noqa: E731
+    if v(x) < v(y):
+        if v(y) < v(z):
+            a[res], a[y] = a[y], a[res]
+        elif v(x) < v(z):
+            a[res], a[z] = a[z], a[res]
+        else:
+            a[res], a[x] = a[x], a[res]
+    elif v(x) < v(z):
+        a[res], a[x] = a[x], a[res]
+    elif v(y) < v(z):
+        a[res], a[z] = a[z], a[res]
+    else:
+        a[res], a[y] = a[y], a[res]
+
+
+def _closed_form_partition(a, lo, hi, p):
+    """k_features.hip wave_partition: k-th left stopper <-> k-th right stopper while left < right;
+    cut = min(g_K, r_{K-1})."""
+    L = [i for i in range(lo, hi) if not (a[i][0] < p)]
+    R = [i for i in range(hi - 1, lo - 1, -1) if not (p < a[i][0])]
+    k1 = 0
+    while k1 < min(len(L), len(R)) and L[k1] < R[k1]:
+        k1 += 1
+    for k in range(k1):
+        a[L[k]], a[R[k]] = a[R[k]], a[L[k]]
+    cut = L[k1] if k1 < len(L) else 1 << 30
+    if k1 > 0:
+        cut = min(cut, R[k1 - 1])
+    return min(cut, hi)
+
+
+def _wave_std_sort(vals):
+    a = [(np.float32(v), i) for i, v in enumerate(vals)]
+    stack = [(0, len(a), 2 * _lg(len(a)))]
+    while stack:
+        first, last, depth = stack.pop()
+        while last - first > 16:
+            assert depth > 0  # heap-sort fallback not exercised by these inputs
+            depth -= 1
+            _move_median_to_first(a, first, first + 1, first + (last - first) // 2, last - 1)
+            cut = _closed_form_partition(a, first + 1, last, a[first][0])
+            stack.append((cut, last, depth))
+            last = cut
+    order = sorted(range(len(a)), key=lambda t: (a[t][0], t))  # the stable final insertion pass
+    return [a[t][1] for t in order]
+
+
+def test_wave_parallel_std_sort_formula_matches_std_sort():
+    """The closed-form partition + stable final pass equals libstdc++ std::sort (the oracle calls
+    the real std::sort) on tie-heavy segments, the case k_features resolves wave-parallel."""
+    rng = np.random.default_rng(1)
+    for _ in range(400):
+        n = int(rng.integers(1, 400))
+        q = rng.choice([0.5, 0.1, 0.01, 1.0])
+        v = (np.round(rng.uniform(0, 5, n) / q) * q).astype(np.float32)
+        if rng.random() < 0.3:
+            v[rng.random(n) < 0.5] = 0
+        assert list(O.sort_smoothness(v)) == _wave_std_sort(v)
