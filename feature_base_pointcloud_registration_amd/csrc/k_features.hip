@@ -457,100 +457,176 @@ k_features(FeatArgs a) {
       return;
     }
     const bool has_stale = (sp <= 4 && 4 < ep);
-    // -- sort [sp, ep) by (curvature bits, position) --
-    int kpow = 1;
-    while (kpow < m) kpow <<= 1;
-    for (int t = lane; t < kpow; t += 64) {
-      uint64_t key = kPadKey;
-      if (t < m) {
-        const int pos = sp + t;
-        const float v = (pos == 4) ? st->smooth4_value : S.curv[pos - S.wlo];
-        key = ((uint64_t)__float_as_uint(v) << 16) | (uint64_t)t;
+    // Visit priority.  The greedy walks depend only on the relative priority of conflicting
+    // neighbours, and the corner cap / output order only on the order of the corner candidates,
+    // so without ties among those no sort is needed: priorities come from curvature comparisons
+    // (corner walk: ep first, then descending; surf walk: the reverse).  The stale-slot segment
+    // and segments with a relevant tie (their order is introsort's) take the sorted path.
+    float* candv = (float*)S.seg;                      // direct path: corner-visit list
+    uint16_t* candu = (uint16_t*)(candv + segcap);
+    uint16_t* vis = candu + segcap;
+    bool direct = !has_stale;
+    int C = 0;
+    if (direct) {
+      bool tf = false;
+      for (int u = lane; u <= m; u += 64) {
+        const int li = sp + u - S.wlo;
+        const int f = reach_fwd(S, li), b = reach_bwd(S, li);
+        const float vu = S.curv[li];
+        float vn[10];
+#pragma unroll
+        for (int d = 1; d <= 5; ++d) {
+          vn[4 + d] = (d <= f && u + d <= m) ? S.curv[li + d] : 0.0f;
+          vn[5 - d] = (d <= b && u - d >= 0) ? S.curv[li - d] : 0.0f;
+        }
+        uint32_t nb = 0, hc = 0;
+#pragma unroll
+        for (int d = 1; d <= 5; ++d) {
+          if (d <= f && u + d <= m) {  // u < m here
+            nb |= 1u << (4 + d);
+            const float vv = vn[4 + d];
+            if (u + d == m || vv > vu) hc |= 1u << (4 + d);
+            else if (!(vv < vu)) tf = true;
+          }
+          if (d <= b && u - d >= 0) {
+            nb |= 1u << (5 - d);
+            const float vv = vn[5 - d];
+            if (u != m) {  // ep outranks every neighbour
+              if (vv > vu) hc |= 1u << (5 - d);
+              else if (!(vv < vu)) tf = true;
+            }
+          }
+        }
+        S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
       }
-      S.keys[t] = key;
+      for (int t0 = 0; t0 <= m; t0 += 64) {  // members with curvature > edgeThreshold
+        const int u = t0 + lane;
+        const bool c = u <= m && S.edgec.get(sp + u - S.wlo);
+        const uint64_t mk = __ballot(c);
+        if (c) {
+          const int q = C + __popcll(mk & ((1ull << lane) - 1ull));
+          candu[q] = (uint16_t)u;
+          candv[q] = S.curv[sp + u - S.wlo];
+        }
+        C += __popcll(mk);
+      }
+      __syncthreads();
+      for (int c = lane; c < C; c += 64) {
+        const int u = candu[c];
+        const float vu = candv[c];
+        int rank = 0;
+        for (int c2 = 0; c2 < C; ++c2) {
+          const float v2 = candv[c2];
+          const int u2 = candu[c2];
+          if (u2 == m) rank += (u != m);
+          else if (u != m && c2 != c) {
+            if (v2 > vu) ++rank;
+            else if (!(v2 < vu)) tf = true;
+          }
+        }
+        vis[rank] = (uint16_t)u;
+      }
+      direct = !__any(tf);
+      __syncthreads();
     }
-    __syncthreads();
-    bitonic_sort_keys<QP>(S.keys, kpow, lane);
-    bool tflag = false, nflag = false;
-    for (int t = lane; t < m; t += 64) {
-      const uint32_t vb = (uint32_t)(S.keys[t] >> 16);
-      nflag |= vb > 0x7f800000u;  // NaN
-      if (t + 1 < m) tflag |= (uint32_t)(S.keys[t + 1] >> 16) == vb;
-    }
-    const bool nan = __any(nflag);
-    const bool tie = __any(tflag) || nan;
-    FBR_STAMP(2);
-    if (tie) {
-      // equal curvatures: their order is introsort's; materialise std::sort's result in S.seg
+    if (!direct) {
+      // -- sort [sp, ep) by (curvature bits, position) --
+      int kpow = 1;
+      while (kpow < m) kpow <<= 1;
+      for (int t = lane; t < kpow; t += 64) {
+        uint64_t key = kPadKey;
+        if (t < m) {
+          const int pos = sp + t;
+          const float v = (pos == 4) ? st->smooth4_value : S.curv[pos - S.wlo];
+          key = ((uint64_t)__float_as_uint(v) << 16) | (uint64_t)t;
+        }
+        S.keys[t] = key;
+      }
+      __syncthreads();
+      bitonic_sort_keys<QP>(S.keys, kpow, lane);
+      bool tflag = false, nflag = false;
       for (int t = lane; t < m; t += 64) {
-        const int pos = sp + t;
-        S.seg[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.curv[pos - S.wlo], pos};
+        const uint32_t vb = (uint32_t)(S.keys[t] >> 16);
+        nflag |= vb > 0x7f800000u;  // NaN
+        if (t + 1 < m) tflag |= (uint32_t)(S.keys[t + 1] >> 16) == vb;
       }
-      __syncthreads();
-      if (nan) {
-        if (lane == 0) std_sort_emul(S.seg, m, S.sstack);
+      const bool nan = __any(nflag);
+      const bool tie = __any(tflag) || nan;
+      FBR_STAMP(2);
+      if (tie) {
+        // equal curvatures: their order is introsort's; materialise std::sort's result in S.seg
+        for (int t = lane; t < m; t += 64) {
+          const int pos = sp + t;
+          S.seg[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.curv[pos - S.wlo], pos};
+        }
         __syncthreads();
-      } else {
-        wave_introsort_partitions(S.seg, m, S.sstack, (int*)S.cm, (int*)S.sorder, lane);
-        for (int t = lane; t < kpow; t += 64)
-          S.keys[t] = t < m ? (((uint64_t)__float_as_uint(S.seg[t].v) << 16) | (uint64_t)t) : kPadKey;
-        __syncthreads();
-        bitonic_sort_keys<QP>(S.keys, kpow, lane);  // stable sort of the partitioned array
-        SmoothEntry* tmp = (SmoothEntry*)S.cm;       // cm + sorder + rankc = 8 B per entry
-        for (int k = lane; k < m; k += 64) tmp[k] = S.seg[S.keys[k] & 0xFFFFu];
-        __syncthreads();
-        for (int k = lane; k < m; k += 64) S.seg[k] = tmp[k];
+        if (nan) {
+          if (lane == 0) std_sort_emul(S.seg, m, S.sstack);
+          __syncthreads();
+        } else {
+          wave_introsort_partitions(S.seg, m, S.sstack, (int*)S.cm, (int*)S.sorder, lane);
+          for (int t = lane; t < kpow; t += 64)
+            S.keys[t] = t < m ? (((uint64_t)__float_as_uint(S.seg[t].v) << 16) | (uint64_t)t) : kPadKey;
+          __syncthreads();
+          bitonic_sort_keys<QP>(S.keys, kpow, lane);  // stable sort of the partitioned array
+          SmoothEntry* tmp = (SmoothEntry*)S.cm;       // cm + sorder + rankc = 8 B per entry
+          for (int k = lane; k < m; k += 64) tmp[k] = S.seg[S.keys[k] & 0xFFFFu];
+          __syncthreads();
+          for (int k = lane; k < m; k += 64) S.seg[k] = tmp[k];
+          __syncthreads();
+        }
+      } else if (has_stale) {
+        for (int k = lane; k < m; k += 64) {
+          const int pos = sp + (int)(S.keys[k] & 0xFFFFu);
+          S.seg[k] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.curv[pos - S.wlo], pos};
+        }
         __syncthreads();
       }
-    } else if (has_stale) {
-      for (int k = lane; k < m; k += 64) {
-        const int pos = sp + (int)(S.keys[k] & 0xFFFFu);
-        S.seg[k] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.curv[pos - S.wlo], pos};
+      if (has_stale) {
+        if (lane == 0) {
+          S.seg[m] = SmoothEntry{S.curv[ep - S.wlo], ep};  // cloudSmoothness[ep] is never sorted (:203)
+          st->smooth4_value = S.seg[4 - sp].v;            // the entry left at position 4 is the next
+          st->smooth4_ind = S.seg[4 - sp].ind;            // scan's stale slot
+        }
+        __syncthreads();
       }
-      __syncthreads();
+      if (!has_stale) {
+        // members u in [0, m] (index sp+u): sorted order, visit ranks, conflict masks
+        for (int k = lane; k <= m; k += 64) {
+          const int u = (k == m) ? m : (tie ? S.seg[k].ind - sp : (int)(S.keys[k] & 0xFFFFu));
+          S.sorder[k] = (uint16_t)u;
+          S.rankc[u] = (uint16_t)(k == m ? 0 : m - k);  // corner visit order: ep, then descending
+        }
+        __syncthreads();
+        for (int u = lane; u <= m; u += 64) {
+          const int li = sp + u - S.wlo;
+          const int f = reach_fwd(S, li), b = reach_bwd(S, li);
+          const int ru = S.rankc[u];
+          uint32_t nb = 0, hc = 0;
+          int rn[10];
+#pragma unroll
+          for (int d = 1; d <= 5; ++d) {  // independent LDS reads, then the masks
+            rn[4 + d] = (d <= f && u + d <= m) ? (int)S.rankc[u + d] : INT_MAX;
+            rn[5 - d] = (d <= b && u - d >= 0) ? (int)S.rankc[u - d] : INT_MAX;
+          }
+#pragma unroll
+          for (int d = 1; d <= 5; ++d) {
+            if (d <= f && u + d <= m) nb |= 1u << (4 + d);
+            if (d <= b && u - d >= 0) nb |= 1u << (5 - d);
+            if (rn[4 + d] < ru) hc |= 1u << (4 + d);
+            if (rn[5 - d] < ru) hc |= 1u << (5 - d);
+          }
+          S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
+        }
+        __syncthreads();
+      }
     }
-    if (has_stale) {
-      if (lane == 0) {
-        S.seg[m] = SmoothEntry{S.curv[ep - S.wlo], ep};  // cloudSmoothness[ep] is never sorted (:203)
-        st->smooth4_value = S.seg[4 - sp].v;            // the entry left at position 4 is the next
-        st->smooth4_ind = S.seg[4 - sp].ind;            // scan's stale slot
-      }
-      __syncthreads();
-    }
+    FBR_STAMP(3);
     if (has_stale) {
       if (lane == 0) serial_walks(S, a, job, m, CL, corner_out, corner_cnt);
       corner_cnt = __shfl(corner_cnt, 0);
       __syncthreads();
     } else {
-      // -- members u in [0, m] (index sp+u): sorted order, visit ranks, conflict masks --
-      for (int k = lane; k <= m; k += 64) {
-        const int u = (k == m) ? m : (tie ? S.seg[k].ind - sp : (int)(S.keys[k] & 0xFFFFu));
-        S.sorder[k] = (uint16_t)u;
-        S.rankc[u] = (uint16_t)(k == m ? 0 : m - k);  // corner visit order: ep, then descending
-      }
-      __syncthreads();
-      for (int u = lane; u <= m; u += 64) {
-        const int li = sp + u - S.wlo;
-        const int f = reach_fwd(S, li), b = reach_bwd(S, li);
-        const int ru = S.rankc[u];
-        uint32_t nb = 0, hc = 0;
-        int rn[10];
-#pragma unroll
-        for (int d = 1; d <= 5; ++d) {  // independent LDS reads, then the masks
-          rn[4 + d] = (d <= f && u + d <= m) ? (int)S.rankc[u + d] : INT_MAX;
-          rn[5 - d] = (d <= b && u - d >= 0) ? (int)S.rankc[u - d] : INT_MAX;
-        }
-#pragma unroll
-        for (int d = 1; d <= 5; ++d) {
-          if (d <= f && u + d <= m) nb |= 1u << (4 + d);
-          if (d <= b && u - d >= 0) nb |= 1u << (5 - d);
-          if (rn[4 + d] < ru) hc |= 1u << (4 + d);
-          if (rn[5 - d] < ru) hc |= 1u << (5 - d);
-        }
-        S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
-      }
-      __syncthreads();
-      FBR_STAMP(3);
       // -- corner walk --
       uint64_t und[WMAX], tak[WMAX];
 #pragma unroll
@@ -574,29 +650,26 @@ k_features(FeatArgs a) {
         S.tmask[lane] = t;
       }
       __syncthreads();
-      int taken = 0, cutoff = m + 1;
-      for (int r0 = 0; r0 <= m && taken <= kCornerPerSeg; r0 += 64) {
+      // the first kCornerPerSeg taken corners in visit order are kept (the walk breaks there)
+      const int R = direct ? C : m + 1;
+      int taken = 0;
+      for (int r0 = 0; r0 < R && taken < kCornerPerSeg; r0 += 64) {
         const int rr = r0 + lane;
         int u = -1;
-        if (rr <= m) u = S.sorder[rr == 0 ? m : m - rr];
+        if (rr < R) u = direct ? (int)vis[rr] : (int)S.sorder[rr == 0 ? m : m - rr];
         const bool acc = u >= 0 && ((S.tmask[u >> 6] >> (u & 63)) & 1ull);
         const uint64_t mk = __ballot(acc);
         const int pos = taken + __popcll(mk & ((1ull << lane) - 1ull));
-        if (acc && pos < kCornerPerSeg) corner_out[corner_cnt + pos] = CL[sp + u];
-        int cut = (acc && pos == kCornerPerSeg) ? rr : (m + 1);
-        for (int o = 32; o > 0; o >>= 1) cut = min(cut, __shfl_xor(cut, o));
-        cutoff = min(cutoff, cut);
-        taken += __popcll(mk);
-      }
-      corner_cnt += min(taken, kCornerPerSeg);
-      for (int u = lane; u <= m; u += 64) {
-        if (((S.tmask[u >> 6] >> (u & 63)) & 1ull) && S.rankc[u] < cutoff) {
+        if (acc && pos < kCornerPerSeg) {
+          corner_out[corner_cnt + pos] = CL[sp + u];
           const int li = sp + u - S.wlo;
           const uint32_t c = S.cm[u];
           atomicOr((unsigned long long*)&S.labpos.w[li >> 6], 1ull << (li & 63));
           or_range(S.picked, li - (int)((c >> 24) & 15u), li + (int)((c >> 20) & 15u));
         }
+        taken += __popcll(mk);
       }
+      corner_cnt += min(taken, kCornerPerSeg);
       __syncthreads();
       FBR_STAMP(5);
       // -- surf walk: ascending, ep last -> higher priority = not higher corner priority --
