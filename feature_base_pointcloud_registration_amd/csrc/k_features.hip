@@ -86,6 +86,13 @@ __device__ __forceinline__ int reach_bwd(const FeatLds& S, int li) {
   return __builtin_clzll(x | (1ull << 58));        // capped at 5
 }
 
+// Bits [off, off+64) of the 192-bit value w0 | w1 << 64 | w2 << 128 (0 <= off < 128).
+__device__ __forceinline__ uint64_t win64(uint64_t w0, uint64_t w1, uint64_t w2, int off) {
+  if (off < 64) return off ? ((w0 >> off) | (w1 << (64 - off))) : w0;
+  off -= 64;
+  return off ? ((w1 >> off) | (w2 << (64 - off))) : w1;
+}
+
 // Mark cloudNeighborPicked over [li-bwd, li+fwd] (the suppression loops :227-240 / :259-274).
 __device__ __forceinline__ void or_range(const Bits& b, int lo, int hi) {
   const int w0 = lo >> 6, w1 = hi >> 6;
@@ -458,78 +465,11 @@ k_features(FeatArgs a) {
     }
     const bool has_stale = (sp <= 4 && 4 < ep);
     // Visit priority.  The greedy walks depend only on the relative priority of conflicting
-    // neighbours, and the corner cap / output order only on the order of the corner candidates,
-    // so without ties among those no sort is needed: priorities come from curvature comparisons
+    // neighbours, and the corner cap / output order only on the order of the taken corners, so
+    // without ties among those no sort is needed: priorities come from curvature comparisons
     // (corner walk: ep first, then descending; surf walk: the reverse).  The stale-slot segment
     // and segments with a relevant tie (their order is introsort's) take the sorted path.
-    float* candv = (float*)S.seg;                      // direct path: corner-visit list
-    uint16_t* candu = (uint16_t*)(candv + segcap);
-    uint16_t* vis = candu + segcap;
-    bool direct = !has_stale;
-    int C = 0;
-    if (direct) {
-      bool tf = false;
-      for (int u = lane; u <= m; u += 64) {
-        const int li = sp + u - S.wlo;
-        const int f = reach_fwd(S, li), b = reach_bwd(S, li);
-        const float vu = S.curv[li];
-        float vn[10];
-#pragma unroll
-        for (int d = 1; d <= 5; ++d) {
-          vn[4 + d] = (d <= f && u + d <= m) ? S.curv[li + d] : 0.0f;
-          vn[5 - d] = (d <= b && u - d >= 0) ? S.curv[li - d] : 0.0f;
-        }
-        uint32_t nb = 0, hc = 0;
-#pragma unroll
-        for (int d = 1; d <= 5; ++d) {
-          if (d <= f && u + d <= m) {  // u < m here
-            nb |= 1u << (4 + d);
-            const float vv = vn[4 + d];
-            if (u + d == m || vv > vu) hc |= 1u << (4 + d);
-            else if (!(vv < vu)) tf = true;
-          }
-          if (d <= b && u - d >= 0) {
-            nb |= 1u << (5 - d);
-            const float vv = vn[5 - d];
-            if (u != m) {  // ep outranks every neighbour
-              if (vv > vu) hc |= 1u << (5 - d);
-              else if (!(vv < vu)) tf = true;
-            }
-          }
-        }
-        S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
-      }
-      for (int t0 = 0; t0 <= m; t0 += 64) {  // members with curvature > edgeThreshold
-        const int u = t0 + lane;
-        const bool c = u <= m && S.edgec.get(sp + u - S.wlo);
-        const uint64_t mk = __ballot(c);
-        if (c) {
-          const int q = C + __popcll(mk & ((1ull << lane) - 1ull));
-          candu[q] = (uint16_t)u;
-          candv[q] = S.curv[sp + u - S.wlo];
-        }
-        C += __popcll(mk);
-      }
-      __syncthreads();
-      for (int c = lane; c < C; c += 64) {
-        const int u = candu[c];
-        const float vu = candv[c];
-        int rank = 0;
-        for (int c2 = 0; c2 < C; ++c2) {
-          const float v2 = candv[c2];
-          const int u2 = candu[c2];
-          if (u2 == m) rank += (u != m);
-          else if (u != m && c2 != c) {
-            if (v2 > vu) ++rank;
-            else if (!(v2 < vu)) tf = true;
-          }
-        }
-        vis[rank] = (uint16_t)u;
-      }
-      direct = !__any(tf);
-      __syncthreads();
-    }
-    if (!direct) {
+    auto sorted_order = [&]() __attribute__((always_inline)) {
       // -- sort [sp, ep) by (curvature bits, position) --
       int kpow = 1;
       while (kpow < m) kpow <<= 1;
@@ -620,7 +560,56 @@ k_features(FeatArgs a) {
         }
         __syncthreads();
       }
+    };
+    float* tlv = (float*)S.seg;                        // direct path: taken corners (value, member)
+    uint16_t* tlu = (uint16_t*)(tlv + segcap);
+    uint16_t* vis = tlu + segcap;                      // taken corners in visit order
+    bool direct = !has_stale;
+    if (direct) {
+      bool tf = false;
+      for (int k0 = 0; k0 <= m; k0 += 64) {
+        const int u = k0 + lane;
+        const int li0 = sp - S.wlo + k0, W0 = li0 >> 6;  // li0 >= 0
+        const uint64_t gm1 = W0 >= 1 ? S.gap.w[W0 - 1] : ~0ull;  // wave-uniform words
+        const uint64_t g0 = W0 < S.nw ? S.gap.w[W0] : 0ull;
+        const uint64_t g1 = W0 + 1 < S.nw ? S.gap.w[W0 + 1] : 0ull;
+        const uint64_t g2 = W0 + 2 < S.nw ? S.gap.w[W0 + 2] : 0ull;
+        const int off = (li0 & 63) + lane;
+        const uint64_t fw = win64(g0, g1, g2, off);   // bit d = gap at li+d
+        const uint64_t bw = win64(gm1, g0, g1, off);  // bit 63-d = gap at li-1-d
+        if (u <= m) {
+          const int li = li0 + lane;
+          const int f = __builtin_ctzll(fw | 0x20ull), b = __builtin_clzll(bw | (1ull << 58));
+          float cv[11];
+#pragma unroll
+          for (int d = 0; d < 11; ++d) cv[d] = S.curv[min(max(li + d - 5, 0), Lcap - 1)];
+          const float vu = cv[5];
+          uint32_t nb = 0, hc = 0;
+#pragma unroll
+          for (int d = 1; d <= 5; ++d) {
+            if (d <= f && u + d <= m) {  // u < m here
+              nb |= 1u << (4 + d);
+              const float vv = cv[5 + d];
+              if (u + d == m || vv > vu) hc |= 1u << (4 + d);
+              else if (!(vv < vu)) tf = true;
+            }
+            if (d <= b && u - d >= 0) {
+              nb |= 1u << (5 - d);
+              const float vv = cv[5 - d];
+              if (u != m) {  // ep outranks every neighbour
+                if (vv > vu) hc |= 1u << (5 - d);
+                else if (!(vv < vu)) tf = true;
+              }
+            }
+          }
+          S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
+        }
+      }
+      direct = !__any(tf);
+      __syncthreads();
+      FBR_STAMP(10);
     }
+    if (!direct) sorted_order();
     FBR_STAMP(3);
     if (has_stale) {
       if (lane == 0) serial_walks(S, a, job, m, CL, corner_out, corner_cnt);
@@ -629,19 +618,60 @@ k_features(FeatArgs a) {
     } else {
       // -- corner walk --
       uint64_t und[WMAX], tak[WMAX];
+      auto corner_walk = [&]() __attribute__((always_inline)) {
 #pragma unroll
-      for (int w = 0; w < WMAX; ++w) {
-        const int u = 64 * w + lane;
-        bool cand = false;
-        if (u <= m) {
-          const int li = sp + u - S.wlo;
-          cand = !S.picked.get(li) && S.edgec.get(li);
+        for (int w = 0; w < WMAX; ++w) {
+          const int u = 64 * w + lane;
+          bool cand = false;
+          if (u <= m) {
+            const int li = sp + u - S.wlo;
+            cand = !S.picked.get(li) && S.edgec.get(li);
+          }
+          und[w] = __ballot(cand);
+          tak[w] = 0ull;
         }
-        und[w] = __ballot(cand);
-        tak[w] = 0ull;
-      }
-      greedy_rounds(m, lane, und, tak, [&](int u) { return S.cm[u] & 1023u; }, a, job);
+        greedy_rounds(m, lane, und, tak, [&](int u) { return S.cm[u] & 1023u; }, a, job);
+      };
+      corner_walk();
       FBR_STAMP(4);
+      int T = 0;
+      if (direct) {  // visit order of the taken corners: ep first, then descending curvature
+#pragma unroll
+        for (int w = 0; w < WMAX; ++w) {
+          if ((tak[w] >> lane) & 1ull) {
+            const int q = T + __popcll(tak[w] & ((1ull << lane) - 1ull));
+            const int u = 64 * w + lane;
+            tlu[q] = (uint16_t)u;
+            tlv[q] = S.curv[sp + u - S.wlo];
+          }
+          T += __popcll(tak[w]);
+        }
+        __syncthreads();
+        bool tf = false;
+        for (int c = lane; c < T; c += 64) {
+          const int u = tlu[c];
+          const float vu = tlv[c];
+          int rank = 0;
+          for (int c2 = 0; c2 < T; ++c2) {
+            const int u2 = tlu[c2];
+            const float v2 = tlv[c2];
+            if (u2 == m) rank += (u != m);
+            else if (u != m && c2 != c) {
+              if (v2 > vu) ++rank;
+              else if (!(v2 < vu)) tf = true;
+            }
+          }
+          vis[rank] = (uint16_t)u;
+        }
+        if (__any(tf)) {  // tied taken corners: their order is introsort's
+          direct = false;
+          __syncthreads();
+          sorted_order();
+          corner_walk();
+        }
+        __syncthreads();
+        FBR_STAMP(11);
+      }
       if (lane < WMAX) {
         uint64_t t = 0;
 #pragma unroll
@@ -651,7 +681,7 @@ k_features(FeatArgs a) {
       }
       __syncthreads();
       // the first kCornerPerSeg taken corners in visit order are kept (the walk breaks there)
-      const int R = direct ? C : m + 1;
+      const int R = direct ? T : m + 1;
       int taken = 0;
       for (int r0 = 0; r0 < R && taken < kCornerPerSeg; r0 += 64) {
         const int rr = r0 + lane;

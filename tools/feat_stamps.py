@@ -30,7 +30,7 @@ ctx.batch_launch(); ctx.batch_wait()
 out = np.zeros((B * H, 12), np.uint64)
 L.fbr_diag_feature_stamps(ctx._h, out.ctypes.data)
 names = ["load", "flags+picked", "seg: sort", "seg: members/cm", "seg: corner rounds", "seg: cap+apply",
-         "seg: surf rounds", "seg: apply surf", "seg: candidates", "outputs", "-", "-"]
+         "seg: surf rounds", "seg: apply surf", "seg: candidates", "outputs", "seg: direct cm", "seg: direct rank"]
 tot = out.astype(np.float64).mean(0)
 print("mean cycles per ring (s_memtime ticks):", int(tot.sum()))
 for n, v in zip(names, tot):
