@@ -81,8 +81,8 @@ struct fbr_ctx {
   int32_t* d_err = nullptr;
   float4 *d_corner_all = nullptr, *d_surf_all = nullptr, *d_cornerDS = nullptr, *d_surfDS = nullptr;
   int32_t *d_ncorner = nullptr, *d_nsurf = nullptr, *d_ncds = nullptr, *d_nsds = nullptr;
-  uint32_t *d_vg_scratch = nullptr, *d_vg_hist = nullptr;
-  int64_t vg_scratch_elems = 0, vg_hist_elems = 0;
+  uint32_t* d_vg_scratch = nullptr;
+  int64_t vg_scratch_elems = 0;
   // registration
   GnState* d_gn = nullptr;
   int4* d_items = nullptr;
@@ -229,10 +229,9 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
   if (n > INT32_MAX / 4) return FBR_ERR_CAPACITY;
   float4 *d_in = nullptr, *d_out = nullptr;
   int32_t* d_cnt = nullptr;
-  uint32_t *d_sc = nullptr, *d_h = nullptr;
-  const int64_t hs = ((n + 255) / 256) * 256;
+  uint32_t* d_sc = nullptr;
   int rc = FBR_OK;
-  if (dalloc(&d_in, n) || dalloc(&d_out, n) || dalloc(&d_cnt, 2) || dalloc(&d_sc, 4 * n) || dalloc(&d_h, hs)) {
+  if (dalloc(&d_in, n) || dalloc(&d_out, n) || dalloc(&d_cnt, 2) || dalloc(&d_sc, 4 * n)) {
     rc = FBR_ERR_HIP;
   } else {
     int32_t nn = (int32_t)n;
@@ -241,17 +240,16 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
       rc = FBR_ERR_HIP;
     } else {
       VgArgs a{};
-      a.in = d_in;
-      a.stride_in = n;
-      a.cnt_in = d_cnt;
-      a.out = d_out;
-      a.stride_out = n;
-      a.cnt_out = d_cnt + 1;
-      a.scratch = d_sc;
-      a.hist = d_h;
-      a.hist_stride = hs;
-      a.leaf = leaf;
-      a.nseg = 1;
+      a.s[0].in = d_in;
+      a.s[0].stride_in = n;
+      a.s[0].cnt_in = d_cnt;
+      a.s[0].cap = n;
+      a.s[0].out = d_out;
+      a.s[0].stride_out = n;
+      a.s[0].cnt_out = d_cnt + 1;
+      a.s[0].scratch = d_sc;
+      a.s[0].leaf = leaf;
+      a.s[0].nseg = 1;
       launch_voxel_grid(c->stream, a);
       int32_t nout = 0;
       if (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
@@ -268,7 +266,6 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
   (void)hipFree(d_out);
   (void)hipFree(d_cnt);
   (void)hipFree(d_sc);
-  (void)hipFree(d_h);
   return rc;
 }
 
@@ -321,17 +318,16 @@ int stage_features(fbr_ctx* c, int B, bool stream_mode) {
   CK(hipMemsetAsync(c->d_err, 0, sizeof(int32_t) * B, c->stream));
   TIMED(c, "features", launch_features(c->stream, a));
   VgArgs v{};
-  v.in = c->d_cand;
-  v.stride_in = c->W;
-  v.cnt_in = c->d_cand_cnt;
-  v.out = c->d_surf_ring;
-  v.stride_out = c->W;
-  v.cnt_out = c->d_surf_ring_cnt;
-  v.scratch = c->d_vg_scratch;
-  v.hist = c->d_vg_hist;
-  v.hist_stride = ((c->W + 255) / 256) * 256;
-  v.leaf = c->P.odometry_surf_leaf_size;
-  v.nseg = B * c->H;
+  v.s[0].in = c->d_cand;
+  v.s[0].stride_in = c->W;
+  v.s[0].cnt_in = c->d_cand_cnt;
+  v.s[0].cap = c->W;
+  v.s[0].out = c->d_surf_ring;
+  v.s[0].stride_out = c->W;
+  v.s[0].cnt_out = c->d_surf_ring_cnt;
+  v.s[0].scratch = c->d_vg_scratch;
+  v.s[0].leaf = c->P.odometry_surf_leaf_size;
+  v.s[0].nseg = B * c->H;
   TIMED(c, "voxel_ring", launch_voxel_grid(c->stream, v));
   TIMED(c, "concat", launch_concat(c->stream, B, c->H, c->W, c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring,
                                    c->d_surf_ring_cnt, c->d_corner_all, c->HW, c->d_ncorner, c->d_surf_all, c->HW,
@@ -374,25 +370,14 @@ GnArgs gn_args(fbr_ctx* c, int B, bool trace) {
 // Registration of the clouds in d_corner_all / d_surf_all (counts d_ncorner / d_nsurf) from d_guess.
 int stage_register(fbr_ctx* c, int B, bool trace) {
   if (!c->has_map) return FBR_ERR_NO_MAP;
+  // downsampleCurrentScan (mapOptmization.h:981-993): corner and surf filters in one launch;
+  // Morton voxel order (internal clouds: spatially compact query order for the kNN waves)
   VgArgs v{};
-  v.scratch = c->d_vg_scratch;
-  v.hist = c->d_vg_hist;
-  v.hist_stride = ((c->HW + 255) / 256) * 256;
-  v.nseg = B;
-  v.in = c->d_corner_all;
-  v.stride_in = c->HW;
-  v.cnt_in = c->d_ncorner;
-  v.out = c->d_cornerDS;
-  v.stride_out = c->HW;
-  v.cnt_out = c->d_ncds;
-  v.leaf = c->P.mapping_corner_leaf_size;
-  v.morton = 1;  // internal clouds: spatially compact query order for the kNN waves
-  TIMED(c, "voxel_scan", launch_voxel_grid(c->stream, v));
-  v.in = c->d_surf_all;
-  v.cnt_in = c->d_nsurf;
-  v.out = c->d_surfDS;
-  v.cnt_out = c->d_nsds;
-  v.leaf = c->P.mapping_surf_leaf_size;
+  const int64_t ccap = std::min<int64_t>(c->HW, (int64_t)kCornerPerRing * c->H);
+  v.s[0] = VgSet{c->d_surf_all, c->HW, c->d_nsurf, c->HW, c->d_surfDS, c->HW, c->d_nsds, c->d_vg_scratch,
+                 c->P.mapping_surf_leaf_size, B, 1};
+  v.s[1] = VgSet{c->d_corner_all, c->HW, c->d_ncorner, ccap, c->d_cornerDS, c->HW, c->d_ncds,
+                 c->d_vg_scratch + (int64_t)B * 4 * c->HW, c->P.mapping_corner_leaf_size, B, 1};
   TIMED(c, "voxel_scan", launch_voxel_grid(c->stream, v));
   GnArgs a = gn_args(c, B, trace);
   if (trace) CK(hipMemsetAsync(c->d_trace, 0, sizeof(float) * B * c->P.max_iterations * 6, c->stream));
@@ -562,8 +547,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
     return FBR_ERR_HIP;
   }
   c->max_items = (int)(B * 2 * ((HW + 255) / 256 + 1));
-  c->vg_scratch_elems = 4 * B * HW;
-  c->vg_hist_elems = B * std::max<int64_t>(((HW + 255) / 256) * 256, H * (((c->W + 255) / 256) * 256));
+  c->vg_scratch_elems = 4 * B * (HW + std::min<int64_t>(HW, (int64_t)kCornerPerRing * H));
   bool fail = dalloc(&c->d_pts, B * c->NMAX) || dalloc(&c->d_nin, B) || dalloc(&c->d_guess, B * 6) ||
               dalloc(&c->d_owner, B * HW) || dalloc(&c->d_rowcnt, B * H) || dalloc(&c->d_col, B * HW) ||
               dalloc(&c->d_start, B * H) || dalloc(&c->d_end, B * H) || dalloc(&c->d_nvalid, B) ||
@@ -574,7 +558,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_surf_ring_cnt, B * H) || dalloc(&c->d_err, B) || dalloc(&c->d_corner_all, B * HW) ||
               dalloc(&c->d_surf_all, B * HW) || dalloc(&c->d_cornerDS, B * HW) || dalloc(&c->d_surfDS, B * HW) ||
               dalloc(&c->d_ncorner, B) || dalloc(&c->d_nsurf, B) || dalloc(&c->d_ncds, B) || dalloc(&c->d_nsds, B) ||
-              dalloc(&c->d_vg_scratch, c->vg_scratch_elems) || dalloc(&c->d_vg_hist, c->vg_hist_elems) ||
+              dalloc(&c->d_vg_scratch, c->vg_scratch_elems) ||
               dalloc(&c->d_gn, B) || dalloc(&c->d_items, c->max_items) || dalloc(&c->d_nitems, 1) ||
               dalloc(&c->d_item_range, 2 * B) || dalloc(&c->d_cropcnt, 2 * B) ||
               dalloc(&c->d_partial, (int64_t)c->max_items * 32) ||
@@ -606,7 +590,7 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_nvalid, c->d_cloud, c->d_range, c->d_sstate, c->d_sstream, c->d_label, c->d_label_stream,
                   c->d_corner_slot, c->d_corner_cnt, c->d_cand, c->d_cand_cnt, c->d_surf_ring, c->d_surf_ring_cnt,
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
-                  c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_vg_hist, c->d_gn, c->d_items, c->d_nitems,
+                  c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_map_c,
                   c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr};
   for (void* p : ptrs)

@@ -41,20 +41,23 @@ size_t features_lds_bytes(const FeatArgs& a);
 void launch_features(hipStream_t s, const FeatArgs& a);
 
 // ---- A9 VoxelGrid over segments (k_voxel.hip) ----
-struct VgArgs {
+struct VgSet {               // nseg segments of one cloud family, one leaf size
   const float4* in;
-  int64_t stride_in;
-  const int32_t* cnt_in;  // per-segment input counts
+  int64_t stride_in;         // input segment stride (points)
+  const int32_t* cnt_in;     // per-segment input counts
+  int64_t cap;               // max points per segment (counts are clamped to it)
   float4* out;
   int64_t stride_out;
   int32_t* cnt_out;
-  uint32_t* scratch;      // [nseg][4][stride_in]
-  uint32_t* hist;         // [nseg][hist_stride]
-  int64_t hist_stride;    // >= ceil(stride_in/256)*256
+  uint32_t* scratch;         // global mode: [nseg][4][cap]
   float leaf;
   int nseg;
-  int morton;             // 1: emit voxels in Morton order of (i,j,k) instead of PCL key order
+  int morton;                // 1: emit voxels in Morton order of (i,j,k) instead of PCL key order
 };
+struct VgArgs {
+  VgSet s[2];                // segments of set 0, then of set 1 (set 1 may be empty)
+};
+constexpr int64_t kVgLdsCap = 4096;  // segments up to this size sort entirely in LDS
 void launch_voxel_grid(hipStream_t s, const VgArgs& a);
 
 // Concatenate per-ring corner slots / per-ring surf DS outputs into per-job clouds (the

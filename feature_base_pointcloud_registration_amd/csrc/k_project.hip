@@ -19,7 +19,7 @@
 
 namespace fbr {
 
-__device__ __forceinline__ bool project_point(const fbr_point_xyzirt& q, int H, int W, int& cell) {
+__device__ __forceinline__ bool project_point(const fbr_point_xyzirt& q, int H, int W, int& row, int& colo) {
   int rowIdn = q.ring;
   if (rowIdn < 0 || rowIdn >= H) return false;
   float horizonAngle = (float)((double)(fd_atan2f(q.x, q.y) * 180.0f) / M_PI);
@@ -29,21 +29,78 @@ __device__ __forceinline__ bool project_point(const fbr_point_xyzirt& q, int H, 
   if (columnIdn < 0 || columnIdn >= W) return false;
   float range = sqrt_rn(q.x * q.x + q.y * q.y + q.z * q.z);
   if (range < 1.0f) return false;
-  cell = rowIdn * W + columnIdn;
+  row = rowIdn;
+  colo = columnIdn;
   return true;
 }
 
-__global__ void k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ nin,
-                          int64_t nmax, int H, int W, int32_t* __restrict__ owner) {
-  const int job = blockIdx.y;
+// K1: a 256-thread block owns a chunk of kProjChunk consecutive input points of one job.  In the
+// sensor's firing order the chunk covers ~kProjChunk/H columns of every ring, so cells are first
+// claimed in an LDS tile [H][tile_cols] (LDS atomicMin on the input index), then the tile's claimed
+// cells are merged into the global owner image with row-contiguous atomicMin (consecutive lanes ->
+// consecutive cells: a wave's atomics leave L2 as 4 line requests instead of 64 scattered ones).
+// min is associative, so the result is the global first-wins claim for any input order; chunks
+// whose column span exceeds the tile (the 0/W seam, shuffled input) claim directly in global.
+constexpr int kProjThreads = 256, kProjPPT = 8, kProjChunk = kProjThreads * kProjPPT;
+
+__global__ void __launch_bounds__(kProjThreads)
+k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ nin, int64_t nmax, int H, int W,
+          int tile_log2, int32_t* __restrict__ owner) {
+  extern __shared__ int32_t tile[];  // [H][1 << tile_log2]
+  __shared__ int red[2][kProjThreads / 64];
+  const int job = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tcols = 1 << tile_log2, tcells = H << tile_log2;
   const int64_t n = nin[job];
   const fbr_point_xyzirt* P = pts + (int64_t)job * nmax;
   int32_t* O = owner + (int64_t)job * H * W;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    fbr_point_xyzirt q = P[i];
-    int cell;
-    if (project_point(q, H, W, cell)) atomicMin(&O[cell], (int32_t)i);
+  for (int64_t base = (int64_t)blockIdx.x * kProjChunk; base < n; base += (int64_t)gridDim.x * kProjChunk) {
+    int rowk[kProjPPT], colk[kProjPPT];
+    int cmin = INT_MAX, cmax = -1;
+#pragma unroll
+    for (int k = 0; k < kProjPPT; ++k) {
+      const int64_t i = base + k * kProjThreads + tid;
+      rowk[k] = -1;
+      colk[k] = 0;
+      if (i < n && project_point(P[i], H, W, rowk[k], colk[k])) {
+        cmin = min(cmin, colk[k]);
+        cmax = max(cmax, colk[k]);
+      } else {
+        rowk[k] = -1;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      cmin = min(cmin, __shfl_xor(cmin, o));
+      cmax = max(cmax, __shfl_xor(cmax, o));
+    }
+    if (lane == 0) {
+      red[0][wv] = cmin;
+      red[1][wv] = cmax;
+    }
+    __syncthreads();
+    cmin = red[0][0];
+    cmax = red[1][0];
+    for (int w = 1; w < kProjThreads / 64; ++w) {
+      cmin = min(cmin, red[0][w]);
+      cmax = max(cmax, red[1][w]);
+    }
+    if (cmax >= 0 && cmax - cmin < tcols) {
+      for (int e = tid; e < tcells; e += kProjThreads) tile[e] = kEmptyOwner;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < kProjPPT; ++k)
+        if (rowk[k] >= 0)
+          atomicMin(&tile[(rowk[k] << tile_log2) + (colk[k] - cmin)], (int32_t)(base + k * kProjThreads + tid));
+      __syncthreads();
+      for (int e = tid; e < tcells; e += kProjThreads) {
+        const int32_t v = tile[e];
+        if (v != kEmptyOwner) atomicMin(&O[(e >> tile_log2) * W + cmin + (e & (tcols - 1))], v);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kProjPPT; ++k)
+        if (rowk[k] >= 0) atomicMin(&O[rowk[k] * W + colk[k]], (int32_t)(base + k * kProjThreads + tid));
+    }
+    __syncthreads();
   }
 }
 
@@ -57,11 +114,17 @@ __global__ void k_rowcount(const int32_t* __restrict__ owner, int H, int W, int3
   if (lane == 0) rowcnt[job * H + row] = cnt;
 }
 
+// Blocks are dealt round-robin over the 8 XCDs (b, b+8, ... share one); the (job, row) mapping
+// keeps every row of a job on one XCD so the owner gathers of the job's raw points hit that
+// XCD's L2 (speed only: correctness never depends on placement).
 __global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, const int32_t* __restrict__ owner,
-                          const int32_t* __restrict__ rowcnt, int H, int W, float4* __restrict__ cloud,
+                          const int32_t* __restrict__ rowcnt, int B, int H, int W, float4* __restrict__ cloud,
                           int32_t* __restrict__ col, float* __restrict__ range, int32_t* __restrict__ start_ring,
                           int32_t* __restrict__ end_ring, int32_t* __restrict__ nvalid) {
-  const int row = blockIdx.x, job = blockIdx.y, lane = threadIdx.x;
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int g = b / (8 * H), x = b % 8;  // job group of 8, XCD slot
+  const int job = g * 8 + x, row = (b / 8) % H;
+  if (job >= B) return;
   const int64_t HW = (int64_t)H * W;
   const int32_t* RC = rowcnt + job * H;
   int off = 0;
@@ -97,18 +160,22 @@ __global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax
 
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
                     int W, int32_t* owner) {
-  int blocks = (int)((nmax + 255) / 256);
-  if (blocks > 512) blocks = 512;
+  int blocks = (int)((nmax + kProjChunk - 1) / kProjChunk);
+  if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_project, dim3(blocks, B), dim3(256), 0, s, pts, nin, nmax, H, W, owner);
+  int tile_log2 = 6;  // 64 columns, shrunk so the tile stays <= 32 KB
+  while (tile_log2 > 3 && ((int64_t)H << tile_log2) > 8192) --tile_log2;
+  const size_t lds = sizeof(int32_t) * ((size_t)H << tile_log2);
+  hipLaunchKernelGGL(k_project, dim3(blocks, B), dim3(kProjThreads), lds, s, pts, nin, nmax, H, W, tile_log2, owner);
 }
 
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,
                     int W, int32_t* rowcnt, float4* cloud, int32_t* col, float* range, int32_t* start_ring,
                     int32_t* end_ring, int32_t* nvalid) {
   hipLaunchKernelGGL(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, rowcnt);
-  hipLaunchKernelGGL(k_compact, dim3(H, B), dim3(64), 0, s, pts, nmax, owner, rowcnt, H, W, cloud, col, range,
-                     start_ring, end_ring, nvalid);
+  const int groups = (B + 7) / 8;
+  hipLaunchKernelGGL(k_compact, dim3(groups * 8 * H), dim3(64), 0, s, pts, nmax, owner, rowcnt, B, H, W, cloud, col,
+                     range, start_ring, end_ring, nvalid);
 }
 
 }  // namespace fbr

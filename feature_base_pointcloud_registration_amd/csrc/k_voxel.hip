@@ -23,15 +23,18 @@
 #include "fbr_common.h"
 #include "fbr_kernels.h"
 
+#include <algorithm>
+
 namespace fbr {
 
-namespace {
-constexpr int kVgThreads = 256;
-constexpr int kVgWaves = kVgThreads / 64;
-}  // namespace
+// Stable LSD radix sort of one segment by one workgroup of T threads ("wave chunks"): wave w owns
+// the contiguous chunk [c0, c1) of the (key, index) array; per pass each wave builds an LDS digit
+// histogram of its chunk, one digit-major / wave-minor exclusive scan gives every (digit, wave)
+// its output base, and each wave scatters its chunk in index order (8..9 ballots give each lane
+// its rank among equal digits in the 64-element step).  Waves in chunk order and steps in index
+// order make the sort stable.  Keys and indices live in LDS when the segment fits (per-ring
+// filters, u16 indices), otherwise in a per-segment global scratch (mapping DS, 1024 threads).
 
-// Block-wide stable LSD radix sort of n (key, val) pairs.  Returns the buffer index (0 or 1)
-// holding the result.  Must be called by all 256 threads.
 __device__ __forceinline__ uint32_t spread3_10(uint32_t v) {  // 10 bits -> every third bit
   v &= 0x3FFu;
   v = (v | (v << 16)) & 0x030000FFu;
@@ -41,130 +44,99 @@ __device__ __forceinline__ uint32_t spread3_10(uint32_t v) {  // 10 bits -> ever
   return v;
 }
 
-__device__ int block_radix_sort(uint32_t* k[2], uint32_t* v[2], uint32_t* hist, int n, int nbits,
-                                uint32_t* lds_hist /*[256]*/, uint32_t* lds_wc /*[kVgWaves][256]*/,
-                                uint32_t* lds_tot /*[256]*/) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntiles = (n + kVgThreads - 1) / kVgThreads;
-  const int passes = (nbits + 7) / 8;
-  int cur = 0;
-  for (int pass = 0; pass < passes; ++pass) {
-    const int shift = 8 * pass;
-    const uint32_t* kin = k[cur];
-    const uint32_t* vin = v[cur];
-    uint32_t* kout = k[cur ^ 1];
-    uint32_t* vout = v[cur ^ 1];
-    // 1) per-tile digit histograms
-    for (int t = 0; t < ntiles; ++t) {
-      lds_hist[tid] = 0;
-      __syncthreads();
-      const int i = t * kVgThreads + tid;
-      if (i < n) atomicAdd(&lds_hist[(kin[i] >> shift) & 255u], 1u);
-      __syncthreads();
-      hist[t * 256 + tid] = lds_hist[tid];
-      __syncthreads();
-    }
-    // 2) exclusive scan in digit-major, tile-minor order
-    uint32_t run = 0;
-    for (int t = 0; t < ntiles; ++t) {
-      const uint32_t c = hist[t * 256 + tid];
-      hist[t * 256 + tid] = run;
-      run += c;
-    }
-    lds_tot[tid] = run;
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t acc = 0;
-      for (int d = 0; d < 256; ++d) {
-        const uint32_t c = lds_tot[d];
-        lds_tot[d] = acc;
-        acc += c;
-      }
-    }
-    __syncthreads();
-    const uint32_t base = lds_tot[tid];
-    for (int t = 0; t < ntiles; ++t) hist[t * 256 + tid] += base;
-    __syncthreads();
-    // 3) stable scatter
-    for (int t = 0; t < ntiles; ++t) {
-      for (int w = 0; w < kVgWaves; ++w) lds_wc[w * 256 + tid] = 0;
-      __syncthreads();
-      const int i = t * kVgThreads + tid;
-      const bool valid = i < n;
-      const uint32_t key = valid ? kin[i] : 0u;
-      const uint32_t d = (key >> shift) & 255u;
-      uint64_t peers = __ballot(valid);
-      for (int b = 0; b < 8; ++b) {
-        const uint64_t bal = __ballot((d >> b) & 1u);
-        peers &= ((d >> b) & 1u) ? bal : ~bal;
-      }
-      const int rank = __popcll(peers & ((1ull << lane) - 1ull));
-      if (valid && rank == 0) lds_wc[wave * 256 + d] = (uint32_t)__popcll(peers);
-      __syncthreads();
-      if (valid) {
-        uint32_t off = hist[t * 256 + d] + rank;
-        for (int w = 0; w < wave; ++w) off += lds_wc[w * 256 + d];
-        kout[off] = key;
-        vout[off] = vin[i];
-      }
-      __syncthreads();
-    }
-    cur ^= 1;
-    __syncthreads();
+// Exclusive scan of nb (<= 512) LDS counters in place by a T-thread workgroup; returns nothing,
+// `wsum` is [T/64] scratch.  Must be called by all threads.
+template <int T>
+__device__ void block_exclusive_scan(uint32_t* arr, int nb, uint32_t* wsum) {
+  constexpr int PER = (512 + T - 1) / T;  // bins per thread (consecutive)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t v[PER], loc = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int b = tid * PER + k;
+    v[k] = b < nb ? arr[b] : 0u;
+    loc += v[k];
   }
-  return cur;
+  uint32_t inc = loc;  // inclusive wave scan of per-thread sums
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int ww = 0; ww < w; ++ww) base += wsum[ww];
+  uint32_t run = base + inc - loc;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int b = tid * PER + k;
+    if (b < nb) arr[b] = run;
+    run += v[k];
+  }
+  __syncthreads();
 }
 
-__global__ void __launch_bounds__(kVgThreads)
-k_voxel_grid(VgArgs a) {
-  __shared__ float red[6][kVgThreads];
-  __shared__ uint32_t lds_hist[256];
-  __shared__ uint32_t lds_wc[kVgWaves * 256];
-  __shared__ uint32_t lds_tot[256];
-  __shared__ int64_t sh_info[8];
-  const int seg = blockIdx.x, tid = threadIdx.x;
-  const int n = (int)min((int64_t)a.cnt_in[seg], a.stride_in);
-  const float4* in = a.in + (int64_t)seg * a.stride_in;
-  float4* out = a.out + (int64_t)seg * a.stride_out;
+template <int T, typename V, bool LDS>
+__global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
+  constexpr int NW = T / 64;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int seg = blockIdx.x;
+  const bool second = seg >= A.s[0].nseg;
+  const VgSet S = second ? A.s[1] : A.s[0];
+  if (second) seg -= A.s[0].nseg;
+  uint32_t* hist = (uint32_t*)smem;  // [NW + 1][512]: per-wave digit counters + digit totals
+  uint32_t* wsum = hist + (NW + 1) * 512;
+  float* mm = (float*)(wsum + NW);
+  int* misc = (int*)(mm + NW * 6);
+  const int n = (int)min((int64_t)S.cnt_in[seg], S.cap);
+  const float4* in = S.in + (int64_t)seg * S.stride_in;
+  float4* out = S.out + (int64_t)seg * S.stride_out;
   if (n <= 0) {
-    if (tid == 0) a.cnt_out[seg] = 0;
+    if (tid == 0) S.cnt_out[seg] = 0;
     return;
   }
-  // getMinMax3D
+  // getMinMax3D (float min / max)
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-  for (int i = tid; i < n; i += kVgThreads) {
+  for (int i = tid; i < n; i += T) {
     const float4 p = in[i];
     const float v[3] = {p.x, p.y, p.z};
+#pragma unroll
     for (int d = 0; d < 3; ++d) {
       mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
       mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
     }
   }
-  for (int d = 0; d < 3; ++d) {
-    red[d][tid] = mn[d];
-    red[3 + d][tid] = mx[d];
-  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+    for (int o = 32; o > 0; o >>= 1) {
+      const float a = __shfl_xor(mn[d], o), b = __shfl_xor(mx[d], o);
+      mn[d] = (a < mn[d]) ? a : mn[d];
+      mx[d] = (mx[d] < b) ? b : mx[d];
+    }
+  if (lane == 0)
+    for (int d = 0; d < 3; ++d) {
+      mm[w * 6 + d] = mn[d];
+      mm[w * 6 + 3 + d] = mx[d];
+    }
   __syncthreads();
-  for (int s = kVgThreads / 2; s > 0; s >>= 1) {
-    if (tid < s)
-      for (int d = 0; d < 3; ++d) {
-        const float b = red[d][tid + s], c = red[3 + d][tid + s];
-        red[d][tid] = (b < red[d][tid]) ? b : red[d][tid];
-        red[3 + d][tid] = (red[3 + d][tid] < c) ? c : red[3 + d][tid];
-      }
-    __syncthreads();
-  }
   for (int d = 0; d < 3; ++d) {
-    mn[d] = red[d][0];
-    mx[d] = red[3 + d][0];
+    mn[d] = mm[d];
+    mx[d] = mm[3 + d];
+    for (int ww = 1; ww < NW; ++ww) {
+      const float a = mm[ww * 6 + d], b = mm[ww * 6 + 3 + d];
+      mn[d] = (a < mn[d]) ? a : mn[d];
+      mx[d] = (mx[d] < b) ? b : mx[d];
+    }
   }
-  const float inv = 1.0f / a.leaf;
+  const float inv = 1.0f / S.leaf;
   const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
   const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
   const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
   if (dx * dy * dz > (int64_t)INT32_MAX) {  // PCL: "Leaf size is too small" -> output = input
-    for (int i = tid; i < n; i += kVgThreads) out[i] = in[i];
-    if (tid == 0) a.cnt_out[seg] = n;
+    for (int i = tid; i < n; i += T) out[i] = in[i];
+    if (tid == 0) S.cnt_out[seg] = n;
     return;
   }
   int min_b[3], div_b[3];
@@ -174,11 +146,38 @@ k_voxel_grid(VgArgs a) {
     div_b[d] = max_b - min_b[d] + 1;
   }
   const uint32_t mul1 = (uint32_t)div_b[0], mul2 = (uint32_t)div_b[0] * (uint32_t)div_b[1];
-  const bool morton = a.morton && div_b[0] <= 1024 && div_b[1] <= 1024 && div_b[2] <= 1024;
-  uint32_t* sc = a.scratch + (int64_t)seg * 4 * a.stride_in;
-  uint32_t* kb[2] = {sc, sc + 2 * a.stride_in};
-  uint32_t* vb[2] = {sc + a.stride_in, sc + 3 * a.stride_in};
-  for (int i = tid; i < n; i += kVgThreads) {
+  const bool morton = S.morton && div_b[0] <= 1024 && div_b[1] <= 1024 && div_b[2] <= 1024;
+  int nbits = 32;
+  if (morton) {
+    int b = 1;
+    for (int d = 0; d < 3; ++d)
+      if (div_b[d] > 1) b = max(b, 32 - __clz((uint32_t)(div_b[d] - 1)));
+    nbits = 3 * b;
+  } else {
+    const uint64_t nkeys = (uint64_t)div_b[0] * (uint64_t)div_b[1] * (uint64_t)div_b[2];
+    if (nkeys <= 0xFFFFFFFFull) {
+      const uint32_t maxk = (uint32_t)(nkeys - 1);
+      nbits = maxk == 0 ? 1 : 32 - __clz(maxk);
+    }
+  }
+  // (key, index) buffers
+  uint32_t* kb[2];
+  V* vb[2];
+  if constexpr (LDS) {
+    unsigned char* q = (unsigned char*)(((uintptr_t)(misc + 4) + 15) & ~(uintptr_t)15);
+    const int cap = (int)S.cap;
+    kb[0] = (uint32_t*)q;
+    kb[1] = kb[0] + cap;
+    vb[0] = (V*)(kb[1] + cap);
+    vb[1] = vb[0] + cap;
+  } else {
+    uint32_t* sc = S.scratch + (int64_t)seg * 4 * S.cap;
+    kb[0] = sc;
+    kb[1] = sc + S.cap;
+    vb[0] = (V*)(sc + 2 * S.cap);
+    vb[1] = (V*)(sc + 3 * S.cap);
+  }
+  for (int i = tid; i < n; i += T) {
     const float4 p = in[i];
     const int ijk0 = (int)(floorf(p.x * inv) - (float)min_b[0]);
     const int ijk1 = (int)(floorf(p.y * inv) - (float)min_b[1]);
@@ -186,37 +185,86 @@ k_voxel_grid(VgArgs a) {
     kb[0][i] = morton ? (spread3_10((uint32_t)ijk0) | (spread3_10((uint32_t)ijk1) << 1) |
                          (spread3_10((uint32_t)ijk2) << 2))
                       : (uint32_t)ijk0 + (uint32_t)ijk1 * mul1 + (uint32_t)ijk2 * mul2;
-    vb[0][i] = (uint32_t)i;
-  }
-  const uint64_t nkeys = (uint64_t)div_b[0] * (uint64_t)div_b[1] * (uint64_t)div_b[2];
-  int nbits = 32;
-  if (morton) {
-    int b = 1;
-    for (int d = 0; d < 3; ++d)
-      if (div_b[d] > 1) b = max(b, 32 - __clz((uint32_t)(div_b[d] - 1)));
-    nbits = 3 * b;
-  } else if (nkeys <= 0xFFFFFFFFull) {
-    const uint32_t maxk = (uint32_t)(nkeys - 1);
-    nbits = maxk == 0 ? 1 : 32 - __clz(maxk);
+    vb[0][i] = (V)i;
   }
   __syncthreads();
-  const int r = block_radix_sort(kb, vb, a.hist + (int64_t)seg * a.hist_stride, n, nbits, lds_hist, lds_wc, lds_tot);
-  const uint32_t* ks = kb[r];
-  const uint32_t* vs = vb[r];
-  // heads -> output voxels in ascending key order
-  int64_t* total = &sh_info[0];
-  if (tid == 0) *total = 0;
-  __syncthreads();
-  for (int t0 = 0; t0 < n; t0 += kVgThreads) {
-    const int i = t0 + tid;
-    const bool head = i < n && (i == 0 || ks[i] != ks[i - 1]);
-    const uint64_t bal = __ballot(head);
-    const int wave = tid >> 6, lane = tid & 63;
-    lds_hist[wave] = (uint32_t)__popcll(bal);
+  // ---- radix sort: passes of <= 9-bit digits ----
+  const int passes = (nbits + 8) / 9;
+  const int dbits = (nbits + passes - 1) / passes;
+  const int nbins = 1 << dbits;
+  const int chunk = (((n + NW - 1) / NW) + 63) & ~63;
+  const int c0 = min(n, w * chunk), c1 = min(n, c0 + chunk);
+  uint32_t* hw = hist + w * 512;
+  int cur = 0;
+  for (int pass = 0; pass < passes; ++pass) {
+    const int shift = dbits * pass;
+    const uint32_t dmask = (uint32_t)nbins - 1u;
+    const uint32_t* kin = kb[cur];
+    const V* vin = vb[cur];
+    uint32_t* kout = kb[cur ^ 1];
+    V* vout = vb[cur ^ 1];
+    for (int b = tid; b < NW * 512; b += T) hist[b] = 0u;
     __syncthreads();
-    int pos = (int)*total;
-    for (int w = 0; w < wave; ++w) pos += (int)lds_hist[w];
-    pos += __popcll(bal & ((1ull << lane) - 1ull));
+    for (int i = c0 + lane; i < c1; i += 64) atomicAdd(&hw[(kin[i] >> shift) & dmask], 1u);
+    __syncthreads();
+    // digit-major, wave-minor exclusive offsets: per digit over waves, then over digits
+    for (int d = tid; d < nbins; d += T) {
+      uint32_t run = 0;
+      for (int ww = 0; ww < NW; ++ww) {
+        const uint32_t t = hist[ww * 512 + d];
+        hist[ww * 512 + d] = run;
+        run += t;
+      }
+      hist[NW * 512 + d] = run;  // digit totals: the extra row NW
+    }
+    __syncthreads();
+    block_exclusive_scan<T>(hist + NW * 512, nbins, wsum);
+    for (int d = tid; d < nbins; d += T) {
+      const uint32_t base = hist[NW * 512 + d];
+      for (int ww = 0; ww < NW; ++ww) hist[ww * 512 + d] += base;
+    }
+    __syncthreads();
+    for (int i0 = c0; i0 < c1; i0 += 64) {
+      const int i = i0 + lane;
+      const bool valid = i < c1;
+      const uint32_t key = valid ? kin[i] : 0u;
+      const uint32_t d = (key >> shift) & dmask;
+      uint64_t peers = __ballot(valid);
+      for (int b = 0; b < dbits; ++b) {
+        const uint64_t bal = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? bal : ~bal;
+      }
+      const int rank = __popcll(peers & ((1ull << lane) - 1ull));
+      const uint32_t base = valid ? hw[d] : 0u;
+      if (valid) {
+        kout[base + rank] = key;
+        vout[base + rank] = vin[i];
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (valid && rank == 0) hw[d] = base + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+    }
+    cur ^= 1;
+    __syncthreads();
+  }
+  const uint32_t* ks = kb[cur];
+  const V* vs = vb[cur];
+  // ---- voxels in ascending key order: heads of equal-key runs, centroid = float sum / count ----
+  int nh = 0;
+  for (int i0 = c0; i0 < c1; i0 += 64) {
+    const int i = i0 + lane;
+    nh += __popcll(__ballot(i < c1 && (i == 0 || ks[i] != ks[i - 1])));
+  }
+  if (lane == 0) wsum[w] = (uint32_t)nh;
+  __syncthreads();
+  int pos = 0;
+  for (int ww = 0; ww < w; ++ww) pos += (int)wsum[ww];
+  int total = pos;
+  for (int ww = w; ww < NW; ++ww) total += (int)wsum[ww];
+  for (int i0 = c0; i0 < c1; i0 += 64) {
+    const int i = i0 + lane;
+    const bool head = i < c1 && (i == 0 || ks[i] != ks[i - 1]);
+    const uint64_t bal = __ballot(head);
     if (head) {
       const uint32_t key = ks[i];
       float4 c = in[vs[i]];
@@ -230,22 +278,38 @@ k_voxel_grid(VgArgs a) {
         ++j;
       }
       const float cnt = (float)(j - i);
-      out[pos] = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
+      out[pos + __popcll(bal & ((1ull << lane) - 1ull))] = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
     }
-    __syncthreads();
-    if (tid == 0) {
-      int add = 0;
-      for (int w = 0; w < kVgWaves; ++w) add += (int)lds_hist[w];
-      *total += add;
-    }
-    __syncthreads();
+    pos += __popcll(bal);
   }
-  if (tid == 0) a.cnt_out[seg] = (int32_t)*total;
+  if (tid == 0) S.cnt_out[seg] = total;
+}
+
+size_t voxel_lds_bytes(const VgArgs& a, int threads, bool lds_mode) {
+  const int nw = threads / 64;
+  size_t b = sizeof(uint32_t) * ((size_t)(nw + 1) * 512 + nw) + sizeof(float) * nw * 6 + sizeof(int) * 4;
+  b = (b + 15) & ~(size_t)15;
+  if (lds_mode) {
+    int64_t cap = 0;
+    for (int k = 0; k < 2; ++k)
+      if (a.s[k].nseg > 0) cap = std::max<int64_t>(cap, a.s[k].cap);
+    b += (size_t)cap * 2 * (sizeof(uint32_t) + sizeof(uint16_t)) + 16;
+  }
+  return b;
 }
 
 void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
-  if (a.nseg <= 0) return;
-  hipLaunchKernelGGL(k_voxel_grid, dim3(a.nseg), dim3(kVgThreads), 0, s, a);
+  const int nseg = a.s[0].nseg + a.s[1].nseg;
+  if (nseg <= 0) return;
+  int64_t cap = 0;
+  for (int k = 0; k < 2; ++k)
+    if (a.s[k].nseg > 0) cap = std::max<int64_t>(cap, a.s[k].cap);
+  if (cap <= kVgLdsCap) {
+    hipLaunchKernelGGL((k_voxel_grid<256, uint16_t, true>), dim3(nseg), dim3(256), voxel_lds_bytes(a, 256, true), s, a);
+  } else {
+    hipLaunchKernelGGL((k_voxel_grid<1024, uint32_t, false>), dim3(nseg), dim3(1024), voxel_lds_bytes(a, 1024, false), s,
+                       a);
+  }
 }
 
 // One workgroup per job: ring-ordered concatenation of the per-ring corner picks and per-ring
