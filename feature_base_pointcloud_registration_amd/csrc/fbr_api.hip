@@ -157,7 +157,8 @@ int check_params(const fbr_params* p) {
 // ---------------------------------------------------------------------------------------------
 // map grid (built once per fbr_set_map; see k_register.hip for why this replaces the KD-trees)
 // ---------------------------------------------------------------------------------------------
-int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pts, int32_t** d_cs, GridDesc* g) {
+int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pts, int32_t** d_cs, GridDesc* g,
+               float max_inv) {
   if (*d_pts) (void)hipFree(*d_pts);
   if (*d_cs) (void)hipFree(*d_cs);
   *d_pts = nullptr;
@@ -168,8 +169,9 @@ int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pt
   float inv = 2.0f;
   if (const char* e = std::getenv("FBR_KNN_CELL")) {
     const float cell = std::strtof(e, nullptr);
-    if (cell > 0.0f) inv = std::exp2(-std::round(std::log2(cell)));
+    if (cell > 0.0f) inv = std::min(4.0f, std::exp2(-std::round(std::log2(cell))));  // >= 0.25 m (R <= 4)
   }
+  inv = std::min(inv, max_inv);
   int64_t lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0}, dims[3] = {1, 1, 1};
   for (int attempt = 0; attempt < 12; ++attempt) {
     for (int d = 0; d < 3; ++d) {
@@ -617,8 +619,11 @@ int fbr_set_map(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corner, cons
   CK(hipSetDevice(c->dev));
   int rc = voxel_grid_once(c, corner, n_corner, c->P.mapping_corner_leaf_size, c->map_c_host);
   if (!rc) rc = voxel_grid_once(c, surf, n_surf, c->P.mapping_surf_leaf_size, c->map_s_host);
-  if (!rc) rc = build_grid(c, c->map_c_host, &c->d_map_c, &c->d_cs_c, &c->gc);
-  if (!rc) rc = build_grid(c, c->map_s_host, &c->d_map_s, &c->d_cs_s, &c->gs);
+  // both grids share one (power-of-two) cell size: the kNN kernel is specialised on it
+  if (!rc) rc = build_grid(c, c->map_c_host, &c->d_map_c, &c->d_cs_c, &c->gc, 4.0f);
+  if (!rc) rc = build_grid(c, c->map_s_host, &c->d_map_s, &c->d_cs_s, &c->gs, c->gc.inv_cell);
+  if (!rc && c->gs.inv_cell < c->gc.inv_cell)
+    rc = build_grid(c, c->map_c_host, &c->d_map_c, &c->d_cs_c, &c->gc, c->gs.inv_cell);
   c->has_map = rc == FBR_OK;
   return rc;
 }
@@ -920,3 +925,4 @@ void fbr_pose_from_affine(const float m[16], float pose[6]) {
 }
 
 }  // extern "C"
+

@@ -87,64 +87,104 @@ __device__ __forceinline__ float axis_lb(float q, float fcell, int o, float c) {
 
 __device__ __forceinline__ int rank_offset(int k, int s) { return k == 0 ? 0 : ((k & 1) ? s * ((k + 1) >> 1) : -s * (k >> 1)); }
 
+#ifdef FBR_KNN_STATS
+// Diagnostic builds only (tools/knn_stats.py): [queries, rows considered, rows scanned, points
+// scanned, points inserted, accepted queries]
+__device__ unsigned long long fbr_knn_stats[8];
+#define FBR_KS(i, v) ks[i] += (v)
+#else
+#define FBR_KS(i, v) \
+  do {               \
+  } while (0)
+#endif
+
 // Exact kNN-5 among map points inside the crop box with d2 < 1.0, ordered by (d2, map index):
 // the neighbour set FLANN's exact search returns on the cropped cloud whenever the reference
-// keeps the correspondence (pointSearchSqDis[4] < 1.0, :1027/:1154).  Cell rows (y,z) are visited
-// nearest-side-first; a row, and the cells of a row, are skipped once their lower-bound distance
-// exceeds the current 5th distance or reaches 1.0.
+// keeps the correspondence (pointSearchSqDis[4] < 1.0, :1027/:1154).  R = cells per side covering
+// radius 1 (compile time: the row loop is fully unrolled).  Cell rows (y,z) are visited in
+// near-side-first rank order; a row, and the cells of a row, are skipped once their lower-bound
+// distance exceeds the current 5th distance or reaches 1.0.  Rows entirely inside the crop box
+// skip the per-point box test.
+template <int R>
 __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
-                          Knn5& r) {
+                          Knn5& r, unsigned* ks) {
+  constexpr int K = 2 * R + 1;
 #pragma unroll
   for (int t = 0; t < 5; ++t) { r.d[t] = __int_as_float(0x7f800000); r.id[t] = 0x7fffffff; r.pos[t] = -1; }
   const float inv = m.g.inv_cell, c = 1.0f / inv;
   const float sx = qx * inv, sy = qy * inv, sz = qz * inv;
   const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
   if (!(fabsf(fx) < 1e7f && fabsf(fy) < 1e7f && fabsf(fz) < 1e7f)) return;
-  const int R = inv > 1.0f ? (int)inv : 1;  // cells per side covering radius 1
   const int cx = (int)fx - (int)m.g.origin[0], cy = (int)fy - (int)m.g.origin[1], cz = (int)fz - (int)m.g.origin[2];
   const int X = m.g.dims[0], Y = m.g.dims[1], Z = m.g.dims[2];
   if (cx < -R || cy < -R || cz < -R || cx >= X + R || cy >= Y + R || cz >= Z + R) return;
   const int sgy = (sy - fy) >= 0.5f ? 1 : -1, sgz = (sz - fz) >= 0.5f ? 1 : -1;
-  const int K = 2 * R;
-  for (int ksum = 0; ksum <= 2 * K; ++ksum) {
-    for (int ky = max(0, ksum - K); ky <= min(K, ksum); ++ky) {
-      const int oy = rank_offset(ky, sgy), oz = rank_offset(ksum - ky, sgz);
-      const int y = cy + oy, z = cz + oz;
-      if (y < 0 || y >= Y || z < 0 || z >= Z) continue;
-      const float ly = axis_lb(qy, fy, oy, c), lz = axis_lb(qz, fz, oz, c);
-      const float ly2 = ly * ly, lz2 = lz * lz;
+  // squared per-axis lower bounds: y/z by visit rank, x by offset (negative / positive side)
+  float ly2[K], lz2[K], lxm2[R + 1], lxp2[R + 1];
+  int oyk[K], ozk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    oyk[k] = rank_offset(k, sgy);
+    ozk[k] = rank_offset(k, sgz);
+    const float ly = axis_lb(qy, fy, oyk[k], c), lz = axis_lb(qz, fz, ozk[k], c);
+    ly2[k] = ly * ly;
+    lz2[k] = lz * lz;
+  }
+#pragma unroll
+  for (int o = 1; o <= R; ++o) {
+    const float a = axis_lb(qx, fx, -o, c), b = axis_lb(qx, fx, o, c);
+    lxm2[o] = a * a;
+    lxp2[o] = b * b;
+  }
+  const float xlo = (fx - (float)R) * c, xhi = (fx + (float)(R + 1)) * c;  // row x extent (max)
+  const bool xin = xlo >= bmin[0] && xhi <= bmax[0];
+#pragma unroll
+  for (int ksum = 0; ksum <= 2 * (K - 1); ++ksum) {
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const int kz = ksum - ky;
+      if (kz < 0 || kz >= K) continue;  // compile time
+      const int y = cy + oyk[ky], z = cz + ozk[kz];
+      FBR_KS(1, 1);
       float lb = 0.0f;
-      lb += ly2;
-      lb += lz2;
-      if (lb > r.d[4] || !(lb < 1.0f)) continue;
+      lb += ly2[ky];
+      lb += lz2[kz];
+      if (y < 0 || y >= Y || z < 0 || z >= Z || lb > r.d[4] || !(lb < 1.0f)) continue;
       int xa = 0, xb = 0;
+      bool go_a = true, go_b = true;
+#pragma unroll
       for (int o = 1; o <= R; ++o) {
-        const float lx = axis_lb(qx, fx, -o, c);
-        float t = 0.0f;
-        t += lx * lx; t += ly2; t += lz2;
-        if (t > r.d[4] || !(t < 1.0f)) break;
-        xa = -o;
-      }
-      for (int o = 1; o <= R; ++o) {
-        const float lx = axis_lb(qx, fx, o, c);
-        float t = 0.0f;
-        t += lx * lx; t += ly2; t += lz2;
-        if (t > r.d[4] || !(t < 1.0f)) break;
-        xb = o;
+        float ta = 0.0f, tb = 0.0f;
+        ta += lxm2[o]; ta += ly2[ky]; ta += lz2[kz];
+        tb += lxp2[o]; tb += ly2[ky]; tb += lz2[kz];
+        go_a = go_a && !(ta > r.d[4]) && ta < 1.0f;
+        go_b = go_b && !(tb > r.d[4]) && tb < 1.0f;
+        if (go_a) xa = -o;
+        if (go_b) xb = o;
       }
       const int x0 = max(cx + xa, 0), x1 = min(cx + xb, X - 1);
       if (x0 > x1) continue;
       const int rowbase = (z * Y + y) * X;
       const int b = m.cell_start[rowbase + x0], e = m.cell_start[rowbase + x1 + 1];
+      FBR_KS(2, 1);
+      FBR_KS(3, e - b);
+      // the whole row inside the crop box (pcl::CropBox, inclusive) -> no per-point test
+      const float ylo = (fy + (float)oyk[ky]) * c, zlo = (fz + (float)ozk[kz]) * c;
+      const bool inside = xin && ylo >= bmin[1] && ylo + c <= bmax[1] && zlo >= bmin[2] && zlo + c <= bmax[2];
       for (int i = b; i < e; ++i) {
         const float4 p = m.pts[i];
-        if (p.x < bmin[0] || p.y < bmin[1] || p.z < bmin[2]) continue;  // pcl::CropBox, inclusive
-        if (p.x > bmax[0] || p.y > bmax[1] || p.z > bmax[2]) continue;
+        if (!inside) {
+          if (p.x < bmin[0] || p.y < bmin[1] || p.z < bmin[2]) continue;
+          if (p.x > bmax[0] || p.y > bmax[1] || p.z > bmax[2]) continue;
+        }
         float dist = 0.0f, diff;
         diff = qx - p.x; dist += diff * diff;                            // flann::L2_Simple
         diff = qy - p.y; dist += diff * diff;
         diff = qz - p.z; dist += diff * diff;
-        if (dist < 1.0f) knn_insert(r, dist, __float_as_int(p.w), i);
+        if (dist < 1.0f) {
+          FBR_KS(4, 1);
+          knn_insert(r, dist, __float_as_int(p.w), i);
+        }
       }
     }
   }
@@ -263,6 +303,8 @@ __global__ void k_gn_init(GnArgs a) {
 }
 
 // kNN pass: one lane per query, writes the 5 neighbour positions (slot 0 = -1: no correspondence).
+// R = grid cells per side covering radius 1 (both map grids share one cell size).
+template <int R>
 __global__ void __launch_bounds__(kResThreads)
 k_gn_knn(GnArgs a) {
   const int tid = threadIdx.x;
@@ -281,8 +323,16 @@ k_gn_knn(GnArgs a) {
     const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
     const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
     Knn5 nn;
-    knn5_grid(corner ? a.mc : a.ms, x0, y0, z0, g.crop_min, g.crop_max, nn);
+    unsigned ks[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+    knn5_grid<R>(corner ? a.mc : a.ms, x0, y0, z0, g.crop_min, g.crop_max, nn, ks);
     const bool ok = nn.pos[4] >= 0 && nn.d[4] < 1.0f;
+#ifdef FBR_KNN_STATS
+    ks[5] = ok;
+    ks[6] = corner;
+    for (int k = 0; k < 7; ++k) atomicAdd(&fbr_knn_stats[k], (unsigned long long)ks[k]);
+#else
+    (void)ks;
+#endif
     int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
 #pragma unroll
     for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? nn.pos[k] : -1;
@@ -536,7 +586,10 @@ void launch_export_records(hipStream_t s, int B, const float* pose_out, const fb
 
 void launch_gn_init(hipStream_t s, const GnArgs& a) { hipLaunchKernelGGL(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid) {
-  hipLaunchKernelGGL(k_gn_knn, dim3(grid), dim3(kResThreads), 0, s, a);
+  const float inv = a.mc.g.inv_cell;  // == a.ms.g.inv_cell (fbr_set_map)
+  if (inv > 2.0f) hipLaunchKernelGGL((k_gn_knn<4>), dim3(grid), dim3(kResThreads), 0, s, a);        // 0.25 m
+  else if (inv > 1.0f) hipLaunchKernelGGL((k_gn_knn<2>), dim3(grid), dim3(kResThreads), 0, s, a);   // 0.5 m
+  else hipLaunchKernelGGL((k_gn_knn<1>), dim3(grid), dim3(kResThreads), 0, s, a);                   // >= 1 m
 }
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
   hipLaunchKernelGGL(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);
@@ -554,3 +607,16 @@ void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* pts, int64_
 }
 
 }  // namespace fbr
+
+#ifdef FBR_KNN_STATS
+// Diagnostic builds only: read (and optionally reset) the kNN counters of k_gn_knn.
+extern "C" int fbr_diag_knn_stats(unsigned long long* out, int reset) {
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(fbr::fbr_knn_stats), sizeof(unsigned long long) * 8) != hipSuccess)
+    return FBR_ERR_HIP;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(fbr::fbr_knn_stats), z, sizeof(z)) != hipSuccess) return FBR_ERR_HIP;
+  }
+  return FBR_OK;
+}
+#endif

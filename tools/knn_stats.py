@@ -1,0 +1,39 @@
+"""Diagnostic: per-query work of the grid kNN (k_gn_knn) on a C2 batch — rows considered /
+scanned, points scanned / inserted — for the grid cell sizes given (FBR_KNN_CELL)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, R)
+from feature_base_pointcloud_registration_amd import build  # noqa: E402
+
+diag = build.build_hip(defines=("FBR_KNN_STATS",), name="libfbr_hip_diag.so")
+os.environ["FBR_LIB"] = diag
+from feature_base_pointcloud_registration_amd import api, synth  # noqa: E402
+from feature_base_pointcloud_registration_amd.fbr_types import default_params  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+P = default_params(64, 1800, max_batch=B)
+cm, sm = synth.config_map("C2")
+jobs = synth.make_jobs("C2", B)
+L = api.lib()
+L.fbr_diag_knn_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
+for cell in (sys.argv[2:] or ["0.5"]):
+    os.environ["FBR_KNN_CELL"] = cell
+    ctx = api.Context(P)
+    ctx.set_map(cm, sm)
+    ctx.batch_stage([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
+    ctx.batch_launch(); ctx.batch_wait()
+    L.fbr_diag_knn_stats(None, 1)
+    ctx.set_profiling(True)
+    ctx.batch_launch(); ctx.batch_wait()
+    st = np.zeros(8, np.uint64)
+    L.fbr_diag_knn_stats(st.ctypes.data, 0)
+    q = float(st[0])
+    print(f"cell {cell}: queries {int(q)} (corner {int(st[6])}) accepted {st[5] / q:.3f} | per query: rows considered "
+          f"{st[1] / q:.1f}, rows scanned {st[2] / q:.1f}, points scanned {st[3] / q:.1f}, inserted {st[4] / q:.1f} | "
+          f"gn_knn ms {ctx.kernel_time('gn_knn')}")
+    ctx.close()
