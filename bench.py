@@ -155,8 +155,8 @@ def main():
         try:
             with open(args.pmc_json) as f:
                 pm = json.load(f)
-            if pm.get("kernel") == dom and pm.get("config") == cfg and pm.get("batch") == B:
-                traffic = pm.get("hbm_bytes_per_launch")
+            if pm.get("config") == cfg and pm.get("batch") == B and dom in pm.get("kernels", {}):
+                traffic = pm["kernels"][dom]["hbm_bytes_per_launch"]
         except Exception:
             traffic = None
 

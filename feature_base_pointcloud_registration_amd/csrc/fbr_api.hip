@@ -92,6 +92,7 @@ struct fbr_ctx {
   unsigned long long* h_iter_flags = nullptr;  // host-mapped, written by k_gn_solve
   unsigned long long* d_iter_flags = nullptr;  // its device address
   unsigned long long gn_gen = 0;
+  bool crop_cached = false;  // d_cropcnt holds the staged batch's CropBox statistics
   int max_items = 0;
   float* d_pose_out = nullptr;
   fbr_reg_stats* d_stats = nullptr;
@@ -370,6 +371,21 @@ GnArgs gn_args(fbr_ctx* c, int B, bool trace) {
 }
 
 // Registration of the clouds in d_corner_all / d_surf_all (counts d_ncorner / d_nsurf) from d_guess.
+// Single-scan entry points reuse job slot 0 of the device buffers: a staged batch is dropped
+// (fbr_batch_launch then reports FBR_ERR_STATE until the next fbr_batch_stage).
+void drop_staged_batch(fbr_ctx* c) {
+  c->staged_B = 0;
+  c->crop_cached = false;
+}
+
+int crop_stats(fbr_ctx* c, int B) {
+  GnArgs a = gn_args(c, B, false);
+  CK(hipMemsetAsync(c->d_cropcnt, 0, sizeof(int32_t) * 2 * B, c->stream));
+  TIMED(c, "crop", launch_crop_count(c->stream, a, c->d_map_c, c->gc.n_points, 0, c->d_cropcnt));
+  TIMED(c, "crop", launch_crop_count(c->stream, a, c->d_map_s, c->gs.n_points, 1, c->d_cropcnt));
+  return FBR_OK;
+}
+
 int stage_register(fbr_ctx* c, int B, bool trace) {
   if (!c->has_map) return FBR_ERR_NO_MAP;
   // downsampleCurrentScan (mapOptmization.h:981-993): corner and surf filters in one launch;
@@ -384,9 +400,11 @@ int stage_register(fbr_ctx* c, int B, bool trace) {
   GnArgs a = gn_args(c, B, trace);
   if (trace) CK(hipMemsetAsync(c->d_trace, 0, sizeof(float) * B * c->P.max_iterations * 6, c->stream));
   TIMED(c, "gn_init", launch_gn_init(c->stream, a));
-  CK(hipMemsetAsync(c->d_cropcnt, 0, sizeof(int32_t) * 2 * B, c->stream));
-  TIMED(c, "crop", launch_crop_count(c->stream, a, c->d_map_c, c->gc.n_points, 0, c->d_cropcnt));
-  TIMED(c, "crop", launch_crop_count(c->stream, a, c->d_map_s, c->gs.n_points, 1, c->d_cropcnt));
+  // map-in-box statistics depend only on the guesses: computed once per staged batch
+  if (!c->crop_cached) {
+    const int rc = crop_stats(c, B);
+    if (rc) return rc;
+  }
   const int grid = std::max(1, std::min(c->max_items, 2048));
   // Iterations run on the device without host round trips; the host stays kLag iterations
   // ahead and stops enqueueing once k_gn_solve reports that no job of the batch is active.
@@ -617,6 +635,7 @@ int fbr_set_map(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corner, cons
                 int64_t n_surf) {
   if (!c || n_corner < 0 || n_surf < 0 || (n_corner && !corner) || (n_surf && !surf)) return FBR_ERR_INVALID_ARG;
   CK(hipSetDevice(c->dev));
+  c->crop_cached = false;
   int rc = voxel_grid_once(c, corner, n_corner, c->P.mapping_corner_leaf_size, c->map_c_host);
   if (!rc) rc = voxel_grid_once(c, surf, n_surf, c->P.mapping_surf_leaf_size, c->map_s_host);
   // both grids share one (power-of-two) cell size: the kNN kernel is specialised on it
@@ -642,6 +661,7 @@ int fbr_project(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, int32_
                 int32_t* col_ind, float* range, fbr_point_xyzi* cloud, int64_t* n_out) {
   if (!c || (n_in && !points)) return FBR_ERR_INVALID_ARG;
   CK(hipSetDevice(c->dev));
+  drop_staged_batch(c);
   int rc = upload_scan(c, 0, points, n_in);
   if (rc) return rc;
   rc = stage_project(c, 1);
@@ -685,6 +705,7 @@ int fbr_register_trace(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corne
   if (!c || !pose_inout) return FBR_ERR_INVALID_ARG;
   if (!c->has_map) return FBR_ERR_NO_MAP;
   CK(hipSetDevice(c->dev));
+  drop_staged_batch(c);
   int rc = upload_cloud(c, c->d_corner_all, c->d_ncorner, corner, n_corner);
   if (!rc) rc = upload_cloud(c, c->d_surf_all, c->d_nsurf, surf, n_surf);
   if (rc) return rc;
@@ -714,6 +735,7 @@ int fbr_process_scan(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, d
                      fbr_reg_stats* stats) {
   if (!c || !pose_inout || (n_in && !points)) return FBR_ERR_INVALID_ARG;
   CK(hipSetDevice(c->dev));
+  drop_staged_batch(c);
   int rc = upload_scan(c, 0, points, n_in);
   if (!rc) rc = stage_project(c, 1);
   if (!rc) rc = stage_features(c, 1, true);
@@ -772,6 +794,12 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
   }
   CK(hipMemcpyAsync(c->d_nin, n_in, sizeof(int64_t) * n_jobs, hipMemcpyHostToDevice, c->stream));
   CK(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * n_jobs, hipMemcpyHostToDevice, c->stream));
+  c->crop_cached = false;
+  if (c->has_map) {
+    const int rc = crop_stats(c, n_jobs);
+    if (rc) return rc;
+    c->crop_cached = true;
+  }
   CK(hipStreamSynchronize(c->stream));
   c->staged_B = n_jobs;
   c->staged_nin.assign(n_in, n_in + n_jobs);

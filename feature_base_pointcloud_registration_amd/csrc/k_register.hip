@@ -552,7 +552,9 @@ __global__ void k_gn_finalize(GnArgs a) {
   s.n_surf_ds = a.nsds[job];
 }
 
-// CropBox counts of the global map for every job's box (statistics only).
+// CropBox counts of the global map for every job's box (laserCloud{Corner,Surf}FromMapDSNum,
+// statistics only: the registration applies the box per kNN candidate).  The box is the guess's
+// translation +- crop_half (registration :289-304), identical to the one k_gn_init stores.
 __global__ void k_crop_count(GnArgs a, const float4* pts, int64_t n, int which, int32_t* counts) {
   extern __shared__ int32_t c[];
   for (int j = threadIdx.x; j < a.B; j += blockDim.x) c[j] = 0;
@@ -560,9 +562,11 @@ __global__ void k_crop_count(GnArgs a, const float4* pts, int64_t n, int which, 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float4 p = pts[i];
     for (int j = 0; j < a.B; ++j) {
-      const GnState& g = a.gn[j];
-      if (p.x < g.crop_min[0] || p.y < g.crop_min[1] || p.z < g.crop_min[2]) continue;
-      if (p.x > g.crop_max[0] || p.y > g.crop_max[1] || p.z > g.crop_max[2]) continue;
+      const float* gp = a.guess + 6 * j;
+      const float mn0 = -a.crop_half[0] + gp[3], mn1 = -a.crop_half[1] + gp[4], mn2 = -a.crop_half[2] + gp[5];
+      const float mx0 = a.crop_half[0] + gp[3], mx1 = a.crop_half[1] + gp[4], mx2 = a.crop_half[2] + gp[5];
+      if (p.x < mn0 || p.y < mn1 || p.z < mn2) continue;
+      if (p.x > mx0 || p.y > mx1 || p.z > mx2) continue;
       atomicAdd(&c[j], 1);
     }
   }

@@ -156,9 +156,12 @@ int fbr_process_batch(fbr_ctx* ctx, const fbr_point_xyzirt* const* scans, const 
                       int n_jobs, float* poses_inout /* [n_jobs][6] */,
                       fbr_reg_stats* stats /* [n_jobs] or NULL */);
 
-/* Device-resident batch (throughput measurement): stage copies the scans and guesses to HBM;
- * launch enqueues the whole path for the staged batch on the ctx stream (asynchronous, inputs
- * are not modified so it may be re-launched); wait blocks; results copies poses/stats out. */
+/* Device-resident batch (throughput measurement): stage copies the scans and guesses to HBM (and
+ * computes the per-job CropBox map statistics, which depend only on the guesses); launch enqueues
+ * the whole path for the staged batch on the ctx stream (asynchronous, inputs are not modified so
+ * it may be re-launched); wait blocks; results copies poses/stats out.  The single-scan entry
+ * points (fbr_project, fbr_register*, fbr_process_scan) share the device buffers and drop a staged
+ * batch: fbr_batch_launch then returns FBR_ERR_STATE until the next fbr_batch_stage. */
 int fbr_batch_stage(fbr_ctx* ctx, const fbr_point_xyzirt* const* scans, const int64_t* n_in,
                     int n_jobs, const float* poses_in /* [n_jobs][6] */);
 int fbr_batch_launch(fbr_ctx* ctx);

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the path kernels from rocprofv3 PMC passes -> profiles/hbm_traffic.json.
+
+Inputs: the FETCH_SIZE pass CSV and the WRITE_SIZE pass CSV (separate passes: on gfx950 the two
+counters do not fit one TCC pass).  Both are in KB.  Per MI355X_MICROARCH.md (HBM/rocprofv3
+section) FETCH_SIZE on gfx950 tallies 128-B requests at 64 B, i.e. reports half the bytes of wide
+streaming reads, so it is doubled; WRITE_SIZE is taken as is.  Infinity-Cache hits are counted by
+these counters (an upper bound on DRAM bytes).
+
+usage: hbm_traffic.py FETCH.csv WRITE.csv CONFIG BATCH [out.json]
+"""
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+
+NAMES = {"gn_knn": r"k_gn_knn", "gn_residual": r"k_gn_residual", "features": r"k_features",
+         "voxel": r"k_voxel_grid", "project": r"k_project\b", "extract": r"k_compact|k_rowcount",
+         "gn_solve": r"k_gn_solve"}
+
+
+def per_launch(path, counter):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        for key, rx in NAMES.items():
+            if re.search(rx, r["Kernel_Name"]):
+                acc[key].append(float(r["Counter_Value"]) * 1024.0)
+    return acc
+
+
+def main():
+    fetch_csv, write_csv, cfg, batch = sys.argv[1:5]
+    out = sys.argv[5] if len(sys.argv) > 5 else "profiles/hbm_traffic.json"
+    f = per_launch(fetch_csv, "FETCH_SIZE")
+    w = per_launch(write_csv, "WRITE_SIZE")
+    kernels = {}
+    for k in NAMES:
+        if f.get(k) and w.get(k):
+            fb = sum(f[k]) / len(f[k])
+            wb = sum(w[k]) / len(w[k])
+            kernels[k] = {"hbm_bytes_per_launch": 2.0 * fb + wb, "fetch_bytes_raw": fb, "write_bytes": wb,
+                          "launches_sampled": len(f[k])}
+    res = {"config": cfg, "batch": int(batch), "kernels": kernels,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of bench.py; "
+                     "bytes = 2*FETCH_SIZE (gfx950 64-B tally of 128-B requests) + WRITE_SIZE, mean per launch",
+           "sources": [fetch_csv, write_csv]}
+    json.dump(res, open(out, "w"), indent=1)
+    for k, v in kernels.items():
+        print(f"{k:12s} {v['hbm_bytes_per_launch'] / 1e6:10.2f} MB/launch")
+
+
+if __name__ == "__main__":
+    main()
