@@ -92,6 +92,7 @@ struct fbr_ctx {
   unsigned long long* h_iter_flags = nullptr;  // host-mapped, written by k_gn_solve
   unsigned long long* d_iter_flags = nullptr;  // its device address
   unsigned long long gn_gen = 0;
+  int32_t* d_iter_cnt = nullptr;
   bool crop_cached = false;  // d_cropcnt holds the staged batch's CropBox statistics
   int max_items = 0;
   float* d_pose_out = nullptr;
@@ -367,6 +368,7 @@ GnArgs gn_args(fbr_ctx* c, int B, bool trace) {
   a.trace = trace ? c->d_trace : nullptr;
   a.nbr = c->d_nbr;
   a.iter_flags = c->d_iter_flags;
+  a.iter_cnt = c->d_iter_cnt;
   return a;
 }
 
@@ -399,6 +401,7 @@ int stage_register(fbr_ctx* c, int B, bool trace) {
   TIMED(c, "voxel_scan", launch_voxel_grid(c->stream, v));
   GnArgs a = gn_args(c, B, trace);
   if (trace) CK(hipMemsetAsync(c->d_trace, 0, sizeof(float) * B * c->P.max_iterations * 6, c->stream));
+  CK(hipMemsetAsync(c->d_iter_cnt, 0, sizeof(int32_t) * 2 * c->P.max_iterations, c->stream));
   TIMED(c, "gn_init", launch_gn_init(c->stream, a));
   // map-in-box statistics depend only on the guesses: computed once per staged batch
   if (!c->crop_cached) {
@@ -583,6 +586,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_item_range, 2 * B) || dalloc(&c->d_cropcnt, 2 * B) ||
               dalloc(&c->d_partial, (int64_t)c->max_items * 32) ||
               dalloc(&c->d_nbr, (int64_t)c->max_items * 5 * 256) ||
+              dalloc(&c->d_iter_cnt, 2 * std::max(1, p->max_iterations)) ||
               hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * std::max(1, p->max_iterations),
                             hipHostMallocMapped) != hipSuccess ||
               hipHostGetDevicePointer((void**)&c->d_iter_flags, c->h_iter_flags, 0) != hipSuccess || dalloc(&c->d_pose_out, B * 6) ||
@@ -612,7 +616,7 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_map_c,
-                  c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr};
+                  c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr, c->d_iter_cnt};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);

@@ -97,6 +97,7 @@ struct GnArgs {
   float* trace;              // [B][max_iter][6] or null
   int32_t* nbr;              // [max_items][5][256] kNN-5 map positions of each query (-1 = rejected)
   unsigned long long* iter_flags;  // host-mapped [max_iter]: (generation << 32) | jobs still active
+  int32_t* iter_cnt;         // [max_iter][2] active-job count / finished workgroups (zeroed per solve)
 };
 void launch_gn_init(hipStream_t s, const GnArgs& a);
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid);

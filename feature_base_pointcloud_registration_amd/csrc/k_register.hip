@@ -414,21 +414,9 @@ k_gn_residual(GnArgs a) {
   }
 }
 
-constexpr int kSolveThreads = 256;
-
-struct SolveLds {  // per-lane strided arrays of the 6x6 degeneracy eigen-decomposition
-  float A[36 * kSolveThreads], V[36 * kSolveThreads], W[6 * kSolveThreads];
-  int R[6 * kSolveThreads], C[6 * kSolveThreads];
-};
-
-__device__ void gn_solve_job(const GnArgs& a, int job, SolveLds& L) {
+// One job's LMOptimization step on one lane (acc = the job's summed normal-equation products).
+__device__ void gn_solve_job(const GnArgs& a, int job, const double* acc) {
   GnState& g = a.gn[job];
-  if (!g.active) return;
-  double acc[28];
-  for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-  const int i0 = a.item_range[2 * job], i1 = a.item_range[2 * job + 1];
-  for (int it = i0; it < i1; ++it)
-    for (int k = 0; k < 28; ++k) acc[k] += a.partial[(int64_t)it * kPartial + k];
   const int iterCount = g.iter;
   g.iter = iterCount + 1;
   const int sel = (int)acc[27];
@@ -459,16 +447,8 @@ __device__ void gn_solve_job(const GnArgs& a, int job, SolveLds& L) {
   for (int k = 0; k < 36; ++k) matP[k] = 0.0f;  // local cv::Mat matP (:1278)
   if (iterCount == 0) {
     float E[6], V[36], V2[36], Vi[36];
-    {
-      const int t = threadIdx.x;
-#pragma unroll
-      for (int k = 0; k < 36; ++k) L.A[k * kSolveThreads + t] = AtA[k];
-      jacobi_eigen_lds<6, kSolveThreads>(L.A + t, L.W + t, L.V + t, L.R + t, L.C + t);
-#pragma unroll
-      for (int k = 0; k < 36; ++k) V[k] = L.V[k * kSolveThreads + t];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) E[k] = L.W[k * kSolveThreads + t];
-    }
+    for (int k = 0; k < 36; ++k) tmp[k] = AtA[k];
+    jacobi_eigen<6>(tmp, E, V);  // register-resident; one job per wave, so no pivot divergence
     for (int k = 0; k < 36; ++k) V2[k] = V[k];
     int deg = 0;
     for (int i = 5; i >= 0; i--) {
@@ -505,24 +485,36 @@ __device__ void gn_solve_job(const GnArgs& a, int job, SolveLds& L) {
   pose_to_T(g.pose, g.T, g.trig);
 }
 
-// One workgroup: every job's LMOptimization step, then the number of jobs still iterating is
-// published to host-mapped memory as (generation << 32 | count) so the host stops enqueueing
-// iterations once the whole batch has converged.
-__global__ void __launch_bounds__(kSolveThreads) k_gn_solve(GnArgs a, int iter_idx, unsigned long long gen) {
-  __shared__ SolveLds L;
-  __shared__ int cnt;
-  if (threadIdx.x == 0) cnt = 0;
-  __syncthreads();
-  int mine = 0;
-  for (int job = threadIdx.x; job < a.B; job += blockDim.x) {
-    gn_solve_job(a, job, L);
-    mine += a.gn[job].active;
+// One wave per job: lanes 0..27 sum the job's item partials (each entry in item order, as before),
+// lane 0 runs the LMOptimization step.  The number of jobs still iterating is accumulated with
+// agent-scope atomics; the last workgroup to finish publishes it to host-mapped memory as
+// (generation << 32 | count) so the host stops enqueueing iterations once the batch converged.
+__global__ void __launch_bounds__(64) k_gn_solve(GnArgs a, int iter_idx, unsigned long long gen) {
+  __shared__ double acc[28];
+  const int job = blockIdx.x, lane = threadIdx.x;
+  GnState& g = a.gn[job];
+  if (g.active) {
+    if (lane < 28) {
+      double sum = 0.0;
+      const int i0 = a.item_range[2 * job], i1 = a.item_range[2 * job + 1];
+      for (int it = i0; it < i1; ++it) sum += a.partial[(int64_t)it * kPartial + lane];
+      acc[lane] = sum;
+    }
+    __syncthreads();
+    if (lane == 0) gn_solve_job(a, job, acc);
   }
-  if (mine) atomicAdd(&cnt, mine);
-  __syncthreads();
-  if (threadIdx.x == 0 && a.iter_flags)
-    __hip_atomic_store(&a.iter_flags[iter_idx], (gen << 32) | (unsigned long long)cnt, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane == 0) {
+    atomicAdd(&a.iter_cnt[2 * iter_idx], g.active);
+    __threadfence();
+    const int done = atomicAdd(&a.iter_cnt[2 * iter_idx + 1], 1);
+    if (done == a.B - 1) {
+      __threadfence();
+      const int cnt = atomicAdd(&a.iter_cnt[2 * iter_idx], 0);
+      if (a.iter_flags)
+        __hip_atomic_store(&a.iter_flags[iter_idx], (gen << 32) | (unsigned long long)cnt, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 __global__ void k_gn_finalize(GnArgs a) {
@@ -599,7 +591,7 @@ void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
   hipLaunchKernelGGL(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);
 }
 void launch_gn_solve(hipStream_t s, const GnArgs& a, int iter_idx, unsigned long long gen) {
-  hipLaunchKernelGGL(k_gn_solve, dim3(1), dim3(kSolveThreads), 0, s, a, iter_idx, gen);
+  hipLaunchKernelGGL(k_gn_solve, dim3(a.B), dim3(64), 0, s, a, iter_idx, gen);
 }
 void launch_gn_finalize(hipStream_t s, const GnArgs& a) {
   hipLaunchKernelGGL(k_gn_finalize, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
