@@ -93,6 +93,7 @@ struct fbr_ctx {
   unsigned long long* d_iter_flags = nullptr;  // its device address
   unsigned long long gn_gen = 0;
   int32_t* d_iter_cnt = nullptr;
+  unsigned char* d_feat_scratch = nullptr;  // k_features sorted-path slots [B*H][gslot_bytes]
   bool crop_cached = false;  // d_cropcnt holds the staged batch's CropBox statistics
   int max_items = 0;
   float* d_pose_out = nullptr;
@@ -146,6 +147,22 @@ void timer_end(fbr_ctx* c, hipEvent_t ev_end) {
   } while (0)
 
 int64_t seg_cap(int W) { return W / 6 + 8; }
+
+// LDS / scratch capacities of k_features for a Horizon_SCAN of W.
+void feat_caps(int W, FeatArgs& a);
+int64_t feat_slot_bytes(int W) {
+  FeatArgs a{};
+  feat_caps(W, a);
+  return a.gslot_bytes;
+}
+void feat_caps(int W, FeatArgs& a) {
+  a.lcap = W + 16;
+  a.segcap = (int)seg_cap(W);
+  a.kseg = 1;
+  while (a.kseg < a.segcap - 1) a.kseg <<= 1;
+  a.nwcap = (a.lcap + 63) / 64 + 1;
+  a.gslot_bytes = (int64_t)features_gslot_bytes(a);
+}
 
 int check_params(const fbr_params* p) {
   if (!p) return FBR_ERR_INVALID_ARG;
@@ -311,13 +328,8 @@ int stage_features(fbr_ctx* c, int B, bool stream_mode) {
   a.cand = c->d_cand;
   a.cand_cnt = c->d_cand_cnt;
   a.err = c->d_err;
-  a.lcap = c->W + 16;
-  a.segcap = (int)seg_cap(c->W);
-  a.kseg = 1;
-  while (a.kseg < a.segcap - 1) a.kseg <<= 1;
-  a.nwcap = (a.lcap + 63) / 64 + 1;
-  a.region_a = (int)std::max<int64_t>((int64_t)6 * a.lcap, (int64_t)8 * a.kseg + (int64_t)16 * a.segcap + 16 + 8 * 12);
-  a.region_a = (a.region_a + 15) & ~15;
+  feat_caps(c->W, a);
+  a.gscratch = c->d_feat_scratch;
   a.stamps = c->d_feat_stamps;
   CK(hipMemsetAsync(c->d_err, 0, sizeof(int32_t) * B, c->stream));
   TIMED(c, "features", launch_features(c->stream, a));
@@ -587,6 +599,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_partial, (int64_t)c->max_items * 32) ||
               dalloc(&c->d_nbr, (int64_t)c->max_items * 5 * 256) ||
               dalloc(&c->d_iter_cnt, 2 * std::max(1, p->max_iterations)) ||
+              dalloc(&c->d_feat_scratch, (int64_t)B * H * feat_slot_bytes(c->W)) ||
               hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * std::max(1, p->max_iterations),
                             hipHostMallocMapped) != hipSuccess ||
               hipHostGetDevicePointer((void**)&c->d_iter_flags, c->h_iter_flags, 0) != hipSuccess || dalloc(&c->d_pose_out, B * 6) ||
@@ -616,7 +629,7 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_map_c,
-                  c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr, c->d_iter_cnt};
+                  c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr, c->d_iter_cnt, c->d_feat_scratch};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);

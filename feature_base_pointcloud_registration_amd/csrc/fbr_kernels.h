@@ -34,10 +34,12 @@ struct FeatArgs {
   int lcap, segcap;      // LDS capacities (window length, segment length)
   int kseg;              // segment sort capacity: next power of two >= segcap - 1 (<= 1024)
   int nwcap;             // 64-bit words per window bit array
-  int region_a;          // bytes of the phase-aliased LDS region
+  unsigned char* gscratch;  // [B*H][gslot_bytes] sorted-path buffers (stale-slot segment, ties)
+  int64_t gslot_bytes;
   unsigned long long* stamps;  // diagnostic builds only: [B*H][12] phase cycle sums
 };
 size_t features_lds_bytes(const FeatArgs& a);
+size_t features_gslot_bytes(const FeatArgs& a);
 void launch_features(hipStream_t s, const FeatArgs& a);
 
 // ---- A9 VoxelGrid over segments (k_voxel.hip) ----

@@ -34,10 +34,13 @@
 #include "fbr_kernels.h"
 #include "fbr_sort.h"
 
+#include <algorithm>
+
 namespace fbr {
 
 namespace {
 constexpr uint64_t kPadKey = ~0ull;
+constexpr int kWin = 256 + 16;  // phase-2 window: 4 chunks + 8 on each side
 }  // namespace
 
 // Window bit-words (index i of the window <-> bit i&63 of word i>>6).
@@ -53,16 +56,15 @@ struct FeatLds {
   Bits gap;           // |col[i+1]-col[i]| > 10
   Bits picked, labpos, labneg, edgec, surfc;
   Bits occa, occb, occc;
-  // region A, phase 1
-  float* r;           // [Lcap]
-  int16_t* col;       // [Lcap]
-  // region A, phase 2 (per segment)
+  uint32_t* cm;       // [segcap] conflict masks
+  unsigned char* rb;  // region B: phase-2 range/col windows, then the taken-corner lists
+  uint64_t* tmask;    // [WMAX] taken mask copy for the cap scan
+  // sorted path (stale-slot segment, relevant ties): per-ring global scratch slot
   uint64_t* keys;     // [kseg]
+  SmoothEntry* seg;   // [segcap] serial-path entries
+  SmoothEntry* tmp;   // [segcap] materialisation scratch
   uint16_t* sorder;   // [segcap] member index at each sorted position
   uint16_t* rankc;    // [segcap] corner visit rank of each member
-  uint32_t* cm;       // [segcap] conflict masks
-  SmoothEntry* seg;   // [segcap] serial-path entries
-  uint64_t* tmask;    // [WMAX] taken mask copy for the cap scan
   SortFrame* sstack;  // [kSortStack] introsort emulation stack (tie segments, lane 0)
 };
 
@@ -346,9 +348,8 @@ k_features(FeatArgs a) {
     return;
   }
   unsigned char* p = smem;
-  unsigned char* regionA = p;        p += a.region_a;
   S.curv = (float*)p;                p += sizeof(float) * Lcap;
-  uint64_t* words = (uint64_t*)p;    // 9 bit arrays of nwcap words
+  uint64_t* words = (uint64_t*)p;    p += sizeof(uint64_t) * 9 * nwcap;  // 9 bit arrays of nwcap words
   S.gap.w = words;
   S.picked.w = words + 1 * nwcap;
   S.labpos.w = words + 2 * nwcap;
@@ -358,64 +359,74 @@ k_features(FeatArgs a) {
   S.occa.w = words + 6 * nwcap;
   S.occb.w = words + 7 * nwcap;
   S.occc.w = words + 8 * nwcap;
-  S.r = (float*)regionA;
-  S.col = (int16_t*)(regionA + sizeof(float) * Lcap);
-  S.keys = (uint64_t*)regionA;
-  S.seg = (SmoothEntry*)(regionA + sizeof(uint64_t) * kseg);
-  S.cm = (uint32_t*)((unsigned char*)S.seg + sizeof(SmoothEntry) * segcap);
-  S.sorder = (uint16_t*)((unsigned char*)S.cm + sizeof(uint32_t) * segcap);
-  S.rankc = S.sorder + segcap;
-  S.tmask = (uint64_t*)(((uintptr_t)(S.rankc + segcap) + 15) & ~(uintptr_t)15);
-  S.sstack = (SortFrame*)(words + 9 * nwcap);
+  S.tmask = (uint64_t*)p;            p += sizeof(uint64_t) * 16;
+  S.sstack = (SortFrame*)p;          p += sizeof(SortFrame) * kSortStack;
+  S.cm = (uint32_t*)p;               p += sizeof(uint32_t) * segcap;
+  S.rb = (unsigned char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+  {
+    unsigned char* g = a.gscratch + (int64_t)slot * a.gslot_bytes;
+    S.keys = (uint64_t*)g;           g += sizeof(uint64_t) * kseg;
+    S.seg = (SmoothEntry*)g;         g += sizeof(SmoothEntry) * segcap;
+    S.tmp = (SmoothEntry*)g;         g += sizeof(SmoothEntry) * segcap;
+    S.sorder = (uint16_t*)g;         g += sizeof(uint16_t) * segcap;
+    S.rankc = (uint16_t*)g;
+  }
 
   const float* R = a.range + job * HW;
   const int32_t* C = a.col + job * HW;
   const float4* CL = a.cloud + job * HW;
   StreamState* st = a.stream + job;
-  // ---- phase 1: stage the window ----
-  for (int i0 = 0; i0 < S.L; i0 += 256) {
-    float rv[4];
-    int cv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = i0 + 64 * q + lane;
-      rv[q] = i < S.L ? R[S.wlo + i] : 0.0f;
-      cv[q] = i < S.L ? C[S.wlo + i] : 0;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = i0 + 64 * q + lane;
-      if (i < S.L) {
-        S.r[i] = rv[q];
-        S.col[i] = (int16_t)cv[q];
-      }
-    }
-  }
   for (int w = lane; w < 9 * nwcap; w += 64) words[w] = 0ull;
   __syncthreads();
   FBR_STAMP(0);
   // ---- phase 2: occlusion marks, column gaps, curvature, threshold bits (chunk c = 64 indices) ----
+  // range / col are staged per group of 4 chunks: window [256g - 8, 256g + 264) in region B
+  float* rw = (float*)S.rb;
+  int16_t* cw = (int16_t*)(rw + kWin);
   for (int c = 0; c < S.nw; ++c) {
+    if ((c & 3) == 0) {
+      const int wb = 64 * c - 8;
+      float rv[(kWin + 63) / 64];
+      int cv[(kWin + 63) / 64];
+#pragma unroll
+      for (int q = 0; q < (kWin + 63) / 64; ++q) {
+        const int t = 64 * q + lane, idx = wb + t;
+        const bool in = t < kWin && idx >= 0 && idx < S.L;
+        rv[q] = in ? R[S.wlo + idx] : 0.0f;
+        cv[q] = in ? C[S.wlo + idx] : 0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < (kWin + 63) / 64; ++q) {
+        const int t = 64 * q + lane;
+        if (t < kWin) {
+          rw[t] = rv[q];
+          cw[t] = (int16_t)cv[q];
+        }
+      }
+      __syncthreads();
+    }
     const int i = 64 * c + lane;
     const int j = S.wlo + i;
+    const int wo = 64 * (c & ~3) - 8;  // window origin of this chunk's group
     bool fa = false, fb = false, fc = false, gp = true;
     float curv = 0.0f;
     if (i < S.L) {
-      if (i + 1 < S.L) gp = abs((int)S.col[i + 1] - (int)S.col[i]) > 10;
+      if (i + 1 < S.L) gp = abs((int)cw[i + 1 - wo] - (int)cw[i - wo]) > 10;
       if (j >= 5 && j < n - 6 && i >= 1 && i + 1 < S.L) {  // markOccludedPoints (:140-175)
-        const float depth1 = S.r[i], depth2 = S.r[i + 1];
-        const int columnDiff = abs((int)S.col[i + 1] - (int)S.col[i]);
+        const float depth1 = rw[i - wo], depth2 = rw[i + 1 - wo];
+        const int columnDiff = abs((int)cw[i + 1 - wo] - (int)cw[i - wo]);
         if (columnDiff < 10) {
           if ((double)(depth1 - depth2) > 0.3) fa = true;
           else if ((double)(depth2 - depth1) > 0.3) fb = true;
         }
-        const float diff1 = fabsf(S.r[i - 1] - S.r[i]);
-        const float diff2 = fabsf(S.r[i + 1] - S.r[i]);
-        fc = (double)diff1 > 0.02 * (double)S.r[i] && (double)diff2 > 0.02 * (double)S.r[i];
+        const float diff1 = fabsf(rw[i - 1 - wo] - rw[i - wo]);
+        const float diff2 = fabsf(rw[i + 1 - wo] - rw[i - wo]);
+        fc = (double)diff1 > 0.02 * (double)rw[i - wo] && (double)diff2 > 0.02 * (double)rw[i - wo];
       }
       if (j >= 5 && j < n - 5 && i >= 5 && i + 5 < S.L) {  // calculateSmoothness (:113-122)
-        const float d = S.r[i - 5] + S.r[i - 4] + S.r[i - 3] + S.r[i - 2] + S.r[i - 1] - S.r[i] * 10.0f +
-                        S.r[i + 1] + S.r[i + 2] + S.r[i + 3] + S.r[i + 4] + S.r[i + 5];
+        const float d = rw[i - 5 - wo] + rw[i - 4 - wo] + rw[i - 3 - wo] + rw[i - 2 - wo] + rw[i - 1 - wo] - rw[i - wo] * 10.0f +
+                        rw[i + 1 - wo] + rw[i + 2 - wo] + rw[i + 3 - wo] + rw[i + 4 - wo] + rw[i + 5 - wo];
         curv = d * d;
       }
       S.curv[i] = curv;  // indices outside [5, n-5) keep the zero-initialised scratch value
@@ -561,7 +572,7 @@ k_features(FeatArgs a) {
         __syncthreads();
       }
     };
-    float* tlv = (float*)S.seg;                        // direct path: taken corners (value, member)
+    float* tlv = (float*)S.rb;                         // direct path: taken corners (value, member)
     uint16_t* tlu = (uint16_t*)(tlv + segcap);
     uint16_t* vis = tlu + segcap;                      // taken corners in visit order
     bool direct = !has_stale;
@@ -764,8 +775,14 @@ k_features(FeatArgs a) {
 }
 
 size_t features_lds_bytes(const FeatArgs& a) {
-  return (size_t)a.region_a + (size_t)a.lcap * sizeof(float) + (size_t)9 * a.nwcap * sizeof(uint64_t) +
-         sizeof(SortFrame) * kSortStack + 64;
+  const size_t region_b = std::max<size_t>((size_t)kWin * (sizeof(float) + sizeof(int16_t)), (size_t)8 * a.segcap);
+  return (size_t)a.lcap * sizeof(float) + (size_t)9 * a.nwcap * sizeof(uint64_t) + sizeof(uint64_t) * 16 +
+         sizeof(SortFrame) * kSortStack + sizeof(uint32_t) * a.segcap + 16 + region_b;
+}
+
+size_t features_gslot_bytes(const FeatArgs& a) {
+  const size_t b = sizeof(uint64_t) * a.kseg + 2 * sizeof(SmoothEntry) * a.segcap + 2 * sizeof(uint16_t) * a.segcap;
+  return (b + 255) & ~(size_t)255;
 }
 
 void launch_features(hipStream_t s, const FeatArgs& a) {

@@ -142,19 +142,29 @@ __global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax
   int32_t* CI = col + job * HW;
   float* R = range + job * HW;
   int base = off;
-  for (int c0 = 0; c0 < W; c0 += 64) {
-    const int c = c0 + lane;
-    const int32_t o = c < W ? O[c] : kEmptyOwner;
-    const bool v = o != kEmptyOwner;
-    const uint64_t m = __ballot(v);
-    if (v) {
-      const int dst = base + __popcll(m & ((1ull << lane) - 1ull));
-      const fbr_point_xyzirt q = P[o];
-      C[dst] = make_float4(q.x, q.y, q.z, q.intensity);
-      CI[dst] = c;
-      R[dst] = sqrt_rn(q.x * q.x + q.y * q.y + q.z * q.z);
+  // two 64-column chunks per step: both chunks' owner loads and point gathers are in flight together
+  for (int c0 = 0; c0 < W; c0 += 128) {
+    const int ca = c0 + lane, cb = c0 + 64 + lane;
+    const int32_t oa = ca < W ? O[ca] : kEmptyOwner, ob = cb < W ? O[cb] : kEmptyOwner;
+    const bool va = oa != kEmptyOwner, vb = ob != kEmptyOwner;
+    const uint64_t ma = __ballot(va), mb = __ballot(vb);
+    fbr_point_xyzirt qa{}, qb{};
+    if (va) qa = P[oa];
+    if (vb) qb = P[ob];
+    if (va) {
+      const int dst = base + __popcll(ma & ((1ull << lane) - 1ull));
+      C[dst] = make_float4(qa.x, qa.y, qa.z, qa.intensity);
+      CI[dst] = ca;
+      R[dst] = sqrt_rn(qa.x * qa.x + qa.y * qa.y + qa.z * qa.z);
     }
-    base += __popcll(m);
+    base += __popcll(ma);
+    if (vb) {
+      const int dst = base + __popcll(mb & ((1ull << lane) - 1ull));
+      C[dst] = make_float4(qb.x, qb.y, qb.z, qb.intensity);
+      CI[dst] = cb;
+      R[dst] = sqrt_rn(qb.x * qb.x + qb.y * qb.y + qb.z * qb.z);
+    }
+    base += __popcll(mb);
   }
 }
 

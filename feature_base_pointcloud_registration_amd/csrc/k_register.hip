@@ -497,6 +497,7 @@ __global__ void __launch_bounds__(64) k_gn_solve(GnArgs a, int iter_idx, unsigne
     if (lane < 28) {
       double sum = 0.0;
       const int i0 = a.item_range[2 * job], i1 = a.item_range[2 * job + 1];
+#pragma unroll 8
       for (int it = i0; it < i1; ++it) sum += a.partial[(int64_t)it * kPartial + lane];
       acc[lane] = sum;
     }
