@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = [
     "fbr_destroy", "fbr_set_map", "fbr_get_map", "fbr_project", "fbr_extract_features",
     "fbr_register", "fbr_register_trace", "fbr_process_scan", "fbr_reset_stream",
     "fbr_process_batch", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
-    "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_kernel_time", "fbr_stream",
+    "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
     "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math",
 ]
 
@@ -77,6 +77,7 @@ def lib():
             "fbr_batch_export": (ctypes.c_int, [_VP, _VP]),
             "fbr_batch_bytes": (ctypes.c_int, [_VP, _VP, _VP]),
             "fbr_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
+            "fbr_set_profiling_kernels": (ctypes.c_int, [_VP, ctypes.c_char_p]),
             "fbr_kernel_time": (ctypes.c_int, [_VP, ctypes.c_char_p, _VP, _VP]),
             "fbr_stream": (_VP, [_VP]),
             "fbr_voxel_grid": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_float, _VP, _VP]),
@@ -278,7 +279,10 @@ class Context:
         _check(lib().fbr_batch_bytes(self._h, ctypes.byref(t), ctypes.byref(g)), "fbr_batch_bytes")
         return t.value, g.value
 
-    def set_profiling(self, on=True):
+    def set_profiling(self, on=True, kernels=None):
+        """Time kernels with HIP events on the ctx stream; `kernels` restricts it to those names."""
+        names = None if not kernels else ",".join(kernels).encode()
+        _check(lib().fbr_set_profiling_kernels(self._h, names), "fbr_set_profiling_kernels")
         _check(lib().fbr_set_profiling(self._h, 1 if on else 0), "fbr_set_profiling")
 
     def kernel_time(self, name):

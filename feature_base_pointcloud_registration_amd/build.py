@@ -42,7 +42,8 @@ def _headers():
 
 
 def build_hip(verbose=False, force=False, defines=(), name="libfbr_hip.so"):
-    obj_dir = OBJ if not defines else OBJ + "_diag"
+    # one object directory per define set: a diagnostic variant never reuses another's objects
+    obj_dir = OBJ if not defines else OBJ + "_" + "_".join(sorted(d.lower() for d in defines))
     os.makedirs(obj_dir, exist_ok=True)
     out = os.path.join(HERE, name)
     hdrs = _headers()

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -92,6 +93,7 @@ struct fbr_ctx {
   unsigned long long* h_iter_flags = nullptr;  // host-mapped, written by k_gn_solve
   unsigned long long* d_iter_flags = nullptr;  // its device address
   unsigned long long gn_gen = 0;
+  std::set<std::string> profile_only;  // empty: time every kernel
   int32_t* d_iter_cnt = nullptr;
   unsigned char* d_feat_scratch = nullptr;  // k_features sorted-path slots [B*H][gslot_bytes]
   bool crop_cached = false;  // d_cropcnt holds the staged batch's CropBox statistics
@@ -121,6 +123,7 @@ namespace {
 void timer_begin(fbr_ctx* c, const char* name, hipEvent_t* ev_end) {
   *ev_end = nullptr;
   if (!c->profiling) return;
+  if (!c->profile_only.empty() && c->profile_only.count(name) == 0) return;
   KernelTimer& t = c->timers[name];
   std::pair<hipEvent_t, hipEvent_t> pr;
   if (!t.pool.empty()) {
@@ -919,6 +922,23 @@ extern "C" int fbr_diag_feature_stamps(fbr_ctx* c, unsigned long long* out /* [m
 int fbr_set_profiling(fbr_ctx* c, int enable) {
   if (!c) return FBR_ERR_INVALID_ARG;
   c->profiling = enable != 0;
+  return FBR_OK;
+}
+
+int fbr_set_profiling_kernels(fbr_ctx* c, const char* names) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  c->profile_only.clear();
+  if (!names) return FBR_OK;
+  std::string cur;
+  for (const char* q = names;; ++q) {
+    if (*q == ',' || *q == '\0') {
+      if (!cur.empty()) c->profile_only.insert(cur);
+      cur.clear();
+      if (*q == '\0') break;
+    } else {
+      cur.push_back(*q);
+    }
+  }
   return FBR_OK;
 }
 

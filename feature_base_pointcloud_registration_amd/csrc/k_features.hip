@@ -172,7 +172,7 @@ __device__ void greedy_rounds(int m, int lane, uint64_t (&und)[WMAX], uint64_t (
     bool any = false;
 #pragma unroll
     for (int w = 0; w < WMAX; ++w) {
-      if (w < nwm) {
+      if (w < nwm && und[w] != 0ull) {  // words whose candidates are all decided are skipped
         bool nt = false, tk = false;
         if ((und[w] >> lane) & 1ull) {
           const uint32_t wt = win10(w > 0 ? tak[w - 1] : 0ull, tak[w], w + 1 < WMAX ? tak[w + 1] : 0ull, lane);
@@ -576,7 +576,15 @@ k_features(FeatArgs a) {
     uint16_t* tlu = (uint16_t*)(tlv + segcap);
     uint16_t* vis = tlu + segcap;                      // taken corners in visit order
     bool direct = !has_stale;
+#ifdef FBR_FEAT_SKIP_CM
     if (direct) {
+      for (int u = lane; u <= m; u += 64) S.cm[u] = 0u;
+      __syncthreads();
+    }
+    if (false) {
+#else
+    if (direct) {
+#endif
       bool tf = false;
       for (int k0 = 0; k0 <= m; k0 += 64) {
         const int u = k0 + lane;
@@ -641,7 +649,9 @@ k_features(FeatArgs a) {
           und[w] = __ballot(cand);
           tak[w] = 0ull;
         }
+#ifndef FBR_FEAT_SKIP_CORNER
         greedy_rounds(m, lane, und, tak, [&](int u) { return S.cm[u] & 1023u; }, a, job);
+#endif
       };
       corner_walk();
       FBR_STAMP(4);
@@ -725,10 +735,12 @@ k_features(FeatArgs a) {
         und[w] = __ballot(cand);
         tak[w] = 0ull;
       }
+#ifndef FBR_FEAT_SKIP_SURF
       greedy_rounds(m, lane, und, tak, [&](int u) {
         const uint32_t c = S.cm[u];
         return ((c >> 10) & 1023u) & ~(c & 1023u);
       }, a, job);
+#endif
       FBR_STAMP(6);
 #pragma unroll
       for (int w = 0; w < WMAX; ++w) {

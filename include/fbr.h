@@ -178,6 +178,8 @@ int fbr_batch_bytes(fbr_ctx* ctx, double* bytes_total, double* bytes_gn);
 /* Kernel timing with HIP events recorded on the ctx stream around every launch of the named
  * kernel ("gn_residual", "project", ...). */
 int fbr_set_profiling(fbr_ctx* ctx, int enable);
+/* Restrict the timing to a comma-separated list of kernel names (NULL or "" = all kernels). */
+int fbr_set_profiling_kernels(fbr_ctx* ctx, const char* names);
 int fbr_kernel_time(fbr_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches);
 void* fbr_stream(fbr_ctx* ctx);
 
