@@ -109,11 +109,11 @@ __device__ __forceinline__ void or_range(const Bits& b, int lo, int hi) {
 }
 
 // Sequential walks (the reference loops verbatim) over S.seg[0..m] (seg[m] = the unsorted ep entry).
-__device__ void serial_walks(const FeatLds& S, const FeatArgs& a, int job, int m, const float4* CL,
-                             float4* corner_out, int& corner_cnt) {
+__device__ void serial_walks(const FeatLds& S, const SmoothEntry* ent, const FeatArgs& a, int job, int m,
+                             const float4* CL, float4* corner_out, int& corner_cnt) {
   int largestPickedNum = 0;
   for (int k = m; k >= 0; k--) {  // corners, k = ep .. sp (:208-242)
-    const int ind = S.seg[k].ind;
+    const int ind = ent[k].ind;
     const int li = ind - S.wlo;
     if (li < 0 || li + 5 >= S.L) { atomicOr(&a.err[job], 4); return; }
     if (!S.picked.get(li) && S.curv[li] > a.edge_thr) {
@@ -131,7 +131,7 @@ __device__ void serial_walks(const FeatLds& S, const FeatArgs& a, int job, int m
     }
   }
   for (int k = 0; k <= m; k++) {  // surf, k = sp .. ep (:245-276)
-    const int ind = S.seg[k].ind;
+    const int ind = ent[k].ind;
     const int li = ind - S.wlo;
     if (li < 0 || li + 5 >= S.L) { atomicOr(&a.err[job], 4); return; }
     if (!S.picked.get(li) && S.curv[li] < a.surf_thr) {
@@ -324,7 +324,12 @@ k_features(FeatArgs a) {
 #endif
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int H = a.H, W = a.W;
-  const int job = blockIdx.x / H, ring = blockIdx.x % H, lane = threadIdx.x;
+  // Ring 0 of every job first: its segment 0 holds the stale cloudSmoothness[4] slot and runs the
+  // serial walk, the longest wave of the launch; dispatching those waves first hides them behind
+  // the other rings instead of leaving the last jobs' ones in the tail.
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int job = b < a.B ? b : (b - a.B) / (H - 1);
+  const int ring = b < a.B ? 0 : 1 + (b - a.B) % (H - 1);
   const int64_t HW = (int64_t)H * W;
   const int n = a.nvalid[job];
   const int s = a.start_ring[job * H + ring], e = a.end_ring[job * H + ring];
@@ -474,7 +479,11 @@ k_features(FeatArgs a) {
       if (lane == 0) atomicOr(&a.err[job], 2);
       return;
     }
+#ifdef FBR_FEAT_SKIP_STALE
+    const bool has_stale = false;  // diagnostic ablation only
+#else
     const bool has_stale = (sp <= 4 && 4 < ep);
+#endif
     // Visit priority.  The greedy walks depend only on the relative priority of conflicting
     // neighbours, and the corner cap / output order only on the order of the taken corners, so
     // without ties among those no sort is needed: priorities come from curvature comparisons
@@ -631,7 +640,10 @@ k_features(FeatArgs a) {
     if (!direct) sorted_order();
     FBR_STAMP(3);
     if (has_stale) {
-      if (lane == 0) serial_walks(S, a, job, m, CL, corner_out, corner_cnt);
+      SmoothEntry* ent = (SmoothEntry*)S.rb;  // the walk's entries in LDS (region B is free here)
+      for (int k = lane; k <= m; k += 64) ent[k] = S.seg[k];
+      __syncthreads();
+      if (lane == 0) serial_walks(S, ent, a, job, m, CL, corner_out, corner_cnt);
       corner_cnt = __shfl(corner_cnt, 0);
       __syncthreads();
     } else {

@@ -30,7 +30,7 @@ print(f"{os.environ.get('FBR_VARIANT', 'base'):8s} features {ms / n:.3f} ms/laun
 sys.path.insert(0, R)
 from feature_base_pointcloud_registration_amd import build  # noqa: E402
 for var, defs in [("base", ()), ("no_cm", ("FBR_FEAT_SKIP_CM",)), ("no_corner", ("FBR_FEAT_SKIP_CORNER",)),
-                  ("no_surf", ("FBR_FEAT_SKIP_SURF",))]:
+                  ("no_surf", ("FBR_FEAT_SKIP_SURF",)), ("no_stale", ("FBR_FEAT_SKIP_STALE",))]:
     lib = build.build_hip(defines=defs + ("FBR_DIAG_VARIANT",), name=f"libfbr_hip_{var}.so") if defs else \
         build.build_hip()
     env = dict(os.environ, FBR_LIB=lib, FBR_VARIANT=var)
