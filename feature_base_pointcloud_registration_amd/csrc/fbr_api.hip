@@ -75,8 +75,6 @@ struct fbr_ctx {
   int8_t* d_label_stream = nullptr;   // [HW]   stream mode (persistent)
   float4* d_corner_slot = nullptr;
   int32_t* d_corner_cnt = nullptr;
-  float4* d_cand = nullptr;
-  int32_t* d_cand_cnt = nullptr;
   float4* d_surf_ring = nullptr;
   int32_t* d_surf_ring_cnt = nullptr;
   int32_t* d_err = nullptr;
@@ -328,26 +326,26 @@ int stage_features(fbr_ctx* c, int B, bool stream_mode) {
   }
   a.corner_slot = c->d_corner_slot;
   a.corner_cnt = c->d_corner_cnt;
-  a.cand = c->d_cand;
-  a.cand_cnt = c->d_cand_cnt;
   a.err = c->d_err;
   feat_caps(c->W, a);
   a.gscratch = c->d_feat_scratch;
   a.stamps = c->d_feat_stamps;
   CK(hipMemsetAsync(c->d_err, 0, sizeof(int32_t) * B, c->stream));
   TIMED(c, "features", launch_features(c->stream, a));
-  VgArgs v{};
-  v.s[0].in = c->d_cand;
-  v.s[0].stride_in = c->W;
-  v.s[0].cnt_in = c->d_cand_cnt;
-  v.s[0].cap = c->W;
-  v.s[0].out = c->d_surf_ring;
-  v.s[0].stride_out = c->W;
-  v.s[0].cnt_out = c->d_surf_ring_cnt;
-  v.s[0].scratch = c->d_vg_scratch;
-  v.s[0].leaf = c->P.odometry_surf_leaf_size;
-  v.s[0].nseg = B * c->H;
-  TIMED(c, "voxel_ring", launch_voxel_grid(c->stream, v));
+  VgRing v{};
+  v.cloud = c->d_cloud;
+  v.label = a.label;
+  v.start_ring = c->d_start;
+  v.end_ring = c->d_end;
+  v.B = B;
+  v.H = c->H;
+  v.HW = c->HW;
+  v.cap = c->W;
+  v.leaf = c->P.odometry_surf_leaf_size;
+  v.out = c->d_surf_ring;
+  v.stride_out = c->W;
+  v.cnt_out = c->d_surf_ring_cnt;
+  TIMED(c, "voxel_ring", launch_voxel_ring(c->stream, v));
   TIMED(c, "concat", launch_concat(c->stream, B, c->H, c->W, c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring,
                                    c->d_surf_ring_cnt, c->d_corner_all, c->HW, c->d_ncorner, c->d_surf_all, c->HW,
                                    c->d_nsurf));
@@ -592,7 +590,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_cloud, B * HW) || dalloc(&c->d_range, B * HW) || dalloc(&c->d_sstate, B) ||
               dalloc(&c->d_sstream, 1) || dalloc(&c->d_label, B * HW) || dalloc(&c->d_label_stream, HW) ||
               dalloc(&c->d_corner_slot, B * H * kCornerPerRing) || dalloc(&c->d_corner_cnt, B * H) ||
-              dalloc(&c->d_cand, B * HW) || dalloc(&c->d_cand_cnt, B * H) || dalloc(&c->d_surf_ring, B * HW) ||
+              dalloc(&c->d_surf_ring, B * HW) ||
               dalloc(&c->d_surf_ring_cnt, B * H) || dalloc(&c->d_err, B) || dalloc(&c->d_corner_all, B * HW) ||
               dalloc(&c->d_surf_all, B * HW) || dalloc(&c->d_cornerDS, B * HW) || dalloc(&c->d_surfDS, B * HW) ||
               dalloc(&c->d_ncorner, B) || dalloc(&c->d_nsurf, B) || dalloc(&c->d_ncds, B) || dalloc(&c->d_nsds, B) ||
@@ -628,7 +626,7 @@ int fbr_destroy(fbr_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_pts, c->d_nin, c->d_guess, c->d_owner, c->d_rowcnt, c->d_col, c->d_start, c->d_end,
                   c->d_nvalid, c->d_cloud, c->d_range, c->d_sstate, c->d_sstream, c->d_label, c->d_label_stream,
-                  c->d_corner_slot, c->d_corner_cnt, c->d_cand, c->d_cand_cnt, c->d_surf_ring, c->d_surf_ring_cnt,
+                  c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring, c->d_surf_ring_cnt,
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_map_c,

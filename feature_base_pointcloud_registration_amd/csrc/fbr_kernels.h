@@ -28,8 +28,6 @@ struct FeatArgs {
   int8_t* label;         // [B][H*W]
   float4* corner_slot;   // [B][H][120]
   int32_t* corner_cnt;   // [B][H]
-  float4* cand;          // [B][H][W]
-  int32_t* cand_cnt;     // [B][H]
   int32_t* err;          // [B]
   int lcap, segcap;      // LDS capacities (window length, segment length)
   int kseg;              // segment sort capacity: next power of two >= segcap - 1 (<= 1024)
@@ -61,6 +59,22 @@ struct VgArgs {
 };
 constexpr int64_t kVgLdsCap = 4096;  // segments up to this size sort entirely in LDS
 void launch_voxel_grid(hipStream_t s, const VgArgs& a);
+
+// Per-ring surf filter reading the projected cloud + label mask directly (no candidate copy).
+struct VgRing {
+  const float4* cloud;       // [B][H*W] projected cloud
+  const int8_t* label;       // [B][H*W] cloudLabel
+  const int32_t* start_ring; // [B][H]
+  const int32_t* end_ring;   // [B][H]
+  int B, H;
+  int64_t HW;
+  int64_t cap;               // Horizon_SCAN (max points per ring, <= 4096)
+  float leaf;
+  float4* out;               // [B*H][stride_out]
+  int64_t stride_out;
+  int32_t* cnt_out;          // [B*H]
+};
+void launch_voxel_ring(hipStream_t s, const VgRing& a);
 
 // Concatenate per-ring corner slots / per-ring surf DS outputs into per-job clouds (the
 // cornerCloud / surfaceCloud push_back order of featureExtraction.h:219,292).

@@ -28,8 +28,8 @@
 //     them is taken — final decisions, identical to the sequential walk.  The corner cap keeps the
 //     first 20 taken in visit order.  The segment holding the stale slot keeps the sequential walk
 //     (its stale index may duplicate a member).
-// Outputs: label (the feature mask), per-ring corner slots in visit order, per-ring surf
-// candidates (label <= 0, index order) for the per-ring VoxelGrid (k_voxel.hip).
+// Outputs: label (the feature mask) and per-ring corner slots in visit order; the per-ring surf
+// candidates (label <= 0, index order) are read from the mask by the per-ring VoxelGrid.
 #include "fbr_common.h"
 #include "fbr_kernels.h"
 #include "fbr_sort.h"
@@ -336,10 +336,7 @@ k_features(FeatArgs a) {
   const int cb = s - 4, ca = e + 6;  // this ring's points [cb, ca)
   const int slot = job * H + ring;
   if (ca <= cb) {
-    if (lane == 0) {
-      a.corner_cnt[slot] = 0;
-      a.cand_cnt[slot] = 0;
-    }
+    if (lane == 0) a.corner_cnt[slot] = 0;
     return;
   }
   FeatLds S;
@@ -467,9 +464,8 @@ k_features(FeatArgs a) {
   FBR_STAMP(1);
 
   // ---- extractFeatures (:188-285) ----
-  int corner_cnt = 0, cand_cnt = 0;
+  int corner_cnt = 0;
   float4* corner_out = a.corner_slot + (int64_t)slot * kCornerPerRing;
-  float4* cand_out = a.cand + (int64_t)slot * W;
   for (int j = 0; j < 6; j++) {
     const int sp = (s * (6 - j) + e * j) / 6;
     const int ep = (s * (5 - j) + e * (j + 1)) / 6 - 1;
@@ -767,15 +763,8 @@ k_features(FeatArgs a) {
       __syncthreads();
     }
     FBR_STAMP(7);
-    // surf candidates: label[k] <= 0 for k in [sp, ep] (:279-284), index order
-    for (int t0 = 0; t0 <= m; t0 += 64) {
-      const int t = t0 + lane;
-      const bool c = t <= m && !S.labpos.get(sp + t - S.wlo);
-      const uint64_t mk = __ballot(c);
-      if (c) cand_out[cand_cnt + __popcll(mk & ((1ull << lane) - 1ull))] = CL[sp + t];
-      cand_cnt += __popcll(mk);
-    }
-    __syncthreads();
+    // surf candidates (label <= 0 in [sp, ep], :279-284) are selected by the per-ring VoxelGrid
+    // straight from the label mask (k_voxel.hip, k_voxel_ring)
     FBR_STAMP(8);
   }
   // ---- outputs ----
@@ -787,10 +776,7 @@ k_features(FeatArgs a) {
     else if (k < 5 && lab != 0) LB[k] = lab;   // stale slots keep earlier values
   }
   if (cb <= 0 && lane < 5 && lane < S.L) st->picked04[lane] = S.picked.get(lane) ? 1 : 0;
-  if (lane == 0) {
-    a.corner_cnt[slot] = corner_cnt;
-    a.cand_cnt[slot] = cand_cnt;
-  }
+  if (lane == 0) a.corner_cnt[slot] = corner_cnt;
 #ifdef FBR_FEAT_STAMPS
   FBR_STAMP(9);
   if (lane == 0 && a.stamps)

@@ -77,37 +77,13 @@ __device__ void block_exclusive_scan(uint32_t* arr, int nb, uint32_t* wsum) {
   __syncthreads();
 }
 
-template <int T, typename V, bool LDS>
-__global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
+// ---- shared pieces of the two VoxelGrid front ends ----
+
+// Block-wide float min / max (getMinMax3D) of per-thread partials; mm = [NW][6] LDS.
+template <int T>
+__device__ void vg_block_minmax(float (&mn)[3], float (&mx)[3], float* mm) {
   constexpr int NW = T / 64;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int seg = blockIdx.x;
-  const bool second = seg >= A.s[0].nseg;
-  const VgSet S = second ? A.s[1] : A.s[0];
-  if (second) seg -= A.s[0].nseg;
-  uint32_t* hist = (uint32_t*)smem;  // [NW + 1][512]: per-wave digit counters + digit totals
-  uint32_t* wsum = hist + (NW + 1) * 512;
-  float* mm = (float*)(wsum + NW);
-  int* misc = (int*)(mm + NW * 6);
-  const int n = (int)min((int64_t)S.cnt_in[seg], S.cap);
-  const float4* in = S.in + (int64_t)seg * S.stride_in;
-  float4* out = S.out + (int64_t)seg * S.stride_out;
-  if (n <= 0) {
-    if (tid == 0) S.cnt_out[seg] = 0;
-    return;
-  }
-  // getMinMax3D (float min / max)
-  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-  for (int i = tid; i < n; i += T) {
-    const float4 p = in[i];
-    const float v[3] = {p.x, p.y, p.z};
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
-      mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
-    }
-  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int d = 0; d < 3; ++d)
     for (int o = 32; o > 0; o >>= 1) {
@@ -130,71 +106,66 @@ __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
       mx[d] = (mx[d] < b) ? b : mx[d];
     }
   }
-  const float inv = 1.0f / S.leaf;
-  const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
-  const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
-  const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
-  if (dx * dy * dz > (int64_t)INT32_MAX) {  // PCL: "Leaf size is too small" -> output = input
-    for (int i = tid; i < n; i += T) out[i] = in[i];
-    if (tid == 0) S.cnt_out[seg] = n;
-    return;
-  }
-  int min_b[3], div_b[3];
-  for (int d = 0; d < 3; ++d) {
-    min_b[d] = (int)floorf(mn[d] * inv);
-    const int max_b = (int)floorf(mx[d] * inv);
-    div_b[d] = max_b - min_b[d] + 1;
-  }
-  const uint32_t mul1 = (uint32_t)div_b[0], mul2 = (uint32_t)div_b[0] * (uint32_t)div_b[1];
-  const bool morton = S.morton && div_b[0] <= 1024 && div_b[1] <= 1024 && div_b[2] <= 1024;
-  int nbits = 32;
-  if (morton) {
-    int b = 1;
-    for (int d = 0; d < 3; ++d)
-      if (div_b[d] > 1) b = max(b, 32 - __clz((uint32_t)(div_b[d] - 1)));
-    nbits = 3 * b;
-  } else {
-    const uint64_t nkeys = (uint64_t)div_b[0] * (uint64_t)div_b[1] * (uint64_t)div_b[2];
-    if (nkeys <= 0xFFFFFFFFull) {
-      const uint32_t maxk = (uint32_t)(nkeys - 1);
-      nbits = maxk == 0 ? 1 : 32 - __clz(maxk);
+}
+
+// PCL applyFilter's grid (leaf inverse, min_b, div_b) and the key function.
+struct VgGrid {
+  float inv;
+  int min_b[3];
+  uint32_t mul1, mul2;
+  bool morton, overflow;
+  int nbits;
+  __device__ void init(const float (&mn)[3], const float (&mx)[3], float leaf, bool want_morton) {
+    inv = 1.0f / leaf;
+    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+    overflow = dx * dy * dz > (int64_t)INT32_MAX;  // PCL: "Leaf size is too small" -> output = input
+    int div_b[3];
+    for (int d = 0; d < 3; ++d) {
+      min_b[d] = (int)floorf(mn[d] * inv);
+      const int max_b = (int)floorf(mx[d] * inv);
+      div_b[d] = max_b - min_b[d] + 1;
+    }
+    mul1 = (uint32_t)div_b[0];
+    mul2 = (uint32_t)div_b[0] * (uint32_t)div_b[1];
+    morton = want_morton && div_b[0] <= 1024 && div_b[1] <= 1024 && div_b[2] <= 1024;
+    nbits = 32;
+    if (morton) {
+      int b = 1;
+      for (int d = 0; d < 3; ++d)
+        if (div_b[d] > 1) b = max(b, 32 - __clz((uint32_t)(div_b[d] - 1)));
+      nbits = 3 * b;
+    } else {
+      const uint64_t nkeys = (uint64_t)div_b[0] * (uint64_t)div_b[1] * (uint64_t)div_b[2];
+      if (nkeys <= 0xFFFFFFFFull) {
+        const uint32_t maxk = (uint32_t)(nkeys - 1);
+        nbits = maxk == 0 ? 1 : 32 - __clz(maxk);
+      }
     }
   }
-  // (key, index) buffers
-  uint32_t* kb[2];
-  V* vb[2];
-  if constexpr (LDS) {
-    unsigned char* q = (unsigned char*)(((uintptr_t)(misc + 4) + 15) & ~(uintptr_t)15);
-    const int cap = (int)S.cap;
-    kb[0] = (uint32_t*)q;
-    kb[1] = kb[0] + cap;
-    vb[0] = (V*)(kb[1] + cap);
-    vb[1] = vb[0] + cap;
-  } else {
-    uint32_t* sc = S.scratch + (int64_t)seg * 4 * S.cap;
-    kb[0] = sc;
-    kb[1] = sc + S.cap;
-    vb[0] = (V*)(sc + 2 * S.cap);
-    vb[1] = (V*)(sc + 3 * S.cap);
-  }
-  for (int i = tid; i < n; i += T) {
-    const float4 p = in[i];
+  __device__ __forceinline__ uint32_t key(const float4& p) const {
     const int ijk0 = (int)(floorf(p.x * inv) - (float)min_b[0]);
     const int ijk1 = (int)(floorf(p.y * inv) - (float)min_b[1]);
     const int ijk2 = (int)(floorf(p.z * inv) - (float)min_b[2]);
-    kb[0][i] = morton ? (spread3_10((uint32_t)ijk0) | (spread3_10((uint32_t)ijk1) << 1) |
-                         (spread3_10((uint32_t)ijk2) << 2))
-                      : (uint32_t)ijk0 + (uint32_t)ijk1 * mul1 + (uint32_t)ijk2 * mul2;
-    vb[0][i] = (V)i;
+    return morton ? (spread3_10((uint32_t)ijk0) | (spread3_10((uint32_t)ijk1) << 1) | (spread3_10((uint32_t)ijk2) << 2))
+                  : (uint32_t)ijk0 + (uint32_t)ijk1 * mul1 + (uint32_t)ijk2 * mul2;
   }
-  __syncthreads();
-  // ---- radix sort: passes of <= 9-bit digits ----
-  const int passes = (nbits + 8) / 9;
+};
+
+// Stable radix sort of kb[0]/vb[0] (n pairs), then one centroid per run of equal keys in
+// ascending key order: out[v] = mean of in[vals of the run].  Returns the voxel count (all threads).
+template <int T, typename V, int MAXD = 9>
+__device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, uint32_t* hist, uint32_t* wsum,
+                            const float4* in, float4* out) {
+  constexpr int NW = T / 64, NB = 1 << MAXD;  // digits of <= MAXD bits; hist rows of NB counters
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int passes = (nbits + MAXD - 1) / MAXD;
   const int dbits = (nbits + passes - 1) / passes;
   const int nbins = 1 << dbits;
   const int chunk = (((n + NW - 1) / NW) + 63) & ~63;
   const int c0 = min(n, w * chunk), c1 = min(n, c0 + chunk);
-  uint32_t* hw = hist + w * 512;
+  uint32_t* hw = hist + w * NB;
   int cur = 0;
   for (int pass = 0; pass < passes; ++pass) {
     const int shift = dbits * pass;
@@ -203,7 +174,7 @@ __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
     const V* vin = vb[cur];
     uint32_t* kout = kb[cur ^ 1];
     V* vout = vb[cur ^ 1];
-    for (int b = tid; b < NW * 512; b += T) hist[b] = 0u;
+    for (int b = tid; b < NW * NB; b += T) hist[b] = 0u;
     __syncthreads();
     for (int i = c0 + lane; i < c1; i += 64) atomicAdd(&hw[(kin[i] >> shift) & dmask], 1u);
     __syncthreads();
@@ -211,17 +182,17 @@ __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
     for (int d = tid; d < nbins; d += T) {
       uint32_t run = 0;
       for (int ww = 0; ww < NW; ++ww) {
-        const uint32_t t = hist[ww * 512 + d];
-        hist[ww * 512 + d] = run;
+        const uint32_t t = hist[ww * NB + d];
+        hist[ww * NB + d] = run;
         run += t;
       }
-      hist[NW * 512 + d] = run;  // digit totals: the extra row NW
+      hist[NW * NB + d] = run;  // digit totals: the extra row NW
     }
     __syncthreads();
-    block_exclusive_scan<T>(hist + NW * 512, nbins, wsum);
+    block_exclusive_scan<T>(hist + NW * NB, nbins, wsum);
     for (int d = tid; d < nbins; d += T) {
-      const uint32_t base = hist[NW * 512 + d];
-      for (int ww = 0; ww < NW; ++ww) hist[ww * 512 + d] += base;
+      const uint32_t base = hist[NW * NB + d];
+      for (int ww = 0; ww < NW; ++ww) hist[ww * NB + d] += base;
     }
     __syncthreads();
     for (int i0 = c0; i0 < c1; i0 += 64) {
@@ -282,7 +253,191 @@ __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
     }
     pos += __popcll(bal);
   }
+  return total;
+}
+
+// Generic front end: segments of a VgArgs (per-job mapping DS, start-up map filter, fbr_voxel_grid).
+template <int T, typename V, bool LDS>
+__global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
+  constexpr int NW = T / 64;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  int seg = blockIdx.x;
+  const bool second = seg >= A.s[0].nseg;
+  const VgSet S = second ? A.s[1] : A.s[0];
+  if (second) seg -= A.s[0].nseg;
+  uint32_t* hist = (uint32_t*)smem;  // [NW + 1][512]: per-wave digit counters + digit totals
+  uint32_t* wsum = hist + (NW + 1) * 512;
+  float* mm = (float*)(wsum + NW);
+  int* misc = (int*)(mm + NW * 6);
+  const int n = (int)min((int64_t)S.cnt_in[seg], S.cap);
+  const float4* in = S.in + (int64_t)seg * S.stride_in;
+  float4* out = S.out + (int64_t)seg * S.stride_out;
+  if (n <= 0) {
+    if (tid == 0) S.cnt_out[seg] = 0;
+    return;
+  }
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int i = tid; i < n; i += T) {
+    const float4 p = in[i];
+    const float v[3] = {p.x, p.y, p.z};
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
+      mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
+    }
+  }
+  vg_block_minmax<T>(mn, mx, mm);
+  VgGrid G;
+  G.init(mn, mx, S.leaf, S.morton != 0);
+  if (G.overflow) {
+    for (int i = tid; i < n; i += T) out[i] = in[i];
+    if (tid == 0) S.cnt_out[seg] = n;
+    return;
+  }
+  uint32_t* kb[2];
+  V* vb[2];
+  if constexpr (LDS) {
+    unsigned char* q = (unsigned char*)(((uintptr_t)(misc + 4) + 15) & ~(uintptr_t)15);
+    const int cap = (int)S.cap;
+    kb[0] = (uint32_t*)q;
+    kb[1] = kb[0] + cap;
+    vb[0] = (V*)(kb[1] + cap);
+    vb[1] = vb[0] + cap;
+  } else {
+    uint32_t* sc = S.scratch + (int64_t)seg * 4 * S.cap;
+    kb[0] = sc;
+    kb[1] = sc + S.cap;
+    vb[0] = (V*)(sc + 2 * S.cap);
+    vb[1] = (V*)(sc + 3 * S.cap);
+  }
+  for (int i = tid; i < n; i += T) {
+    kb[0][i] = G.key(in[i]);
+    vb[0][i] = (V)i;
+  }
+  __syncthreads();
+  const int total = vg_sort_emit<T, V>(kb, vb, n, G.nbits, hist, wsum, in, out);
   if (tid == 0) S.cnt_out[seg] = total;
+}
+
+// Per-ring front end (featureExtraction.h:279-292): the surf candidates of (job, ring) are the
+// points k of the ring's non-empty segments [sp, ep] (sp < ep, :195-200) with cloudLabel[k] <= 0,
+// in index order, read straight from the projected cloud and the label mask (the label of
+// index 4 may be stale across scans exactly as the reference's cloudLabel[4]).  One register
+// pass feeds min/max, the keys and the compaction; the sort runs in LDS (u16 ring offsets).
+template <int T, int KPT>
+__global__ void __launch_bounds__(T) k_voxel_ring(VgRing A) {
+  constexpr int NW = T / 64, MAXD = 8;  // 8-bit digits: 3 passes cover the <= 24-bit ring keys
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int slot = blockIdx.x, job = slot / A.H;
+  uint32_t* hist = (uint32_t*)smem;
+  uint32_t* wsum = hist + (NW + 1) * (1 << MAXD);
+  float* mm = (float*)(wsum + NW);
+  int* cnts = (int*)(mm + NW * 6);  // [KPT][NW]
+  const int s = A.start_ring[slot], e = A.end_ring[slot];
+  float4* out = A.out + (int64_t)slot * A.stride_out;
+  if (e <= s) {
+    if (tid == 0) A.cnt_out[slot] = 0;
+    return;
+  }
+  int sp6[6], ep6[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    sp6[j] = (s * (6 - j) + e * j) / 6;
+    ep6[j] = (s * (5 - j) + e * (j + 1)) / 6 - 1;
+  }
+  const float4* CL = A.cloud + (int64_t)job * A.HW + s;
+  const int8_t* LB = A.label + (int64_t)job * A.HW;
+  float4 pt[KPT];
+  bool cd[KPT];
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+#pragma unroll
+  for (int r = 0; r < KPT; ++r) {
+    const int k = s + r * T + tid;
+    bool in = false;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) in |= sp6[j] < ep6[j] && k >= sp6[j] && k <= ep6[j];
+    cd[r] = in && LB[k] <= 0;
+    pt[r] = cd[r] ? CL[k - s] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (cd[r]) {
+      const float v[3] = {pt[r].x, pt[r].y, pt[r].z};
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
+        mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
+      }
+    }
+  }
+  // compaction positions in index order: per step r, waves in order
+  uint64_t bal[KPT];
+#pragma unroll
+  for (int r = 0; r < KPT; ++r) {
+    bal[r] = __ballot(cd[r]);
+    if (lane == 0) cnts[r * NW + w] = __popcll(bal[r]);
+  }
+  vg_block_minmax<T>(mn, mx, mm);  // (its barrier also publishes cnts)
+  int n = 0, pos[KPT];
+#pragma unroll
+  for (int r = 0; r < KPT; ++r) {
+    int before = 0, all = 0;
+    for (int ww = 0; ww < NW; ++ww) {
+      const int c = cnts[r * NW + ww];
+      before += ww < w ? c : 0;
+      all += c;
+    }
+    pos[r] = n + before + __popcll(bal[r] & ((1ull << lane) - 1ull));
+    n += all;
+  }
+  if (n == 0) {
+    if (tid == 0) A.cnt_out[slot] = 0;
+    return;
+  }
+  VgGrid G;
+  G.init(mn, mx, A.leaf, false);
+  unsigned char* q = (unsigned char*)(((uintptr_t)(cnts + KPT * NW) + 15) & ~(uintptr_t)15);
+  uint32_t* kb[2];
+  uint16_t* vb[2];
+  kb[0] = (uint32_t*)q;
+  kb[1] = kb[0] + A.cap;
+  vb[0] = (uint16_t*)(kb[1] + A.cap);
+  vb[1] = vb[0] + A.cap;
+  if (G.overflow) {  // output = input, in index order
+#pragma unroll
+    for (int r = 0; r < KPT; ++r)
+      if (cd[r]) out[pos[r]] = pt[r];
+    if (tid == 0) A.cnt_out[slot] = n;
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < KPT; ++r)
+    if (cd[r]) {
+      kb[0][pos[r]] = G.key(pt[r]);
+      vb[0][pos[r]] = (uint16_t)(r * T + tid);  // offset from the ring start s
+    }
+  __syncthreads();
+  const int total = vg_sort_emit<T, uint16_t, MAXD>(kb, vb, n, G.nbits, hist, wsum, CL, out);
+  if (tid == 0) A.cnt_out[slot] = total;
+}
+
+size_t voxel_ring_lds_bytes(const VgRing& a, int threads, int kpt) {
+  const int nw = threads / 64;
+  size_t b = sizeof(uint32_t) * ((size_t)(nw + 1) * 256 + nw) + sizeof(float) * nw * 6 + sizeof(int) * kpt * nw;
+  b = (b + 15) & ~(size_t)15;
+  return b + (size_t)a.cap * 2 * (sizeof(uint32_t) + sizeof(uint16_t)) + 16;
+}
+
+void launch_voxel_ring(hipStream_t s, const VgRing& a) {
+  const int nseg = a.B * a.H;
+  if (nseg <= 0) return;
+  // 512 threads, KPT = ceil(W / 512) points per thread (instances up to W = 4096)
+  const int kpt = (int)((a.cap + 511) / 512);
+  if (kpt <= 2)
+    hipLaunchKernelGGL((k_voxel_ring<512, 2>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 2), s, a);
+  else if (kpt <= 4)
+    hipLaunchKernelGGL((k_voxel_ring<512, 4>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 4), s, a);
+  else
+    hipLaunchKernelGGL((k_voxel_ring<512, 8>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 8), s, a);
 }
 
 size_t voxel_lds_bytes(const VgArgs& a, int threads, bool lds_mode) {
