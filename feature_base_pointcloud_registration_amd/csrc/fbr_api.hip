@@ -56,8 +56,11 @@ int dalloc(T** p, size_t count) {
 struct fbr_ctx {
   fbr_params P;
   int dev = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // primary stream (single-scan calls, batch sub-batch 0, export)
+  hipStream_t stream2 = nullptr;  // batch sub-batch 1
+  hipEvent_t join_ev = nullptr;   // stream2 -> stream join at the end of a batch launch
   int H = 0, W = 0, Bcap = 0;
+  int items_per_job = 0;
   int64_t HW = 0, NMAX = 0;
   // inputs
   fbr_point_xyzirt* d_pts = nullptr;
@@ -118,7 +121,7 @@ struct fbr_ctx {
 
 namespace {
 
-void timer_begin(fbr_ctx* c, const char* name, hipEvent_t* ev_end) {
+void timer_begin(fbr_ctx* c, hipStream_t st, const char* name, hipEvent_t* ev_end) {
   *ev_end = nullptr;
   if (!c->profiling) return;
   if (!c->profile_only.empty() && c->profile_only.count(name) == 0) return;
@@ -131,21 +134,23 @@ void timer_begin(fbr_ctx* c, const char* name, hipEvent_t* ev_end) {
     (void)hipEventCreate(&pr.first);
     (void)hipEventCreate(&pr.second);
   }
-  (void)hipEventRecord(pr.first, c->stream);
+  (void)hipEventRecord(pr.first, st);
   t.pending.push_back(pr);
   *ev_end = pr.second;
 }
-void timer_end(fbr_ctx* c, hipEvent_t ev_end) {
-  if (ev_end) (void)hipEventRecord(ev_end, c->stream);
+void timer_end(hipStream_t st, hipEvent_t ev_end) {
+  if (ev_end) (void)hipEventRecord(ev_end, st);
 }
 
-#define TIMED(ctx, name, launch)      \
-  do {                                \
-    hipEvent_t ev_;                   \
-    timer_begin(ctx, name, &ev_);     \
-    launch;                           \
-    timer_end(ctx, ev_);              \
+// Kernel launch bracketed by HIP events on the stream it is launched on (when profiling).
+#define TIMED_ON(ctx, st, name, launch)   \
+  do {                                    \
+    hipEvent_t ev_;                       \
+    timer_begin(ctx, st, name, &ev_);     \
+    launch;                               \
+    timer_end(st, ev_);                   \
   } while (0)
+#define TIMED(ctx, name, launch) TIMED_ON(ctx, (ctx)->stream, name, launch)
 
 int64_t seg_cap(int W) { return W / 6 + 8; }
 
@@ -294,94 +299,113 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
 // ---------------------------------------------------------------------------------------------
 // pipeline stages
 // ---------------------------------------------------------------------------------------------
-int stage_project(fbr_ctx* c, int B) {
-  CK(hipMemsetAsync(c->d_owner, 0x7F, sizeof(int32_t) * B * c->HW, c->stream));
-  TIMED(c, "project", launch_project(c->stream, c->d_pts, c->d_nin, c->NMAX, B, c->H, c->W, c->d_owner));
-  TIMED(c, "extract", launch_extract(c->stream, c->d_pts, c->NMAX, c->d_owner, B, c->H, c->W, c->d_rowcnt,
-                                     c->d_cloud, c->d_col, c->d_range, c->d_start, c->d_end, c->d_nvalid));
+// A contiguous sub-batch of jobs [j0, j0 + B) driven on one stream.  The stages below offset every
+// per-job device array by j0, and the Gauss-Newton work-item arrays by j0 * items_per_job, so
+// sub-batches share the context's buffers without overlapping.
+struct Sub {
+  int j0, B, k;  // first job, job count, sub-batch index (0 or 1)
+  hipStream_t st;
+};
+
+Sub single_sub(fbr_ctx* c) { return Sub{0, 1, 0, c->stream}; }
+
+int stage_project(fbr_ctx* c, const Sub& sb) {
+  const int64_t j0 = sb.j0;
+  int32_t* owner = c->d_owner + j0 * c->HW;
+  CK(hipMemsetAsync(owner, 0x7F, sizeof(int32_t) * sb.B * c->HW, sb.st));
+  TIMED_ON(c, sb.st, "project", launch_project(sb.st, c->d_pts + j0 * c->NMAX, c->d_nin + j0, c->NMAX, sb.B, c->H,
+                                               c->W, owner));
+  TIMED_ON(c, sb.st, "extract",
+           launch_extract(sb.st, c->d_pts + j0 * c->NMAX, c->NMAX, owner, sb.B, c->H, c->W, c->d_rowcnt + j0 * c->H,
+                          c->d_cloud + j0 * c->HW, c->d_col + j0 * c->HW, c->d_range + j0 * c->HW,
+                          c->d_start + j0 * c->H, c->d_end + j0 * c->H, c->d_nvalid + j0));
   return FBR_OK;
 }
 
-int stage_features(fbr_ctx* c, int B, bool stream_mode) {
+int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode) {
+  const int64_t j0 = sb.j0, HW = c->HW, H = c->H;
   FeatArgs a{};
-  a.B = B;
+  a.B = sb.B;
   a.H = c->H;
   a.W = c->W;
-  a.cloud = c->d_cloud;
-  a.col = c->d_col;
-  a.range = c->d_range;
-  a.start_ring = c->d_start;
-  a.end_ring = c->d_end;
-  a.nvalid = c->d_nvalid;
+  a.cloud = c->d_cloud + j0 * HW;
+  a.col = c->d_col + j0 * HW;
+  a.range = c->d_range + j0 * HW;
+  a.start_ring = c->d_start + j0 * H;
+  a.end_ring = c->d_end + j0 * H;
+  a.nvalid = c->d_nvalid + j0;
   a.edge_thr = c->P.edge_threshold;
   a.surf_thr = c->P.surf_threshold;
   if (stream_mode) {
     a.stream = c->d_sstream;
     a.label = c->d_label_stream;
   } else {
-    CK(hipMemsetAsync(c->d_sstate, 0, sizeof(StreamState) * B, c->stream));
-    CK(hipMemsetAsync(c->d_label, 0, (size_t)B * c->HW, c->stream));
-    a.stream = c->d_sstate;
-    a.label = c->d_label;
+    CK(hipMemsetAsync(c->d_sstate + j0, 0, sizeof(StreamState) * sb.B, sb.st));
+    CK(hipMemsetAsync(c->d_label + j0 * HW, 0, (size_t)sb.B * HW, sb.st));
+    a.stream = c->d_sstate + j0;
+    a.label = c->d_label + j0 * HW;
   }
-  a.corner_slot = c->d_corner_slot;
-  a.corner_cnt = c->d_corner_cnt;
-  a.err = c->d_err;
+  a.corner_slot = c->d_corner_slot + j0 * H * kCornerPerRing;
+  a.corner_cnt = c->d_corner_cnt + j0 * H;
+  a.err = c->d_err + j0;
   feat_caps(c->W, a);
-  a.gscratch = c->d_feat_scratch;
-  a.stamps = c->d_feat_stamps;
-  CK(hipMemsetAsync(c->d_err, 0, sizeof(int32_t) * B, c->stream));
-  TIMED(c, "features", launch_features(c->stream, a));
+  a.gscratch = c->d_feat_scratch + j0 * H * a.gslot_bytes;
+  a.stamps = c->d_feat_stamps ? c->d_feat_stamps + j0 * H * 12 : nullptr;
+  CK(hipMemsetAsync(c->d_err + j0, 0, sizeof(int32_t) * sb.B, sb.st));
+  TIMED_ON(c, sb.st, "features", launch_features(sb.st, a));
   VgRing v{};
-  v.cloud = c->d_cloud;
+  v.cloud = a.cloud;
   v.label = a.label;
-  v.start_ring = c->d_start;
-  v.end_ring = c->d_end;
-  v.B = B;
+  v.start_ring = a.start_ring;
+  v.end_ring = a.end_ring;
+  v.B = sb.B;
   v.H = c->H;
-  v.HW = c->HW;
+  v.HW = HW;
   v.cap = c->W;
   v.leaf = c->P.odometry_surf_leaf_size;
-  v.out = c->d_surf_ring;
+  v.out = c->d_surf_ring + j0 * HW;
   v.stride_out = c->W;
-  v.cnt_out = c->d_surf_ring_cnt;
-  TIMED(c, "voxel_ring", launch_voxel_ring(c->stream, v));
-  TIMED(c, "concat", launch_concat(c->stream, B, c->H, c->W, c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring,
-                                   c->d_surf_ring_cnt, c->d_corner_all, c->HW, c->d_ncorner, c->d_surf_all, c->HW,
-                                   c->d_nsurf));
+  v.cnt_out = c->d_surf_ring_cnt + j0 * H;
+  TIMED_ON(c, sb.st, "voxel_ring", launch_voxel_ring(sb.st, v));
+  TIMED_ON(c, sb.st, "concat",
+           launch_concat(sb.st, sb.B, c->H, c->W, a.corner_slot, a.corner_cnt, v.out, v.cnt_out,
+                         c->d_corner_all + j0 * HW, HW, c->d_ncorner + j0, c->d_surf_all + j0 * HW, HW,
+                         c->d_nsurf + j0));
   return FBR_OK;
 }
 
-GnArgs gn_args(fbr_ctx* c, int B, bool trace) {
+GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
+  const int64_t j0 = sb.j0, HW = c->HW, ib = j0 * c->items_per_job;
+  const int mi = std::max(1, c->P.max_iterations);
   GnArgs a{};
-  a.B = B;
+  a.B = sb.B;
   a.max_iter = c->P.max_iterations;
-  a.cornerDS = c->d_cornerDS;
-  a.capc = c->HW;
-  a.ncds = c->d_ncds;
-  a.surfDS = c->d_surfDS;
-  a.caps = c->HW;
-  a.nsds = c->d_nsds;
+  a.cornerDS = c->d_cornerDS + j0 * HW;
+  a.capc = HW;
+  a.ncds = c->d_ncds + j0;
+  a.surfDS = c->d_surfDS + j0 * HW;
+  a.caps = HW;
+  a.nsds = c->d_nsds + j0;
   a.mc = MapGrid{c->d_map_c, c->d_cs_c, c->gc};
   a.ms = MapGrid{c->d_map_s, c->d_cs_s, c->gs};
-  a.gn = c->d_gn;
-  a.guess = c->d_guess;
-  a.items = c->d_items;
-  a.nitems = c->d_nitems;
-  a.item_range = c->d_item_range;
-  a.partial = c->d_partial;
-  a.max_items = c->max_items;
+  a.gn = c->d_gn + j0;
+  a.guess = c->d_guess + j0 * 6;
+  a.items = c->d_items + ib;
+  a.nitems = c->d_nitems + sb.k;
+  a.item_range = c->d_item_range + j0 * 2;
+  a.partial = c->d_partial + ib * 32;
+  a.max_items = sb.B * c->items_per_job;
   a.edge_min = c->P.edge_feature_min_valid_num;
   a.surf_min = c->P.surf_feature_min_valid_num;
   for (int k = 0; k < 3; ++k) a.crop_half[k] = c->P.crop_half[k];
   a.rot_tol = c->P.rotation_tollerance;
   a.z_tol = c->P.z_tollerance;
-  a.pose_out = c->d_pose_out;
-  a.stats = c->d_stats;
-  a.trace = trace ? c->d_trace : nullptr;
-  a.nbr = c->d_nbr;
-  a.iter_flags = c->d_iter_flags;
-  a.iter_cnt = c->d_iter_cnt;
+  a.pose_out = c->d_pose_out + j0 * 6;
+  a.stats = c->d_stats + j0;
+  a.trace = trace ? c->d_trace + j0 * c->P.max_iterations * 6 : nullptr;
+  a.nbr = c->d_nbr + ib * 5 * 256;
+  a.iter_flags = c->d_iter_flags + (int64_t)sb.k * mi;
+  a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 2 * mi;
   return a;
 }
 
@@ -393,63 +417,91 @@ void drop_staged_batch(fbr_ctx* c) {
   c->crop_cached = false;
 }
 
-int crop_stats(fbr_ctx* c, int B) {
-  GnArgs a = gn_args(c, B, false);
-  CK(hipMemsetAsync(c->d_cropcnt, 0, sizeof(int32_t) * 2 * B, c->stream));
-  TIMED(c, "crop", launch_crop_count(c->stream, a, c->d_map_c, c->gc.n_points, 0, c->d_cropcnt));
-  TIMED(c, "crop", launch_crop_count(c->stream, a, c->d_map_s, c->gs.n_points, 1, c->d_cropcnt));
+int crop_stats(fbr_ctx* c, const Sub& sb) {
+  GnArgs a = gn_args(c, sb, false);
+  int32_t* cnt = c->d_cropcnt + (int64_t)sb.j0 * 2;
+  CK(hipMemsetAsync(cnt, 0, sizeof(int32_t) * 2 * sb.B, sb.st));
+  TIMED_ON(c, sb.st, "crop", launch_crop_count(sb.st, a, c->d_map_c, c->gc.n_points, 0, cnt));
+  TIMED_ON(c, sb.st, "crop", launch_crop_count(sb.st, a, c->d_map_s, c->gs.n_points, 1, cnt));
   return FBR_OK;
 }
 
-int stage_register(fbr_ctx* c, int B, bool trace) {
-  if (!c->has_map) return FBR_ERR_NO_MAP;
-  // downsampleCurrentScan (mapOptmization.h:981-993): corner and surf filters in one launch;
-  // Morton voxel order (internal clouds: spatially compact query order for the kNN waves)
+// downsampleCurrentScan (mapOptmization.h:981-993) + the Gauss-Newton set-up of a sub-batch.
+int register_prepare(fbr_ctx* c, const Sub& sb, bool trace) {
+  const int64_t j0 = sb.j0, HW = c->HW;
+  // corner and surf filters in one launch; Morton voxel order (internal clouds: spatially compact
+  // query order for the kNN waves)
   VgArgs v{};
-  const int64_t ccap = std::min<int64_t>(c->HW, (int64_t)kCornerPerRing * c->H);
-  v.s[0] = VgSet{c->d_surf_all, c->HW, c->d_nsurf, c->HW, c->d_surfDS, c->HW, c->d_nsds, c->d_vg_scratch,
-                 c->P.mapping_surf_leaf_size, B, 1};
-  v.s[1] = VgSet{c->d_corner_all, c->HW, c->d_ncorner, ccap, c->d_cornerDS, c->HW, c->d_ncds,
-                 c->d_vg_scratch + (int64_t)B * 4 * c->HW, c->P.mapping_corner_leaf_size, B, 1};
-  TIMED(c, "voxel_scan", launch_voxel_grid(c->stream, v));
-  GnArgs a = gn_args(c, B, trace);
-  if (trace) CK(hipMemsetAsync(c->d_trace, 0, sizeof(float) * B * c->P.max_iterations * 6, c->stream));
-  CK(hipMemsetAsync(c->d_iter_cnt, 0, sizeof(int32_t) * 2 * c->P.max_iterations, c->stream));
-  TIMED(c, "gn_init", launch_gn_init(c->stream, a));
+  const int64_t ccap = std::min<int64_t>(HW, (int64_t)kCornerPerRing * c->H);
+  v.s[0] = VgSet{c->d_surf_all + j0 * HW, HW, c->d_nsurf + j0, HW, c->d_surfDS + j0 * HW, HW, c->d_nsds + j0,
+                 c->d_vg_scratch + j0 * 4 * HW, c->P.mapping_surf_leaf_size, sb.B, 1};
+  v.s[1] = VgSet{c->d_corner_all + j0 * HW, HW, c->d_ncorner + j0, ccap, c->d_cornerDS + j0 * HW, HW, c->d_ncds + j0,
+                 c->d_vg_scratch + (int64_t)c->Bcap * 4 * HW + j0 * 4 * ccap, c->P.mapping_corner_leaf_size, sb.B, 1};
+  TIMED_ON(c, sb.st, "voxel_scan", launch_voxel_grid(sb.st, v));
+  GnArgs a = gn_args(c, sb, trace);
+  if (trace) CK(hipMemsetAsync(a.trace, 0, sizeof(float) * sb.B * c->P.max_iterations * 6, sb.st));
+  CK(hipMemsetAsync(a.iter_cnt, 0, sizeof(int32_t) * 2 * std::max(1, c->P.max_iterations), sb.st));
+  TIMED_ON(c, sb.st, "gn_init", launch_gn_init(sb.st, a));
   // map-in-box statistics depend only on the guesses: computed once per staged batch
   if (!c->crop_cached) {
-    const int rc = crop_stats(c, B);
+    const int rc = crop_stats(c, sb);
     if (rc) return rc;
   }
-  const int grid = std::max(1, std::min(c->max_items, 2048));
-  // Iterations run on the device without host round trips; the host stays kLag iterations
-  // ahead and stops enqueueing once k_gn_solve reports that no job of the batch is active.
+  return FBR_OK;
+}
+
+// The Gauss-Newton iterations of one or two sub-batches.  Iterations run on the device without
+// host round trips; for each sub-batch the host stays kLag iterations ahead and stops enqueueing
+// once its k_gn_solve reports that no job is active (flags in host-mapped memory).
+int register_iterate(fbr_ctx* c, const Sub* subs, int nsub, bool trace) {
   constexpr int kLag = 2;
   const unsigned long long gen = ++c->gn_gen;
-  bool watch = c->h_iter_flags != nullptr;
-  for (int it = 0; it < c->P.max_iterations; ++it) {
-    if (watch && it >= kLag) {
-      volatile unsigned long long* f = c->h_iter_flags + (it - kLag);
-      unsigned long long v = *f;
-      for (long spins = 0; (v >> 32) != (gen & 0xFFFFFFFFull); ++spins) {
-        if ((spins & 1023) == 1023) {
-          const hipError_t q = hipStreamQuery(c->stream);
-          if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
-          if (q == hipSuccess && ((v = *f) >> 32) != (gen & 0xFFFFFFFFull)) {
-            watch = false;  // flag not visible although the stream drained: enqueue the rest
-            break;
-          }
-        }
-        v = *f;
-      }
-      if (watch && (v & 0xFFFFFFFFull) == 0) break;
-    }
-    TIMED(c, "gn_knn", launch_gn_knn(c->stream, a, grid));
-    TIMED(c, "gn_residual", launch_gn_residual(c->stream, a, grid));
-    TIMED(c, "gn_solve", launch_gn_solve(c->stream, a, it, gen));
+  const int mi = std::max(1, c->P.max_iterations);
+  GnArgs a[2];
+  bool live[2] = {false, false}, watch[2] = {false, false};
+  for (int k = 0; k < nsub; ++k) {
+    a[k] = gn_args(c, subs[k], trace);
+    live[k] = true;
+    watch[k] = c->h_iter_flags != nullptr;
   }
-  TIMED(c, "gn_finalize", launch_gn_finalize(c->stream, a));
+  for (int it = 0; it < c->P.max_iterations; ++it) {
+    for (int k = 0; k < nsub; ++k) {
+      if (!live[k]) continue;
+      const Sub& sb = subs[k];
+      if (watch[k] && it >= kLag) {
+        volatile unsigned long long* f = c->h_iter_flags + (int64_t)sb.k * mi + (it - kLag);
+        unsigned long long v = *f;
+        for (long spins = 0; (v >> 32) != (gen & 0xFFFFFFFFull); ++spins) {
+          if ((spins & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(sb.st);
+            if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
+            if (q == hipSuccess && ((v = *f) >> 32) != (gen & 0xFFFFFFFFull)) {
+              watch[k] = false;  // flag not visible although the stream drained: enqueue the rest
+              break;
+            }
+          }
+          v = *f;
+        }
+        if (watch[k] && (v & 0xFFFFFFFFull) == 0) {
+          live[k] = false;
+          continue;
+        }
+      }
+      const int grid = std::max(1, std::min(a[k].max_items, 2048));
+      TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a[k], grid));
+      TIMED_ON(c, sb.st, "gn_residual", launch_gn_residual(sb.st, a[k], grid));
+      TIMED_ON(c, sb.st, "gn_solve", launch_gn_solve(sb.st, a[k], it, gen));
+    }
+  }
+  for (int k = 0; k < nsub; ++k) TIMED_ON(c, subs[k].st, "gn_finalize", launch_gn_finalize(subs[k].st, a[k]));
   return FBR_OK;
+}
+
+int stage_register(fbr_ctx* c, const Sub& sb, bool trace) {
+  if (!c->has_map) return FBR_ERR_NO_MAP;
+  int rc = register_prepare(c, sb, trace);
+  if (!rc) rc = register_iterate(c, &sb, 1, trace);
+  return rc;
 }
 
 int copy_stats(fbr_ctx* c, int B, fbr_reg_stats* stats) {
@@ -578,11 +630,14 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   c->Bcap = p->max_batch;
   c->NMAX = p->max_points_per_scan;
   const int64_t B = c->Bcap, HW = c->HW, H = c->H;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) {
+    fbr_destroy(c);
     return FBR_ERR_HIP;
   }
-  c->max_items = (int)(B * 2 * ((HW + 255) / 256 + 1));
+  c->items_per_job = (int)(2 * ((HW + 255) / 256 + 1));
+  c->max_items = (int)(B * c->items_per_job);
   c->vg_scratch_elems = 4 * B * (HW + std::min<int64_t>(HW, (int64_t)kCornerPerRing * H));
   bool fail = dalloc(&c->d_pts, B * c->NMAX) || dalloc(&c->d_nin, B) || dalloc(&c->d_guess, B * 6) ||
               dalloc(&c->d_owner, B * HW) || dalloc(&c->d_rowcnt, B * H) || dalloc(&c->d_col, B * HW) ||
@@ -595,13 +650,13 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_surf_all, B * HW) || dalloc(&c->d_cornerDS, B * HW) || dalloc(&c->d_surfDS, B * HW) ||
               dalloc(&c->d_ncorner, B) || dalloc(&c->d_nsurf, B) || dalloc(&c->d_ncds, B) || dalloc(&c->d_nsds, B) ||
               dalloc(&c->d_vg_scratch, c->vg_scratch_elems) ||
-              dalloc(&c->d_gn, B) || dalloc(&c->d_items, c->max_items) || dalloc(&c->d_nitems, 1) ||
+              dalloc(&c->d_gn, B) || dalloc(&c->d_items, c->max_items) || dalloc(&c->d_nitems, 2) ||
               dalloc(&c->d_item_range, 2 * B) || dalloc(&c->d_cropcnt, 2 * B) ||
               dalloc(&c->d_partial, (int64_t)c->max_items * 32) ||
               dalloc(&c->d_nbr, (int64_t)c->max_items * 5 * 256) ||
-              dalloc(&c->d_iter_cnt, 2 * std::max(1, p->max_iterations)) ||
+              dalloc(&c->d_iter_cnt, 2 * 2 * std::max(1, p->max_iterations)) ||
               dalloc(&c->d_feat_scratch, (int64_t)B * H * feat_slot_bytes(c->W)) ||
-              hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * std::max(1, p->max_iterations),
+              hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * 2 * std::max(1, p->max_iterations),
                             hipHostMallocMapped) != hipSuccess ||
               hipHostGetDevicePointer((void**)&c->d_iter_flags, c->h_iter_flags, 0) != hipSuccess || dalloc(&c->d_pose_out, B * 6) ||
               dalloc(&c->d_stats, B) || dalloc(&c->d_trace, B * p->max_iterations * 6);
@@ -609,7 +664,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
     fbr_destroy(c);
     return FBR_ERR_HIP;
   }
-  std::memset(c->h_iter_flags, 0, sizeof(unsigned long long) * std::max(1, p->max_iterations));
+  std::memset(c->h_iter_flags, 0, sizeof(unsigned long long) * 2 * std::max(1, p->max_iterations));
   if (hipMemset(c->d_sstream, 0, sizeof(StreamState)) != hipSuccess ||
       hipMemset(c->d_label_stream, 0, HW) != hipSuccess || hipMemset(c->d_col, 0, sizeof(int32_t) * B * HW) != hipSuccess ||
       hipMemset(c->d_range, 0, sizeof(float) * B * HW) != hipSuccess) {
@@ -624,6 +679,7 @@ int fbr_destroy(fbr_ctx* c) {
   if (!c) return FBR_ERR_INVALID_ARG;
   (void)hipSetDevice(c->dev);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->stream2) (void)hipStreamSynchronize(c->stream2);
   void* ptrs[] = {c->d_pts, c->d_nin, c->d_guess, c->d_owner, c->d_rowcnt, c->d_col, c->d_start, c->d_end,
                   c->d_nvalid, c->d_cloud, c->d_range, c->d_sstate, c->d_sstream, c->d_label, c->d_label_stream,
                   c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring, c->d_surf_ring_cnt,
@@ -645,6 +701,8 @@ int fbr_destroy(fbr_ctx* c) {
     }
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
+  if (c->join_ev) (void)hipEventDestroy(c->join_ev);
   delete c;
   return FBR_OK;
 }
@@ -682,7 +740,7 @@ int fbr_project(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, int32_
   drop_staged_batch(c);
   int rc = upload_scan(c, 0, points, n_in);
   if (rc) return rc;
-  rc = stage_project(c, 1);
+  rc = stage_project(c, single_sub(c));
   if (rc) return rc;
   int32_t n = 0;
   CK(hipMemcpyAsync(&n, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -702,7 +760,7 @@ int fbr_extract_features(fbr_ctx* c, int8_t* label, fbr_point_xyzi* corner, int6
   if (!c) return FBR_ERR_INVALID_ARG;
   if (!c->have_projection) return FBR_ERR_STATE;
   CK(hipSetDevice(c->dev));
-  int rc = stage_features(c, 1, true);
+  int rc = stage_features(c, single_sub(c), true);
   if (rc) return rc;
   rc = check_err(c, 1);
   if (rc) return rc;
@@ -729,7 +787,7 @@ int fbr_register_trace(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corne
   if (rc) return rc;
   CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->stream));
   CK(hipMemsetAsync(c->d_nvalid, 0, sizeof(int32_t), c->stream));
-  rc = stage_register(c, 1, trace != nullptr);
+  rc = stage_register(c, single_sub(c), trace != nullptr);
   if (rc) return rc;
   CK(hipMemcpyAsync(pose_inout, c->d_pose_out, sizeof(float) * 6, hipMemcpyDeviceToHost, c->stream));
   if (trace)
@@ -755,8 +813,8 @@ int fbr_process_scan(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, d
   CK(hipSetDevice(c->dev));
   drop_staged_batch(c);
   int rc = upload_scan(c, 0, points, n_in);
-  if (!rc) rc = stage_project(c, 1);
-  if (!rc) rc = stage_features(c, 1, true);
+  if (!rc) rc = stage_project(c, single_sub(c));
+  if (!rc) rc = stage_features(c, single_sub(c), true);
   if (!rc) rc = check_err(c, 1);
   if (rc) return rc;
   c->have_projection = true;
@@ -766,7 +824,7 @@ int fbr_process_scan(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, d
     if (!c->has_map) return FBR_ERR_NO_MAP;
     c->time_last = stamp;
     CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->stream));
-    rc = stage_register(c, 1, false);
+    rc = stage_register(c, single_sub(c), false);
     if (rc) return rc;
     CK(hipMemcpyAsync(pose_inout, c->d_pose_out, sizeof(float) * 6, hipMemcpyDeviceToHost, c->stream));
     rc = copy_stats(c, 1, &st);
@@ -814,7 +872,7 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
   CK(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * n_jobs, hipMemcpyHostToDevice, c->stream));
   c->crop_cached = false;
   if (c->has_map) {
-    const int rc = crop_stats(c, n_jobs);
+    const int rc = crop_stats(c, Sub{0, n_jobs, 0, c->stream});
     if (rc) return rc;
     c->crop_cached = true;
   }
@@ -829,9 +887,31 @@ int fbr_batch_launch(fbr_ctx* c) {
   if (c->staged_B <= 0) return FBR_ERR_STATE;
   if (!c->has_map) return FBR_ERR_NO_MAP;
   CK(hipSetDevice(c->dev));
-  int rc = stage_project(c, c->staged_B);
-  if (!rc) rc = stage_features(c, c->staged_B, false);
-  if (!rc) rc = stage_register(c, c->staged_B, false);
+  // Two sub-batches on two streams: one sub-batch's low-occupancy phases (the features' ring-0
+  // waves, the last Gauss-Newton iterations) overlap the other's work.
+  const int B = c->staged_B;
+  Sub subs[2];
+  int nsub = 1;
+  subs[0] = Sub{0, B, 0, c->stream};
+  if (B >= 16 && c->stream2) {
+    nsub = 2;
+    subs[0].B = B / 2;
+    subs[1] = Sub{B / 2, B - B / 2, 1, c->stream2};
+    // stream2 must not start before the staged inputs (copied on stream) are in place
+    CK(hipEventRecord(c->join_ev, c->stream));
+    CK(hipStreamWaitEvent(c->stream2, c->join_ev, 0));
+  }
+  int rc = FBR_OK;
+  for (int k = 0; k < nsub && !rc; ++k) {
+    rc = stage_project(c, subs[k]);
+    if (!rc) rc = stage_features(c, subs[k], false);
+    if (!rc) rc = register_prepare(c, subs[k], false);
+  }
+  if (!rc) rc = register_iterate(c, subs, nsub, false);
+  if (!rc && nsub == 2) {  // join: later work on stream (results, export) sees both halves
+    CK(hipEventRecord(c->join_ev, c->stream2));
+    CK(hipStreamWaitEvent(c->stream, c->join_ev, 0));
+  }
   return rc;
 }
 
