@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--cpu-sample", type=int, default=24, help="jobs timed on the CPU oracle (N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist", action="store_true",
+                    help="use the torch.distributed (RCCL) path even at world size 1 (tests)")
     ap.add_argument("--profile", default="dominant", choices=["all", "dominant", "off"],
                     help="HIP-event kernel timing inside the timed region: every kernel, only the roofline "
                          "kernels (default), or none")
@@ -67,7 +69,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 or args.dist:
         import torch  # noqa: F401  (load torch's HIP runtime first; the library shares it)
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)

@@ -59,3 +59,27 @@ def test_record_roundtrip():
     st = np.array([0, 1, 0, 2, 0, 0, 1], np.int32)
     p2, it2, st2 = shard.decode_records(shard.encode_records(p, it, st))
     assert np.array_equal(p, p2) and np.array_equal(it, it2) and np.array_equal(st, st2)
+
+
+@pytest.mark.gpu
+def test_bench_rccl_path_one_rank(tmp_path):
+    """The multi-GPU bench path (torch.distributed.run launch, RCCL process group, device-side
+    pose-record export, all_gather) end to end on the one GPU of the box (world size 1)."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(repo, "bench.py"), "--steps", "2", "--warmup", "1",
+           "--batch", "16", "--no-cpu-baseline", "--dist"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=repo)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 1 and res["value"] > 0 and res["registration_status_ok"] == 16
