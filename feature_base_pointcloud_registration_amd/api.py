@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = [
     "fbr_process_batch", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
     "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
     "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math",
+    "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
 ]
 
 
@@ -84,6 +85,10 @@ def lib():
             "fbr_affine_from_pose": (None, [_VP, _VP]),
             "fbr_pose_from_affine": (None, [_VP, _VP]),
             "fbr_selftest_math": (ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP]),
+            "fbr_load_map": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_char_p]),
+            "fbr_pcd_read": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64, _VP]),
+            "fbr_pcd_write_ascii": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64]),
+            "fbr_pcd_write_binary": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -129,6 +134,23 @@ def pose_from_affine(m):
     return p
 
 
+def pcd_read(path):
+    """pcl::io::loadPCDFile<PointXYZI> (mapOptmization.h:247-248) -> POINT_XYZI array (host only)."""
+    p = os.fsencode(path)
+    n = _I64()
+    _check(lib().fbr_pcd_read(p, None, 0, ctypes.byref(n)), f"fbr_pcd_read({path})")
+    out = np.zeros(max(n.value, 1), POINT_XYZI)
+    _check(lib().fbr_pcd_read(p, ptr(out), len(out), ctypes.byref(n)), f"fbr_pcd_read({path})")
+    return out[:n.value].copy()
+
+
+def pcd_write(path, points, binary=False):
+    """pcl::io::savePCDFileASCII (mapOptmization.h:511-515), or DATA binary when `binary`."""
+    pts = _as_points(points, POINT_XYZI)
+    f = lib().fbr_pcd_write_binary if binary else lib().fbr_pcd_write_ascii
+    _check(f(os.fsencode(path), ptr(pts) if len(pts) else None, len(pts)), f"fbr_pcd_write({path})")
+
+
 def _as_points(a, dtype):
     a = np.ascontiguousarray(a)
     if a.dtype != dtype:
@@ -166,6 +188,10 @@ class Context:
         corner = _as_points(corner, POINT_XYZI)
         surf = _as_points(surf, POINT_XYZI)
         _check(lib().fbr_set_map(self._h, ptr(corner), len(corner), ptr(surf), len(surf)), "fbr_set_map")
+
+    def load_map(self, corner_pcd, surf_pcd):
+        """loadPCDFile(cloudCorner.pcd / cloudSurf.pcd) + the start-up DS (mapOptmization.h:245-260)."""
+        _check(lib().fbr_load_map(self._h, os.fsencode(corner_pcd), os.fsencode(surf_pcd)), "fbr_load_map")
 
     def get_map(self):
         nc, ns = _I64(), _I64()
@@ -301,4 +327,4 @@ class Context:
 
 
 __all__ = ["Context", "FbrError", "FbrParams", "default_params", "lib", "device_count",
-           "affine_from_pose", "pose_from_affine", "EXPORTED_SYMBOLS"]
+           "affine_from_pose", "pose_from_affine", "pcd_read", "pcd_write", "EXPORTED_SYMBOLS"]

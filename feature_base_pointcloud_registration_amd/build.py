@@ -18,6 +18,7 @@ REPO = os.path.dirname(HERE)
 OBJ = os.path.join(HERE, "build")
 
 HIP_SOURCES = ["k_project.hip", "k_features.hip", "k_voxel.hip", "k_register.hip", "k_selftest.hip", "fbr_api.hip"]
+HOST_SOURCES = ["fbr_pcd.cpp"]  # host-only C++ in the same library (PCD I/O)
 ARCH = os.environ.get("FBR_OFFLOAD_ARCH", "gfx950")
 
 
@@ -57,6 +58,13 @@ def build_hip(verbose=False, force=False, defines=(), name="libfbr_hip.so"):
         objs.append(o)
         if force or _newer(o, [s] + hdrs):
             jobs.append([hipcc(), *flags, "-c", s, "-o", o])
+    for src in HOST_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(obj_dir, os.path.splitext(src)[0] + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + hdrs):
+            jobs.append(["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-I", CSRC, "-I", os.path.join(REPO, "include"),
+                         *[f"-D{d}" for d in defines], "-c", s, "-o", o])
 
     def run(cmd):
         if verbose:

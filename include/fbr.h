@@ -114,6 +114,21 @@ int fbr_destroy(fbr_ctx* ctx);
  * mapping_surf_leaf_size), replacing mapOptmization.h:245-260.  Builds the device search grid. */
 int fbr_set_map(fbr_ctx* ctx, const fbr_point_xyzi* corner, int64_t n_corner,
                 const fbr_point_xyzi* surf, int64_t n_surf);
+/* pcl::io::loadPCDFile(HOME + savePCDDirectory + "cloudCorner.pcd" / "cloudSurf.pcd") followed by
+ * fbr_set_map — the whole start-up block mapOptmization.h:245-260 (host-side PCD parsing). */
+int fbr_load_map(fbr_ctx* ctx, const char* corner_pcd, const char* surf_pcd);
+
+/* PCD v0.7 I/O for PointXYZI clouds (host only, no device needed).
+ * fbr_pcd_read replaces pcl::io::loadPCDFile<PointXYZI> (mapOptmization.h:247-248): DATA ascii,
+ * binary and binary_compressed (LZF); x, y, z and intensity are taken by name from any field
+ * layout (F/U/I types, other fields skipped, missing intensity = 0).  Call with out == NULL to get
+ * the point count in *n, then with a buffer of cap >= *n points (FBR_ERR_CAPACITY otherwise).
+ * fbr_pcd_write_ascii replaces pcl::io::savePCDFileASCII (mapOptmization.h:511-515): PCL's header
+ * and 8 significant digits per value.  fbr_pcd_write_binary writes DATA binary (exact floats). */
+int fbr_pcd_read(const char* path, fbr_point_xyzi* out, int64_t cap, int64_t* n);
+int fbr_pcd_write_ascii(const char* path, const fbr_point_xyzi* points, int64_t n);
+int fbr_pcd_write_binary(const char* path, const fbr_point_xyzi* points, int64_t n);
+
 /* Down-sampled global map actually used (sizes, then optional copies; pass NULL to skip). */
 int fbr_get_map(fbr_ctx* ctx, int64_t* n_corner, int64_t* n_surf, fbr_point_xyzi* corner,
                 fbr_point_xyzi* surf);

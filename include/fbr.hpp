@@ -21,6 +21,7 @@
 #define FBR_HPP_
 
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -159,6 +160,18 @@ class MapOptimization {
   void setGlobalMap(const std::vector<fbr_point_xyzi>& corner, const std::vector<fbr_point_xyzi>& surf) {
     check(fbr_set_map(c_.get(), corner.data(), (int64_t)corner.size(), surf.data(), (int64_t)surf.size()),
           "fbr_set_map");
+  }
+
+  /* The start-up block itself (:245-260): loadPCDFile(getenv("HOME") + savePCDDirectory +
+   * "cloudCorner.pcd" / "cloudSurf.pcd") then the DS.  Unlike the reference (which ignores
+   * loadPCDFile's return value and runs with an empty map), an unreadable file throws. */
+  void loadGlobalMap(const std::string& savePCDDirectory) {
+    const char* home = std::getenv("HOME");
+    const std::string dir = std::string(home ? home : "") + savePCDDirectory;
+    loadGlobalMapFiles(dir + "cloudCorner.pcd", dir + "cloudSurf.pcd");
+  }
+  void loadGlobalMapFiles(const std::string& corner_pcd, const std::string& surf_pcd) {
+    check(fbr_load_map(c_.get(), corner_pcd.c_str(), surf_pcd.c_str()), "fbr_load_map");
   }
 
   /* registration (:263-343): mappingProcessInterval gate, getTranslationAndEulerAngles of the

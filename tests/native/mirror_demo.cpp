@@ -9,6 +9,9 @@
 // output: per scan { int64 n_out; int32 start[H], end[H]; int32 col[n_out]; float range[n_out];
 //         int8 label[n_out]; int64 nc; nc x 16 B; int64 ns; ns x 16 B; float affine[16];
 //         fbr_reg_stats }
+// argv[3] (optional): savePCDDirectory — the map is then loaded from $HOME<dir>cloudCorner.pcd /
+//         cloudSurf.pcd (MapOptimization::loadGlobalMap, mapOptmization.h:245-260) instead of
+//         from the input file's map points.
 // exit  : 0 ok, 2 bad input, 3 fbr::Error (prints the status)
 #include <cstdio>
 #include <vector>
@@ -27,8 +30,8 @@ void wr(FILE* f, const T* p, size_t n = 1) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  if (argc != 3) {
-    fprintf(stderr, "usage: mirror_demo <in> <out>\n");
+  if (argc != 3 && argc != 4) {
+    fprintf(stderr, "usage: mirror_demo <in> <out> [savePCDDirectory]\n");
     return 2;
   }
   FILE* in = fopen(argv[1], "rb");
@@ -48,7 +51,10 @@ int main(int argc, char** argv) {
     p.horizon_scan = W;
     fbr::Context ctx(p, 0);
     fbr::Node node(ctx);
-    node.matcher().setGlobalMap(cmap, smap);
+    if (argc == 4)
+      node.matcher().loadGlobalMap(argv[3]);
+    else
+      node.matcher().setGlobalMap(cmap, smap);
     node.setPose(fbr::Affine3f::fromPose(pose0));
     for (int s = 0; s < n_scans; ++s) {
       double stamp;

@@ -13,7 +13,7 @@ import pytest
 
 import pyoracle as O
 from conftest import build_mirror_demo
-from feature_base_pointcloud_registration_amd import synth
+from feature_base_pointcloud_registration_amd import api, synth
 from feature_base_pointcloud_registration_amd.fbr_types import POINT_XYZI, REG_STATS, default_params
 
 POSE_TOL = 1e-4
@@ -69,11 +69,34 @@ def test_mirror_compiles_and_fails_cleanly_without_device(tmp_path):
     assert "fbr::Error" in r.stderr
 
 
+def _pcd_map_dir(tmp_path, cmap, smap):
+    """The reference's map round trip: savePCDFileASCII (mapOptmization.h:511-515) into
+    $HOME<savePCDDirectory>, read back at start-up (:247-248).  Returns (HOME, savePCDDirectory) and
+    the map as parsed independently of the library (numpy on the ASCII text)."""
+    home = tmp_path / "home"
+    d = home / "maps" / "LOAM"
+    d.mkdir(parents=True)
+    parsed = []
+    for name, m in (("cloudCorner.pcd", cmap), ("cloudSurf.pcd", smap)):
+        api.pcd_write(d / name, m)
+        v = np.loadtxt(d / name, skiprows=11, dtype=np.float64, ndmin=2).astype(np.float32)
+        q = np.zeros(len(v), POINT_XYZI)
+        for j, k in enumerate(("x", "y", "z", "intensity")):
+            q[k] = v[:, j]
+        parsed.append(q)
+    return str(home), "/maps/LOAM/", parsed
+
+
 @pytest.mark.gpu
-def test_mirror_node_chain_matches_oracle(tmp_path):
+@pytest.mark.parametrize("map_source", ["points", "pcd"])
+def test_mirror_node_chain_matches_oracle(tmp_path, map_source):
     H, W = synth.CONFIGS["C1"][:2]
     P = default_params(H, W)
     cmap, smap = synth.config_map("C1")
+    extra, env = [], None
+    if map_source == "pcd":
+        home, rel, (cmap_rt, smap_rt) = _pcd_map_dir(tmp_path, cmap, smap)
+        extra, env = [rel], dict(os.environ, HOME=home)
     _, pose0 = synth.job(60)
     traj = synth.trajectory(60, 4)
     scans = [(stamp, synth.scan(gt, H, W, seed=60 + k))  # stamp 0.3 is gated out (0.15 s interval)
@@ -81,9 +104,12 @@ def test_mirror_node_chain_matches_oracle(tmp_path):
     inp, outp = tmp_path / "in.bin", tmp_path / "out.bin"
     write_input(inp, H, W, cmap, smap, pose0, scans)
     exe = build_mirror_demo()
-    r = subprocess.run([exe, str(inp), str(outp)], capture_output=True, text=True, timeout=600)
+    r = subprocess.run([exe, str(inp), str(outp), *extra], capture_output=True, text=True, timeout=600,
+                       env=env)
     assert r.returncode == 0, r.stderr
     res = read_output(outp, H, len(scans))
+    if map_source == "pcd":
+        cmap, smap = cmap_rt, smap_rt
 
     st = O.Stream(P)
     m = O.Map(P, cmap, smap)
