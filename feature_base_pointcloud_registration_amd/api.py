@@ -15,8 +15,8 @@ import os
 
 import numpy as np
 
-from .fbr_types import (POINT_XYZI, POINT_XYZIRT, REG_STATS, FbrParams, FbrRegStats,
-                        default_params, ptr)
+from .fbr_types import (PF_FLOAT32, POINT_XYZI, POINT_XYZIRT, REG_STATS, FbrParams, FbrRegStats,
+                        PointCloud2, default_params, ptr)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = [
     "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
     "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math",
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
+    "fbr_msg_to_points", "fbr_points_to_msg_data", "fbr_project_msg", "fbr_process_msg",
 ]
 
 
@@ -89,6 +90,10 @@ def lib():
             "fbr_pcd_read": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64, _VP]),
             "fbr_pcd_write_ascii": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64]),
             "fbr_pcd_write_binary": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64]),
+            "fbr_msg_to_points": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP]),
+            "fbr_points_to_msg_data": (ctypes.c_int, [_VP, _I64, _VP]),
+            "fbr_project_msg": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
+            "fbr_process_msg": (ctypes.c_int, [_VP, _VP, ctypes.c_double, _VP, _VP, _VP]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -149,6 +154,29 @@ def pcd_write(path, points, binary=False):
     pts = _as_points(points, POINT_XYZI)
     f = lib().fbr_pcd_write_binary if binary else lib().fbr_pcd_write_ascii
     _check(f(os.fsencode(path), ptr(pts) if len(pts) else None, len(pts)), f"fbr_pcd_write({path})")
+
+
+def msg_to_points(msg):
+    """cachePointCloud's fromROSMsg + checks (imageProjection.cpp:253-298) on the host.
+    Returns (POINT_XYZIRT array, msg_flags)."""
+    n, fl = _I64(), _I32()
+    _check(lib().fbr_msg_to_points(ctypes.byref(msg.c), None, 0, ctypes.byref(n), ctypes.byref(fl)),
+           "fbr_msg_to_points")
+    out = np.zeros(max(n.value, 1), POINT_XYZIRT)
+    _check(lib().fbr_msg_to_points(ctypes.byref(msg.c), ptr(out), len(out), ctypes.byref(n), ctypes.byref(fl)),
+           "fbr_msg_to_points")
+    return out[:n.value].copy(), fl.value
+
+
+def points_to_msg(points):
+    """pcl::toROSMsg of a PointXYZI cloud (publishCloud, utility.h:255-264) -> PointCloud2."""
+    pts = _as_points(points, POINT_XYZI)
+    data = np.zeros(32 * len(pts), np.uint8)
+    _check(lib().fbr_points_to_msg_data(ptr(pts) if len(pts) else None, len(pts), ptr(data) if len(pts) else None),
+           "fbr_points_to_msg_data")
+    fields = [("x", 0, PF_FLOAT32, 1), ("y", 4, PF_FLOAT32, 1), ("z", 8, PF_FLOAT32, 1),
+              ("intensity", 16, PF_FLOAT32, 1)]
+    return PointCloud2(data.tobytes(), fields, width=len(pts), point_step=32)
 
 
 def _as_points(a, dtype):
@@ -260,6 +288,26 @@ class Context:
                                       ctypes.byref(st)), "fbr_process_scan")
         return pose, st.as_dict()
 
+    def project_msg(self, msg):
+        """project() from a raw PointCloud2 (unpacked on the device); also returns msg_flags."""
+        H = self.params.n_scan
+        cap = max(msg.c.width * msg.c.height, 1)
+        start, end = np.zeros(H, np.int32), np.zeros(H, np.int32)
+        col, rng, cloud = np.zeros(cap, np.int32), np.zeros(cap, np.float32), np.zeros(cap, POINT_XYZI)
+        n, fl = _I64(), _I32()
+        _check(lib().fbr_project_msg(self._h, ctypes.byref(msg.c), ptr(start), ptr(end), ptr(col), ptr(rng),
+                                     ptr(cloud), ctypes.byref(n), ctypes.byref(fl)), "fbr_project_msg")
+        k = n.value
+        return dict(start_ring=start, end_ring=end, col_ind=col[:k].copy(), range=rng[:k].copy(),
+                    cloud=cloud[:k].copy(), msg_flags=fl.value)
+
+    def process_msg(self, msg, stamp, pose):
+        pose = np.ascontiguousarray(pose, dtype=np.float32).copy()
+        st, fl = FbrRegStats(), _I32()
+        _check(lib().fbr_process_msg(self._h, ctypes.byref(msg.c), ctypes.c_double(stamp), ptr(pose),
+                                     ctypes.byref(st), ctypes.byref(fl)), "fbr_process_msg")
+        return pose, st.as_dict(), fl.value
+
     def reset_stream(self):
         _check(lib().fbr_reset_stream(self._h), "fbr_reset_stream")
 
@@ -327,4 +375,5 @@ class Context:
 
 
 __all__ = ["Context", "FbrError", "FbrParams", "default_params", "lib", "device_count",
-           "affine_from_pose", "pose_from_affine", "pcd_read", "pcd_write", "EXPORTED_SYMBOLS"]
+           "affine_from_pose", "pose_from_affine", "pcd_read", "pcd_write", "msg_to_points", "points_to_msg", "PointCloud2",
+           "EXPORTED_SYMBOLS"]

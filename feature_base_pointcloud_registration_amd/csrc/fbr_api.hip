@@ -22,6 +22,7 @@
 
 #include "fbr_common.h"
 #include "fbr_kernels.h"
+#include "fbr_msg.h"
 
 using namespace fbr;
 
@@ -100,6 +101,8 @@ struct fbr_ctx {
   std::set<std::string> profile_only;  // empty: time every kernel
   int32_t* d_iter_cnt = nullptr;
   unsigned char* d_feat_scratch = nullptr;  // k_features sorted-path slots [B*H][gslot_bytes]
+  uint8_t* d_msg = nullptr;                 // raw PointCloud2 bytes of the last *_msg call (grown on demand)
+  uint64_t msg_cap = 0;
   bool crop_cached = false;  // d_cropcnt holds the staged batch's CropBox statistics
   int max_items = 0;
   float* d_pose_out = nullptr;
@@ -543,6 +546,36 @@ int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n) {
   return FBR_OK;
 }
 
+// The raw PointCloud2 goes to HBM as it is; k_unpack_msg writes job 0's scan buffer
+// (cachePointCloud's fromROSMsg, imageProjection.cpp:253, on the device).
+int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags) {
+  MsgLayout L;
+  int rc = resolve_msg(msg, &L);
+  if (rc) return rc;
+  if (L.n > c->NMAX) return FBR_ERR_CAPACITY;
+  if (L.bytes > c->msg_cap) {
+    CK(hipStreamSynchronize(c->stream));
+    if (c->d_msg) CK(hipFree(c->d_msg));
+    c->d_msg = nullptr;
+    c->msg_cap = 0;
+    CK(hipMalloc(&c->d_msg, L.bytes));
+    c->msg_cap = L.bytes;
+  }
+  if (L.bytes) CK(hipMemcpyAsync(c->d_msg, msg->data, L.bytes, hipMemcpyHostToDevice, c->stream));
+  MsgDev D;
+  D.n = L.n;
+  D.width = L.width;
+  D.row_step = L.row_step;
+  D.point_step = L.point_step;
+  for (int k = 0; k < kMsgFields; ++k) D.off[k] = L.off[k];
+  TIMED(c, "unpack_msg", launch_unpack_msg(c->stream, c->d_msg, D, c->d_pts));
+  const int64_t n = L.n;
+  CK(hipMemcpyAsync(c->d_nin, &n, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+  CK(hipStreamSynchronize(c->stream));  // n lives on this stack; msg->data is the caller's
+  if (msg_flags) *msg_flags = L.flags;
+  return FBR_OK;
+}
+
 int check_err(fbr_ctx* c, int B) {
   std::vector<int32_t> e(B);
   CK(hipMemcpyAsync(e.data(), c->d_err, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
@@ -601,6 +634,7 @@ const char* fbr_strerror(int s) {
     case FBR_ERR_UNSUPPORTED: return "configuration not supported by the device kernels";
     case FBR_ERR_NO_DEVICE: return "no HIP device available";
     case FBR_ERR_STATE: return "call order violated";
+    case FBR_ERR_MSG: return "point cloud message rejected (not dense, or no ring field)";
     default: return "unknown status";
   }
 }
@@ -694,7 +728,7 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_map_c,
-                  c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr, c->d_iter_cnt, c->d_feat_scratch};
+                  c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr, c->d_iter_cnt, c->d_feat_scratch, c->d_msg};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);
@@ -743,6 +777,14 @@ int fbr_get_map(fbr_ctx* c, int64_t* n_corner, int64_t* n_surf, fbr_point_xyzi* 
   return FBR_OK;
 }
 
+namespace {
+// fbr_project after the scan is in job 0's buffer
+int project_uploaded(fbr_ctx* c, int32_t* start_ring, int32_t* end_ring, int32_t* col_ind, float* range,
+                     fbr_point_xyzi* cloud, int64_t* n_out);
+// fbr_process_scan after the scan is in job 0's buffer
+int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stats* stats);
+}  // namespace
+
 int fbr_project(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, int32_t* start_ring, int32_t* end_ring,
                 int32_t* col_ind, float* range, fbr_point_xyzi* cloud, int64_t* n_out) {
   if (!c || (n_in && !points)) return FBR_ERR_INVALID_ARG;
@@ -750,7 +792,23 @@ int fbr_project(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, int32_
   drop_staged_batch(c);
   int rc = upload_scan(c, 0, points, n_in);
   if (rc) return rc;
-  rc = stage_project(c, single_sub(c));
+  return project_uploaded(c, start_ring, end_ring, col_ind, range, cloud, n_out);
+}
+
+int fbr_project_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* start_ring, int32_t* end_ring, int32_t* col_ind,
+                    float* range, fbr_point_xyzi* cloud, int64_t* n_out, int32_t* msg_flags) {
+  if (!c || !msg) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  drop_staged_batch(c);
+  int rc = upload_msg(c, msg, msg_flags);
+  if (rc) return rc;
+  return project_uploaded(c, start_ring, end_ring, col_ind, range, cloud, n_out);
+}
+
+namespace {
+int project_uploaded(fbr_ctx* c, int32_t* start_ring, int32_t* end_ring, int32_t* col_ind, float* range,
+                     fbr_point_xyzi* cloud, int64_t* n_out) {
+  int rc = stage_project(c, single_sub(c));
   if (rc) return rc;
   int32_t n = 0;
   CK(hipMemcpyAsync(&n, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -764,6 +822,7 @@ int fbr_project(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, int32_
   c->have_projection = true;
   return FBR_OK;
 }
+}  // namespace
 
 int fbr_extract_features(fbr_ctx* c, int8_t* label, fbr_point_xyzi* corner, int64_t* n_corner, fbr_point_xyzi* surf,
                          int64_t* n_surf) {
@@ -823,7 +882,23 @@ int fbr_process_scan(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, d
   CK(hipSetDevice(c->dev));
   drop_staged_batch(c);
   int rc = upload_scan(c, 0, points, n_in);
-  if (!rc) rc = stage_project(c, single_sub(c));
+  if (rc) return rc;
+  return process_uploaded(c, stamp, pose_inout, stats);
+}
+
+int fbr_process_msg(fbr_ctx* c, const fbr_pointcloud2* msg, double stamp, float pose_inout[6], fbr_reg_stats* stats,
+                    int32_t* msg_flags) {
+  if (!c || !msg || !pose_inout) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  drop_staged_batch(c);
+  int rc = upload_msg(c, msg, msg_flags);
+  if (rc) return rc;
+  return process_uploaded(c, stamp, pose_inout, stats);
+}
+
+namespace {
+int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stats* stats) {
+  int rc = stage_project(c, single_sub(c));
   if (!rc) rc = stage_features(c, single_sub(c), true);
   if (!rc) rc = check_err(c, 1);
   if (rc) return rc;
@@ -852,6 +927,7 @@ int fbr_process_scan(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, d
   if (stats) *stats = st;
   return FBR_OK;
 }
+}  // namespace
 
 int fbr_reset_stream(fbr_ctx* c) {
   if (!c) return FBR_ERR_INVALID_ARG;

@@ -8,6 +8,13 @@
 namespace fbr {
 
 // ---- A2+A4 (k_project.hip) ----
+// Device copy of the resolved PointCloud2 layout (fbr_msg.h): offsets x, y, z, intensity, ring,
+// time (-1 = unmapped).
+struct MsgDev {
+  int64_t n, width, row_step, point_step;
+  int32_t off[6];
+};
+void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_point_xyzirt* out);
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
                     int W, int32_t* owner);
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,

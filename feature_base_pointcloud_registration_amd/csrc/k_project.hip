@@ -168,6 +168,53 @@ __global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax
   }
 }
 
+// K0 k_unpack_msg: sensor_msgs/PointCloud2 bytes (row-major, point_step / row_step strided
+// records, as they arrive) -> the 24-B fbr_point_xyzirt scan buffer; pcl::fromROSMsg's field
+// mapping was resolved on the host (fbr_msg.cpp), unmapped fields are 0.  One lane per point;
+// dword loads when every offset and stride is aligned (the usual driver layouts), byte loads
+// otherwise.  HBM-bound: point_step B read + 24 B written per point.
+template <bool kAligned>
+__device__ __forceinline__ float msg_f32(const uint8_t* p, int off) {
+  if (off < 0) return 0.0f;
+  if (kAligned) return *reinterpret_cast<const float*>(p + off);
+  uint32_t u = (uint32_t)p[off] | ((uint32_t)p[off + 1] << 8) | ((uint32_t)p[off + 2] << 16) |
+               ((uint32_t)p[off + 3] << 24);
+  return __uint_as_float(u);
+}
+
+template <bool kAligned>
+__global__ void __launch_bounds__(256)
+k_unpack_msg(const uint8_t* __restrict__ data, MsgDev L, fbr_point_xyzirt* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= L.n) return;
+  const int64_t r = i / L.width, c = i - r * L.width;
+  const uint8_t* p = data + r * L.row_step + c * L.point_step;
+  fbr_point_xyzirt q;
+  q.x = msg_f32<kAligned>(p, L.off[0]);
+  q.y = msg_f32<kAligned>(p, L.off[1]);
+  q.z = msg_f32<kAligned>(p, L.off[2]);
+  q.intensity = msg_f32<kAligned>(p, L.off[3]);
+  const int orr = L.off[4];
+  q.ring = orr < 0 ? 0
+           : kAligned ? *reinterpret_cast<const uint16_t*>(p + orr)
+                      : (uint16_t)(p[orr] | (p[orr + 1] << 8));
+  q.pad_ = 0;
+  q.time = msg_f32<kAligned>(p, L.off[5]);
+  out[i] = q;
+}
+
+void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_point_xyzirt* out) {
+  if (L.n <= 0) return;
+  bool aligned = (L.point_step % 4 == 0) && (L.row_step % 4 == 0);
+  for (int k = 0; k < 6; ++k)
+    if (L.off[k] >= 0) aligned = aligned && (L.off[k] % (k == 4 ? 2 : 4) == 0);
+  const dim3 grid((unsigned)((L.n + 255) / 256));
+  if (aligned)
+    hipLaunchKernelGGL(k_unpack_msg<true>, grid, dim3(256), 0, s, data, L, out);
+  else
+    hipLaunchKernelGGL(k_unpack_msg<false>, grid, dim3(256), 0, s, data, L, out);
+}
+
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
                     int W, int32_t* owner) {
   int blocks = (int)((nmax + kProjChunk - 1) / kProjChunk);

@@ -92,3 +92,64 @@ def ptr(a, ctype=ctypes.c_void_p):
         return None
     assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
     return ctypes.cast(a.ctypes.data, ctype)
+
+
+# ---- sensor_msgs/PointCloud2 (include/fbr.h "PointCloud2 wire format") ----
+PF_INT8, PF_UINT8, PF_INT16, PF_UINT16, PF_INT32, PF_UINT32, PF_FLOAT32, PF_FLOAT64 = range(1, 9)
+FBR_ERR_MSG = -8
+FBR_MSG_NO_TIME, FBR_MSG_RING_UNMAPPED, FBR_MSG_XYZI_UNMAPPED = 1, 2, 4
+_PF_OF_NUMPY = {"i1": PF_INT8, "u1": PF_UINT8, "i2": PF_INT16, "u2": PF_UINT16, "i4": PF_INT32,
+                "u4": PF_UINT32, "f4": PF_FLOAT32, "f8": PF_FLOAT64}
+
+
+class FbrPointField(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("offset", ctypes.c_uint32), ("datatype", ctypes.c_uint8),
+                ("count", ctypes.c_uint32)]
+
+
+class FbrPointCloud2(ctypes.Structure):
+    _fields_ = [("height", ctypes.c_uint32), ("width", ctypes.c_uint32),
+                ("fields", ctypes.POINTER(FbrPointField)), ("n_fields", ctypes.c_int32),
+                ("is_bigendian", ctypes.c_uint8), ("point_step", ctypes.c_uint32),
+                ("row_step", ctypes.c_uint32), ("data", ctypes.c_void_p), ("data_size", ctypes.c_uint64),
+                ("is_dense", ctypes.c_uint8)]
+
+
+class PointCloud2:
+    """A sensor_msgs/PointCloud2 view for the C-ABI: keeps the byte buffer and field names alive.
+
+    fields: list of (name, offset, datatype, count).  `data` is bytes-like of at least
+    (height-1)*row_step + width*point_step bytes."""
+
+    def __init__(self, data, fields, width, height=1, point_step=None, row_step=None, is_dense=True):
+        self.buf = np.frombuffer(bytes(data), np.uint8)
+        self.fields = [(str(n), int(o), int(t), int(c)) for n, o, t, c in fields]
+        self._names = [n.encode() for n, _, _, _ in self.fields]
+        self._fa = (FbrPointField * max(len(self.fields), 1))()
+        for k, ((_, o, t, c), nm) in enumerate(zip(self.fields, self._names)):
+            self._fa[k] = FbrPointField(nm, o, t, c)
+        ps = point_step if point_step is not None else (len(self.buf) // max(width * height, 1))
+        m = FbrPointCloud2()
+        m.height, m.width = height, width
+        m.fields = ctypes.cast(self._fa, ctypes.POINTER(FbrPointField))
+        m.n_fields = len(self.fields)
+        m.is_bigendian = 0
+        m.point_step = ps
+        m.row_step = row_step if row_step is not None else ps * width
+        m.data = self.buf.ctypes.data if len(self.buf) else None
+        m.data_size = len(self.buf)
+        m.is_dense = 1 if is_dense else 0
+        self.c = m
+
+    @classmethod
+    def from_array(cls, arr, height=1, is_dense=True):
+        """Message whose points are the records of a numpy structured array (fields by dtype)."""
+        arr = np.ascontiguousarray(arr)
+        fields = []
+        for name in arr.dtype.names:
+            dt, off = arr.dtype.fields[name][:2]
+            base, shape = (dt.subdtype if dt.subdtype else (dt, ()))
+            count = int(np.prod(shape)) if shape else 1
+            fields.append((name, off, _PF_OF_NUMPY[base.str[1:]], count))
+        return cls(arr.tobytes(), fields, width=len(arr) // height, height=height,
+                   point_step=arr.dtype.itemsize, is_dense=is_dense)

@@ -38,6 +38,9 @@ extern "C" {
 #define FBR_ERR_UNSUPPORTED (-5)  /* configuration outside what the kernels handle          */
 #define FBR_ERR_NO_DEVICE (-6)    /* no HIP device / extension not usable                   */
 #define FBR_ERR_STATE (-7)        /* call order violated (e.g. features before projection)  */
+#define FBR_ERR_MSG (-8)          /* PointCloud2 rejected by cachePointCloud's checks: not
+                                     is_dense, or no "ring" field (imageProjection.cpp:256-281,
+                                     where the reference calls ros::shutdown())               */
 
 /* ---- registration outcome (fbr_reg_stats.status) -------------------------------------------- */
 #define FBR_REG_OK 0                    /* scan2MapOptimization ran                           */
@@ -99,6 +102,40 @@ typedef struct fbr_reg_stats {
 
 typedef struct fbr_ctx fbr_ctx;
 
+/* ---- sensor_msgs/PointCloud2 wire format ------------------------------ */
+/* sensor_msgs/PointField datatypes */
+#define FBR_PF_INT8 1
+#define FBR_PF_UINT8 2
+#define FBR_PF_INT16 3
+#define FBR_PF_UINT16 4
+#define FBR_PF_INT32 5
+#define FBR_PF_UINT32 6
+#define FBR_PF_FLOAT32 7
+#define FBR_PF_FLOAT64 8
+
+typedef struct fbr_point_field { /* sensor_msgs/PointField */
+  const char* name;
+  uint32_t offset;
+  uint8_t datatype;              /* FBR_PF_* */
+  uint32_t count;
+} fbr_point_field;
+
+typedef struct fbr_pointcloud2 { /* sensor_msgs/PointCloud2 without the header */
+  uint32_t height, width;
+  const fbr_point_field* fields;
+  int32_t n_fields;
+  uint8_t is_bigendian;          /* ignored, as pcl::fromROSMsg does (host byte order assumed) */
+  uint32_t point_step, row_step;
+  const uint8_t* data;
+  uint64_t data_size;            /* bytes at data (>= (height-1)*row_step + width*point_step) */
+  uint8_t is_dense;
+} fbr_pointcloud2;
+
+/* msg_flags bits reported by the *_msg entry points (warnings, the call still succeeds) */
+#define FBR_MSG_NO_TIME 1        /* no "time" field: deskewFlag = -1, ROS_WARN (:285-298); time = 0 */
+#define FBR_MSG_RING_UNMAPPED 2  /* "ring" exists but is not UINT16 x1: fromROSMsg leaves ring = 0 */
+#define FBR_MSG_XYZI_UNMAPPED 4  /* x, y, z or intensity missing / not FLOAT32 x1: left 0          */
+
 void fbr_params_default(fbr_params* p);
 const char* fbr_strerror(int status);
 int fbr_abi_version(void);
@@ -128,6 +165,28 @@ int fbr_load_map(fbr_ctx* ctx, const char* corner_pcd, const char* surf_pcd);
 int fbr_pcd_read(const char* path, fbr_point_xyzi* out, int64_t cap, int64_t* n);
 int fbr_pcd_write_ascii(const char* path, const fbr_point_xyzi* points, int64_t n);
 int fbr_pcd_write_binary(const char* path, const fbr_point_xyzi* points, int64_t n);
+
+/* cachePointCloud's conversion and checks (imageProjection.cpp:255-298) on the host:
+ * pcl::fromROSMsg<PointXYZIRT> (fields mapped by name with matching datatype and count, points in
+ * row-major order, unmapped fields 0), then the is_dense and "ring" checks (FBR_ERR_MSG) and the
+ * "time" check (FBR_MSG_NO_TIME).  out == NULL queries *n.  The reference runs the ring/time
+ * checks on the first message only (static flags); these entry points check every message. */
+int fbr_msg_to_points(const fbr_pointcloud2* msg, fbr_point_xyzirt* out, int64_t cap, int64_t* n,
+                      int32_t* msg_flags);
+/* pcl::toROSMsg of a PointXYZI cloud (publishCloud, utility.h:255-264): height 1, width n,
+ * fields x@0 y@4 z@8 intensity@16 (FLOAT32 x1), point_step 32, row_step 32n, with PCL's padding
+ * (1.0f at offset 12, zeros after intensity).  data_out holds 32*n bytes. */
+int fbr_points_to_msg_data(const fbr_point_xyzi* points, int64_t n, uint8_t* data_out);
+
+/* Device variants of fbr_project / fbr_process_scan that take the raw PointCloud2: the message
+ * bytes are copied to HBM as they are and unpacked by a kernel (field mapping as
+ * fbr_msg_to_points), so the host does no per-point work (cachePointCloud + cloudHandler,
+ * imageProjection.cpp:182-226). */
+int fbr_project_msg(fbr_ctx* ctx, const fbr_pointcloud2* msg, int32_t* start_ring, int32_t* end_ring,
+                    int32_t* col_ind, float* range, fbr_point_xyzi* cloud, int64_t* n_out,
+                    int32_t* msg_flags);
+int fbr_process_msg(fbr_ctx* ctx, const fbr_pointcloud2* msg, double stamp, float pose_inout[6],
+                    fbr_reg_stats* stats, int32_t* msg_flags);
 
 /* Down-sampled global map actually used (sizes, then optional copies; pass NULL to skip). */
 int fbr_get_map(fbr_ctx* ctx, int64_t* n_corner, int64_t* n_surf, fbr_point_xyzi* corner,

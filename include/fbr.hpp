@@ -22,6 +22,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <deque>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -93,10 +94,27 @@ class Context {
   fbr_ctx* ctx_ = nullptr;
 };
 
+/* sensor_msgs/PointCloud2 as the node receives it (an owned copy: what cloudQueue holds,
+ * imageProjection.cpp:233). */
+struct PointCloud2 {
+  struct Field {
+    std::string name;
+    uint32_t offset = 0;
+    uint8_t datatype = FBR_PF_FLOAT32;
+    uint32_t count = 1;
+  };
+  double stamp = 0.0;  // header.stamp.toSec()
+  uint32_t height = 1, width = 0, point_step = 0, row_step = 0;
+  bool is_bigendian = false, is_dense = true;
+  std::vector<Field> fields;
+  std::vector<uint8_t> data;
+};
+
 /* ImageProjection (imageProjection.cpp:29): projectPointCloud + cloudExtraction on the device. */
 class ImageProjection {
  public:
   explicit ImageProjection(Context& c) : c_(c) {}
+  ImageProjection(const ImageProjection&) = delete;
 
   /* cloudHandler's projection half (:197-199).  Returns false where cachePointCloud drops the
    * scan (:229-301: a ring outside [0, N_SCAN) is not an error there, only points are skipped;
@@ -122,8 +140,64 @@ class ImageProjection {
     return true;
   }
 
+  /* cachePointCloud (:229-301): the 2-message delay queue; returns false while it fills, else
+   * makes the oldest message current (timeScanCur = its stamp). */
+  bool cachePointCloud(const PointCloud2& msg) {
+    cloudQueue_.push_back(msg);
+    if (cloudQueue_.size() <= 2) return false;
+    current_ = std::move(cloudQueue_.front());
+    cloudQueue_.pop_front();
+    return true;
+  }
+
+  /* cloudHandler's projection half on a raw message: the cache queue, then the message bytes are
+   * unpacked on the device (fromROSMsg), checked (is_dense / ring -> fbr::Error with FBR_ERR_MSG
+   * where the reference calls ros::shutdown()), and projected.  msgFlags() reports the warnings
+   * (FBR_MSG_NO_TIME: the reference's "deskew function disabled" ROS_WARN). */
+  bool cloudHandler(const PointCloud2& msg, CloudInfo& info) {
+    if (!cachePointCloud(msg)) return false;
+    std::vector<fbr_point_field> f(current_.fields.size());
+    for (size_t k = 0; k < f.size(); ++k)
+      f[k] = fbr_point_field{current_.fields[k].name.c_str(), current_.fields[k].offset, current_.fields[k].datatype,
+                             current_.fields[k].count};
+    fbr_pointcloud2 m;
+    m.height = current_.height;
+    m.width = current_.width;
+    m.fields = f.data();
+    m.n_fields = (int32_t)f.size();
+    m.is_bigendian = current_.is_bigendian;
+    m.point_step = current_.point_step;
+    m.row_step = current_.row_step;
+    m.data = current_.data.data();
+    m.data_size = current_.data.size();
+    m.is_dense = current_.is_dense;
+    const int H = c_.params().n_scan;
+    const int64_t n = (int64_t)current_.width * current_.height;
+    info.stamp = current_.stamp;
+    info.startRingIndex.assign(H, 0);
+    info.endRingIndex.assign(H, 0);
+    info.pointColInd.resize(n);
+    info.pointRange.resize(n);
+    info.cloud_deskewed.resize(n);
+    int64_t n_out = 0;
+    check(fbr_project_msg(c_.get(), &m, info.startRingIndex.data(), info.endRingIndex.data(), info.pointColInd.data(),
+                          info.pointRange.data(), info.cloud_deskewed.data(), &n_out, &msg_flags_),
+          "fbr_project_msg");
+    info.pointColInd.resize(n_out);
+    info.pointRange.resize(n_out);
+    info.cloud_deskewed.resize(n_out);
+    info.cloud_corner.clear();
+    info.cloud_surface.clear();
+    info.cloudLabel.clear();
+    return true;
+  }
+  int msgFlags() const { return msg_flags_; }
+
  private:
   Context& c_;
+  std::deque<PointCloud2> cloudQueue_;
+  PointCloud2 current_;
+  int msg_flags_ = 0;
 };
 
 /* FeatureExtraction (featureExtraction.h:19): featureExtra(cloud_info) on the projection the
@@ -215,6 +289,15 @@ class Node {
     map_.registration(info_, pose_);
     return true;
   }
+  /* The reference's entry point proper: cloudHandler(const sensor_msgs::PointCloud2ConstPtr&)
+   * (:182-226), including the 2-message cache queue (returns false while it fills). */
+  bool cloudHandler(const PointCloud2& msg) {
+    if (!proj_.cloudHandler(msg, info_)) return false;
+    feat_.featureExtra(info_);
+    map_.registration(info_, pose_);
+    return true;
+  }
+  ImageProjection& projection() { return proj_; }
 
  private:
   ImageProjection proj_;

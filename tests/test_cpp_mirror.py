@@ -88,15 +88,19 @@ def _pcd_map_dir(tmp_path, cmap, smap):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("map_source", ["points", "pcd"])
+@pytest.mark.parametrize("map_source", ["points", "pcd", "msg"])
 def test_mirror_node_chain_matches_oracle(tmp_path, map_source):
+    """map_source "pcd": the map goes through savePCDFileASCII / loadPCDFile; "msg": the scans
+    arrive as PointCloud2 messages through the 2-message cache queue (imageProjection.cpp:229-249)."""
     H, W = synth.CONFIGS["C1"][:2]
     P = default_params(H, W)
     cmap, smap = synth.config_map("C1")
     extra, env = [], None
     if map_source == "pcd":
         home, rel, (cmap_rt, smap_rt) = _pcd_map_dir(tmp_path, cmap, smap)
-        extra, env = [rel], dict(os.environ, HOME=home)
+        extra, env = ["--pcd", rel], dict(os.environ, HOME=home)
+    elif map_source == "msg":
+        extra = ["--msg"]
     _, pose0 = synth.job(60)
     traj = synth.trajectory(60, 4)
     scans = [(stamp, synth.scan(gt, H, W, seed=60 + k))  # stamp 0.3 is gated out (0.15 s interval)
