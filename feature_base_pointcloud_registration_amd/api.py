@@ -15,8 +15,8 @@ import os
 
 import numpy as np
 
-from .fbr_types import (PF_FLOAT32, POINT_XYZI, POINT_XYZIRT, REG_STATS, FbrParams, FbrRegStats,
-                        PointCloud2, default_params, ptr)
+from .fbr_types import (DESKEW_TABLE, IMU_SAMPLE, PF_FLOAT32, POINT_XYZI, POINT_XYZIRT, REG_STATS, FbrParams,
+                        FbrRegStats, PointCloud2, default_params, ptr)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = [
     "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math",
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
     "fbr_msg_to_points", "fbr_points_to_msg_data", "fbr_project_msg", "fbr_process_msg",
+    "fbr_imu_convert", "fbr_imu_deskew_info", "fbr_set_deskew",
 ]
 
 
@@ -94,6 +95,9 @@ def lib():
             "fbr_points_to_msg_data": (ctypes.c_int, [_VP, _I64, _VP]),
             "fbr_project_msg": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
             "fbr_process_msg": (ctypes.c_int, [_VP, _VP, ctypes.c_double, _VP, _VP, _VP]),
+            "fbr_imu_convert": (ctypes.c_int, [_VP, _VP, _VP]),
+            "fbr_imu_deskew_info": (ctypes.c_int, [_VP, _I64, ctypes.c_double, ctypes.c_double, _VP, _VP]),
+            "fbr_set_deskew": (ctypes.c_int, [_VP, _VP, ctypes.c_int]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -177,6 +181,30 @@ def points_to_msg(points):
     fields = [("x", 0, PF_FLOAT32, 1), ("y", 4, PF_FLOAT32, 1), ("z", 8, PF_FLOAT32, 1),
               ("intensity", 16, PF_FLOAT32, 1)]
     return PointCloud2(data.tobytes(), fields, width=len(pts), point_step=32)
+
+
+def imu_convert(ext, samples):
+    """imuConverter (utility.h:219-253) on each sample (IMU_SAMPLE array) with IMU_EXTRINSICS `ext`."""
+    samples = _as_points(np.atleast_1d(samples), IMU_SAMPLE)
+    ext = np.ascontiguousarray(ext)
+    out = np.zeros_like(samples)
+    for i in range(len(samples)):
+        _check(lib().fbr_imu_convert(ptr(ext), ctypes.c_void_p(samples.ctypes.data + i * IMU_SAMPLE.itemsize),
+                                     ctypes.c_void_p(out.ctypes.data + i * IMU_SAMPLE.itemsize)), "fbr_imu_convert")
+    return out
+
+
+def imu_deskew_info(queue, time_scan_cur, time_scan_next, previous=None):
+    """deskewInfo + imuDeskewInfo (imageProjection.cpp:303-393) on a queue of converted samples.
+    Returns (DESKEW_TABLE record, number of leading samples popped).  `previous` carries the
+    imu*Init fields forward as the reference's cloudInfo member does."""
+    queue = _as_points(np.atleast_1d(queue), IMU_SAMPLE)
+    tab = np.zeros(1, DESKEW_TABLE) if previous is None else np.array(previous, DESKEW_TABLE).reshape(1).copy()
+    n_pop = _I64()
+    _check(lib().fbr_imu_deskew_info(ptr(queue) if len(queue) else None, len(queue), ctypes.c_double(time_scan_cur),
+                                     ctypes.c_double(time_scan_next), ptr(tab), ctypes.byref(n_pop)),
+           "fbr_imu_deskew_info")
+    return tab[0], n_pop.value
 
 
 def _as_points(a, dtype):
@@ -308,6 +336,15 @@ class Context:
                                      ctypes.byref(st), ctypes.byref(fl)), "fbr_process_msg")
         return pose, st.as_dict(), fl.value
 
+    def set_deskew(self, tables):
+        """IMU deskew tables (DESKEW_TABLE records) for the following calls: job j of a batch uses
+        tables[j], single-scan calls tables[0]; None restores the reference's runtime path."""
+        if tables is None:
+            _check(lib().fbr_set_deskew(self._h, None, 0), "fbr_set_deskew")
+            return
+        t = np.ascontiguousarray(np.array(tables, DESKEW_TABLE).reshape(-1))
+        _check(lib().fbr_set_deskew(self._h, ptr(t), len(t)), "fbr_set_deskew")
+
     def reset_stream(self):
         _check(lib().fbr_reset_stream(self._h), "fbr_reset_stream")
 
@@ -376,4 +413,5 @@ class Context:
 
 __all__ = ["Context", "FbrError", "FbrParams", "default_params", "lib", "device_count",
            "affine_from_pose", "pose_from_affine", "pcd_read", "pcd_write", "msg_to_points", "points_to_msg", "PointCloud2",
+           "imu_convert", "imu_deskew_info",
            "EXPORTED_SYMBOLS"]

@@ -18,7 +18,7 @@ REPO = os.path.dirname(HERE)
 OBJ = os.path.join(HERE, "build")
 
 HIP_SOURCES = ["k_project.hip", "k_features.hip", "k_voxel.hip", "k_register.hip", "k_selftest.hip", "fbr_api.hip"]
-HOST_SOURCES = ["fbr_pcd.cpp", "fbr_msg.cpp"]  # host-only C++ in the same library (PCD, PointCloud2)
+HOST_SOURCES = ["fbr_pcd.cpp", "fbr_msg.cpp", "fbr_imu.cpp"]  # host-only C++ in the same library (PCD, PointCloud2, IMU)
 ARCH = os.environ.get("FBR_OFFLOAD_ARCH", "gfx950")
 
 

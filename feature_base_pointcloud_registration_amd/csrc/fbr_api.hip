@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "fbr_common.h"
+#include "fbr_imu.h"
 #include "fbr_kernels.h"
 #include "fbr_msg.h"
 
@@ -123,6 +124,12 @@ struct fbr_ctx {
   std::map<std::string, KernelTimer> timers;
   std::vector<int32_t> last_iters, last_q, last_n, last_m;
   unsigned long long* d_feat_stamps = nullptr;  // diagnostic builds (FBR_FEAT_STAMPS) only
+  // IMU deskew (fbr_set_deskew)
+  fbr_deskew_table* d_desk = nullptr;  // [Bcap] tables (allocated on first use)
+  int32_t* d_desk_mode = nullptr;      // [Bcap] kDesk* bits per job
+  int32_t* d_rowmin = nullptr;         // [Bcap][H] minimum owner per row
+  bool desk_any = false;               // some job has a non-zero mode
+  bool no_time_call = false;           // the current call's PointCloud2 has no "time" field
 };
 
 namespace {
@@ -317,6 +324,9 @@ Sub single_sub(fbr_ctx* c) { return Sub{0, 1, 0, c->stream}; }
 
 int stage_project(fbr_ctx* c, const Sub& sb) {
   const int64_t j0 = sb.j0;
+  DeskArgs desk{nullptr, nullptr, nullptr};
+  if (c->desk_any && !c->no_time_call)  // deskewFlag == -1 without a "time" field (:296-297, :548)
+    desk = DeskArgs{c->d_desk_mode + j0, c->d_desk + j0, c->d_rowmin + j0 * c->H};
   int32_t* owner = c->d_owner + j0 * c->HW;
   CK(hipMemsetAsync(owner, 0x7F, sizeof(int32_t) * sb.B * c->HW, sb.st));
   TIMED_ON(c, sb.st, "project", launch_project(sb.st, c->d_pts + j0 * c->NMAX, c->d_nin + j0, c->NMAX, sb.B, c->H,
@@ -324,7 +334,7 @@ int stage_project(fbr_ctx* c, const Sub& sb) {
   TIMED_ON(c, sb.st, "extract",
            launch_extract(sb.st, c->d_pts + j0 * c->NMAX, c->NMAX, owner, sb.B, c->H, c->W, c->d_rowcnt + j0 * c->H,
                           c->d_cloud + j0 * c->HW, c->d_col + j0 * c->HW, c->d_range + j0 * c->HW,
-                          c->d_start + j0 * c->H, c->d_end + j0 * c->H, c->d_nvalid + j0));
+                          c->d_start + j0 * c->H, c->d_end + j0 * c->H, c->d_nvalid + j0, desk));
   return FBR_OK;
 }
 
@@ -412,6 +422,8 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   a.nbr = c->d_nbr + ib * 5 * 256;
   a.iter_flags = c->d_iter_flags + (int64_t)sb.k * mi;
   a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 2 * mi;
+  a.desk_mode = c->desk_any ? c->d_desk_mode + j0 : nullptr;
+  a.desk = c->desk_any ? c->d_desk + j0 : nullptr;
   return a;
 }
 
@@ -540,6 +552,7 @@ int copy_stats(fbr_ctx* c, int B, fbr_reg_stats* stats) {
 
 int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n) {
   if (n < 0 || n > c->NMAX) return FBR_ERR_CAPACITY;
+  c->no_time_call = false;
   if (n) CK(hipMemcpyAsync(c->d_pts + job * c->NMAX, pts, sizeof(fbr_point_xyzirt) * n, hipMemcpyHostToDevice, c->stream));
   CK(hipMemcpyAsync(c->d_nin + job, &n, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
   CK(hipStreamSynchronize(c->stream));  // n lives on the caller's stack
@@ -573,6 +586,7 @@ int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags) {
   CK(hipMemcpyAsync(c->d_nin, &n, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
   CK(hipStreamSynchronize(c->stream));  // n lives on this stack; msg->data is the caller's
   if (msg_flags) *msg_flags = L.flags;
+  c->no_time_call = (L.flags & FBR_MSG_NO_TIME) != 0;
   return FBR_OK;
 }
 
@@ -700,7 +714,8 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * kMaxSub * std::max(1, p->max_iterations),
                             hipHostMallocMapped) != hipSuccess ||
               hipHostGetDevicePointer((void**)&c->d_iter_flags, c->h_iter_flags, 0) != hipSuccess || dalloc(&c->d_pose_out, B * 6) ||
-              dalloc(&c->d_stats, B) || dalloc(&c->d_trace, B * p->max_iterations * 6);
+              dalloc(&c->d_stats, B) || dalloc(&c->d_trace, B * p->max_iterations * 6) ||
+              dalloc(&c->d_desk_mode, B) || dalloc(&c->d_rowmin, B * H);
   if (fail) {
     fbr_destroy(c);
     return FBR_ERR_HIP;
@@ -708,7 +723,8 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   std::memset(c->h_iter_flags, 0, sizeof(unsigned long long) * kMaxSub * std::max(1, p->max_iterations));
   if (hipMemset(c->d_sstream, 0, sizeof(StreamState)) != hipSuccess ||
       hipMemset(c->d_label_stream, 0, HW) != hipSuccess || hipMemset(c->d_col, 0, sizeof(int32_t) * B * HW) != hipSuccess ||
-      hipMemset(c->d_range, 0, sizeof(float) * B * HW) != hipSuccess) {
+      hipMemset(c->d_range, 0, sizeof(float) * B * HW) != hipSuccess ||
+      hipMemset(c->d_desk_mode, 0, sizeof(int32_t) * B) != hipSuccess) {
     fbr_destroy(c);
     return FBR_ERR_HIP;
   }
@@ -728,7 +744,8 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_map_c,
-                  c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr, c->d_iter_cnt, c->d_feat_scratch, c->d_msg};
+                  c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
+                  c->d_desk, c->d_desk_mode, c->d_rowmin};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);
@@ -947,6 +964,7 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
   if (!c || !scans || !n_in || !poses_in || n_jobs <= 0) return FBR_ERR_INVALID_ARG;
   if (n_jobs > c->Bcap) return FBR_ERR_CAPACITY;
   CK(hipSetDevice(c->dev));
+  c->no_time_call = false;
   for (int j = 0; j < n_jobs; ++j) {
     if (n_in[j] < 0 || n_in[j] > c->NMAX) return FBR_ERR_CAPACITY;
     if (n_in[j] && !scans[j]) return FBR_ERR_INVALID_ARG;
@@ -965,6 +983,27 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
   CK(hipStreamSynchronize(c->stream));
   c->staged_B = n_jobs;
   c->staged_nin.assign(n_in, n_in + n_jobs);
+  return FBR_OK;
+}
+
+int fbr_set_deskew(fbr_ctx* c, const fbr_deskew_table* tables, int n_tables) {
+  if (!c || n_tables < 0 || (n_tables > 0 && !tables)) return FBR_ERR_INVALID_ARG;
+  if (n_tables > c->Bcap) return FBR_ERR_CAPACITY;
+  CK(hipSetDevice(c->dev));
+  std::vector<int32_t> mode(c->Bcap, 0);
+  bool any = false;
+  for (int j = 0; j < n_tables; ++j) {
+    if (tables[j].imu_available && (tables[j].imu_pointer_cur < 1 || tables[j].imu_pointer_cur >= FBR_IMU_QUEUE))
+      return FBR_ERR_INVALID_ARG;
+    // deskewPoint and transformUpdate both key on cloudInfo.imuAvailable (:548, mapOptmization.h:1447)
+    mode[j] = tables[j].imu_available ? (kDeskPoints | kDeskImu) : 0;
+    any = any || mode[j] != 0;
+  }
+  if (any && !c->d_desk) CK(hipMalloc((void**)&c->d_desk, sizeof(fbr_deskew_table) * c->Bcap));
+  CK(hipStreamSynchronize(c->stream));
+  if (any) CK(hipMemcpy(c->d_desk, tables, sizeof(fbr_deskew_table) * n_tables, hipMemcpyHostToDevice));
+  CK(hipMemcpy(c->d_desk_mode, mode.data(), sizeof(int32_t) * c->Bcap, hipMemcpyHostToDevice));
+  c->desk_any = any;
   return FBR_OK;
 }
 

@@ -17,9 +17,17 @@ struct MsgDev {
 void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_point_xyzirt* out);
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
                     int W, int32_t* owner);
+// Optional IMU deskew of the kept points (deskewPoint, imageProjection.cpp:545-580): desk_mode
+// [B] (kDesk* bits, fbr_imu.h) and desk [B] tables, both null when no job deskews; rowmin [B][H]
+// receives each row's minimum owner (the scan's first deskewed point is the minimum over rows).
+struct DeskArgs {
+  const int32_t* mode;
+  const fbr_deskew_table* table;
+  int32_t* rowmin;
+};
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,
                     int W, int32_t* rowcnt, float4* cloud, int32_t* col, float* range, int32_t* start_ring,
-                    int32_t* end_ring, int32_t* nvalid);
+                    int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk);
 
 // ---- A6-A8 (k_features.hip) ----
 struct FeatArgs {
@@ -121,6 +129,8 @@ struct GnArgs {
   int32_t* nbr;              // [max_items][5][256] kNN-5 map positions of each query (-1 = rejected)
   unsigned long long* iter_flags;  // host-mapped [max_iter]: (generation << 32) | jobs still active
   int32_t* iter_cnt;         // [max_iter][2] active-job count / finished workgroups (zeroed per solve)
+  const int32_t* desk_mode;  // [B] kDesk* bits or null (transformUpdate's IMU slerp, :1447-1474)
+  const fbr_deskew_table* desk;  // [B]
 };
 void launch_gn_init(hipStream_t s, const GnArgs& a);
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid);

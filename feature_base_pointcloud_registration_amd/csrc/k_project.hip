@@ -11,10 +11,16 @@
 // K2 k_rowcount / k_compact: one wave per (job, ring row); ballot + popcount compaction keeps the
 //                 row-major (ring, column) order of cloudExtraction.  Range is recomputed from the
 //                 owning point (same expression, same bits) instead of storing a range image.
+//                 With an IMU deskew table (fbr_set_deskew) the gathered point goes through
+//                 deskewPoint (:545-580) on the way: the range stays the raw point's (rangeMat is
+//                 written before deskewPoint, :633-635), and transStartInverse comes from the first
+//                 point deskewPoint sees, which is the minimum owner of the scan (the first point
+//                 in input order that passes every check always wins its cell).
 // Roofline: HBM-bound.  Algorithmic bytes: 24 B per raw point read (K1), 4 B/cell owner
 // write+read, 24 B per valid point written (xyzi 16 + col 4 + range 4).
 #include "fbr_common.h"
 #include "fbr_fdlibm.h"
+#include "fbr_imu.h"
 #include "fbr_kernels.h"
 
 namespace fbr {
@@ -104,14 +110,38 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
   }
 }
 
-// One wave per (job,row): number of claimed cells in the row.
-__global__ void k_rowcount(const int32_t* __restrict__ owner, int H, int W, int32_t* __restrict__ rowcnt) {
+// One wave per (job,row): number of claimed cells in the row (and, for deskew, its minimum owner).
+__global__ void k_rowcount(const int32_t* __restrict__ owner, int H, int W, int32_t* __restrict__ rowcnt,
+                           int32_t* __restrict__ rowmin) {
   const int row = blockIdx.x, job = blockIdx.y, lane = threadIdx.x;
   const int32_t* O = owner + ((int64_t)job * H + row) * W;
-  int cnt = 0;
-  for (int c = lane; c < W; c += 64) cnt += (O[c] != kEmptyOwner);
-  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-  if (lane == 0) rowcnt[job * H + row] = cnt;
+  int cnt = 0, mn = kEmptyOwner;
+  for (int c = lane; c < W; c += 64) {
+    const int32_t o = O[c];
+    cnt += (o != kEmptyOwner);
+    mn = min(mn, o);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    cnt += __shfl_xor(cnt, off);
+    if (rowmin) mn = min(mn, __shfl_xor(mn, off));
+  }
+  if (lane == 0) {
+    rowcnt[job * H + row] = cnt;
+    if (rowmin) rowmin[job * H + row] = mn;
+  }
+}
+
+// deskewPoint (imageProjection.cpp:545-580) of one kept point: findRotation at timeScanCur + the
+// point's relative time, transBt = transStartInverse * getTransformation(0, 0, 0, rot).
+__device__ __forceinline__ float4 deskew_point(const fbr_point_xyzirt& q, const fbr_deskew_table& T, const Rot3& Ls,
+                                               const float ts[3]) {
+  float rx, ry, rz;
+  find_rotation(T, T.time_scan_cur + (double)q.time, &rx, &ry, &rz);
+  Rot3 Rb;
+  float tb[3], o[3];
+  compose(Ls, ts, rot_rpy(rx, ry, rz), Rb, tb);
+  apply_affine(Rb, tb, q.x, q.y, q.z, o);
+  return make_float4(o[0], o[1], o[2], q.intensity);
 }
 
 // Blocks are dealt round-robin over the 8 XCDs (b, b+8, ... share one); the (job, row) mapping
@@ -120,7 +150,7 @@ __global__ void k_rowcount(const int32_t* __restrict__ owner, int H, int W, int3
 __global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, const int32_t* __restrict__ owner,
                           const int32_t* __restrict__ rowcnt, int B, int H, int W, float4* __restrict__ cloud,
                           int32_t* __restrict__ col, float* __restrict__ range, int32_t* __restrict__ start_ring,
-                          int32_t* __restrict__ end_ring, int32_t* __restrict__ nvalid) {
+                          int32_t* __restrict__ end_ring, int32_t* __restrict__ nvalid, DeskArgs desk) {
   const int b = blockIdx.x, lane = threadIdx.x;
   const int g = b / (8 * H), x = b % 8;  // job group of 8, XCD slot
   const int job = g * 8 + x, row = (b / 8) % H;
@@ -141,6 +171,19 @@ __global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax
   float4* C = cloud + job * HW;
   int32_t* CI = col + job * HW;
   float* R = range + job * HW;
+  // deskew: transStartInverse from the scan's first deskewed point (the minimum owner)
+  const bool dsk = desk.mode && (desk.mode[job] & kDeskPoints);
+  const fbr_deskew_table* DT = dsk ? desk.table + job : nullptr;
+  Rot3 Ls;
+  float ts[3] = {0.0f, 0.0f, 0.0f};
+  if (dsk) {
+    int mn = kEmptyOwner;
+    for (int r = lane; r < H; r += 64) mn = min(mn, desk.rowmin[job * H + r]);
+    for (int s = 32; s > 0; s >>= 1) mn = min(mn, __shfl_xor(mn, s));
+    float rx = 0.0f, ry = 0.0f, rz = 0.0f;
+    if (mn != kEmptyOwner) find_rotation(*DT, DT->time_scan_cur + (double)P[mn].time, &rx, &ry, &rz);
+    affine_inverse(rot_rpy(rx, ry, rz), Ls, ts);
+  }
   int base = off;
   // two 64-column chunks per step: both chunks' owner loads and point gathers are in flight together
   for (int c0 = 0; c0 < W; c0 += 128) {
@@ -153,14 +196,14 @@ __global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax
     if (vb) qb = P[ob];
     if (va) {
       const int dst = base + __popcll(ma & ((1ull << lane) - 1ull));
-      C[dst] = make_float4(qa.x, qa.y, qa.z, qa.intensity);
+      C[dst] = dsk ? deskew_point(qa, *DT, Ls, ts) : make_float4(qa.x, qa.y, qa.z, qa.intensity);
       CI[dst] = ca;
       R[dst] = sqrt_rn(qa.x * qa.x + qa.y * qa.y + qa.z * qa.z);
     }
     base += __popcll(ma);
     if (vb) {
       const int dst = base + __popcll(mb & ((1ull << lane) - 1ull));
-      C[dst] = make_float4(qb.x, qb.y, qb.z, qb.intensity);
+      C[dst] = dsk ? deskew_point(qb, *DT, Ls, ts) : make_float4(qb.x, qb.y, qb.z, qb.intensity);
       CI[dst] = cb;
       R[dst] = sqrt_rn(qb.x * qb.x + qb.y * qb.y + qb.z * qb.z);
     }
@@ -228,11 +271,11 @@ void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* n
 
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,
                     int W, int32_t* rowcnt, float4* cloud, int32_t* col, float* range, int32_t* start_ring,
-                    int32_t* end_ring, int32_t* nvalid) {
-  hipLaunchKernelGGL(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, rowcnt);
+                    int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk) {
+  hipLaunchKernelGGL(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, rowcnt, desk.mode ? desk.rowmin : nullptr);
   const int groups = (B + 7) / 8;
   hipLaunchKernelGGL(k_compact, dim3(groups * 8 * H), dim3(64), 0, s, pts, nmax, owner, rowcnt, B, H, W, cloud, col,
-                     range, start_ring, end_ring, nvalid);
+                     range, start_ring, end_ring, nvalid, desk);
 }
 
 }  // namespace fbr

@@ -8,7 +8,8 @@
 //   LMOptimization()          :1246-1401 camera-frame Jacobian rows, AtA/AtB, QR solve,
 //                                        iteration-0 degeneracy (eigen < 100), update, 0.05/0.05 stop
 //   scan2MapOptimization()    :1403-1442 feature gate, <= 30 iterations
-//   transformUpdate()         :1444-1489 tolerance clamps (imuAvailable == 0)
+//   transformUpdate()         :1444-1489 IMU roll/pitch slerp when a deskew table says
+//                                        imuAvailable (fbr_set_deskew), tolerance clamps
 //
 // Design (MI355X-first, results identical to the reference's KD-tree path):
 //   * The reference rebuilds two FLANN KD-trees on the cropped local map every scan.  Here the
@@ -30,6 +31,7 @@
 // Roofline: HBM/L2 gather-bound.  Algorithmic bytes per query per iteration: 16 (query) +
 // 5 x 16 (neighbours) = 96 B.
 #include "fbr_common.h"
+#include "fbr_imu.h"
 #include "fbr_kernels.h"
 #include "fbr_solvers.h"
 
@@ -524,7 +526,9 @@ __global__ void k_gn_finalize(GnArgs a) {
   GnState& g = a.gn[job];
   float p[6];
   for (int k = 0; k < 6; ++k) p[k] = g.pose[k];
-  if (g.status == FBR_REG_OK) {  // transformUpdate clamps (:1476-1478)
+  if (g.status == FBR_REG_OK) {  // transformUpdate (:1444-1479)
+    if (a.desk_mode && (a.desk_mode[job] & kDeskImu))  // cloudInfo.imuAvailable: IMU slerp (:1447-1474)
+      imu_slerp_update(p, a.desk[job].imu_roll_init, a.desk[job].imu_pitch_init);
     auto clampf = [](float v, float lim) {
       if (v < -lim) v = -lim;
       if (v > lim) v = lim;

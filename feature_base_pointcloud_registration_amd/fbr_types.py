@@ -21,6 +21,19 @@ REG_STATS_FIELDS = ["status", "iterations", "converged", "degenerate", "n_sel", 
                     "n_surf_ds", "n_corner_map", "n_surf_map", "n_points", "n_corner", "n_surf"]
 REG_STATS = np.dtype([(f, "<i4") for f in REG_STATS_FIELDS])
 
+# IMU deskew (include/fbr.h "IMU deskew"): sensor_msgs/Imu fields, extrinsics, imuDeskewInfo table
+IMU_QUEUE = 500  # queueLength, imageProjection.cpp:23
+IMU_SAMPLE = np.dtype([("stamp", "<f8"), ("linear_acceleration", "<f8", 3), ("angular_velocity", "<f8", 3),
+                       ("orientation", "<f8", 4)])
+assert IMU_SAMPLE.itemsize == 88
+IMU_EXTRINSICS = np.dtype([("ext_rot", "<f8", 9), ("ext_rpy", "<f8", 9)])
+DESKEW_TABLE = np.dtype([("status", "<i4"), ("imu_available", "<i4"), ("imu_pointer_cur", "<i4"),
+                         ("imu_roll_init", "<f4"), ("imu_pitch_init", "<f4"), ("imu_yaw_init", "<f4"),
+                         ("time_scan_cur", "<f8"), ("imu_time", "<f8", IMU_QUEUE), ("imu_rot_x", "<f8", IMU_QUEUE),
+                         ("imu_rot_y", "<f8", IMU_QUEUE), ("imu_rot_z", "<f8", IMU_QUEUE)], align=True)
+assert DESKEW_TABLE.itemsize == 32 + 4 * 8 * IMU_QUEUE
+FBR_DESKEW_READY, FBR_DESKEW_WAIT_IMU = 0, 1
+
 FBR_OK = 0
 FBR_REG_OK = 0
 FBR_REG_NOT_ENOUGH_FEATURES = 1

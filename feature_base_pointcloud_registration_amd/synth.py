@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-from .fbr_types import POINT_XYZI, POINT_XYZIRT, ptr
+from .fbr_types import IMU_SAMPLE, POINT_XYZI, POINT_XYZIRT, ptr
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
@@ -110,3 +110,22 @@ def make_jobs(config, n_jobs, base_seed=1000):
 def config_map(config, seed=11):
     _, _, radius, sd, cd = CONFIGS[config]
     return prior_map(radius, sd, cd, seed=seed)
+
+
+def imu_queue(t0, t1, rate=200.0, gyro=(0.04, -0.03, 0.5), rpy0=(0.01, -0.02, 0.3), seed=0):
+    """IMU samples (IMU_SAMPLE, lidar frame) at `rate` Hz over [t0, t1]: angular velocity `gyro`
+    rad/s plus N(0, 0.002) noise, orientation the integrated attitude from `rpy0` (x, y, z, w),
+    gravity-only acceleration.  Input of fbr_imu_deskew_info (imuDeskewInfo's queue)."""
+    rng = np.random.default_rng(seed)
+    ts = np.arange(t0, t1 + 0.5 / rate, 1.0 / rate)
+    q = np.zeros(len(ts), IMU_SAMPLE)
+    q["stamp"] = ts
+    q["angular_velocity"] = np.asarray(gyro) + rng.normal(0.0, 0.002, (len(ts), 3))
+    q["linear_acceleration"] = (0.0, 0.0, 9.80511)
+    rpy = np.asarray(rpy0) + np.outer(ts - ts[0], gyro)
+    cr, sr = np.cos(rpy[:, 0] / 2), np.sin(rpy[:, 0] / 2)
+    cp, sp = np.cos(rpy[:, 1] / 2), np.sin(rpy[:, 1] / 2)
+    cy, sy = np.cos(rpy[:, 2] / 2), np.sin(rpy[:, 2] / 2)
+    q["orientation"] = np.stack([sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy,
+                                 cr * cp * sy - sr * sp * cy, cr * cp * cy + sr * sp * sy], axis=1)
+    return q

@@ -188,6 +188,68 @@ int fbr_project_msg(fbr_ctx* ctx, const fbr_pointcloud2* msg, int32_t* start_rin
 int fbr_process_msg(fbr_ctx* ctx, const fbr_pointcloud2* msg, double stamp, float pose_inout[6],
                     fbr_reg_stats* stats, int32_t* msg_flags);
 
+/* ---- IMU deskew --------------------------------------------------------
+ * The reference carries LIO-SAM's IMU deskew but calls it nowhere: deskewInfo() is commented out
+ * in cloudHandler (imageProjection.cpp:189-191), so imuAvailable stays 0 and deskewPoint() is the
+ * identity (:548-549).  These entry points restore the path as it runs with that call enabled:
+ *   fbr_imu_convert      imuConverter (utility.h:219-253), applied by imuHandler to each sample
+ *   fbr_imu_deskew_info  deskewInfo + imuDeskewInfo (imageProjection.cpp:303-393) on the host:
+ *                        a serial pass over the ~20 queued samples that builds the scan's table
+ *   fbr_set_deskew       hands tables to the device: the compaction kernel then applies
+ *                        deskewPoint / findRotation (:494-580) to every kept point, and
+ *                        transformUpdate (mapOptmization.h:1444-1474) slerps roll and pitch towards
+ *                        imuRollInit / imuPitchInit.
+ * findPosition is all-zero in the reference (:528-542, positional deskew commented out), and the
+ * odometry half of deskewInfo only fills initial-guess fields read by the disabled
+ * updateInitialGuess; neither has an observable effect on this path. */
+#define FBR_IMU_QUEUE 500 /* queueLength, imageProjection.cpp:23 */
+
+typedef struct fbr_imu_sample { /* the sensor_msgs/Imu fields the path reads */
+  double stamp;                 /* header.stamp.toSec()                                  */
+  double linear_acceleration[3];
+  double angular_velocity[3];
+  double orientation[4];        /* x, y, z, w                                             */
+} fbr_imu_sample;
+
+typedef struct fbr_imu_extrinsics { /* ParamServer extrinsics (utility.h:172-178), row-major */
+  double ext_rot[9];                /* extrinsicRot                                          */
+  double ext_rpy[9];                /* extrinsicRPY (-> extQRPY)                             */
+} fbr_imu_extrinsics;
+
+/* fbr_deskew_table.status */
+#define FBR_DESKEW_READY 0    /* deskewInfo() returned true: the scan is processed                */
+#define FBR_DESKEW_WAIT_IMU 1 /* deskewInfo() returned false (the IMU queue does not cover the
+                                 scan, :310-314): the reference's cloudHandler drops the scan     */
+
+typedef struct fbr_deskew_table { /* imuDeskewInfo() state of one scan (imageProjection.cpp:52-57) */
+  int32_t status;                 /* FBR_DESKEW_*                                                   */
+  int32_t imu_available;          /* cloudInfo.imuAvailable                                         */
+  int32_t imu_pointer_cur;        /* imuPointerCur                                                  */
+  float imu_roll_init, imu_pitch_init, imu_yaw_init; /* cloudInfo.imu{Roll,Pitch,Yaw}Init          */
+  double time_scan_cur;           /* timeScanCur                                                    */
+  double imu_time[FBR_IMU_QUEUE]; /* imuTime                                                        */
+  double imu_rot_x[FBR_IMU_QUEUE], imu_rot_y[FBR_IMU_QUEUE], imu_rot_z[FBR_IMU_QUEUE];
+} fbr_deskew_table;
+
+/* imuConverter: acceleration and angular velocity rotated by extrinsicRot, orientation =
+ * extQRPY * q (Eigen, double).  FBR_ERR_INVALID_ARG for the |q| < 0.1 "please use a 9-axis IMU"
+ * case, where the reference shuts the node down (:246-250). */
+int fbr_imu_convert(const fbr_imu_extrinsics* ext, const fbr_imu_sample* in, fbr_imu_sample* out);
+/* deskewInfo()'s IMU half on a queue of converted samples in arrival order.  *n_pop receives the
+ * number of leading samples imuDeskewInfo pops (stamp < time_scan_cur - 0.01, :328-335), which the
+ * caller removes from its queue (0 when the scan is dropped: deskewInfo returns before popping).
+ * The table's imu_*_init fields are only overwritten when a sample at or before time_scan_cur
+ * remains (:354-355): pass the previous scan's table to keep the reference's carry-over.
+ * FBR_ERR_CAPACITY if the scan needs more than FBR_IMU_QUEUE samples (the reference overruns its
+ * arrays there). */
+int fbr_imu_deskew_info(const fbr_imu_sample* imu_queue, int64_t n_imu, double time_scan_cur,
+                        double time_scan_next, fbr_deskew_table* out, int64_t* n_pop);
+/* Deskew tables for the following calls: job j of a staged batch uses tables[j] (j < n_tables),
+ * the single-scan calls use tables[0].  tables == NULL or n_tables == 0 restores the reference's
+ * runtime behaviour (no deskew, imuAvailable = 0).  A PointCloud2 without a "time" field disables
+ * the point deskew for that call (deskewFlag = -1, :296-297, :548) but not the IMU update. */
+int fbr_set_deskew(fbr_ctx* ctx, const fbr_deskew_table* tables, int n_tables);
+
 /* Down-sampled global map actually used (sizes, then optional copies; pass NULL to skip). */
 int fbr_get_map(fbr_ctx* ctx, int64_t* n_corner, int64_t* n_surf, fbr_point_xyzi* corner,
                 fbr_point_xyzi* surf);

@@ -41,6 +41,185 @@ static inline int x86_cvt(double v) {
 }
 
 // =============================================================================================
+// Pose conversions: pcl::getTransformation / pcl::getTranslationAndEulerAngles (PCL common/eigen)
+// =============================================================================================
+struct Affine {
+  float m[3][4];
+};
+
+static Affine get_transformation(float x, float y, float z, float roll, float pitch, float yaw) {
+  float A = std::cos(yaw), B = std::sin(yaw), C = std::cos(pitch), D = std::sin(pitch),
+        E = std::cos(roll), F = std::sin(roll), DE = D * E, DF = D * F;
+  Affine t;
+  t.m[0][0] = A * C; t.m[0][1] = A * DF - B * E; t.m[0][2] = B * F + A * DE; t.m[0][3] = x;
+  t.m[1][0] = B * C; t.m[1][1] = A * E + B * DF; t.m[1][2] = B * DE - A * F; t.m[1][3] = y;
+  t.m[2][0] = -D;    t.m[2][1] = C * F;          t.m[2][2] = C * E;          t.m[2][3] = z;
+  return t;
+}
+
+static void get_translation_euler(const Affine& t, float pose[6]) {
+  pose[3] = t.m[0][3];
+  pose[4] = t.m[1][3];
+  pose[5] = t.m[2][3];
+  pose[0] = std::atan2(t.m[2][1], t.m[2][2]);
+  pose[1] = std::asin(-t.m[2][0]);
+  pose[2] = std::atan2(t.m[1][0], t.m[0][0]);
+}
+
+// trans2Affine3f (mapOptmization.h:444-448)
+static Affine trans2affine(const float tr[6]) { return get_transformation(tr[3], tr[4], tr[5], tr[0], tr[1], tr[2]); }
+
+// pointAssociateToMap (mapOptmization.h:397-403)
+static inline P4 associate(const Affine& T, const P4& p) {
+  P4 o;
+  o.x = T.m[0][0] * p.x + T.m[0][1] * p.y + T.m[0][2] * p.z + T.m[0][3];
+  o.y = T.m[1][0] * p.x + T.m[1][1] * p.y + T.m[1][2] * p.z + T.m[1][3];
+  o.z = T.m[2][0] * p.x + T.m[2][1] * p.y + T.m[2][2] * p.z + T.m[2][3];
+  o.intensity = p.intensity;
+  return o;
+}
+
+
+// =============================================================================================
+// A3: deskewPoint / findRotation / findPosition (imageProjection.cpp:494-580) on the table that
+// imuDeskewInfo (:323-393) builds.  The reference never runs this: deskewInfo() is commented out
+// at :189-191, so imuAvailable == 0 and deskewPoint returns the point (:548-549).  It is restated
+// for the path with that call enabled.  Third-party pieces: pcl::
+// getTransformation (float, glibc sinf/cosf), Eigen 3.3 Affine3f::inverse (3x3 cofactor inverse,
+// InverseImpl.h) and Affine3f * Affine3f (linear * linear, linear * t + t); Eigen's fixed-size
+// 3-term sums reduce as x0 + (x1 + x2) (redux_novec_unroller).
+// =============================================================================================
+static void find_rotation(const fbr_deskew_table& T, double pointTime, float* rotXCur, float* rotYCur,
+                          float* rotZCur) {  // :494-526
+  *rotXCur = 0;
+  *rotYCur = 0;
+  *rotZCur = 0;
+  int imuPointerFront = 0;
+  while (imuPointerFront < T.imu_pointer_cur) {
+    if (pointTime < T.imu_time[imuPointerFront]) break;
+    ++imuPointerFront;
+  }
+  if (pointTime > T.imu_time[imuPointerFront] || imuPointerFront == 0) {
+    *rotXCur = T.imu_rot_x[imuPointerFront];
+    *rotYCur = T.imu_rot_y[imuPointerFront];
+    *rotZCur = T.imu_rot_z[imuPointerFront];
+  } else {
+    int imuPointerBack = imuPointerFront - 1;
+    double ratioFront = (pointTime - T.imu_time[imuPointerBack]) / (T.imu_time[imuPointerFront] - T.imu_time[imuPointerBack]);
+    double ratioBack = (T.imu_time[imuPointerFront] - pointTime) / (T.imu_time[imuPointerFront] - T.imu_time[imuPointerBack]);
+    *rotXCur = T.imu_rot_x[imuPointerFront] * ratioFront + T.imu_rot_x[imuPointerBack] * ratioBack;
+    *rotYCur = T.imu_rot_y[imuPointerFront] * ratioFront + T.imu_rot_y[imuPointerBack] * ratioBack;
+    *rotZCur = T.imu_rot_z[imuPointerFront] * ratioFront + T.imu_rot_z[imuPointerBack] * ratioBack;
+  }
+}
+
+static inline float eig_sum3(float a, float b, float c) { return a + (b + c); }
+
+static Affine eigen_affine_inverse(const Affine& a) {  // Transform<float,3,Affine>::inverse()
+  auto cof = [&](int i, int j) {  // cofactor_3x3<i,j>
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    return a.m[i1][j1] * a.m[i2][j2] - a.m[i1][j2] * a.m[i2][j1];
+  };
+  const float c0 = cof(0, 0), c1 = cof(1, 0), c2 = cof(2, 0);
+  const float det = eig_sum3(c0 * a.m[0][0], c1 * a.m[1][0], c2 * a.m[2][0]);
+  const float invdet = 1.0f / det;
+  Affine r;
+  r.m[0][0] = c0 * invdet;
+  r.m[0][1] = c1 * invdet;
+  r.m[0][2] = c2 * invdet;
+  r.m[1][0] = cof(0, 1) * invdet;
+  r.m[1][1] = cof(1, 1) * invdet;
+  r.m[1][2] = cof(2, 1) * invdet;
+  r.m[2][0] = cof(0, 2) * invdet;
+  r.m[2][1] = cof(1, 2) * invdet;
+  r.m[2][2] = cof(2, 2) * invdet;
+  for (int i = 0; i < 3; ++i)  // (-L^-1) * t
+    r.m[i][3] = eig_sum3(-r.m[i][0] * a.m[0][3], -r.m[i][1] * a.m[1][3], -r.m[i][2] * a.m[2][3]);
+  return r;
+}
+
+static Affine eigen_affine_mul(const Affine& l, const Affine& r) {  // Affine3f * Affine3f
+  Affine o;
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) o.m[i][j] = eig_sum3(l.m[i][0] * r.m[0][j], l.m[i][1] * r.m[1][j], l.m[i][2] * r.m[2][j]);
+    o.m[i][3] = eig_sum3(l.m[i][0] * r.m[0][3], l.m[i][1] * r.m[1][3], l.m[i][2] * r.m[2][3]) + l.m[i][3];
+  }
+  return o;
+}
+
+struct Deskewer {  // deskewPoint (:545-580) with its per-scan firstPointFlag / transStartInverse
+  const fbr_deskew_table* T;
+  bool firstPointFlag = true;
+  Affine transStartInverse;
+  P4 operator()(const P4& point, double relTime) {
+    double pointTime = T->time_scan_cur + relTime;
+    float rotXCur, rotYCur, rotZCur;
+    find_rotation(*T, pointTime, &rotXCur, &rotYCur, &rotZCur);
+    float posXCur = 0, posYCur = 0, posZCur = 0;  // findPosition (:528-542): positional deskew commented out
+    if (firstPointFlag) {
+      transStartInverse = eigen_affine_inverse(get_transformation(posXCur, posYCur, posZCur, rotXCur, rotYCur, rotZCur));
+      firstPointFlag = false;
+    }
+    Affine transFinal = get_transformation(posXCur, posYCur, posZCur, rotXCur, rotYCur, rotZCur);
+    Affine transBt = eigen_affine_mul(transStartInverse, transFinal);
+    P4 newPoint;
+    newPoint.x = transBt.m[0][0] * point.x + transBt.m[0][1] * point.y + transBt.m[0][2] * point.z + transBt.m[0][3];
+    newPoint.y = transBt.m[1][0] * point.x + transBt.m[1][1] * point.y + transBt.m[1][2] * point.z + transBt.m[1][3];
+    newPoint.z = transBt.m[2][0] * point.x + transBt.m[2][1] * point.y + transBt.m[2][2] * point.z + transBt.m[2][3];
+    newPoint.intensity = point.intensity;
+    return newPoint;
+  }
+};
+
+// ---- tf LinearMath (tfScalar = double): Quaternion::setRPY / slerp, Matrix3x3::getRPY ----
+struct TfQuaternion {
+  double x, y, z, w;
+};
+static TfQuaternion tf_setRPY(double roll, double pitch, double yaw) {
+  double halfYaw = yaw * 0.5, halfPitch = pitch * 0.5, halfRoll = roll * 0.5;
+  double cosYaw = std::cos(halfYaw), sinYaw = std::sin(halfYaw);
+  double cosPitch = std::cos(halfPitch), sinPitch = std::sin(halfPitch);
+  double cosRoll = std::cos(halfRoll), sinRoll = std::sin(halfRoll);
+  return TfQuaternion{sinRoll * cosPitch * cosYaw - cosRoll * sinPitch * sinYaw,
+                      cosRoll * sinPitch * cosYaw + sinRoll * cosPitch * sinYaw,
+                      cosRoll * cosPitch * sinYaw - sinRoll * sinPitch * cosYaw,
+                      cosRoll * cosPitch * cosYaw + sinRoll * sinPitch * sinYaw};
+}
+static double tf_dot(const TfQuaternion& a, const TfQuaternion& b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+static double tfAcos(double x) { return std::acos(x < -1 ? -1 : (x > 1 ? 1 : x)); }
+static double tfAsin(double x) { return std::asin(x < -1 ? -1 : (x > 1 ? 1 : x)); }
+static TfQuaternion tf_slerp(const TfQuaternion& a, const TfQuaternion& q, double t) {
+  double s = std::sqrt(tf_dot(a, a) * tf_dot(q, q));  // angleShortestPath
+  double angle = tf_dot(a, q) < 0 ? tfAcos(tf_dot(a, TfQuaternion{-q.x, -q.y, -q.z, -q.w}) / s) * 2.0
+                                  : tfAcos(tf_dot(a, q) / s) * 2.0;
+  double theta = angle / 2.0;
+  if (theta == 0.0) return a;
+  double d = 1.0 / std::sin(theta), s0 = std::sin((1.0 - t) * theta), s1 = std::sin(t * theta);
+  if (tf_dot(a, q) < 0)
+    return TfQuaternion{(a.x * s0 + -q.x * s1) * d, (a.y * s0 + -q.y * s1) * d, (a.z * s0 + -q.z * s1) * d,
+                        (a.w * s0 + -q.w * s1) * d};
+  return TfQuaternion{(a.x * s0 + q.x * s1) * d, (a.y * s0 + q.y * s1) * d, (a.z * s0 + q.z * s1) * d,
+                      (a.w * s0 + q.w * s1) * d};
+}
+static void tf_getRPY(const TfQuaternion& q, double& roll, double& pitch, double& yaw) {
+  double d = tf_dot(q, q), s = 2.0 / d;  // Matrix3x3::setRotation
+  double xs = q.x * s, ys = q.y * s, zs = q.z * s;
+  double wx = q.w * xs, wy = q.w * ys, wz = q.w * zs;
+  double xx = q.x * xs, xy = q.x * ys, xz = q.x * zs;
+  double yy = q.y * ys, yz = q.y * zs, zz = q.z * zs;
+  double el[3][3] = {{1.0 - (yy + zz), xy - wz, xz + wy}, {xy + wz, 1.0 - (xx + zz), yz - wx}, {xz - wy, yz + wx, 1.0 - (xx + yy)}};
+  if (std::fabs(el[2][0]) >= 1) {  // getEulerYPR, solution 1
+    yaw = 0;
+    pitch = el[2][0] < 0 ? M_PI / 2.0 : -M_PI / 2.0;
+    roll = std::atan2(el[2][1], el[2][2]);
+  } else {
+    pitch = -tfAsin(el[2][0]);
+    roll = std::atan2(el[2][1] / std::cos(pitch), el[2][2] / std::cos(pitch));
+    yaw = std::atan2(el[1][0] / std::cos(pitch), el[0][0] / std::cos(pitch));
+  }
+}
+
+// =============================================================================================
 // A2 + A4: ImageProjection::projectPointCloud + cloudExtraction (imageProjection.cpp:583-670)
 // =============================================================================================
 struct Projection {
@@ -49,8 +228,11 @@ struct Projection {
   std::vector<P4> cloud;
 };
 
-static void project(const fbr_params& P, const fbr_point_xyzirt* pts, int64_t n_in, Projection& out) {
+static void project(const fbr_params& P, const fbr_point_xyzirt* pts, int64_t n_in, Projection& out,
+                    const fbr_deskew_table* T = nullptr) {
   const int H = P.n_scan, W = P.horizon_scan;
+  const bool deskew = T && T->imu_available;  // deskewPoint (:548): deskewFlag != -1 is the caller's
+  Deskewer deskewPoint{T};
   std::vector<float> rangeMat((size_t)H * W, FLT_MAX);  // :130
   std::vector<P4> full((size_t)H * W);                   // :114
   for (int64_t i = 0; i < n_in; ++i) {
@@ -69,7 +251,9 @@ static void project(const fbr_params& P, const fbr_point_xyzirt* pts, int64_t n_
     size_t c = (size_t)rowIdn * W + columnIdn;
     if (rangeMat[c] != FLT_MAX) continue;                                              // :623
     rangeMat[c] = range;                                                               // :633
-    full[c] = P4{q.x, q.y, q.z, q.intensity};  // deskewPoint is identity: imuAvailable==0 (:548)
+    P4 thisPoint{q.x, q.y, q.z, q.intensity};
+    if (deskew) thisPoint = deskewPoint(thisPoint, q.time);                           // :635
+    full[c] = thisPoint;  // without a table deskewPoint is the identity (imuAvailable == 0, :548)
   }
   out.start.assign(H, 0);
   out.end.assign(H, 0);
@@ -294,45 +478,6 @@ static void extract_features(const fbr_params& P, FeatState& S, const Projection
     voxel_grid(surfScan.data(), (int64_t)surfScan.size(), P.odometry_surf_leaf_size, surfScanDS);
     F.surf.insert(F.surf.end(), surfScanDS.begin(), surfScanDS.end());
   }
-}
-
-// =============================================================================================
-// Pose conversions: pcl::getTransformation / pcl::getTranslationAndEulerAngles (PCL common/eigen)
-// =============================================================================================
-struct Affine {
-  float m[3][4];
-};
-
-static Affine get_transformation(float x, float y, float z, float roll, float pitch, float yaw) {
-  float A = std::cos(yaw), B = std::sin(yaw), C = std::cos(pitch), D = std::sin(pitch),
-        E = std::cos(roll), F = std::sin(roll), DE = D * E, DF = D * F;
-  Affine t;
-  t.m[0][0] = A * C; t.m[0][1] = A * DF - B * E; t.m[0][2] = B * F + A * DE; t.m[0][3] = x;
-  t.m[1][0] = B * C; t.m[1][1] = A * E + B * DF; t.m[1][2] = B * DE - A * F; t.m[1][3] = y;
-  t.m[2][0] = -D;    t.m[2][1] = C * F;          t.m[2][2] = C * E;          t.m[2][3] = z;
-  return t;
-}
-
-static void get_translation_euler(const Affine& t, float pose[6]) {
-  pose[3] = t.m[0][3];
-  pose[4] = t.m[1][3];
-  pose[5] = t.m[2][3];
-  pose[0] = std::atan2(t.m[2][1], t.m[2][2]);
-  pose[1] = std::asin(-t.m[2][0]);
-  pose[2] = std::atan2(t.m[1][0], t.m[0][0]);
-}
-
-// trans2Affine3f (mapOptmization.h:444-448)
-static Affine trans2affine(const float tr[6]) { return get_transformation(tr[3], tr[4], tr[5], tr[0], tr[1], tr[2]); }
-
-// pointAssociateToMap (mapOptmization.h:397-403)
-static inline P4 associate(const Affine& T, const P4& p) {
-  P4 o;
-  o.x = T.m[0][0] * p.x + T.m[0][1] * p.y + T.m[0][2] * p.z + T.m[0][3];
-  o.y = T.m[1][0] * p.x + T.m[1][1] * p.y + T.m[1][2] * p.z + T.m[1][3];
-  o.z = T.m[2][0] * p.x + T.m[2][1] * p.y + T.m[2][2] * p.z + T.m[2][3];
-  o.intensity = p.intensity;
-  return o;
 }
 
 // =============================================================================================
@@ -770,7 +915,8 @@ static void crop(const std::vector<P4>& in, const float mn[3], const float mx[3]
 }
 
 static void registration_core(const fbr_params& P, const Map& map, const P4* cornerLast, int64_t ncl,
-                              const P4* surfLast, int64_t nsl, float tr[6], RegResult& R, int nthreads) {
+                              const P4* surfLast, int64_t nsl, float tr[6], RegResult& R, int nthreads,
+                              const fbr_deskew_table* T = nullptr) {
   fbr_reg_stats& st = R.st;
   std::memset(&st, 0, sizeof(st));
   R.trace.clear();
@@ -986,7 +1132,21 @@ static void registration_core(const fbr_params& P, const Map& map, const P4* cor
       break;
     }
   }
-  // transformUpdate (:1444-1479): imuAvailable == 0, only the tolerance clamps apply
+  // transformUpdate (:1444-1479)
+  if (T && T->imu_available) {  // cloudInfo.imuAvailable (:1447)
+    if (std::abs(T->imu_pitch_init) < 1.4) {
+      double imuWeight = 0.05;
+      double rollMid, pitchMid, yawMid;
+      TfQuaternion transformQuaternion = tf_setRPY(tr[0], 0, 0);
+      TfQuaternion imuQuaternion = tf_setRPY(T->imu_roll_init, 0, 0);
+      tf_getRPY(tf_slerp(transformQuaternion, imuQuaternion, imuWeight), rollMid, pitchMid, yawMid);
+      tr[0] = rollMid;
+      transformQuaternion = tf_setRPY(0, tr[1], 0);
+      imuQuaternion = tf_setRPY(0, T->imu_pitch_init, 0);
+      tf_getRPY(tf_slerp(transformQuaternion, imuQuaternion, imuWeight), rollMid, pitchMid, yawMid);
+      tr[1] = pitchMid;
+    }
+  }
   auto clampf = [](float v, float lim) {
     if (v < -lim) v = -lim;
     if (v > lim) v = lim;
@@ -1008,14 +1168,18 @@ struct orc_stream {
   fbr_params P;
   FeatState fs;
   double timeLastProcessing = -1;
+  bool has_desk = false;  // deskewInfo() enabled for the next scans (orc_stream_set_deskew)
+  fbr_deskew_table desk;
+  const fbr_deskew_table* table() const { return has_desk ? &desk : nullptr; }
 };
 
 extern "C" {
 
 int64_t orc_project(const fbr_params* P, const fbr_point_xyzirt* pts, int64_t n_in, int32_t* start_ring,
-                    int32_t* end_ring, int32_t* col_ind, float* range, fbr_point_xyzi* cloud) {
+                    int32_t* end_ring, int32_t* col_ind, float* range, fbr_point_xyzi* cloud,
+                    const fbr_deskew_table* desk) {
   Projection pr;
-  project(*P, pts, n_in, pr);
+  project(*P, pts, n_in, pr, desk);
   const int64_t n = (int64_t)pr.col.size();
   if (start_ring) std::memcpy(start_ring, pr.start.data(), sizeof(int32_t) * P->n_scan);
   if (end_ring) std::memcpy(end_ring, pr.end.data(), sizeof(int32_t) * P->n_scan);
@@ -1039,6 +1203,11 @@ void* orc_stream_create(const fbr_params* P) {
   return s;
 }
 void orc_stream_destroy(void* s) { delete (orc_stream*)s; }
+void orc_stream_set_deskew(void* s, const fbr_deskew_table* t) {
+  orc_stream* st = (orc_stream*)s;
+  st->has_desk = t != nullptr;
+  if (t) st->desk = *t;
+}
 void orc_stream_reset(void* s) {
   orc_stream* st = (orc_stream*)s;
   st->fs.init(st->P.n_scan, st->P.horizon_scan);
@@ -1050,7 +1219,7 @@ int orc_features(void* s, const fbr_point_xyzirt* pts, int64_t n_in, int8_t* lab
                  int64_t* n_corner, fbr_point_xyzi* surf, int64_t* n_surf, int64_t* n_points) {
   orc_stream* st = (orc_stream*)s;
   Projection pr;
-  project(st->P, pts, n_in, pr);
+  project(st->P, pts, n_in, pr, st->table());
   Features F;
   extract_features(st->P, st->fs, pr, F);
   const int64_t n = (int64_t)pr.col.size();
@@ -1082,9 +1251,10 @@ int orc_map_get(void* mp, int64_t* nc, int64_t* ns, fbr_point_xyzi* corner, fbr_
 }
 
 int orc_register(const fbr_params* P, void* map, const fbr_point_xyzi* corner, int64_t nc, const fbr_point_xyzi* surf,
-                 int64_t ns, float pose[6], fbr_reg_stats* st, float* trace, int nthreads) {
+                 int64_t ns, float pose[6], fbr_reg_stats* st, float* trace, int nthreads,
+                 const fbr_deskew_table* desk) {
   RegResult R;
-  registration_core(*P, *(Map*)map, corner, nc, surf, ns, pose, R, nthreads);
+  registration_core(*P, *(Map*)map, corner, nc, surf, ns, pose, R, nthreads, desk);
   if (st) *st = R.st;
   if (trace) std::memcpy(trace, R.trace.data(), sizeof(float) * R.trace.size());
   return 0;
@@ -1095,7 +1265,7 @@ int orc_process_scan(void* s, void* map, const fbr_point_xyzirt* pts, int64_t n_
                      fbr_reg_stats* st, int nthreads) {
   orc_stream* S = (orc_stream*)s;
   Projection pr;
-  project(S->P, pts, n_in, pr);
+  project(S->P, pts, n_in, pr, S->table());
   Features F;
   extract_features(S->P, S->fs, pr, F);
   RegResult R;
@@ -1103,7 +1273,7 @@ int orc_process_scan(void* s, void* map, const fbr_point_xyzirt* pts, int64_t n_
   if (stamp - S->timeLastProcessing >= S->P.mapping_process_interval) {
     S->timeLastProcessing = stamp;
     registration_core(S->P, *(Map*)map, F.corner.data(), (int64_t)F.corner.size(), F.surf.data(),
-                      (int64_t)F.surf.size(), pose, R, nthreads);
+                      (int64_t)F.surf.size(), pose, R, nthreads, S->table());
   } else {
     R.st.status = FBR_REG_SKIPPED_INTERVAL;
   }
@@ -1126,6 +1296,122 @@ void orc_pose_from_affine(const float m[16], float pose[6]) {
   for (int r = 0; r < 3; ++r)
     for (int c = 0; c < 4; ++c) t.m[r][c] = m[r * 4 + c];
   get_translation_euler(t, pose);
+}
+
+// imuConverter (utility.h:219-253) for the CPU tests of fbr_imu_convert: Eigen Matrix3d * Vector3d
+// (coefficient products summed x0 + (x1 + x2)), Quaterniond(Matrix3d), generic quaternion product.
+int orc_imu_convert(const fbr_imu_extrinsics* ext, const fbr_imu_sample* in, fbr_imu_sample* out) {
+  *out = *in;
+  const double* R = ext->ext_rot;
+  for (int r = 0; r < 3; ++r) {
+    const double* a = in->linear_acceleration;
+    const double* g = in->angular_velocity;
+    out->linear_acceleration[r] = R[3 * r] * a[0] + (R[3 * r + 1] * a[1] + R[3 * r + 2] * a[2]);
+    out->angular_velocity[r] = R[3 * r] * g[0] + (R[3 * r + 1] * g[1] + R[3 * r + 2] * g[2]);
+  }
+  const double* m = ext->ext_rpy;  // extQRPY = Eigen::Quaterniond(extRPY): x, y, z, w
+  double e[4];
+  double t = m[0] + (m[4] + m[8]);
+  if (t > 0) {
+    t = std::sqrt(t + 1.0);
+    e[3] = 0.5 * t;
+    t = 0.5 / t;
+    e[0] = (m[7] - m[5]) * t;
+    e[1] = (m[2] - m[6]) * t;
+    e[2] = (m[3] - m[1]) * t;
+  } else {
+    int i = 0;
+    if (m[4] > m[0]) i = 1;
+    if (m[8] > m[4 * i]) i = 2;
+    int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = std::sqrt(m[4 * i] - m[4 * j] - m[4 * k] + 1.0);
+    e[i] = 0.5 * t;
+    t = 0.5 / t;
+    e[3] = (m[3 * k + j] - m[3 * j + k]) * t;
+    e[j] = (m[3 * j + i] + m[3 * i + j]) * t;
+    e[k] = (m[3 * k + i] + m[3 * i + k]) * t;
+  }
+  const double* b = in->orientation;  // q_final = extQRPY * q_from
+  double w = e[3] * b[3] - e[0] * b[0] - e[1] * b[1] - e[2] * b[2];
+  double x = e[3] * b[0] + e[0] * b[3] + e[1] * b[2] - e[2] * b[1];
+  double y = e[3] * b[1] + e[1] * b[3] + e[2] * b[0] - e[0] * b[2];
+  double z = e[3] * b[2] + e[2] * b[3] + e[0] * b[1] - e[1] * b[0];
+  out->orientation[0] = x;
+  out->orientation[1] = y;
+  out->orientation[2] = z;
+  out->orientation[3] = w;
+  if (std::sqrt(x * x + y * y + z * z + w * w) < 0.1) return -1;  // "please use a 9-axis IMU!"
+  return 0;
+}
+
+// deskewInfo + imuDeskewInfo (imageProjection.cpp:303-393) on a copy of the queue, run as written
+// (pop_front, then the integration loop); *n_pop = samples popped.  imu*Init: imuRPY2rosRPY
+// (tf::quaternionMsgToTF, normalised when |length2 - 1| > 0.1, then Matrix3x3::getRPY).
+int orc_imu_deskew_info(const fbr_imu_sample* q, int64_t n, double timeScanCur, double timeScanNext,
+                        fbr_deskew_table* out, int64_t* n_pop) {
+  std::vector<fbr_imu_sample> imuQueue(q, q + n);
+  size_t front = 0;
+  const float ri = out->imu_roll_init, pi = out->imu_pitch_init, yi = out->imu_yaw_init;
+  std::memset(out, 0, sizeof(*out));
+  out->imu_roll_init = ri;
+  out->imu_pitch_init = pi;
+  out->imu_yaw_init = yi;
+  out->time_scan_cur = timeScanCur;
+  *n_pop = 0;
+  if (imuQueue.empty() || imuQueue.front().stamp > timeScanCur || imuQueue.back().stamp < timeScanNext) {
+    out->status = FBR_DESKEW_WAIT_IMU;  // "Waiting for IMU data ..." (:310-314)
+    return 0;
+  }
+  out->status = FBR_DESKEW_READY;
+  out->imu_available = 0;
+  while (front < imuQueue.size()) {
+    if (imuQueue[front].stamp < timeScanCur - 0.01) ++front;
+    else break;
+  }
+  *n_pop = (int64_t)front;
+  if (front == imuQueue.size()) return 0;
+  int imuPointerCur = 0;
+  for (size_t i = front; i < imuQueue.size(); ++i) {
+    const fbr_imu_sample& thisImuMsg = imuQueue[i];
+    double currentImuTime = thisImuMsg.stamp;
+    if (currentImuTime <= timeScanCur) {
+      TfQuaternion o{thisImuMsg.orientation[0], thisImuMsg.orientation[1], thisImuMsg.orientation[2],
+                     thisImuMsg.orientation[3]};
+      double l2 = tf_dot(o, o);
+      if (std::fabs(l2 - 1) > 0.1f) {
+        double f = 1.0 / std::sqrt(l2);
+        o = TfQuaternion{o.x * f, o.y * f, o.z * f, o.w * f};
+      }
+      double imuRoll, imuPitch, imuYaw;
+      tf_getRPY(o, imuRoll, imuPitch, imuYaw);
+      out->imu_roll_init = imuRoll;
+      out->imu_pitch_init = imuPitch;
+      out->imu_yaw_init = imuYaw;
+    }
+    if (currentImuTime > timeScanNext + 0.01) break;
+    if (imuPointerCur >= FBR_IMU_QUEUE) return -4;
+    if (imuPointerCur == 0) {
+      out->imu_rot_x[0] = 0;
+      out->imu_rot_y[0] = 0;
+      out->imu_rot_z[0] = 0;
+      out->imu_time[0] = currentImuTime;
+      ++imuPointerCur;
+      continue;
+    }
+    double angular_x = thisImuMsg.angular_velocity[0], angular_y = thisImuMsg.angular_velocity[1],
+           angular_z = thisImuMsg.angular_velocity[2];
+    double timeDiff = currentImuTime - out->imu_time[imuPointerCur - 1];
+    out->imu_rot_x[imuPointerCur] = out->imu_rot_x[imuPointerCur - 1] + angular_x * timeDiff;
+    out->imu_rot_y[imuPointerCur] = out->imu_rot_y[imuPointerCur - 1] + angular_y * timeDiff;
+    out->imu_rot_z[imuPointerCur] = out->imu_rot_z[imuPointerCur - 1] + angular_z * timeDiff;
+    out->imu_time[imuPointerCur] = currentImuTime;
+    ++imuPointerCur;
+  }
+  --imuPointerCur;
+  out->imu_pointer_cur = imuPointerCur < 0 ? 0 : imuPointerCur;  // (-1 in the reference: unused then)
+  if (imuPointerCur <= 0) return 0;
+  out->imu_available = 1;
+  return 0;
 }
 
 // Small-solver probes for unit tests.
