@@ -28,6 +28,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "registered scans/sec + pose RMSE vs ref, 64×1800 synthetic Velodyne"
+WORKLOAD = {"C1": "VLP-16-style scans, local corner+surf map",
+            "C2": "HDL-64-style scans, ~100k-pt local corner+surf map",
+            "C3": "Ouster-style scans, ~500k-pt local corner+surf map (mapping leaves 0.1/0.2)",
+            "C5": "dense scans, ~5.8M-pt map inside the crop box (mapping leaves 0.05)"}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 # Algorithmic bytes per unit for each kernel family (DESIGN.md "Kernels and rooflines").
@@ -49,9 +53,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="jobs per GPU per step")
-    ap.add_argument("--config", default="C2")
-    ap.add_argument("--cpu-sample", type=int, default=24, help="jobs timed on the CPU oracle (N=1)")
+    ap.add_argument("--batch", type=int, default=256, help="jobs per GPU per step")
+    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C5"])
+    ap.add_argument("--cpu-sample", type=int, default=96, help="jobs timed on the CPU oracle (N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="worker threads of the all-cores CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist", action="store_true",
                     help="use the torch.distributed (RCCL) path even at world size 1 (tests)")
@@ -76,19 +82,20 @@ def main():
         dist.init_process_group(backend="nccl", init_method="env://")
 
     from feature_base_pointcloud_registration_amd import api, shard, synth
-    from feature_base_pointcloud_registration_amd.fbr_types import default_params
 
     cfg = args.config
     H, W, *_ = synth.CONFIGS[cfg]
     B = args.batch
-    P = default_params(H, W, max_batch=B)
+    P = synth.config_params(cfg, max_batch=B)
     corner_map, surf_map = synth.config_map(cfg)
     jobs = synth.make_jobs(cfg, B, base_seed=1000 + rank * B)
     scans = [j[0] for j in jobs]
     guesses = np.stack([j[1] for j in jobs]).astype(np.float32)
     gts = np.stack([j[2] for j in jobs])
 
-    ctx = api.Context(P, device=local_rank if world > 1 else 0)
+    dev = local_rank if world > 1 else 0
+    stream_gbps = api.stream_copy_bandwidth(dev) if rank == 0 else None  # achievable HBM copy rate
+    ctx = api.Context(P, device=dev)
     ctx.set_map(corner_map, surf_map)
     ctx.batch_stage(scans, guesses)
 
@@ -193,7 +200,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": f"{cfg}: {H}x{W} HDL-64-style scans, ~100k-pt local corner+surf map; "
+            "workload": f"{cfg}: {H}x{W} {WORKLOAD[cfg]}; "
                         f"{B} independent scan-to-map jobs per GPU per step (C4 shard)",
             "jobs_per_gpu_per_step": B,
             "mean_points_per_scan": round(tot["n_in"] / B, 1),
@@ -209,6 +216,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "stream_copy_GBps": round(stream_gbps, 1),
+            "frac_vs_stream_copy": round(achieved / stream_gbps, 5),
             "traffic": traffic,
             "bytes_per_launch": bytes_per_launch,
             "avg_launch_us": round(avg_launch_s * 1e6, 3),
@@ -219,6 +228,7 @@ def main():
         "kernel_ms_per_step": {k: round(v[0], 4) for k, v in prof.items()},  # profiled untimed step
         "path_bytes_per_step": tb,
         "path_achieved_GBps": round(tb / (elapsed / args.steps) / 1e9, 2),
+        "path_frac_of_peak": round(tb / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 5),
         "max_abs_trans_err_vs_gt_m": float(err_gt),
         "registration_status_ok": int((stats["status"] == 0).sum()),
     }
@@ -253,6 +263,21 @@ def main():
             "n": S,
         }
         result["gpu_vs_cpu_speedup"] = round(value / (S / cpu_s), 2)
+        # all-cores batch: one independent job per worker thread, one OpenMP thread each
+        # (ctypes releases the GIL inside the oracle calls)
+        import concurrent.futures
+        nth = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
+
+        def one(j):
+            return O.Stream(P).process_scan(omap, scans[j], 0.0, guesses[j], n_threads=1)[0]
+
+        t2 = time.perf_counter()
+        with concurrent.futures.ThreadPoolExecutor(nth) as ex:
+            list(ex.map(one, range(S)))
+        cpu_all_s = time.perf_counter() - t2
+        result["cpu_baseline_all_cores"] = {
+            "value": round(S / cpu_all_s, 3), "unit": "scans/s", "cores": nth, "kind": "port",
+            "sample": f"the same {S} jobs, {nth} independent single-threaded jobs at a time"}
     print(json.dumps(result), flush=True)
     ctx.close()
     if dist is not None:

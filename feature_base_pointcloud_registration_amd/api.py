@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = [
     "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math",
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
     "fbr_msg_to_points", "fbr_points_to_msg_data", "fbr_project_msg", "fbr_process_msg",
-    "fbr_imu_convert", "fbr_imu_deskew_info", "fbr_set_deskew",
+    "fbr_imu_convert", "fbr_imu_deskew_info", "fbr_set_deskew", "fbr_stream_copy_bandwidth",
 ]
 
 
@@ -98,6 +98,7 @@ def lib():
             "fbr_imu_convert": (ctypes.c_int, [_VP, _VP, _VP]),
             "fbr_imu_deskew_info": (ctypes.c_int, [_VP, _I64, ctypes.c_double, ctypes.c_double, _VP, _VP]),
             "fbr_set_deskew": (ctypes.c_int, [_VP, _VP, ctypes.c_int]),
+            "fbr_stream_copy_bandwidth": (ctypes.c_int, [ctypes.c_int, _I64, ctypes.c_int, _VP]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -129,6 +130,13 @@ def selftest_math(a, b):
     out = np.zeros((len(a), 4), np.float32)
     _check(lib().fbr_selftest_math(len(a), ptr(a), ptr(b), ptr(out)), "fbr_selftest_math")
     return out
+
+
+def stream_copy_bandwidth(device=0, nbytes=2 << 30, iters=20):
+    """Achievable HBM GB/s of a device float4 copy (read + write), fbr_stream_copy_bandwidth."""
+    g = ctypes.c_double()
+    _check(lib().fbr_stream_copy_bandwidth(device, nbytes, iters, ctypes.byref(g)), "fbr_stream_copy_bandwidth")
+    return g.value
 
 
 def affine_from_pose(pose):

@@ -40,3 +40,41 @@ extern "C" int fbr_selftest_math(int n, const float* a, const float* b, float* o
   (void)hipFree(dout);
   return rc;
 }
+
+// STREAM-copy probe (measurement helper, BASELINE.md "report vs measured STREAM-copy bandwidth"):
+// a grid-stride float4 copy of `bytes` per direction, timed with HIP events over `iters` launches.
+namespace fbr {
+__global__ void __launch_bounds__(256) k_stream_copy(const float4* __restrict__ a, float4* __restrict__ b, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) b[i] = a[i];
+}
+}  // namespace fbr
+
+extern "C" int fbr_stream_copy_bandwidth(int hip_device, int64_t bytes, int iters, double* gbps) {
+  if (bytes < 16 || iters <= 0 || !gbps) return FBR_ERR_INVALID_ARG;
+  if (hipSetDevice(hip_device) != hipSuccess) return FBR_ERR_NO_DEVICE;
+  const int64_t n = bytes / 16;
+  float4 *a = nullptr, *b = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = FBR_OK;
+  if (hipMalloc(&a, sizeof(float4) * n) != hipSuccess || hipMalloc(&b, sizeof(float4) * n) != hipSuccess ||
+      hipMemset(a, 0, sizeof(float4) * n) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+      hipEventCreate(&e1) != hipSuccess) {
+    rc = FBR_ERR_HIP;
+  } else {
+    const int grid = 256 * 8 * 4;  // 8 XCDs x 32 CUs, several workgroups per CU
+    hipLaunchKernelGGL(fbr::k_stream_copy, dim3(grid), dim3(256), 0, 0, a, b, n);  // warm-up
+    (void)hipEventRecord(e0, 0);
+    for (int k = 0; k < iters; ++k) hipLaunchKernelGGL(fbr::k_stream_copy, dim3(grid), dim3(256), 0, 0, a, b, n);
+    (void)hipEventRecord(e1, 0);
+    float ms = 0.0f;
+    if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess || ms <= 0.0f)
+      rc = FBR_ERR_HIP;
+    else
+      *gbps = 2.0 * 16.0 * (double)n * iters / (ms * 1e-3) / 1e9;  // read + write
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(a);
+  (void)hipFree(b);
+  return rc;
+}

@@ -42,9 +42,25 @@ SCENE_SEED = 7
 # Config -> (N_SCAN, Horizon_SCAN, map radius, surf density /m^2, corner density /m)
 CONFIGS = {
     "C1": (16, 1800, 45.0, 12.0, 12.0),
-    "C2": (64, 1800, 45.0, 12.0, 12.0),
-    "C3": (128, 2048, 60.0, 12.0, 12.0),
+    "C2": (64, 1800, 45.0, 12.0, 12.0),     # ~100k-point local map (BASELINE configs[1])
+    "C3": (128, 2048, 60.0, 100.0, 100.0),  # ~500k-point local map (configs[2])
+    "C5": (512, 2048, 40.0, 600.0, 250.0),  # ~5M-point map inside the crop box (configs[4])
 }
+# Mapping leaf sizes (mappingCornerLeafSize, mappingSurfLeafSize) of the denser configs: with the
+# params.yaml leaves (0.2 / 0.4) the start-up VoxelGrid (mapOptmization.h:251-257) caps a 60 x 60 m
+# local map far below the 500k / 5M points BASELINE.json names, so these configs use finer leaves.
+MAP_LEAVES = {"C3": (0.1, 0.2), "C5": (0.05, 0.05)}
+
+
+def config_params(config, **overrides):
+    """default_params for a config: its scan shape and its mapping leaf sizes."""
+    from .fbr_types import default_params
+    H, W = CONFIGS[config][:2]
+    kw = {}
+    if config in MAP_LEAVES:
+        kw["mapping_corner_leaf_size"], kw["mapping_surf_leaf_size"] = MAP_LEAVES[config]
+    kw.update(overrides)
+    return default_params(H, W, **kw)
 
 
 def scan(pose_world, n_scan, horizon_scan, seed, scene_seed=SCENE_SEED):

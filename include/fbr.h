@@ -328,6 +328,11 @@ int fbr_voxel_grid(fbr_ctx* ctx, const fbr_point_xyzi* in, int64_t n, float leaf
  * the host libm the reference uses). */
 int fbr_selftest_math(int n, const float* a, const float* b, float* out);
 
+/* Measurement helper: achievable HBM bandwidth of a device-wide float4 copy of `bytes` (read +
+ * write counted), averaged over `iters` launches (the STREAM-copy figure bench.py reports next to
+ * the 8 TB/s spec peak). */
+int fbr_stream_copy_bandwidth(int hip_device, int64_t bytes, int iters, double* gbps);
+
 /* pcl::getTransformation / pcl::getTranslationAndEulerAngles (row-major 4x4 float). */
 void fbr_affine_from_pose(const float pose[6], float m[16]);
 void fbr_pose_from_affine(const float m[16], float pose[6]);

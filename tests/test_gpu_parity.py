@@ -297,3 +297,48 @@ def test_full_size_batch_properties(c2_map):
     assert (s1["status"] == 0).all() and (s1["converged"] == 1).all()
     assert np.abs(p1[:, 3:] - gts[:, 3:]).max() < 0.05
     assert (s1["n_corner_map"] + s1["n_surf_map"]).mean() > 80000  # ~100k-point local map
+
+
+# ------------------------------------------------------------------------------- C3 / C5 configs
+def test_c3_ouster_registration_matches_oracle():
+    """BASELINE configs[2]: 128x2048 Ouster-style scans against a ~500k-point local map."""
+    P = synth.config_params("C3", max_batch=2)
+    cmap, smap = synth.config_map("C3")
+    jobs = synth.make_jobs("C3", 2, base_seed=5000)
+    m = O.Map(P, cmap, smap)
+    with api.Context(P) as ctx:
+        ctx.set_map(cmap, smap)
+        poses, stats = ctx.process_batch([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
+    for k, (pts, guess, gt) in enumerate(jobs):
+        po, so = O.Stream(P).process_scan(m, pts, 0.0, guess, n_threads=8)
+        assert stats["status"][k] == so["status"] == 0 and stats["iterations"][k] == so["iterations"]
+        for f in ("n_points", "n_corner", "n_corner_map", "n_surf_map"):
+            assert stats[f][k] == so[f], f
+        assert stats["n_corner_map"][k] + stats["n_surf_map"][k] > 450000  # ~500k-point local map
+        assert_pose_close(poses[k], po)
+        assert np.abs(poses[k][3:] - gt[3:]).max() < 0.05
+
+
+def test_c5_dense_scan_matches_oracle():
+    """BASELINE configs[4]: a ~1M-point 512x2048 scan against a ~5.8M-point map inside the crop
+    box.  The device kNN is the exact grid search (same neighbours as the brute-force / KD-tree
+    search under the d2 < 1 gate, k_register.hip); the oracle runs the KD-tree restatement."""
+    P = synth.config_params("C5")
+    cmap, smap = synth.config_map("C5")
+    gt, guess = synth.job(5)
+    pts = synth.scan(gt, 512, 2048, seed=5)
+    assert len(pts) > 900000
+    st = O.Stream(P)
+    fo = st.features(pts)
+    with api.Context(P) as ctx:
+        ctx.set_map(cmap, smap)
+        fg = ctx.features(pts)
+        assert_features_equal(fo, fg)
+        ctx.reset_stream()
+        pg, sg = ctx.process_scan(pts, 0.0, guess)
+    po, so = O.Stream(P).process_scan(O.Map(P, cmap, smap), pts, 0.0, guess, n_threads=16)
+    assert sg["status"] == so["status"] == 0 and sg["iterations"] == so["iterations"]
+    assert (sg["n_corner_map"], sg["n_surf_map"]) == (so["n_corner_map"], so["n_surf_map"])
+    assert sg["n_corner_map"] + sg["n_surf_map"] > 5000000
+    assert_pose_close(pg, po)
+    assert np.abs(pg[3:] - gt[3:]).max() < 0.05
