@@ -506,7 +506,7 @@ int register_iterate(fbr_ctx* c, const Sub* subs, int nsub, bool trace) {
         }
       }
       const int grid = std::max(1, std::min(a[k].max_items, 2048));
-      TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a[k], grid));
+      TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a[k], grid, it));
       TIMED_ON(c, sb.st, "gn_residual", launch_gn_residual(sb.st, a[k], grid));
       TIMED_ON(c, sb.st, "gn_solve", launch_gn_solve(sb.st, a[k], it, gen));
     }

@@ -133,7 +133,7 @@ struct GnArgs {
   const fbr_deskew_table* desk;  // [B]
 };
 void launch_gn_init(hipStream_t s, const GnArgs& a);
-void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid);
+void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter);
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid);
 void launch_gn_solve(hipStream_t s, const GnArgs& a, int iter_idx, unsigned long long gen);
 void launch_gn_finalize(hipStream_t s, const GnArgs& a);

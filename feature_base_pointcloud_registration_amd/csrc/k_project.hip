@@ -49,10 +49,15 @@ __device__ __forceinline__ bool project_point(const fbr_point_xyzirt& q, int H, 
 // whose column span exceeds the tile (the 0/W seam, shuffled input) claim directly in global.
 constexpr int kProjThreads = 256, kProjPPT = 8, kProjChunk = kProjThreads * kProjPPT;
 
+// The per-point (row, col) results are parked in LDS (packed row << 16 | col, -1 = rejected)
+// rather than in registers across the claim phase: the column arithmetic (fdlibm atan2f, double
+// conversions) then runs two points at a time and the kernel stays at a register count that lets
+// 8 waves per SIMD hide the atomic latency.
 __global__ void __launch_bounds__(kProjThreads)
 k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ nin, int64_t nmax, int H, int W,
           int tile_log2, int32_t* __restrict__ owner) {
   extern __shared__ int32_t tile[];  // [H][1 << tile_log2]
+  __shared__ int32_t cellk[kProjChunk];
   __shared__ int red[2][kProjThreads / 64];
   const int job = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int tcols = 1 << tile_log2, tcells = H << tile_log2;
@@ -60,19 +65,17 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
   const fbr_point_xyzirt* P = pts + (int64_t)job * nmax;
   int32_t* O = owner + (int64_t)job * H * W;
   for (int64_t base = (int64_t)blockIdx.x * kProjChunk; base < n; base += (int64_t)gridDim.x * kProjChunk) {
-    int rowk[kProjPPT], colk[kProjPPT];
     int cmin = INT_MAX, cmax = -1;
-#pragma unroll
+#pragma unroll 2
     for (int k = 0; k < kProjPPT; ++k) {
       const int64_t i = base + k * kProjThreads + tid;
-      rowk[k] = -1;
-      colk[k] = 0;
-      if (i < n && project_point(P[i], H, W, rowk[k], colk[k])) {
-        cmin = min(cmin, colk[k]);
-        cmax = max(cmax, colk[k]);
-      } else {
-        rowk[k] = -1;
+      int row, col, v = -1;
+      if (i < n && project_point(P[i], H, W, row, col)) {
+        v = (row << 16) | col;
+        cmin = min(cmin, col);
+        cmax = max(cmax, col);
       }
+      cellk[k * kProjThreads + tid] = v;
     }
     for (int o = 32; o > 0; o >>= 1) {
       cmin = min(cmin, __shfl_xor(cmin, o));
@@ -92,19 +95,21 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
     if (cmax >= 0 && cmax - cmin < tcols) {
       for (int e = tid; e < tcells; e += kProjThreads) tile[e] = kEmptyOwner;
       __syncthreads();
-#pragma unroll
-      for (int k = 0; k < kProjPPT; ++k)
-        if (rowk[k] >= 0)
-          atomicMin(&tile[(rowk[k] << tile_log2) + (colk[k] - cmin)], (int32_t)(base + k * kProjThreads + tid));
+      for (int k = 0; k < kProjPPT; ++k) {
+        const int v = cellk[k * kProjThreads + tid];
+        if (v >= 0)
+          atomicMin(&tile[((v >> 16) << tile_log2) + ((v & 0xFFFF) - cmin)], (int32_t)(base + k * kProjThreads + tid));
+      }
       __syncthreads();
       for (int e = tid; e < tcells; e += kProjThreads) {
         const int32_t v = tile[e];
         if (v != kEmptyOwner) atomicMin(&O[(e >> tile_log2) * W + cmin + (e & (tcols - 1))], v);
       }
     } else {
-#pragma unroll
-      for (int k = 0; k < kProjPPT; ++k)
-        if (rowk[k] >= 0) atomicMin(&O[rowk[k] * W + colk[k]], (int32_t)(base + k * kProjThreads + tid));
+      for (int k = 0; k < kProjPPT; ++k) {
+        const int v = cellk[k * kProjThreads + tid];
+        if (v >= 0) atomicMin(&O[(v >> 16) * W + (v & 0xFFFF)], (int32_t)(base + k * kProjThreads + tid));
+      }
     }
     __syncthreads();
   }
@@ -147,6 +152,7 @@ __device__ __forceinline__ float4 deskew_point(const fbr_point_xyzirt& q, const 
 // Blocks are dealt round-robin over the 8 XCDs (b, b+8, ... share one); the (job, row) mapping
 // keeps every row of a job on one XCD so the owner gathers of the job's raw points hit that
 // XCD's L2 (speed only: correctness never depends on placement).
+template <bool kDesk>
 __global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, const int32_t* __restrict__ owner,
                           const int32_t* __restrict__ rowcnt, int B, int H, int W, float4* __restrict__ cloud,
                           int32_t* __restrict__ col, float* __restrict__ range, int32_t* __restrict__ start_ring,
@@ -172,7 +178,7 @@ __global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax
   int32_t* CI = col + job * HW;
   float* R = range + job * HW;
   // deskew: transStartInverse from the scan's first deskewed point (the minimum owner)
-  const bool dsk = desk.mode && (desk.mode[job] & kDeskPoints);
+  const bool dsk = kDesk && (desk.mode[job] & kDeskPoints);
   const fbr_deskew_table* DT = dsk ? desk.table + job : nullptr;
   Rot3 Ls;
   float ts[3] = {0.0f, 0.0f, 0.0f};
@@ -274,8 +280,12 @@ void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, co
                     int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk) {
   hipLaunchKernelGGL(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, rowcnt, desk.mode ? desk.rowmin : nullptr);
   const int groups = (B + 7) / 8;
-  hipLaunchKernelGGL(k_compact, dim3(groups * 8 * H), dim3(64), 0, s, pts, nmax, owner, rowcnt, B, H, W, cloud, col,
-                     range, start_ring, end_ring, nvalid, desk);
+  if (desk.mode)
+    hipLaunchKernelGGL(k_compact<true>, dim3(groups * 8 * H), dim3(64), 0, s, pts, nmax, owner, rowcnt, B, H, W, cloud,
+                       col, range, start_ring, end_ring, nvalid, desk);
+  else
+    hipLaunchKernelGGL(k_compact<false>, dim3(groups * 8 * H), dim3(64), 0, s, pts, nmax, owner, rowcnt, B, H, W, cloud,
+                       col, range, start_ring, end_ring, nvalid, desk);
 }
 
 }  // namespace fbr

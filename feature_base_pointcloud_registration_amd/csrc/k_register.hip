@@ -107,9 +107,13 @@ __device__ unsigned long long fbr_knn_stats[8];
 // near-side-first rank order; a row, and the cells of a row, are skipped once their lower-bound
 // distance exceeds the current 5th distance or reaches 1.0.  Rows entirely inside the crop box
 // skip the per-point box test.
+// `bound` is an upper bound of the 5th-neighbour distance known before the search (the largest
+// distance to the previous iteration's 5 neighbours, 5 distinct candidates of the same crop box):
+// cells whose lower bound exceeds it cannot hold any of the 5 nearest, ties included, so they are
+// pruned from the start instead of only once 5 points have been inserted.
 template <int R>
 __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
-                          Knn5& r, unsigned* ks) {
+                          float bound, Knn5& r, unsigned* ks) {
   constexpr int K = 2 * R + 1;
 #pragma unroll
   for (int t = 0; t < 5; ++t) { r.d[t] = __int_as_float(0x7f800000); r.id[t] = 0x7fffffff; r.pos[t] = -1; }
@@ -151,7 +155,8 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       float lb = 0.0f;
       lb += ly2[ky];
       lb += lz2[kz];
-      if (y < 0 || y >= Y || z < 0 || z >= Z || lb > r.d[4] || !(lb < 1.0f)) continue;
+      const float cut = fminf(r.d[4], bound);
+      if (y < 0 || y >= Y || z < 0 || z >= Z || lb > cut || !(lb < 1.0f)) continue;
       int xa = 0, xb = 0;
       bool go_a = true, go_b = true;
 #pragma unroll
@@ -159,8 +164,8 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         float ta = 0.0f, tb = 0.0f;
         ta += lxm2[o]; ta += ly2[ky]; ta += lz2[kz];
         tb += lxp2[o]; tb += ly2[ky]; tb += lz2[kz];
-        go_a = go_a && !(ta > r.d[4]) && ta < 1.0f;
-        go_b = go_b && !(tb > r.d[4]) && tb < 1.0f;
+        go_a = go_a && !(ta > cut) && ta < 1.0f;
+        go_b = go_b && !(tb > cut) && tb < 1.0f;
         if (go_a) xa = -o;
         if (go_b) xb = o;
       }
@@ -308,7 +313,7 @@ __global__ void k_gn_init(GnArgs a) {
 // R = grid cells per side covering radius 1 (both map grids share one cell size).
 template <int R>
 __global__ void __launch_bounds__(kResThreads)
-k_gn_knn(GnArgs a) {
+k_gn_knn(GnArgs a, int use_prev) {
   const int tid = threadIdx.x;
   const int nitems = a.nitems[0];
   for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
@@ -324,9 +329,25 @@ k_gn_knn(GnArgs a) {
     const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
     const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
     const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
+    const MapGrid& mg = corner ? a.mc : a.ms;
+    int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
+    float bound = __int_as_float(0x7f800000);
+    if (use_prev && o[0] >= 0) {  // warm start: the previous iteration's neighbours of this query
+      float mx = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const float4 q = mg.pts[o[k * kResThreads]];
+        float dist = 0.0f, diff;
+        diff = x0 - q.x; dist += diff * diff;
+        diff = y0 - q.y; dist += diff * diff;
+        diff = z0 - q.z; dist += diff * diff;
+        mx = fmaxf(mx, dist);
+      }
+      bound = mx;
+    }
     Knn5 nn;
     unsigned ks[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-    knn5_grid<R>(corner ? a.mc : a.ms, x0, y0, z0, g.crop_min, g.crop_max, nn, ks);
+    knn5_grid<R>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
     const bool ok = nn.pos[4] >= 0 && nn.d[4] < 1.0f;
 #ifdef FBR_KNN_STATS
     ks[5] = ok;
@@ -335,7 +356,6 @@ k_gn_knn(GnArgs a) {
 #else
     (void)ks;
 #endif
-    int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
 #pragma unroll
     for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? nn.pos[k] : -1;
   }
@@ -586,11 +606,12 @@ void launch_export_records(hipStream_t s, int B, const float* pose_out, const fb
 }
 
 void launch_gn_init(hipStream_t s, const GnArgs& a) { hipLaunchKernelGGL(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
-void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid) {
+void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter) {
   const float inv = a.mc.g.inv_cell;  // == a.ms.g.inv_cell (fbr_set_map)
-  if (inv > 2.0f) hipLaunchKernelGGL((k_gn_knn<4>), dim3(grid), dim3(kResThreads), 0, s, a);        // 0.25 m
-  else if (inv > 1.0f) hipLaunchKernelGGL((k_gn_knn<2>), dim3(grid), dim3(kResThreads), 0, s, a);   // 0.5 m
-  else hipLaunchKernelGGL((k_gn_knn<1>), dim3(grid), dim3(kResThreads), 0, s, a);                   // >= 1 m
+  const int use_prev = iter > 0;      // nbr holds this launch's previous iteration
+  if (inv > 2.0f) hipLaunchKernelGGL((k_gn_knn<4>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.25 m
+  else if (inv > 1.0f) hipLaunchKernelGGL((k_gn_knn<2>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
+  else hipLaunchKernelGGL((k_gn_knn<1>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
 }
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
   hipLaunchKernelGGL(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);
