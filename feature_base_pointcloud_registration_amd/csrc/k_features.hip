@@ -52,7 +52,9 @@ struct Bits {
 
 struct FeatLds {
   int wlo, L, nw;
-  float* curv;        // [Lcap]
+  float* gcurv;       // [Lcap] the ring window's curvature, in the ring's global scratch slot
+  float* scurv;       // [segcap + 16] LDS copy of the current segment's [sp-6, ep+7) curvature
+  int sbase;          // window index of scurv[0]
   Bits gap;           // |col[i+1]-col[i]| > 10
   Bits picked, labpos, labneg, edgec, surfc;
   Bits occa, occb, occc;
@@ -108,15 +110,22 @@ __device__ __forceinline__ void or_range(const Bits& b, int lo, int hi) {
   }
 }
 
+// cloudCurvature at window index li: the segment's LDS copy, or the global slot outside it (the
+// stale cloudSmoothness[4] index may point anywhere in the ring window).
+__device__ __forceinline__ float curv_at(const FeatLds& S, int li, int slen) {
+  const int k = li - S.sbase;
+  return (k >= 0 && k < slen) ? S.scurv[k] : S.gcurv[li];
+}
+
 // Sequential walks (the reference loops verbatim) over S.seg[0..m] (seg[m] = the unsorted ep entry).
-__device__ void serial_walks(const FeatLds& S, const SmoothEntry* ent, const FeatArgs& a, int job, int m,
+__device__ void serial_walks(const FeatLds& S, int slen, const SmoothEntry* ent, const FeatArgs& a, int job, int m,
                              const float4* CL, float4* corner_out, int& corner_cnt) {
   int largestPickedNum = 0;
   for (int k = m; k >= 0; k--) {  // corners, k = ep .. sp (:208-242)
     const int ind = ent[k].ind;
     const int li = ind - S.wlo;
     if (li < 0 || li + 5 >= S.L) { atomicOr(&a.err[job], 4); return; }
-    if (!S.picked.get(li) && S.curv[li] > a.edge_thr) {
+    if (!S.picked.get(li) && curv_at(S, li, slen) > a.edge_thr) {
       largestPickedNum++;
       if (largestPickedNum <= kCornerPerSeg) {
         S.labpos.set_serial(li);
@@ -134,7 +143,7 @@ __device__ void serial_walks(const FeatLds& S, const SmoothEntry* ent, const Fea
     const int ind = ent[k].ind;
     const int li = ind - S.wlo;
     if (li < 0 || li + 5 >= S.L) { atomicOr(&a.err[job], 4); return; }
-    if (!S.picked.get(li) && S.curv[li] < a.surf_thr) {
+    if (!S.picked.get(li) && curv_at(S, li, slen) < a.surf_thr) {
       S.labneg.set_serial(li);
       S.picked.set_serial(li);
       const int f = reach_fwd(S, li), b = reach_bwd(S, li);
@@ -350,7 +359,8 @@ k_features(FeatArgs a) {
     return;
   }
   unsigned char* p = smem;
-  S.curv = (float*)p;                p += sizeof(float) * Lcap;
+  S.scurv = (float*)p;               p += sizeof(float) * ((segcap + 19) & ~3);  // 16-B multiple: the
+                                                                                 // bit words below are 64-bit
   uint64_t* words = (uint64_t*)p;    p += sizeof(uint64_t) * 9 * nwcap;  // 9 bit arrays of nwcap words
   S.gap.w = words;
   S.picked.w = words + 1 * nwcap;
@@ -371,8 +381,10 @@ k_features(FeatArgs a) {
     S.seg = (SmoothEntry*)g;         g += sizeof(SmoothEntry) * segcap;
     S.tmp = (SmoothEntry*)g;         g += sizeof(SmoothEntry) * segcap;
     S.sorder = (uint16_t*)g;         g += sizeof(uint16_t) * segcap;
-    S.rankc = (uint16_t*)g;
+    S.rankc = (uint16_t*)g;          g += sizeof(uint16_t) * segcap;
+    S.gcurv = (float*)(((uintptr_t)g + 15) & ~(uintptr_t)15);
   }
+  S.sbase = 0;
 
   const float* R = a.range + job * HW;
   const int32_t* C = a.col + job * HW;
@@ -431,7 +443,7 @@ k_features(FeatArgs a) {
                         rw[i + 1 - wo] + rw[i + 2 - wo] + rw[i + 3 - wo] + rw[i + 4 - wo] + rw[i + 5 - wo];
         curv = d * d;
       }
-      S.curv[i] = curv;  // indices outside [5, n-5) keep the zero-initialised scratch value
+      S.gcurv[i] = curv;  // indices outside [5, n-5) keep the zero-initialised scratch value
     }
     const uint64_t ba = __ballot(fa), bb = __ballot(fb), bc = __ballot(fc), bg = __ballot(gp);
     const uint64_t be = __ballot(i < S.L && curv > a.edge_thr);
@@ -475,6 +487,11 @@ k_features(FeatArgs a) {
       if (lane == 0) atomicOr(&a.err[job], 2);
       return;
     }
+    // stage this segment's curvature window [sp-6, ep+7) in LDS (members +-5 plus ep)
+    S.sbase = max(sp - S.wlo - 6, 0);
+    const int slen = min(ep - S.wlo + 7, S.L) - S.sbase;
+    for (int t = lane; t < slen; t += 64) S.scurv[t] = S.gcurv[S.sbase + t];
+    __syncthreads();
 #ifdef FBR_FEAT_SKIP_STALE
     const bool has_stale = false;  // diagnostic ablation only
 #else
@@ -493,7 +510,7 @@ k_features(FeatArgs a) {
         uint64_t key = kPadKey;
         if (t < m) {
           const int pos = sp + t;
-          const float v = (pos == 4) ? st->smooth4_value : S.curv[pos - S.wlo];
+          const float v = (pos == 4) ? st->smooth4_value : S.scurv[pos - S.wlo - S.sbase];
           key = ((uint64_t)__float_as_uint(v) << 16) | (uint64_t)t;
         }
         S.keys[t] = key;
@@ -513,7 +530,7 @@ k_features(FeatArgs a) {
         // equal curvatures: their order is introsort's; materialise std::sort's result in S.seg
         for (int t = lane; t < m; t += 64) {
           const int pos = sp + t;
-          S.seg[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.curv[pos - S.wlo], pos};
+          S.seg[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.scurv[pos - S.wlo - S.sbase], pos};
         }
         __syncthreads();
         if (nan) {
@@ -534,13 +551,13 @@ k_features(FeatArgs a) {
       } else if (has_stale) {
         for (int k = lane; k < m; k += 64) {
           const int pos = sp + (int)(S.keys[k] & 0xFFFFu);
-          S.seg[k] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.curv[pos - S.wlo], pos};
+          S.seg[k] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.scurv[pos - S.wlo - S.sbase], pos};
         }
         __syncthreads();
       }
       if (has_stale) {
         if (lane == 0) {
-          S.seg[m] = SmoothEntry{S.curv[ep - S.wlo], ep};  // cloudSmoothness[ep] is never sorted (:203)
+          S.seg[m] = SmoothEntry{S.scurv[ep - S.wlo - S.sbase], ep};  // cloudSmoothness[ep] is never sorted (:203)
           st->smooth4_value = S.seg[4 - sp].v;            // the entry left at position 4 is the next
           st->smooth4_ind = S.seg[4 - sp].ind;            // scan's stale slot
         }
@@ -606,7 +623,7 @@ k_features(FeatArgs a) {
           const int f = __builtin_ctzll(fw | 0x20ull), b = __builtin_clzll(bw | (1ull << 58));
           float cv[11];
 #pragma unroll
-          for (int d = 0; d < 11; ++d) cv[d] = S.curv[min(max(li + d - 5, 0), Lcap - 1)];
+          for (int d = 0; d < 11; ++d) cv[d] = S.scurv[max(li + d - 5, 0) - S.sbase];
           const float vu = cv[5];
           uint32_t nb = 0, hc = 0;
 #pragma unroll
@@ -639,7 +656,7 @@ k_features(FeatArgs a) {
       SmoothEntry* ent = (SmoothEntry*)S.rb;  // the walk's entries in LDS (region B is free here)
       for (int k = lane; k <= m; k += 64) ent[k] = S.seg[k];
       __syncthreads();
-      if (lane == 0) serial_walks(S, ent, a, job, m, CL, corner_out, corner_cnt);
+      if (lane == 0) serial_walks(S, slen, ent, a, job, m, CL, corner_out, corner_cnt);
       corner_cnt = __shfl(corner_cnt, 0);
       __syncthreads();
     } else {
@@ -671,7 +688,7 @@ k_features(FeatArgs a) {
             const int q = T + __popcll(tak[w] & ((1ull << lane) - 1ull));
             const int u = 64 * w + lane;
             tlu[q] = (uint16_t)u;
-            tlv[q] = S.curv[sp + u - S.wlo];
+            tlv[q] = S.scurv[sp + u - S.wlo - S.sbase];
           }
           T += __popcll(tak[w]);
         }
@@ -786,12 +803,13 @@ k_features(FeatArgs a) {
 
 size_t features_lds_bytes(const FeatArgs& a) {
   const size_t region_b = std::max<size_t>((size_t)kWin * (sizeof(float) + sizeof(int16_t)), (size_t)8 * a.segcap);
-  return (size_t)a.lcap * sizeof(float) + (size_t)9 * a.nwcap * sizeof(uint64_t) + sizeof(uint64_t) * 16 +
+  return (size_t)((a.segcap + 19) & ~3) * sizeof(float) + (size_t)9 * a.nwcap * sizeof(uint64_t) + sizeof(uint64_t) * 16 +
          sizeof(SortFrame) * kSortStack + sizeof(uint32_t) * a.segcap + 16 + region_b;
 }
 
 size_t features_gslot_bytes(const FeatArgs& a) {
-  const size_t b = sizeof(uint64_t) * a.kseg + 2 * sizeof(SmoothEntry) * a.segcap + 2 * sizeof(uint16_t) * a.segcap;
+  const size_t b = sizeof(uint64_t) * a.kseg + 2 * sizeof(SmoothEntry) * a.segcap + 2 * sizeof(uint16_t) * a.segcap +
+                   16 + sizeof(float) * a.lcap;  // + the ring window's curvature
   return (b + 255) & ~(size_t)255;
 }
 

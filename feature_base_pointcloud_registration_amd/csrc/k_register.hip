@@ -408,24 +408,17 @@ k_gn_residual(GnArgs a) {
         b = -c.w;
       }
     }
-    // fp64 products: 21 upper AtA entries, 6 AtB, count
-    double v[28];
-    int q = 0;
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-      for (int c2 = r; c2 < 6; ++c2) v[q++] = (double)row[r] * (double)row[c2];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) v[q++] = (double)row[r] * (double)b;
-    v[27] = ok ? 1.0 : 0.0;
+    // fp64 products (21 upper AtA entries, 6 AtB, count), each formed and wave-reduced in turn so
+    // that only a few doubles are live at once
 #pragma unroll
     for (int k = 0; k < 28; ++k) {
-      double x = v[k];
+      constexpr int kR[21] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 5};
+      constexpr int kC[21] = {0, 1, 2, 3, 4, 5, 1, 2, 3, 4, 5, 2, 3, 4, 5, 3, 4, 5, 4, 5, 5};
+      const int rr = k < 21 ? kR[k] : 0, cc = k < 21 ? kC[k] : 0;  // upper-triangle (row, column)
+      double x = k < 21 ? (double)row[rr] * (double)row[cc] : (k < 27 ? (double)row[k - 21] * (double)b : (ok ? 1.0 : 0.0));
       for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-      v[k] = x;
+      if (lane == 0) red[wave][k] = x;
     }
-    if (lane == 0)
-      for (int k = 0; k < 28; ++k) red[wave][k] = v[k];
     __syncthreads();
     if (tid < 28) {
       double s = 0.0;
