@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="jobs per GPU per step")
+    ap.add_argument("--batch", type=int, default=512, help="jobs per GPU per step")
     ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C5"])
     ap.add_argument("--cpu-sample", type=int, default=96, help="jobs timed on the CPU oracle (N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16,

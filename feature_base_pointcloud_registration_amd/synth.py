@@ -112,15 +112,20 @@ def trajectory(seed, n, step=0.4, dyaw=np.deg2rad(1.0)):
     return out
 
 
-def make_jobs(config, n_jobs, base_seed=1000):
-    """n_jobs independent (scan, guess, gt) registration jobs of a config (C4: seed 1000+j)."""
+def make_jobs(config, n_jobs, base_seed=1000, threads=16):
+    """n_jobs independent (scan, guess, gt) registration jobs of a config (C4: seed 1000+j).  The
+    ray casting runs in a thread pool (the C generator releases the GIL); results are identical to
+    a serial loop."""
+    import concurrent.futures
     n_scan, w, *_ = CONFIGS[config]
-    jobs = []
-    for j in range(n_jobs):
+
+    def one(j):
         gt, guess = job(base_seed + j)
-        pts = scan(gt, n_scan, w, seed=base_seed + j)
-        jobs.append((pts, guess, gt))
-    return jobs
+        return scan(gt, n_scan, w, seed=base_seed + j), guess, gt
+
+    nth = max(1, min(threads, n_jobs, len(os.sched_getaffinity(0))))
+    with concurrent.futures.ThreadPoolExecutor(nth) as ex:
+        return list(ex.map(one, range(n_jobs)))
 
 
 def config_map(config, seed=11):
