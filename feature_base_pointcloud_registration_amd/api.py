@@ -15,7 +15,7 @@ import os
 
 import numpy as np
 
-from .fbr_types import (DESKEW_TABLE, IMU_SAMPLE, PF_FLOAT32, POINT_XYZI, POINT_XYZIRT, REG_STATS, FbrParams,
+from .fbr_types import (DESKEW_TABLE, IMU_SAMPLE, KEYPOSE, PF_FLOAT32, POINT_XYZI, POINT_XYZIRT, REG_STATS, FbrParams,
                         FbrRegStats, PointCloud2, default_params, ptr)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -34,6 +34,8 @@ EXPORTED_SYMBOLS = [
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
     "fbr_msg_to_points", "fbr_points_to_msg_data", "fbr_project_msg", "fbr_process_msg",
     "fbr_imu_convert", "fbr_imu_deskew_info", "fbr_set_deskew", "fbr_stream_copy_bandwidth",
+    "fbr_keyframe_params_default", "fbr_keyframes_add", "fbr_keyframes_set_pose", "fbr_keyframes_count",
+    "fbr_keyframes_reset", "fbr_extract_surrounding_keyframes",
 ]
 
 
@@ -99,6 +101,12 @@ def lib():
             "fbr_imu_deskew_info": (ctypes.c_int, [_VP, _I64, ctypes.c_double, ctypes.c_double, _VP, _VP]),
             "fbr_set_deskew": (ctypes.c_int, [_VP, _VP, ctypes.c_int]),
             "fbr_stream_copy_bandwidth": (ctypes.c_int, [ctypes.c_int, _I64, ctypes.c_int, _VP]),
+            "fbr_keyframe_params_default": (None, [_VP]),
+            "fbr_keyframes_add": (ctypes.c_int, [_VP, _VP, _VP, _I64, _VP, _I64]),
+            "fbr_keyframes_set_pose": (ctypes.c_int, [_VP, _I64, _VP]),
+            "fbr_keyframes_count": (ctypes.c_int, [_VP, _VP]),
+            "fbr_keyframes_reset": (ctypes.c_int, [_VP]),
+            "fbr_extract_surrounding_keyframes": (ctypes.c_int, [_VP, ctypes.c_double, _VP, _VP, _VP, _VP]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -352,6 +360,36 @@ class Context:
             return
         t = np.ascontiguousarray(np.array(tables, DESKEW_TABLE).reshape(-1))
         _check(lib().fbr_set_deskew(self._h, ptr(t), len(t)), "fbr_set_deskew")
+
+    # ---- LIO-SAM keyframe local map (mapOptmization.h:857-978) ----
+    def keyframes_add(self, pose, corner, surf):
+        """cloudKeyPoses3D/6D + corner/surfCloudKeyFrames push_back (pose: KEYPOSE record)."""
+        p = np.array(pose, KEYPOSE).reshape(1)
+        corner = _as_points(corner, POINT_XYZI)
+        surf = _as_points(surf, POINT_XYZI)
+        _check(lib().fbr_keyframes_add(self._h, ptr(p), ptr(corner) if len(corner) else None, len(corner),
+                                       ptr(surf) if len(surf) else None, len(surf)), "fbr_keyframes_add")
+
+    def keyframes_set_pose(self, index, pose):
+        p = np.array(pose, KEYPOSE).reshape(1)
+        _check(lib().fbr_keyframes_set_pose(self._h, index, ptr(p)), "fbr_keyframes_set_pose")
+
+    def keyframes_count(self):
+        n = _I64()
+        _check(lib().fbr_keyframes_count(self._h, ctypes.byref(n)), "fbr_keyframes_count")
+        return n.value
+
+    def keyframes_reset(self):
+        _check(lib().fbr_keyframes_reset(self._h), "fbr_keyframes_reset")
+
+    def extract_surrounding_keyframes(self, stamp, kparams):
+        """extractSurroundingKeyFrames: the local map becomes the registration map (no CropBox).
+        Returns (n_corner_map, n_surf_map, n_frames)."""
+        nc, ns, nf = _I64(), _I64(), ctypes.c_int32()
+        _check(lib().fbr_extract_surrounding_keyframes(self._h, ctypes.c_double(stamp), ctypes.byref(kparams),
+                                                       ctypes.byref(nc), ctypes.byref(ns), ctypes.byref(nf)),
+               "fbr_extract_surrounding_keyframes")
+        return nc.value, ns.value, nf.value
 
     def reset_stream(self):
         _check(lib().fbr_reset_stream(self._h), "fbr_reset_stream")

@@ -130,6 +130,19 @@ struct fbr_ctx {
   int32_t* d_rowmin = nullptr;         // [Bcap][H] minimum owner per row
   bool desk_any = false;               // some job has a non-zero mode
   bool no_time_call = false;           // the current call's PointCloud2 has no "time" field
+  // LIO-SAM keyframe store (fbr_keyframes_*) and the local map built from it
+  std::vector<fbr_keypose> kf_poses;
+  std::vector<int64_t> kf_c_off, kf_c_cnt, kf_s_off, kf_s_cnt;
+  float4 *d_kf_c = nullptr, *d_kf_s = nullptr;  // lidar-frame keyframe clouds, appended
+  int64_t kf_c_cap = 0, kf_s_cap = 0, kf_c_used = 0, kf_s_used = 0;
+  float4 *d_kraw_c = nullptr, *d_kraw_s = nullptr;  // concatenated transformed clouds
+  int64_t kraw_c_cap = 0, kraw_s_cap = 0;
+  float4 *d_kds_c = nullptr, *d_kds_s = nullptr;    // their VoxelGrids (laserCloud*FromMapDS)
+  int64_t kds_c_n = 0, kds_s_n = 0;
+  KfSeg* d_kf_segs = nullptr;
+  int64_t kf_segs_cap = 0;
+  int* d_bounds = nullptr;
+  bool map_nocrop = false;  // the registration map is a keyframe local map
 };
 
 namespace {
@@ -424,6 +437,7 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 2 * mi;
   a.desk_mode = c->desk_any ? c->d_desk_mode + j0 : nullptr;
   a.desk = c->desk_any ? c->d_desk + j0 : nullptr;
+  a.nocrop = c->map_nocrop ? 1 : 0;
   return a;
 }
 
@@ -438,6 +452,16 @@ void drop_staged_batch(fbr_ctx* c) {
 int crop_stats(fbr_ctx* c, const Sub& sb) {
   GnArgs a = gn_args(c, sb, false);
   int32_t* cnt = c->d_cropcnt + (int64_t)sb.j0 * 2;
+  if (c->map_nocrop) {  // keyframe local map: laserCloud*FromMapDSNum = the whole DS map
+    std::vector<int32_t> v(2 * sb.B);
+    for (int j = 0; j < sb.B; ++j) {
+      v[2 * j] = (int32_t)c->gc.n_points;
+      v[2 * j + 1] = (int32_t)c->gs.n_points;
+    }
+    CK(hipMemcpyAsync(cnt, v.data(), sizeof(int32_t) * 2 * sb.B, hipMemcpyHostToDevice, sb.st));
+    CK(hipStreamSynchronize(sb.st));
+    return FBR_OK;
+  }
   CK(hipMemsetAsync(cnt, 0, sizeof(int32_t) * 2 * sb.B, sb.st));
   TIMED_ON(c, sb.st, "crop", launch_crop_count(sb.st, a, c->d_map_c, c->gc.n_points, 0, cnt));
   TIMED_ON(c, sb.st, "crop", launch_crop_count(sb.st, a, c->d_map_s, c->gs.n_points, 1, cnt));
@@ -611,6 +635,110 @@ int upload_cloud(fbr_ctx* c, float4* dst, int32_t* dcnt, const fbr_point_xyzi* s
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------------
+// keyframe local map helpers (fbr_extract_surrounding_keyframes)
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+// Grow a device array to hold `need` elements (keeping `keep` of them).
+template <typename T>
+int grow(T** p, int64_t* cap, int64_t need, int64_t keep, hipStream_t st) {
+  if (need <= *cap) return FBR_OK;
+  const int64_t ncap = std::max<int64_t>(need, *cap * 2 + 1024);
+  T* q = nullptr;
+  CK(hipMalloc((void**)&q, sizeof(T) * ncap));
+  if (*p && keep > 0) CK(hipMemcpyAsync(q, *p, sizeof(T) * keep, hipMemcpyDeviceToDevice, st));
+  CK(hipStreamSynchronize(st));
+  if (*p) CK(hipFree(*p));
+  *p = q;
+  *cap = ncap;
+  return FBR_OK;
+}
+
+// One-segment device VoxelGrid of a device-resident cloud into a device buffer of n points.
+int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4* d_out, int64_t* n_out) {
+  *n_out = 0;
+  if (n <= 0) return FBR_OK;
+  if (n > INT32_MAX / 4) return FBR_ERR_CAPACITY;
+  int32_t* d_cnt = nullptr;
+  uint32_t* d_sc = nullptr;
+  int rc = FBR_OK;
+  if (dalloc(&d_cnt, 2) || dalloc(&d_sc, 4 * n)) {
+    rc = FBR_ERR_HIP;
+  } else {
+    int32_t nn = (int32_t)n, nout = 0;
+    VgArgs a{};
+    a.s[0].in = d_in;
+    a.s[0].stride_in = n;
+    a.s[0].cnt_in = d_cnt;
+    a.s[0].cap = n;
+    a.s[0].out = d_out;
+    a.s[0].stride_out = n;
+    a.s[0].cnt_out = d_cnt + 1;
+    a.s[0].scratch = d_sc;
+    a.s[0].leaf = leaf;
+    a.s[0].nseg = 1;
+    if (hipMemcpyAsync(d_cnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+      rc = FBR_ERR_HIP;
+    } else {
+      launch_voxel_grid(c->stream, a);
+      if (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+          hipStreamSynchronize(c->stream) != hipSuccess)
+        rc = FBR_ERR_HIP;
+      *n_out = nout;
+    }
+  }
+  (void)hipFree(d_cnt);
+  (void)hipFree(d_sc);
+  return rc;
+}
+
+// Device grid over a device-resident map (cell size as build_grid: 0.5 m, at most max_inv, halved
+// until the dense grid has <= 2^26 cells).
+int build_grid_dev(fbr_ctx* c, const float4* d_src, int64_t n, float4** d_pts, int32_t** d_cs, GridDesc* g,
+                   float max_inv) {
+  if (*d_pts) (void)hipFree(*d_pts);
+  if (*d_cs) (void)hipFree(*d_cs);
+  *d_pts = nullptr;
+  *d_cs = nullptr;
+  if (!c->d_bounds && dalloc(&c->d_bounds, 6)) return FBR_ERR_HIP;
+  float inv = 2.0f;
+  if (const char* e = std::getenv("FBR_KNN_CELL")) {
+    const float cell = std::strtof(e, nullptr);
+    if (cell > 0.0f) inv = std::min(4.0f, std::exp2(-std::round(std::log2(cell))));
+  }
+  inv = std::min(inv, max_inv);
+  int64_t dims[3] = {1, 1, 1};
+  int b[6] = {0, 0, 0, 0, 0, 0};
+  for (int attempt = 0; attempt < 12; ++attempt) {
+    const int rc = grid_bounds_device(c->stream, d_src, n, inv, c->d_bounds, b);
+    if (rc) return rc;
+    if (n == 0)
+      for (int d = 0; d < 6; ++d) b[d] = 0;
+    for (int d = 0; d < 3; ++d) dims[d] = (int64_t)b[3 + d] - b[d] + 1;
+    if (dims[0] * dims[1] * dims[2] <= (int64_t)1 << 26) break;
+    inv *= 0.5f;
+  }
+  g->inv_cell = inv;
+  for (int d = 0; d < 3; ++d) {
+    g->origin[d] = (float)b[d];
+    g->dims[d] = (int32_t)dims[d];
+  }
+  g->n_cells = (int32_t)(dims[0] * dims[1] * dims[2]);
+  g->n_points = n;
+  if (dalloc(d_pts, std::max<int64_t>(n, 1)) || dalloc(d_cs, (int64_t)g->n_cells + 1)) return FBR_ERR_HIP;
+  int rc = grid_fill_device(c->stream, d_src, n, *g, *d_cs, *d_pts);
+  if (!rc) CK(hipStreamSynchronize(c->stream));
+  return rc;
+}
+
+// pointDistance (utility.h:312-315) of two key poses
+float key_distance(const fbr_keypose& a, const fbr_keypose& b) {
+  return std::sqrt((a.x - b.x) * (a.x - b.x) + (a.y - b.y) * (a.y - b.y) + (a.z - b.z) * (a.z - b.z));
+}
+
+}  // namespace
+
 // =============================================================================================
 extern "C" {
 
@@ -745,7 +873,8 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_map_c,
                   c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
-                  c->d_desk, c->d_desk_mode, c->d_rowmin};
+                  c->d_desk, c->d_desk_mode, c->d_rowmin,
+                  c->d_kf_c, c->d_kf_s, c->d_kraw_c, c->d_kraw_s, c->d_kds_c, c->d_kds_s, c->d_kf_segs, c->d_bounds};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);
@@ -773,6 +902,7 @@ int fbr_set_map(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corner, cons
   if (!c || n_corner < 0 || n_surf < 0 || (n_corner && !corner) || (n_surf && !surf)) return FBR_ERR_INVALID_ARG;
   CK(hipSetDevice(c->dev));
   c->crop_cached = false;
+  c->map_nocrop = false;
   int rc = voxel_grid_once(c, corner, n_corner, c->P.mapping_corner_leaf_size, c->map_c_host);
   if (!rc) rc = voxel_grid_once(c, surf, n_surf, c->P.mapping_surf_leaf_size, c->map_s_host);
   // both grids share one (power-of-two) cell size: the kNN kernel is specialised on it
@@ -787,6 +917,14 @@ int fbr_set_map(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corner, cons
 int fbr_get_map(fbr_ctx* c, int64_t* n_corner, int64_t* n_surf, fbr_point_xyzi* corner, fbr_point_xyzi* surf) {
   if (!c) return FBR_ERR_INVALID_ARG;
   if (!c->has_map) return FBR_ERR_NO_MAP;
+  if (c->map_nocrop) {  // keyframe local map (device-resident)
+    CK(hipSetDevice(c->dev));
+    if (n_corner) *n_corner = c->kds_c_n;
+    if (n_surf) *n_surf = c->kds_s_n;
+    if (corner && c->kds_c_n) CK(hipMemcpy(corner, c->d_kds_c, sizeof(float4) * c->kds_c_n, hipMemcpyDeviceToHost));
+    if (surf && c->kds_s_n) CK(hipMemcpy(surf, c->d_kds_s, sizeof(float4) * c->kds_s_n, hipMemcpyDeviceToHost));
+    return FBR_OK;
+  }
   if (n_corner) *n_corner = (int64_t)c->map_c_host.size();
   if (n_surf) *n_surf = (int64_t)c->map_s_host.size();
   if (corner) std::memcpy(corner, c->map_c_host.data(), sizeof(fbr_point_xyzi) * c->map_c_host.size());
@@ -1189,6 +1327,186 @@ void fbr_pose_from_affine(const float m[16], float pose[6]) {
   pose[0] = std::atan2(m[9], m[10]);
   pose[1] = std::asin(-m[8]);
   pose[2] = std::atan2(m[4], m[0]);
+}
+
+
+void fbr_keyframe_params_default(fbr_keyframe_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->search_radius = 50.0f;  // params.yaml:66-71
+  p->pose_density = 2.0f;
+  p->loop_closure = 0;
+  p->submap_size = 25;
+  p->recent_window = 10.0;   // mapOptmization.h:900
+}
+
+int fbr_keyframes_add(fbr_ctx* c, const fbr_keypose* pose, const fbr_point_xyzi* corner, int64_t n_corner,
+                      const fbr_point_xyzi* surf, int64_t n_surf) {
+  if (!c || !pose || n_corner < 0 || n_surf < 0 || (n_corner && !corner) || (n_surf && !surf)) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  int rc = grow(&c->d_kf_c, &c->kf_c_cap, c->kf_c_used + n_corner, c->kf_c_used, c->stream);
+  if (!rc) rc = grow(&c->d_kf_s, &c->kf_s_cap, c->kf_s_used + n_surf, c->kf_s_used, c->stream);
+  if (rc) return rc;
+  if (n_corner)
+    CK(hipMemcpyAsync(c->d_kf_c + c->kf_c_used, corner, sizeof(float4) * n_corner, hipMemcpyHostToDevice, c->stream));
+  if (n_surf) CK(hipMemcpyAsync(c->d_kf_s + c->kf_s_used, surf, sizeof(float4) * n_surf, hipMemcpyHostToDevice, c->stream));
+  CK(hipStreamSynchronize(c->stream));
+  fbr_keypose p = *pose;
+  p.intensity = (float)c->kf_poses.size();  // "this can be used as index" (:1687, :1694)
+  c->kf_poses.push_back(p);
+  c->kf_c_off.push_back(c->kf_c_used);
+  c->kf_c_cnt.push_back(n_corner);
+  c->kf_s_off.push_back(c->kf_s_used);
+  c->kf_s_cnt.push_back(n_surf);
+  c->kf_c_used += n_corner;
+  c->kf_s_used += n_surf;
+  return FBR_OK;
+}
+
+int fbr_keyframes_set_pose(fbr_ctx* c, int64_t index, const fbr_keypose* pose) {
+  if (!c || !pose || index < 0 || index >= (int64_t)c->kf_poses.size()) return FBR_ERR_INVALID_ARG;
+  fbr_keypose& k = c->kf_poses[index];  // correctPoses (:1746-1757): x, y, z, roll, pitch, yaw
+  k.x = pose->x;
+  k.y = pose->y;
+  k.z = pose->z;
+  k.roll = pose->roll;
+  k.pitch = pose->pitch;
+  k.yaw = pose->yaw;
+  return FBR_OK;
+}
+
+int fbr_keyframes_count(fbr_ctx* c, int64_t* n) {
+  if (!c || !n) return FBR_ERR_INVALID_ARG;
+  *n = (int64_t)c->kf_poses.size();
+  return FBR_OK;
+}
+
+int fbr_keyframes_reset(fbr_ctx* c) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  c->kf_poses.clear();
+  c->kf_c_off.clear();
+  c->kf_c_cnt.clear();
+  c->kf_s_off.clear();
+  c->kf_s_cnt.clear();
+  c->kf_c_used = c->kf_s_used = 0;
+  return FBR_OK;
+}
+
+int fbr_extract_surrounding_keyframes(fbr_ctx* c, double stamp, const fbr_keyframe_params* kp, int64_t* n_corner_map,
+                                      int64_t* n_surf_map, int32_t* n_frames) {
+  if (!c || !kp || !(kp->search_radius >= 0) || !(kp->pose_density > 0)) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  if (n_frames) *n_frames = 0;
+  const int64_t N = (int64_t)c->kf_poses.size();
+  if (N == 0) {  // extractSurroundingKeyFrames (:967-968): nothing to extract, map unchanged
+    if (n_corner_map) *n_corner_map = c->map_nocrop ? c->kds_c_n : 0;
+    if (n_surf_map) *n_surf_map = c->map_nocrop ? c->kds_s_n : 0;
+    return FBR_OK;
+  }
+  const fbr_keypose& back = c->kf_poses.back();
+  std::vector<fbr_keypose> toExtract;  // cloudToExtract (x, y, z, intensity = key index)
+  if (kp->loop_closure) {  // extractForLoopClosure (:857-870)
+    for (int64_t i = N - 1; i >= 0; --i) {
+      if ((int)toExtract.size() <= kp->submap_size) toExtract.push_back(c->kf_poses[i]);
+      else break;
+    }
+  } else {  // extractNearby (:872-907)
+    // kdtreeSurroundingKeyPoses->radiusSearch(back, radius): d2 = ((dx dx + dy dy) + dz dz) < r^2,
+    // sorted by distance (ties by index)
+    const float r2 = (float)((double)kp->search_radius * (double)kp->search_radius);
+    std::vector<std::pair<float, int64_t>> hits;
+    for (int64_t i = 0; i < N; ++i) {
+      const fbr_keypose& q = c->kf_poses[i];
+      float d = 0.0f, diff;
+      diff = back.x - q.x; d += diff * diff;
+      diff = back.y - q.y; d += diff * diff;
+      diff = back.z - q.z; d += diff * diff;
+      if (d < r2) hits.emplace_back(d, i);
+    }
+    std::stable_sort(hits.begin(), hits.end(),
+                     [](const std::pair<float, int64_t>& a, const std::pair<float, int64_t>& b) { return a.first < b.first; });
+    std::vector<fbr_point_xyzi> sur(hits.size());
+    for (size_t k = 0; k < hits.size(); ++k) {
+      const fbr_keypose& q = c->kf_poses[hits[k].second];
+      sur[k] = fbr_point_xyzi{q.x, q.y, q.z, q.intensity};
+    }
+    std::vector<fbr_point_xyzi> ds;  // downSizeFilterSurroundingKeyPoses (leaf surroundingKeyframeDensity)
+    const int rc = voxel_grid_once(c, sur.data(), (int64_t)sur.size(), kp->pose_density, ds);
+    if (rc) return rc;
+    for (const fbr_point_xyzi& p : ds) {
+      fbr_keypose k{};
+      k.x = p.x;
+      k.y = p.y;
+      k.z = p.z;
+      k.intensity = p.intensity;
+      toExtract.push_back(k);
+    }
+    for (int64_t i = N - 1; i >= 0; --i) {  // the last recent_window seconds of keyframes (:896-904)
+      if (stamp - c->kf_poses[i].time < kp->recent_window) toExtract.push_back(c->kf_poses[i]);
+      else break;
+    }
+  }
+  // extractCloud (:909-955): transform + concatenate the selected keyframes' clouds, then DS
+  std::vector<KfSeg> segs;
+  int64_t tot_c = 0, tot_s = 0, max_cnt = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (const fbr_keypose& e : toExtract) {
+      if (key_distance(e, back) > kp->search_radius) continue;  // :924-925
+      const int k = (int)e.intensity;                              // :927
+      if (k < 0 || k >= N) return FBR_ERR_STATE;
+      const fbr_keypose& pose = c->kf_poses[k];
+      KfSeg g;
+      const float tr[6] = {pose.roll, pose.pitch, pose.yaw, pose.x, pose.y, pose.z};
+      float m[16];
+      fbr_affine_from_pose(tr, m);  // pcl::getTransformation(x, y, z, roll, pitch, yaw), host libm
+      for (int q = 0; q < 12; ++q) g.T[q] = m[q];
+      if (pass == 0) {
+        g.src = c->kf_c_off[k];
+        g.count = c->kf_c_cnt[k];
+        g.dst = tot_c;
+        tot_c += g.count;
+      } else {
+        g.src = c->kf_s_off[k];
+        g.count = c->kf_s_cnt[k];
+        g.dst = tot_s;
+        tot_s += g.count;
+      }
+      max_cnt = std::max(max_cnt, g.count);
+      segs.push_back(g);
+    }
+  }
+  const int nseg_c = (int)(segs.size() / 2);
+  if (n_frames) *n_frames = (int32_t)toExtract.size();
+  int rc = grow(&c->d_kraw_c, &c->kraw_c_cap, std::max<int64_t>(tot_c, 1), 0, c->stream);
+  if (!rc) rc = grow(&c->d_kraw_s, &c->kraw_s_cap, std::max<int64_t>(tot_s, 1), 0, c->stream);
+  if (!rc) rc = grow(&c->d_kf_segs, &c->kf_segs_cap, std::max<int64_t>((int64_t)segs.size(), 1), 0, c->stream);
+  if (rc) return rc;
+  if (!segs.empty())
+    CK(hipMemcpyAsync(c->d_kf_segs, segs.data(), sizeof(KfSeg) * segs.size(), hipMemcpyHostToDevice, c->stream));
+  launch_kf_transform(c->stream, c->d_kf_c, c->d_kf_segs, nseg_c, max_cnt, c->d_kraw_c);
+  launch_kf_transform(c->stream, c->d_kf_s, c->d_kf_segs + nseg_c, (int)segs.size() - nseg_c, max_cnt, c->d_kraw_s);
+  CK(hipGetLastError());
+  if (c->d_kds_c) CK(hipFree(c->d_kds_c));
+  if (c->d_kds_s) CK(hipFree(c->d_kds_s));
+  c->d_kds_c = c->d_kds_s = nullptr;
+  if (dalloc(&c->d_kds_c, std::max<int64_t>(tot_c, 1)) || dalloc(&c->d_kds_s, std::max<int64_t>(tot_s, 1))) return FBR_ERR_HIP;
+  // downSizeFilterCorner / downSizeFilterSurf (:946-954)
+  rc = voxel_grid_dev(c, c->d_kraw_c, tot_c, c->P.mapping_corner_leaf_size, c->d_kds_c, &c->kds_c_n);
+  if (!rc) rc = voxel_grid_dev(c, c->d_kraw_s, tot_s, c->P.mapping_surf_leaf_size, c->d_kds_s, &c->kds_s_n);
+  // the kNN grids (both maps share one cell size, as in fbr_set_map)
+  if (!rc) rc = build_grid_dev(c, c->d_kds_c, c->kds_c_n, &c->d_map_c, &c->d_cs_c, &c->gc, 4.0f);
+  if (!rc) rc = build_grid_dev(c, c->d_kds_s, c->kds_s_n, &c->d_map_s, &c->d_cs_s, &c->gs, c->gc.inv_cell);
+  if (!rc && c->gs.inv_cell < c->gc.inv_cell)
+    rc = build_grid_dev(c, c->d_kds_c, c->kds_c_n, &c->d_map_c, &c->d_cs_c, &c->gc, c->gs.inv_cell);
+  c->has_map = rc == FBR_OK;
+  c->map_nocrop = rc == FBR_OK;
+  c->crop_cached = false;
+  c->map_c_host.clear();
+  c->map_s_host.clear();
+  if (rc) return rc;
+  if (n_corner_map) *n_corner_map = c->kds_c_n;
+  if (n_surf_map) *n_surf_map = c->kds_s_n;
+  return FBR_OK;
 }
 
 }  // extern "C"

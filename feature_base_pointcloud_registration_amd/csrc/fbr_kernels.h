@@ -131,6 +131,7 @@ struct GnArgs {
   int32_t* iter_cnt;         // [max_iter][2] active-job count / finished workgroups (zeroed per solve)
   const int32_t* desk_mode;  // [B] kDesk* bits or null (transformUpdate's IMU slerp, :1447-1474)
   const fbr_deskew_table* desk;  // [B]
+  int nocrop;                // 1: keyframe local map, no CropBox (scan2MapOptimization on it)
 };
 void launch_gn_init(hipStream_t s, const GnArgs& a);
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter);
@@ -141,5 +142,16 @@ void launch_gn_finalize(hipStream_t s, const GnArgs& a);
 void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, float* dst);
 void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* map_pts, int64_t n, int which,
                        int32_t* counts /* [B][2] */);
+
+// ---- keyframe local map (k_keyframe.hip) ----
+struct KfSeg {               // one selected keyframe cloud: pool[src .. src+count) -> out[dst ..]
+  int64_t src, dst, count;
+  float T[12];               // pcl::getTransformation of the key pose, row-major 3x4
+};
+void launch_kf_transform(hipStream_t s, const float4* pool, const KfSeg* segs, int nseg, int64_t max_count, float4* out);
+// Device kNN grid build: cell bounds of pts at 1/inv cells (h_bounds = lo xyz, hi xyz), then the
+// per-cell counts, exclusive scan into d_cs [n_cells + 1] and the scatter into d_out.
+int grid_bounds_device(hipStream_t s, const float4* pts, int64_t n, float inv, int* d_bounds, int h_bounds[6]);
+int grid_fill_device(hipStream_t s, const float4* pts, int64_t n, const GridDesc& g, int32_t* d_cs, float4* d_out);
 
 }  // namespace fbr

@@ -267,8 +267,8 @@ __global__ void k_gn_init(GnArgs a) {
       for (int k = 0; k < 6; ++k) g.pose[k] = a.guess[job * 6 + k];
       pose_to_T(g.pose, g.T, g.trig);
       for (int k = 0; k < 3; ++k) {  // edge = size + origin (float), :289-292
-        g.crop_min[k] = -a.crop_half[k] + g.pose[3 + k];
-        g.crop_max[k] = a.crop_half[k] + g.pose[3 + k];
+        g.crop_min[k] = a.nocrop ? -FLT_MAX : -a.crop_half[k] + g.pose[3 + k];  // keyframe map: no CropBox
+        g.crop_max[k] = a.nocrop ? FLT_MAX : a.crop_half[k] + g.pose[3 + k];
       }
       for (int k = 0; k < 36; ++k) g.matP[k] = 0.0f;
       const int nc = a.ncds[job], ns = a.nsds[job];

@@ -34,6 +34,26 @@ DESKEW_TABLE = np.dtype([("status", "<i4"), ("imu_available", "<i4"), ("imu_poin
 assert DESKEW_TABLE.itemsize == 32 + 4 * 8 * IMU_QUEUE
 FBR_DESKEW_READY, FBR_DESKEW_WAIT_IMU = 0, 1
 
+# LIO-SAM keyframe store (include/fbr.h "LIO-SAM keyframe local map")
+KEYPOSE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("intensity", "<f4"), ("roll", "<f4"),
+                    ("pitch", "<f4"), ("yaw", "<f4"), ("pad_", "<f4"), ("time", "<f8")])
+assert KEYPOSE.itemsize == 40
+
+
+class FbrKeyframeParams(ctypes.Structure):
+    _fields_ = [("search_radius", ctypes.c_float), ("pose_density", ctypes.c_float),
+                ("loop_closure", ctypes.c_int32), ("submap_size", ctypes.c_int32),
+                ("recent_window", ctypes.c_double)]
+
+
+def keyframe_params(**kw):
+    """fbr_keyframe_params_default (params.yaml:66-71, the 10 s window of mapOptmization.h:900)."""
+    p = FbrKeyframeParams(50.0, 2.0, 0, 25, 10.0)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
 FBR_OK = 0
 FBR_REG_OK = 0
 FBR_REG_NOT_ENOUGH_FEATURES = 1

@@ -250,7 +250,50 @@ int fbr_imu_deskew_info(const fbr_imu_sample* imu_queue, int64_t n_imu, double t
  * the point deskew for that call (deskewFlag = -1, :296-297, :548) but not the IMU update. */
 int fbr_set_deskew(fbr_ctx* ctx, const fbr_deskew_table* tables, int n_tables);
 
-/* Down-sampled global map actually used (sizes, then optional copies; pass NULL to skip). */
+/* ---- LIO-SAM keyframe local map ------------------------------------
+ * The reference's mapping back-end (laserCloudInfoHandler, mapOptmization.h:346-389) registers
+ * each scan against a local map built from its keyframes instead of the cropped prior map:
+ * extractSurroundingKeyFrames (:964-978) -> extractNearby (:872-907) or extractForLoopClosure
+ * (:857-870) -> extractCloud (:909-955).  The keyframe store mirrors cloudKeyPoses3D/6D and
+ * corner/surfCloudKeyFrames; GTSAM (saveKeyFramesAndFactor / correctPoses) stays with the caller,
+ * which pushes each new key pose + its down-sampled feature clouds (fbr_keyframes_add) and
+ * rewrites poses after a loop closure (fbr_keyframes_set_pose).  Selection runs on the host (a few
+ * hundred poses), the transforms, concatenation, VoxelGrids and the kNN grid on the device. */
+typedef struct fbr_keypose {   /* PointXYZIRPYT (mapOptmization.h:34-51) */
+  float x, y, z;
+  float intensity;             /* key index: set to the keyframe's position by fbr_keyframes_add,
+                                  as saveKeyFramesAndFactor does (:1687, :1694)                   */
+  float roll, pitch, yaw;
+  float pad_;
+  double time;                 /* timeLaserCloudInfoLast when the keyframe was saved (:1698)     */
+} fbr_keypose;
+
+typedef struct fbr_keyframe_params {
+  float search_radius;         /* surroundingKeyframeSearchRadius 50 m   params.yaml:67        */
+  float pose_density;          /* surroundingKeyframeDensity 2 m          params.yaml:66        */
+  int32_t loop_closure;        /* loopClosureEnableFlag 0                 params.yaml:70        */
+  int32_t submap_size;         /* surroundingKeyframeSize 25              params.yaml:71        */
+  double recent_window;        /* 10 s of most recent keyframes           mapOptmization.h:900  */
+} fbr_keyframe_params;
+
+void fbr_keyframe_params_default(fbr_keyframe_params* p);
+/* cloudKeyPoses3D/6D->push_back + corner/surfCloudKeyFrames.push_back (lidar-frame clouds). */
+int fbr_keyframes_add(fbr_ctx* ctx, const fbr_keypose* pose, const fbr_point_xyzi* corner, int64_t n_corner,
+                      const fbr_point_xyzi* surf, int64_t n_surf);
+/* correctPoses (:1740-1770): new x, y, z, roll, pitch, yaw of keyframe `index` (index and time kept). */
+int fbr_keyframes_set_pose(fbr_ctx* ctx, int64_t index, const fbr_keypose* pose);
+int fbr_keyframes_count(fbr_ctx* ctx, int64_t* n);
+int fbr_keyframes_reset(fbr_ctx* ctx);
+/* extractSurroundingKeyFrames at timeLaserCloudInfoLast = `stamp`: the down-sampled local corner /
+ * surf maps become the registration map of the following fbr_register / fbr_process_scan calls
+ * (registered without the CropBox, as scan2MapOptimization does on them), until fbr_set_map /
+ * fbr_load_map restores a prior map.  With no keyframe the previous map is kept (:967-968).
+ * n_frames (optional) = entries of cloudToExtract. */
+int fbr_extract_surrounding_keyframes(fbr_ctx* ctx, double stamp, const fbr_keyframe_params* kp,
+                                      int64_t* n_corner_map, int64_t* n_surf_map, int32_t* n_frames);
+
+/* Down-sampled global map actually used (sizes, then optional copies; pass NULL to skip).  After
+ * fbr_extract_surrounding_keyframes: the keyframe local map (laserCloud{Corner,Surf}FromMapDS). */
 int fbr_get_map(fbr_ctx* ctx, int64_t* n_corner, int64_t* n_surf, fbr_point_xyzi* corner,
                 fbr_point_xyzi* surf);
 

@@ -193,6 +193,11 @@ class ImageProjection {
   }
   int msgFlags() const { return msg_flags_; }
 
+  /* deskewInfo() enabled (imageProjection.cpp:189-191 uncommented): the table fbr_imu_deskew_info
+   * built for the next scan; deskewPoint then runs inside the device compaction. */
+  void setDeskew(const fbr_deskew_table& t) { check(fbr_set_deskew(c_.get(), &t, 1), "fbr_set_deskew"); }
+  void clearDeskew() { check(fbr_set_deskew(c_.get(), nullptr, 0), "fbr_set_deskew"); }
+
  private:
   Context& c_;
   std::deque<PointCloud2> cloudQueue_;
@@ -266,6 +271,22 @@ class MapOptimization {
   }
 
   const fbr_reg_stats& lastStats() const { return stats_; }
+
+  /* LIO-SAM keyframe back-end (mapOptmization.h:857-978, 1667-1770): the caller's GTSAM step pushes
+   * each key pose with its DS'd feature clouds and corrects poses after a loop closure;
+   * extractSurroundingKeyFrames then makes the keyframe local map the registration map. */
+  void addKeyFrame(const fbr_keypose& pose, const std::vector<fbr_point_xyzi>& corner,
+                   const std::vector<fbr_point_xyzi>& surf) {
+    check(fbr_keyframes_add(c_.get(), &pose, corner.data(), (int64_t)corner.size(), surf.data(), (int64_t)surf.size()),
+          "fbr_keyframes_add");
+  }
+  void correctPose(int64_t index, const fbr_keypose& pose) {
+    check(fbr_keyframes_set_pose(c_.get(), index, &pose), "fbr_keyframes_set_pose");
+  }
+  void extractSurroundingKeyFrames(double timeLaserCloudInfoLast, const fbr_keyframe_params& kp) {
+    check(fbr_extract_surrounding_keyframes(c_.get(), timeLaserCloudInfoLast, &kp, nullptr, nullptr, nullptr),
+          "fbr_extract_surrounding_keyframes");
+  }
 
  private:
   Context& c_;

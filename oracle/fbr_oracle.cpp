@@ -916,7 +916,7 @@ static void crop(const std::vector<P4>& in, const float mn[3], const float mx[3]
 
 static void registration_core(const fbr_params& P, const Map& map, const P4* cornerLast, int64_t ncl,
                               const P4* surfLast, int64_t nsl, float tr[6], RegResult& R, int nthreads,
-                              const fbr_deskew_table* T = nullptr) {
+                              const fbr_deskew_table* T = nullptr, bool no_crop = false) {
   fbr_reg_stats& st = R.st;
   std::memset(&st, 0, sizeof(st));
   R.trace.clear();
@@ -928,8 +928,13 @@ static void registration_core(const fbr_params& P, const Map& map, const P4* cor
     mx[i] = P.crop_half[i] + origin[i];
   }
   std::vector<P4> cornerMap, surfMap;
-  crop(map.corner, mn, mx, cornerMap);
-  crop(map.surf, mn, mx, surfMap);
+  if (no_crop) {  // LIO-SAM path: scan2MapOptimization on laserCloud*FromMapDS as extracted
+    cornerMap = map.corner;
+    surfMap = map.surf;
+  } else {
+    crop(map.corner, mn, mx, cornerMap);
+    crop(map.surf, mn, mx, surfMap);
+  }
   st.n_corner_map = (int)cornerMap.size();
   st.n_surf_map = (int)surfMap.size();
   // downsampleCurrentScan (:981-993)
@@ -1241,6 +1246,87 @@ void* orc_map_create(const fbr_params* P, const fbr_point_xyzi* corner, int64_t 
   return m;
 }
 void orc_map_destroy(void* m) { delete (Map*)m; }
+// A map taken as it is (the keyframe local map is already down-sampled by extractCloud).
+void* orc_map_create_raw(const fbr_point_xyzi* corner, int64_t nc, const fbr_point_xyzi* surf, int64_t ns) {
+  Map* m = new Map();
+  m->corner.assign(corner, corner + nc);
+  m->surf.assign(surf, surf + ns);
+  return m;
+}
+
+// extractSurroundingKeyFrames (mapOptmization.h:964-978): extractNearby (:872-907) or
+// extractForLoopClosure (:857-870), then extractCloud (:909-955) with transformPointCloud
+// (:405-425).  Key clouds are given as pools + per-keyframe offsets / counts; poses are
+// PointXYZIRPYT with intensity = key index.  The radius search restates KdTreeFLANN::radiusSearch
+// (d2 < r^2, results sorted by distance; equal distances by index).
+int orc_kf_extract(const fbr_params* P, const fbr_keypose* poses, int64_t N, const fbr_point_xyzi* cpool,
+                   const int64_t* c_off, const int64_t* c_cnt, const fbr_point_xyzi* spool, const int64_t* s_off,
+                   const int64_t* s_cnt, const fbr_keyframe_params* kp, double timeLaserCloudInfoLast,
+                   fbr_point_xyzi* corner_out, int64_t* n_corner, fbr_point_xyzi* surf_out, int64_t* n_surf,
+                   int32_t* n_frames) {
+  std::vector<P4> cloudToExtract;
+  const fbr_keypose& back = poses[N - 1];
+  auto pose3D = [&](int64_t i) { return P4{poses[i].x, poses[i].y, poses[i].z, poses[i].intensity}; };
+  if (kp->loop_closure) {
+    for (int64_t i = N - 1; i >= 0; --i) {
+      if ((int)cloudToExtract.size() <= kp->submap_size) cloudToExtract.push_back(pose3D(i));
+      else break;
+    }
+  } else {
+    std::vector<std::pair<float, int64_t>> found;
+    const float radius2 = (float)((double)kp->search_radius * (double)kp->search_radius);
+    for (int64_t i = 0; i < N; ++i) {
+      float dist = 0, diff;
+      diff = back.x - poses[i].x; dist += diff * diff;
+      diff = back.y - poses[i].y; dist += diff * diff;
+      diff = back.z - poses[i].z; dist += diff * diff;
+      if (dist < radius2) found.emplace_back(dist, i);
+    }
+    std::stable_sort(found.begin(), found.end(), [](const std::pair<float, int64_t>& a, const std::pair<float, int64_t>& b) {
+      return a.first < b.first;
+    });
+    std::vector<P4> surroundingKeyPoses;
+    for (auto& f : found) surroundingKeyPoses.push_back(pose3D(f.second));
+    voxel_grid(surroundingKeyPoses.data(), (int64_t)surroundingKeyPoses.size(), kp->pose_density, cloudToExtract);
+    for (int64_t i = N - 1; i >= 0; --i) {
+      if (timeLaserCloudInfoLast - poses[i].time < kp->recent_window) cloudToExtract.push_back(pose3D(i));
+      else break;
+    }
+  }
+  *n_frames = (int32_t)cloudToExtract.size();
+  std::vector<P4> cornerFromMap, surfFromMap;
+  for (const P4& e : cloudToExtract) {
+    const float dist = std::sqrt((e.x - back.x) * (e.x - back.x) + (e.y - back.y) * (e.y - back.y) +
+                                 (e.z - back.z) * (e.z - back.z));  // pointDistance (utility.h:312-315)
+    if (dist > kp->search_radius) continue;
+    const int thisKeyInd = (int)e.intensity;
+    if (thisKeyInd < 0 || thisKeyInd >= N) return -1;
+    const fbr_keypose& t = poses[thisKeyInd];
+    const Affine transCur = get_transformation(t.x, t.y, t.z, t.roll, t.pitch, t.yaw);
+    for (int pass = 0; pass < 2; ++pass) {
+      const P4* src = pass ? spool + s_off[thisKeyInd] : cpool + c_off[thisKeyInd];
+      const int64_t cnt = pass ? s_cnt[thisKeyInd] : c_cnt[thisKeyInd];
+      std::vector<P4>& dst = pass ? surfFromMap : cornerFromMap;
+      for (int64_t i = 0; i < cnt; ++i) {
+        const P4& pf = src[i];
+        P4 o;
+        o.x = transCur.m[0][0] * pf.x + transCur.m[0][1] * pf.y + transCur.m[0][2] * pf.z + transCur.m[0][3];
+        o.y = transCur.m[1][0] * pf.x + transCur.m[1][1] * pf.y + transCur.m[1][2] * pf.z + transCur.m[1][3];
+        o.z = transCur.m[2][0] * pf.x + transCur.m[2][1] * pf.y + transCur.m[2][2] * pf.z + transCur.m[2][3];
+        o.intensity = pf.intensity;
+        dst.push_back(o);
+      }
+    }
+  }
+  std::vector<P4> cds, sds;
+  voxel_grid(cornerFromMap.data(), (int64_t)cornerFromMap.size(), P->mapping_corner_leaf_size, cds);
+  voxel_grid(surfFromMap.data(), (int64_t)surfFromMap.size(), P->mapping_surf_leaf_size, sds);
+  *n_corner = (int64_t)cds.size();
+  *n_surf = (int64_t)sds.size();
+  if (corner_out) std::memcpy(corner_out, cds.data(), sizeof(P4) * cds.size());
+  if (surf_out) std::memcpy(surf_out, sds.data(), sizeof(P4) * sds.size());
+  return 0;
+}
 int orc_map_get(void* mp, int64_t* nc, int64_t* ns, fbr_point_xyzi* corner, fbr_point_xyzi* surf) {
   Map* m = (Map*)mp;
   if (nc) *nc = (int64_t)m->corner.size();
@@ -1252,9 +1338,9 @@ int orc_map_get(void* mp, int64_t* nc, int64_t* ns, fbr_point_xyzi* corner, fbr_
 
 int orc_register(const fbr_params* P, void* map, const fbr_point_xyzi* corner, int64_t nc, const fbr_point_xyzi* surf,
                  int64_t ns, float pose[6], fbr_reg_stats* st, float* trace, int nthreads,
-                 const fbr_deskew_table* desk) {
+                 const fbr_deskew_table* desk, int no_crop) {
   RegResult R;
-  registration_core(*P, *(Map*)map, corner, nc, surf, ns, pose, R, nthreads, desk);
+  registration_core(*P, *(Map*)map, corner, nc, surf, ns, pose, R, nthreads, desk, no_crop != 0);
   if (st) *st = R.st;
   if (trace) std::memcpy(trace, R.trace.data(), sizeof(float) * R.trace.size());
   return 0;

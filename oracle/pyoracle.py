@@ -53,7 +53,11 @@ def lib():
         L.orc_map_create.argtypes = [_VP, _VP, _I64, _VP, _I64]
         L.orc_map_destroy.argtypes = [_VP]
         L.orc_map_get.argtypes = [_VP, _VP, _VP, _VP, _VP]
-        L.orc_register.argtypes = [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP, ctypes.c_int, _VP]
+        L.orc_register.argtypes = [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP, ctypes.c_int, _VP, ctypes.c_int]
+        L.orc_map_create_raw.restype = _VP
+        L.orc_map_create_raw.argtypes = [_VP, _I64, _VP, _I64]
+        L.orc_kf_extract.argtypes = [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_double, _VP, _VP,
+                                     _VP, _VP, _VP]
         L.orc_process_scan.argtypes = [_VP, _VP, _VP, _I64, ctypes.c_double, _VP, _VP, ctypes.c_int]
         L.orc_affine_from_pose.argtypes = [_VP, _VP]
         L.orc_pose_from_affine.argtypes = [_VP, _VP]
@@ -137,10 +141,16 @@ class Stream:
 class Map:
     """Global prior map after the start-up VoxelGrid (mapOptmization.h:245-260)."""
 
-    def __init__(self, params, corner, surf):
+    def __init__(self, params, corner, surf, raw=False):
+        """raw=False: the prior map after the start-up VoxelGrid; raw=True: the clouds as given (a
+        keyframe local map from kf_extract), registered without the CropBox."""
         self.params = params
-        self.h = lib().orc_map_create(ctypes.byref(params), ptr(corner), len(corner), ptr(surf),
-                                      len(surf))
+        self.raw = raw
+        if raw:
+            self.h = lib().orc_map_create_raw(ptr(corner), len(corner), ptr(surf), len(surf))
+        else:
+            self.h = lib().orc_map_create(ctypes.byref(params), ptr(corner), len(corner), ptr(surf),
+                                          len(surf))
 
     def arrays(self):
         nc, ns = _I64(), _I64()
@@ -157,7 +167,7 @@ class Map:
         st = FbrRegStats()
         trace = np.zeros((self.params.max_iterations, 6), np.float32)
         lib().orc_register(ctypes.byref(self.params), self.h, ptr(corner), len(corner), ptr(surf),
-                           len(surf), ptr(pose), ctypes.byref(st), ptr(trace), n_threads, ptr(tab))
+                           len(surf), ptr(pose), ctypes.byref(st), ptr(trace), n_threads, ptr(tab), int(self.raw))
         d = st.as_dict()
         return pose, d, trace[:d["iterations"]].copy()
 
@@ -185,6 +195,26 @@ def sort_smoothness(values):
     out = np.zeros(len(v), np.int64)
     lib().orc_sort_smoothness(ptr(v), len(v), ptr(out))
     return out
+
+
+def kf_extract(params, poses, corner_clouds, surf_clouds, kparams, stamp):
+    """extractSurroundingKeyFrames on a keyframe list: poses (KEYPOSE array, intensity = index),
+    per-keyframe lidar-frame clouds -> (local corner map, local surf map, n_frames)."""
+    poses = np.ascontiguousarray(poses)
+    cpool = np.ascontiguousarray(np.concatenate(corner_clouds) if corner_clouds else np.zeros(0, POINT_XYZI))
+    spool = np.ascontiguousarray(np.concatenate(surf_clouds) if surf_clouds else np.zeros(0, POINT_XYZI))
+    c_cnt = np.array([len(c) for c in corner_clouds], np.int64)
+    s_cnt = np.array([len(c) for c in surf_clouds], np.int64)
+    c_off = np.ascontiguousarray(np.concatenate([[0], np.cumsum(c_cnt)[:-1]]).astype(np.int64))
+    s_off = np.ascontiguousarray(np.concatenate([[0], np.cumsum(s_cnt)[:-1]]).astype(np.int64))
+    oc = np.zeros(max(len(cpool), 1), POINT_XYZI)
+    os_ = np.zeros(max(len(spool), 1), POINT_XYZI)
+    nc, ns, nf = _I64(), _I64(), ctypes.c_int32()
+    rc = lib().orc_kf_extract(ctypes.byref(params), ptr(poses), len(poses), ptr(cpool), ptr(c_off), ptr(c_cnt),
+                              ptr(spool), ptr(s_off), ptr(s_cnt), ctypes.byref(kparams), ctypes.c_double(stamp),
+                              ptr(oc), ctypes.byref(nc), ptr(os_), ctypes.byref(ns), ctypes.byref(nf))
+    assert rc == 0
+    return oc[:nc.value].copy(), os_[:ns.value].copy(), nf.value
 
 
 def imu_convert(ext, samples):
