@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="worker threads of the all-cores CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--deskew", action="store_true",
+                    help="enable the IMU deskew path (SURVEY 8f row 3): one imuDeskewInfo table per job")
     ap.add_argument("--dist", action="store_true",
                     help="use the torch.distributed (RCCL) path even at world size 1 (tests)")
     ap.add_argument("--profile", default="dominant", choices=["all", "dominant", "off"],
@@ -97,6 +99,10 @@ def main():
     stream_gbps = api.stream_copy_bandwidth(dev) if rank == 0 else None  # achievable HBM copy rate
     ctx = api.Context(P, device=dev)
     ctx.set_map(corner_map, surf_map)
+    if args.deskew:  # per-job IMU tables: 200 Hz queue around each job's scan time
+        tabs = [api.imu_deskew_info(synth.imu_queue(10.0 * j - 0.05, 10.0 * j + 0.16, gyro=(0.0, 0.0, 0.0), seed=j), 10.0 * j,
+                                    10.0 * j + 0.1)[0] for j in range(B)]
+        ctx.set_deskew(tabs)
     ctx.batch_stage(scans, guesses)
 
     gather_buf = None
@@ -208,6 +214,7 @@ def main():
             "mean_queries_per_scan": round(tot["Q"] / B, 1),
             "mean_gn_iterations": round(float(stats["iterations"].mean()), 3),
             "parallelism": f"scan-shard x{world}, RCCL pose all-gather" if world > 1 else "single GPU",
+            "imu_deskew": bool(args.deskew),
         },
         "roofline": {
             "bound": "hbm",

@@ -275,6 +275,16 @@ int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pt
   return FBR_OK;
 }
 
+// Clouds at least this large take the device-wide VoxelGrid (FBR_VG_LARGE_MIN overrides; tests
+// use it to compare both kernels on the same input).
+int64_t vg_large_min() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("FBR_VG_LARGE_MIN");
+    return e ? std::max<int64_t>(1, std::atoll(e)) : kVgLargeMin;
+  }();
+  return v;
+}
+
 // One-segment device VoxelGrid with temporary buffers (map start-up filter, fbr_voxel_grid).
 int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf, std::vector<fbr_point_xyzi>& out) {
   out.clear();
@@ -284,13 +294,25 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
   int32_t* d_cnt = nullptr;
   uint32_t* d_sc = nullptr;
   int rc = FBR_OK;
-  if (dalloc(&d_in, n) || dalloc(&d_out, n) || dalloc(&d_cnt, 2) || dalloc(&d_sc, 4 * n)) {
+  const bool large = n >= vg_large_min();
+  if (dalloc(&d_in, n) || dalloc(&d_out, n) || dalloc(&d_cnt, 2) || (!large && dalloc(&d_sc, 4 * n))) {
     rc = FBR_ERR_HIP;
   } else {
     int32_t nn = (int32_t)n;
     if (hipMemcpyAsync(d_in, in, sizeof(float4) * n, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
         hipMemcpyAsync(d_cnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
       rc = FBR_ERR_HIP;
+    } else if (large) {
+      rc = voxel_grid_large(c->stream, d_in, n, leaf, 0, d_out, d_cnt + 1);
+      int32_t nout = 0;
+      if (!rc && (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                  hipStreamSynchronize(c->stream) != hipSuccess))
+        rc = FBR_ERR_HIP;
+      if (!rc) {
+        out.resize(nout);
+        if (nout && hipMemcpy(out.data(), d_out, sizeof(float4) * nout, hipMemcpyDeviceToHost) != hipSuccess)
+          rc = FBR_ERR_HIP;
+      }
     } else {
       VgArgs a{};
       a.s[0].in = d_in;
@@ -663,6 +685,17 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
   int32_t* d_cnt = nullptr;
   uint32_t* d_sc = nullptr;
   int rc = FBR_OK;
+  if (n >= vg_large_min()) {
+    int32_t nout = 0;
+    if (dalloc(&d_cnt, 1)) return FBR_ERR_HIP;
+    rc = voxel_grid_large(c->stream, d_in, n, leaf, 0, d_out, d_cnt);
+    if (!rc && (hipMemcpyAsync(&nout, d_cnt, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                hipStreamSynchronize(c->stream) != hipSuccess))
+      rc = FBR_ERR_HIP;
+    *n_out = nout;
+    (void)hipFree(d_cnt);
+    return rc;
+  }
   if (dalloc(&d_cnt, 2) || dalloc(&d_sc, 4 * n)) {
     rc = FBR_ERR_HIP;
   } else {

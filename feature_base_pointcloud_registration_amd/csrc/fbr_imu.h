@@ -12,9 +12,9 @@
 //                            (redux_novec_unroller splits 3 into 1 + 2)
 //   tf::Quaternion::setRPY / slerp / angleShortestPath, tf::Matrix3x3(q).getRPY
 //                            (tf/LinearMath/Quaternion.h, Matrix3x3.h; tfScalar = double)
-// Float sin/cos here are (float)sin((double)x) (correctly rounded); the reference's glibc
-// sinf/cosf are IFUNC-dispatched (FMA or SSE2 variant by host CPU) and differ from that by at most
-// one ulp, so deskewed coordinates match the reference to float rounding, not bit for bit.
+// Float sin/cos differ from the reference's glibc sinf/cosf (IFUNC-dispatched: FMA or SSE2
+// variant by host CPU) by an ulp or two on the device, so deskewed coordinates match the
+// reference to float rounding, not bit for bit.
 #pragma once
 #include <math.h>
 #include <stdint.h>
@@ -37,8 +37,10 @@ struct Rot3 {
   float m[3][3];
 };
 
-FBR_HD inline float fsin(float x) { return (float)sin((double)x); }
-FBR_HD inline float fcos(float x) { return (float)cos((double)x); }
+// sinf / cosf: glibc's on the host; on the device the ROCm f32 routines (within an ulp or two,
+// like glibc's IFUNC variants, and far cheaper than the double routines per deskewed point).
+FBR_HD inline float fsin(float x) { return sinf(x); }
+FBR_HD inline float fcos(float x) { return cosf(x); }
 
 // findRotation (:494-526)
 FBR_HD inline void find_rotation(const fbr_deskew_table& T, double pointTime, float* rx, float* ry, float* rz) {

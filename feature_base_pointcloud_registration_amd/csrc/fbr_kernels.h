@@ -74,6 +74,9 @@ struct VgArgs {
 };
 constexpr int64_t kVgLdsCap = 4096;  // segments up to this size sort entirely in LDS
 void launch_voxel_grid(hipStream_t s, const VgArgs& a);
+// One large cloud on the whole device (rocprim stable radix sort); *d_nout gets the voxel count.
+constexpr int64_t kVgLargeMin = 32768;  // below this the one-workgroup kernel is faster
+int voxel_grid_large(hipStream_t s, const float4* in, int64_t n, float leaf, int morton, float4* out, int32_t* d_nout);
 
 // Per-ring surf filter reading the projected cloud + label mask directly (no candidate copy).
 struct VgRing {

@@ -20,6 +20,9 @@
 // (8-bit digits, only as many passes as the key range needs) whose ping-pong buffers live in a
 // per-segment global scratch (L2-resident at these sizes); stability inside a 256-element tile
 // comes from wave ballot peer masks.
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
 #include "fbr_common.h"
 #include "fbr_kernels.h"
 
@@ -505,6 +508,140 @@ void launch_concat(hipStream_t s, int B, int H, int W, const float4* corner_slot
                    int32_t* n_corner, float4* surf_all, int64_t caps, int32_t* n_surf) {
   hipLaunchKernelGGL(k_concat, dim3(B), dim3(256), sizeof(int32_t) * 2 * (H + 1), s, H, W, corner_slot,
                      corner_cnt, surf_ring, surf_ring_cnt, corner_all, capc, n_corner, surf_all, caps, n_surf);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Device-wide VoxelGrid of one large cloud (the start-up map filter, the keyframe local map,
+// fbr_voxel_grid): the per-segment kernel above gives a whole workgroup to a segment, which leaves
+// the chip idle for a single cloud of 10^5-10^7 points.  Same semantics (PCL box, overflow
+// fallback, key, float centroids in ascending key order); the (key, index) sort is rocprim's
+// stable LSD radix sort, so points inside a voxel are summed in index order exactly as in the
+// segmented kernel.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t f2ord(float f) {  // order-preserving float -> uint
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u); }
+
+__global__ void __launch_bounds__(256) k_vgl_minmax(const float4* __restrict__ in, int64_t n, uint32_t* mm) {
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float4 p = in[i];
+    const float v[3] = {p.x, p.y, p.z};
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {  // getMinMax3D's comparisons (NaN never replaces)
+      mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
+      mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    for (int o = 32; o > 0; o >>= 1) {
+      const float a = __shfl_xor(mn[d], o), b = __shfl_xor(mx[d], o);
+      mn[d] = (a < mn[d]) ? a : mn[d];
+      mx[d] = (mx[d] < b) ? b : mx[d];
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicMin(&mm[d], f2ord(mn[d]));
+      atomicMax(&mm[3 + d], f2ord(mx[d]));
+    }
+  }
+}
+
+struct VglState {
+  VgGrid G;
+  int32_t nvox;
+};
+
+__global__ void k_vgl_grid(const uint32_t* mm, float leaf, int morton, VglState* st) {
+  float mn[3], mx[3];
+  for (int d = 0; d < 3; ++d) {
+    mn[d] = ord2f(mm[d]);
+    mx[d] = ord2f(mm[3 + d]);
+  }
+  st->G.init(mn, mx, leaf, morton != 0);
+}
+
+__global__ void __launch_bounds__(256)
+k_vgl_keys(const float4* __restrict__ in, int64_t n, const VglState* __restrict__ st, uint32_t* keys, uint32_t* vals) {
+  const VgGrid G = st->G;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    keys[i] = G.overflow ? 0u : G.key(in[i]);
+    vals[i] = (uint32_t)i;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_vgl_heads(const uint32_t* __restrict__ keys, int64_t n, uint32_t* head) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    head[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(256)
+k_vgl_emit(const float4* __restrict__ in, int64_t n, const VglState* __restrict__ st, const uint32_t* __restrict__ keys,
+           const uint32_t* __restrict__ vals, const uint32_t* __restrict__ vox, float4* __restrict__ out,
+           int32_t* __restrict__ nout) {
+  const bool overflow = st->G.overflow;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if (overflow) {  // PCL: "Leaf size is too small" -> output = input
+      out[i] = in[i];
+      if (i == 0) *nout = (int32_t)n;
+      continue;
+    }
+    if (!(i == 0 || keys[i] != keys[i - 1])) continue;
+    const uint32_t key = keys[i];
+    float4 c = in[vals[i]];
+    int64_t j = i + 1;
+    while (j < n && keys[j] == key) {
+      const float4 p = in[vals[j]];
+      c.x += p.x;
+      c.y += p.y;
+      c.z += p.z;
+      c.w += p.w;
+      ++j;
+    }
+    const float cnt = (float)(j - i);
+    out[vox[i]] = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
+    if (j == n) *nout = (int32_t)vox[i] + 1;
+  }
+}
+
+int voxel_grid_large(hipStream_t s, const float4* in, int64_t n, float leaf, int morton, float4* out, int32_t* d_nout) {
+  if (n <= 0) return hipMemsetAsync(d_nout, 0, sizeof(int32_t), s) == hipSuccess ? FBR_OK : FBR_ERR_HIP;
+  if (n > (int64_t)INT32_MAX) return FBR_ERR_CAPACITY;
+  uint32_t *mm = nullptr, *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *vox = nullptr;
+  VglState* st = nullptr;
+  void* tmp = nullptr;
+  size_t tb_sort = 0, tb_scan = 0;
+  int rc = FBR_OK;
+  auto ok = [&](hipError_t e) {
+    if (e != hipSuccess) rc = FBR_ERR_HIP;
+    return rc == FBR_OK;
+  };
+  const size_t N = (size_t)n;
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+  if (ok(hipMallocAsync((void**)&mm, sizeof(init), s)) && ok(hipMallocAsync((void**)&st, sizeof(VglState), s)) &&
+      ok(hipMallocAsync((void**)&k0, 4 * N, s)) && ok(hipMallocAsync((void**)&k1, 4 * N, s)) &&
+      ok(hipMallocAsync((void**)&v0, 4 * N, s)) && ok(hipMallocAsync((void**)&v1, 4 * N, s)) &&
+      ok(hipMallocAsync((void**)&vox, 4 * N, s)) &&
+      ok(hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, s))) {
+    hipLaunchKernelGGL(k_vgl_minmax, dim3(grid), dim3(256), 0, s, in, n, mm);
+    hipLaunchKernelGGL(k_vgl_grid, dim3(1), dim3(1), 0, s, mm, leaf, morton, st);
+    hipLaunchKernelGGL(k_vgl_keys, dim3(grid), dim3(256), 0, s, in, n, st, k0, v0);
+    if (ok(rocprim::radix_sort_pairs(nullptr, tb_sort, k0, k1, v0, v1, N, 0, 32, s)) &&
+        ok(rocprim::exclusive_scan(nullptr, tb_scan, vox, vox, 0u, N, rocprim::plus<uint32_t>(), s)) &&
+        ok(hipMallocAsync(&tmp, std::max<size_t>(std::max(tb_sort, tb_scan), 16), s)) &&
+        ok(rocprim::radix_sort_pairs(tmp, tb_sort, k0, k1, v0, v1, N, 0, 32, s))) {
+      hipLaunchKernelGGL(k_vgl_heads, dim3(grid), dim3(256), 0, s, k1, n, vox);
+      if (ok(rocprim::exclusive_scan(tmp, tb_scan, vox, vox, 0u, N, rocprim::plus<uint32_t>(), s)))
+        hipLaunchKernelGGL(k_vgl_emit, dim3(grid), dim3(256), 0, s, in, n, st, k1, v1, vox, out, d_nout);
+    }
+  }
+  for (void* p : {(void*)mm, (void*)st, (void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)vox, tmp})
+    if (p) (void)hipFreeAsync(p, s);
+  return rc;
 }
 
 }  // namespace fbr

@@ -342,3 +342,34 @@ def test_c5_dense_scan_matches_oracle():
     assert sg["n_corner_map"] + sg["n_surf_map"] > 5000000
     assert_pose_close(pg, po)
     assert np.abs(pg[3:] - gt[3:]).max() < 0.05
+
+
+def test_voxel_grid_large_cloud_kernel():
+    """Device-wide VoxelGrid (single clouds >= 32768 points: map start-up filter, keyframe map)
+    against the oracle, and bit-identical to the one-workgroup kernel on the same input (run in a
+    child process with FBR_VG_LARGE_MIN raised)."""
+    import subprocess
+    import sys
+    rng = np.random.default_rng(12)
+    n = 300000
+    pts = np.zeros(n, POINT_XYZI)
+    pts["x"], pts["y"] = rng.uniform(-40, 40, n), rng.uniform(-40, 40, n)
+    pts["z"] = rng.normal(0, 0.3, n) + (rng.random(n) < 0.2) * rng.uniform(0, 8, n)
+    pts["intensity"] = rng.uniform(0, 255, n)
+    with api.Context(default_params(16, 900)) as ctx:
+        a = ctx.voxel_grid(pts, 0.2)
+    b = O.voxel_grid(pts, 0.2)
+    assert len(a) == len(b)
+    A, Bv = a.view(np.float32).reshape(-1, 4), b.view(np.float32).reshape(-1, 4)
+    assert np.abs(A[:, :3] - Bv[:, :3]).max() <= 1e-5
+    assert np.array_equal(np.floor(A[:, :3] * np.float32(5.0)), np.floor(Bv[:, :3] * np.float32(5.0)))
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_vg_large_in.npy")
+    np.save(path, pts)
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api; "
+            "from feature_base_pointcloud_registration_amd.fbr_types import default_params; "
+            "c = api.Context(default_params(16, 900)); o = c.voxel_grid(np.load(%r), 0.2); "
+            "sys.stdout.buffer.write(o.tobytes())" % (REPO, path))
+    env = dict(os.environ, FBR_VG_LARGE_MIN=str(10 ** 9))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout == a.tobytes()
