@@ -514,6 +514,15 @@ int register_prepare(fbr_ctx* c, const Sub& sb, bool trace) {
   return FBR_OK;
 }
 
+// Workgroups of the per-iteration GN kernels (each loops over the work items; FBR_GN_GRID overrides).
+int gn_grid_cap() {
+  static const int v = [] {
+    const char* e = std::getenv("FBR_GN_GRID");
+    return e ? std::max(1, std::atoi(e)) : 8192;
+  }();
+  return v;
+}
+
 // The Gauss-Newton iterations of one or two sub-batches.  Iterations run on the device without
 // host round trips; for each sub-batch the host stays kLag iterations ahead and stops enqueueing
 // once its k_gn_solve reports that no job is active (flags in host-mapped memory).
@@ -551,7 +560,7 @@ int register_iterate(fbr_ctx* c, const Sub* subs, int nsub, bool trace) {
           continue;
         }
       }
-      const int grid = std::max(1, std::min(a[k].max_items, 2048));
+      const int grid = std::max(1, std::min(a[k].max_items, gn_grid_cap()));
       TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a[k], grid, it));
       TIMED_ON(c, sb.st, "gn_residual", launch_gn_residual(sb.st, a[k], grid));
       TIMED_ON(c, sb.st, "gn_solve", launch_gn_solve(sb.st, a[k], it, gen));

@@ -191,29 +191,34 @@ __global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax
     affine_inverse(rot_rpy(rx, ry, rz), Ls, ts);
   }
   int base = off;
-  // two 64-column chunks per step: both chunks' owner loads and point gathers are in flight together
-  for (int c0 = 0; c0 < W; c0 += 128) {
-    const int ca = c0 + lane, cb = c0 + 64 + lane;
-    const int32_t oa = ca < W ? O[ca] : kEmptyOwner, ob = cb < W ? O[cb] : kEmptyOwner;
-    const bool va = oa != kEmptyOwner, vb = ob != kEmptyOwner;
-    const uint64_t ma = __ballot(va), mb = __ballot(vb);
-    fbr_point_xyzirt qa{}, qb{};
-    if (va) qa = P[oa];
-    if (vb) qb = P[ob];
-    if (va) {
-      const int dst = base + __popcll(ma & ((1ull << lane) - 1ull));
-      C[dst] = dsk ? deskew_point(qa, *DT, Ls, ts) : make_float4(qa.x, qa.y, qa.z, qa.intensity);
-      CI[dst] = ca;
-      R[dst] = sqrt_rn(qa.x * qa.x + qa.y * qa.y + qa.z * qa.z);
+  // kCC 64-column chunks per step: all their owner loads, then all their point gathers, are in
+  // flight together (the gather depends on the owner load)
+  constexpr int kCC = 4;
+  for (int c0 = 0; c0 < W; c0 += 64 * kCC) {
+    int32_t ow[kCC];
+    uint64_t mk[kCC];
+    fbr_point_xyzirt q[kCC];
+#pragma unroll
+    for (int k = 0; k < kCC; ++k) {
+      const int cc = c0 + 64 * k + lane;
+      ow[k] = cc < W ? O[cc] : kEmptyOwner;
     }
-    base += __popcll(ma);
-    if (vb) {
-      const int dst = base + __popcll(mb & ((1ull << lane) - 1ull));
-      C[dst] = dsk ? deskew_point(qb, *DT, Ls, ts) : make_float4(qb.x, qb.y, qb.z, qb.intensity);
-      CI[dst] = cb;
-      R[dst] = sqrt_rn(qb.x * qb.x + qb.y * qb.y + qb.z * qb.z);
+#pragma unroll
+    for (int k = 0; k < kCC; ++k) {
+      mk[k] = __ballot(ow[k] != kEmptyOwner);
+      if (ow[k] != kEmptyOwner) q[k] = P[ow[k]];
     }
-    base += __popcll(mb);
+#pragma unroll
+    for (int k = 0; k < kCC; ++k) {
+      if (ow[k] != kEmptyOwner) {
+        const int dst = base + __popcll(mk[k] & ((1ull << lane) - 1ull));
+        const fbr_point_xyzirt& qq = q[k];
+        C[dst] = dsk ? deskew_point(qq, *DT, Ls, ts) : make_float4(qq.x, qq.y, qq.z, qq.intensity);
+        CI[dst] = c0 + 64 * k + lane;
+        R[dst] = sqrt_rn(qq.x * qq.x + qq.y * qq.y + qq.z * qq.z);
+      }
+      base += __popcll(mk[k]);
+    }
   }
 }
 
