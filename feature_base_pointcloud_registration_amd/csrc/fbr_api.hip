@@ -208,23 +208,39 @@ int check_params(const fbr_params* p) {
 // ---------------------------------------------------------------------------------------------
 // map grid (built once per fbr_set_map; see k_register.hip for why this replaces the KD-trees)
 // ---------------------------------------------------------------------------------------------
+// kNN grid cell sizes (powers of two, so cell coordinates and edges are exact): 1 m along y and
+// z, 0.25 m along x by default (FBR_KNN_CELL / FBR_KNN_CELL_X override; both maps share them).
+void grid_cell_sizes(float* inv_yz, float* inv_x) {
+  auto pick = [](const char* name, float def, float lo, float hi) {
+    float inv = def;
+    if (const char* e = std::getenv(name)) {
+      const float cell = std::strtof(e, nullptr);
+      if (cell > 0.0f) inv = std::min(hi, std::max(lo, std::exp2(-std::round(std::log2(cell)))));
+    }
+    return inv;
+  };
+  *inv_yz = pick("FBR_KNN_CELL", 1.0f, 0.5f, 4.0f);  // 2 m .. 0.25 m
+  *inv_x = pick("FBR_KNN_CELL_X", 4.0f, 0.5f, 8.0f);  // 2 m .. 0.125 m
+}
+
+// Host grid over host points (the start-up map): counting sort by cell, index order kept inside a
+// cell; `max` caps both inverse cell sizes (the second map follows the first one's cells).
 int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pts, int32_t** d_cs, GridDesc* g,
-               float max_inv) {
+               const GridDesc* max) {
   if (*d_pts) (void)hipFree(*d_pts);
   if (*d_cs) (void)hipFree(*d_cs);
   *d_pts = nullptr;
   *d_cs = nullptr;
   const int64_t n = (int64_t)pts.size();
-  // Power-of-two cell (floor(p * inv) is exact).  0.5 m by default: with the kNN's lower-bound
-  // pruning the visited volume tracks the 5th-neighbour ball; FBR_KNN_CELL overrides (tuning).
-  float inv = 2.0f;
-  if (const char* e = std::getenv("FBR_KNN_CELL")) {
-    const float cell = std::strtof(e, nullptr);
-    if (cell > 0.0f) inv = std::min(4.0f, std::exp2(-std::round(std::log2(cell))));  // >= 0.25 m (R <= 4)
+  float inv, invx;
+  grid_cell_sizes(&inv, &invx);
+  if (max) {
+    inv = std::min(inv, max->inv_cell);
+    invx = std::min(invx, max->inv_x);
   }
-  inv = std::min(inv, max_inv);
   int64_t lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0}, dims[3] = {1, 1, 1};
   for (int attempt = 0; attempt < 12; ++attempt) {
+    const float iv[3] = {invx, inv, inv};
     for (int d = 0; d < 3; ++d) {
       lo[d] = INT64_MAX;
       hi[d] = INT64_MIN;
@@ -232,7 +248,7 @@ int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pt
     for (const auto& p : pts) {
       const float v[3] = {p.x, p.y, p.z};
       for (int d = 0; d < 3; ++d) {
-        const int64_t cidx = (int64_t)std::floor(v[d] * inv);
+        const int64_t cidx = (int64_t)std::floor(v[d] * iv[d]);
         lo[d] = std::min(lo[d], cidx);
         hi[d] = std::max(hi[d], cidx);
       }
@@ -242,12 +258,13 @@ int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pt
     for (int d = 0; d < 3; ++d) dims[d] = hi[d] - lo[d] + 1;
     if (dims[0] * dims[1] * dims[2] <= (int64_t)1 << 26) break;
     inv *= 0.5f;
+    invx *= 0.5f;
   }
   const int64_t ncell = dims[0] * dims[1] * dims[2];
   std::vector<int32_t> cell(n), start(ncell + 1, 0);
   for (int64_t i = 0; i < n; ++i) {
     const fbr_point_xyzi& p = pts[i];
-    const int64_t cx = (int64_t)std::floor(p.x * inv) - lo[0], cy = (int64_t)std::floor(p.y * inv) - lo[1],
+    const int64_t cx = (int64_t)std::floor(p.x * invx) - lo[0], cy = (int64_t)std::floor(p.y * inv) - lo[1],
                   cz = (int64_t)std::floor(p.z * inv) - lo[2];
     cell[i] = (int32_t)((cz * dims[1] + cy) * dims[0] + cx);
     start[cell[i] + 1]++;
@@ -266,6 +283,7 @@ int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pt
   if (n) CK(hipMemcpy(*d_pts, sorted.data(), sizeof(float4) * n, hipMemcpyHostToDevice));
   CK(hipMemcpy(*d_cs, start.data(), sizeof(int32_t) * (ncell + 1), hipMemcpyHostToDevice));
   g->inv_cell = inv;
+  g->inv_x = invx;
   for (int d = 0; d < 3; ++d) {
     g->origin[d] = (float)lo[d];
     g->dims[d] = (int32_t)dims[d];
@@ -738,30 +756,32 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
 // Device grid over a device-resident map (cell size as build_grid: 0.5 m, at most max_inv, halved
 // until the dense grid has <= 2^26 cells).
 int build_grid_dev(fbr_ctx* c, const float4* d_src, int64_t n, float4** d_pts, int32_t** d_cs, GridDesc* g,
-                   float max_inv) {
+                   const GridDesc* max) {
   if (*d_pts) (void)hipFree(*d_pts);
   if (*d_cs) (void)hipFree(*d_cs);
   *d_pts = nullptr;
   *d_cs = nullptr;
   if (!c->d_bounds && dalloc(&c->d_bounds, 6)) return FBR_ERR_HIP;
-  float inv = 2.0f;
-  if (const char* e = std::getenv("FBR_KNN_CELL")) {
-    const float cell = std::strtof(e, nullptr);
-    if (cell > 0.0f) inv = std::min(4.0f, std::exp2(-std::round(std::log2(cell))));
+  float inv, invx;
+  grid_cell_sizes(&inv, &invx);
+  if (max) {
+    inv = std::min(inv, max->inv_cell);
+    invx = std::min(invx, max->inv_x);
   }
-  inv = std::min(inv, max_inv);
   int64_t dims[3] = {1, 1, 1};
   int b[6] = {0, 0, 0, 0, 0, 0};
   for (int attempt = 0; attempt < 12; ++attempt) {
-    const int rc = grid_bounds_device(c->stream, d_src, n, inv, c->d_bounds, b);
+    const int rc = grid_bounds_device(c->stream, d_src, n, invx, inv, c->d_bounds, b);
     if (rc) return rc;
     if (n == 0)
       for (int d = 0; d < 6; ++d) b[d] = 0;
     for (int d = 0; d < 3; ++d) dims[d] = (int64_t)b[3 + d] - b[d] + 1;
     if (dims[0] * dims[1] * dims[2] <= (int64_t)1 << 26) break;
     inv *= 0.5f;
+    invx *= 0.5f;
   }
   g->inv_cell = inv;
+  g->inv_x = invx;
   for (int d = 0; d < 3; ++d) {
     g->origin[d] = (float)b[d];
     g->dims[d] = (int32_t)dims[d];
@@ -948,10 +968,10 @@ int fbr_set_map(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corner, cons
   int rc = voxel_grid_once(c, corner, n_corner, c->P.mapping_corner_leaf_size, c->map_c_host);
   if (!rc) rc = voxel_grid_once(c, surf, n_surf, c->P.mapping_surf_leaf_size, c->map_s_host);
   // both grids share one (power-of-two) cell size: the kNN kernel is specialised on it
-  if (!rc) rc = build_grid(c, c->map_c_host, &c->d_map_c, &c->d_cs_c, &c->gc, 4.0f);
-  if (!rc) rc = build_grid(c, c->map_s_host, &c->d_map_s, &c->d_cs_s, &c->gs, c->gc.inv_cell);
-  if (!rc && c->gs.inv_cell < c->gc.inv_cell)
-    rc = build_grid(c, c->map_c_host, &c->d_map_c, &c->d_cs_c, &c->gc, c->gs.inv_cell);
+  if (!rc) rc = build_grid(c, c->map_c_host, &c->d_map_c, &c->d_cs_c, &c->gc, nullptr);
+  if (!rc) rc = build_grid(c, c->map_s_host, &c->d_map_s, &c->d_cs_s, &c->gs, &c->gc);
+  if (!rc && (c->gs.inv_cell < c->gc.inv_cell || c->gs.inv_x < c->gc.inv_x))
+    rc = build_grid(c, c->map_c_host, &c->d_map_c, &c->d_cs_c, &c->gc, &c->gs);
   c->has_map = rc == FBR_OK;
   return rc;
 }
@@ -1536,10 +1556,10 @@ int fbr_extract_surrounding_keyframes(fbr_ctx* c, double stamp, const fbr_keyfra
   rc = voxel_grid_dev(c, c->d_kraw_c, tot_c, c->P.mapping_corner_leaf_size, c->d_kds_c, &c->kds_c_n);
   if (!rc) rc = voxel_grid_dev(c, c->d_kraw_s, tot_s, c->P.mapping_surf_leaf_size, c->d_kds_s, &c->kds_s_n);
   // the kNN grids (both maps share one cell size, as in fbr_set_map)
-  if (!rc) rc = build_grid_dev(c, c->d_kds_c, c->kds_c_n, &c->d_map_c, &c->d_cs_c, &c->gc, 4.0f);
-  if (!rc) rc = build_grid_dev(c, c->d_kds_s, c->kds_s_n, &c->d_map_s, &c->d_cs_s, &c->gs, c->gc.inv_cell);
-  if (!rc && c->gs.inv_cell < c->gc.inv_cell)
-    rc = build_grid_dev(c, c->d_kds_c, c->kds_c_n, &c->d_map_c, &c->d_cs_c, &c->gc, c->gs.inv_cell);
+  if (!rc) rc = build_grid_dev(c, c->d_kds_c, c->kds_c_n, &c->d_map_c, &c->d_cs_c, &c->gc, nullptr);
+  if (!rc) rc = build_grid_dev(c, c->d_kds_s, c->kds_s_n, &c->d_map_s, &c->d_cs_s, &c->gs, &c->gc);
+  if (!rc && (c->gs.inv_cell < c->gc.inv_cell || c->gs.inv_x < c->gc.inv_x))
+    rc = build_grid_dev(c, c->d_kds_c, c->kds_c_n, &c->d_map_c, &c->d_cs_c, &c->gc, &c->gs);
   c->has_map = rc == FBR_OK;
   c->map_nocrop = rc == FBR_OK;
   c->crop_cached = false;

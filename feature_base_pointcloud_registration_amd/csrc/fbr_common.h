@@ -67,9 +67,11 @@ struct GnState {
   int32_t pad[2];
 };
 
-struct GridDesc {        // dense 3D grid over a map
-  float origin[3];       // world coordinate of cell (0,0,0) corner
-  float inv_cell;
+struct GridDesc {        // dense 3D grid over a map (cell indices, not metres, in origin)
+  float origin[3];       // cell index of cell (0,0,0) per axis
+  float inv_cell;        // 1 / cell size along y and z (a power of two)
+  float inv_x;           // 1 / cell size along x (a power of two): cells may be shorter in x, the
+                         // axis a grid row runs along, so rows scanned stay few and short
   int32_t dims[3];
   int32_t n_cells;
   int64_t n_points;

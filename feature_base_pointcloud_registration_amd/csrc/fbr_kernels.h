@@ -154,7 +154,8 @@ struct KfSeg {               // one selected keyframe cloud: pool[src .. src+cou
 void launch_kf_transform(hipStream_t s, const float4* pool, const KfSeg* segs, int nseg, int64_t max_count, float4* out);
 // Device kNN grid build: cell bounds of pts at 1/inv cells (h_bounds = lo xyz, hi xyz), then the
 // per-cell counts, exclusive scan into d_cs [n_cells + 1] and the scatter into d_out.
-int grid_bounds_device(hipStream_t s, const float4* pts, int64_t n, float inv, int* d_bounds, int h_bounds[6]);
+int grid_bounds_device(hipStream_t s, const float4* pts, int64_t n, float invx, float inv, int* d_bounds,
+                       int h_bounds[6]);
 int grid_fill_device(hipStream_t s, const float4* pts, int64_t n, const GridDesc& g, int32_t* d_cs, float4* d_out);
 
 }  // namespace fbr

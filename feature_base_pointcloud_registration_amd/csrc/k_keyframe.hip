@@ -51,11 +51,12 @@ void launch_kf_transform(hipStream_t s, const float4* pool, const KfSeg* segs, i
 }
 
 // ---- device grid build ----
-__global__ void __launch_bounds__(256) k_grid_bounds(const float4* __restrict__ pts, int64_t n, float inv, int* bounds) {
+__global__ void __launch_bounds__(256)
+k_grid_bounds(const float4* __restrict__ pts, int64_t n, float invx, float inv, int* bounds) {
   int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float4 p = pts[i];
-    const int c[3] = {(int)floorf(p.x * inv), (int)floorf(p.y * inv), (int)floorf(p.z * inv)};
+    const int c[3] = {(int)floorf(p.x * invx), (int)floorf(p.y * inv), (int)floorf(p.z * inv)};
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
       lo[d] = min(lo[d], c[d]);
@@ -76,7 +77,7 @@ __global__ void __launch_bounds__(256) k_grid_bounds(const float4* __restrict__ 
 }
 
 __device__ __forceinline__ int grid_cell(const float4& p, const GridDesc& g) {
-  const int cx = (int)floorf(p.x * g.inv_cell) - (int)g.origin[0];
+  const int cx = (int)floorf(p.x * g.inv_x) - (int)g.origin[0];
   const int cy = (int)floorf(p.y * g.inv_cell) - (int)g.origin[1];
   const int cz = (int)floorf(p.z * g.inv_cell) - (int)g.origin[2];
   return (cz * g.dims[1] + cy) * g.dims[0] + cx;
@@ -96,12 +97,13 @@ k_grid_scatter(const float4* __restrict__ pts, int64_t n, GridDesc g, int32_t* f
   }
 }
 
-int grid_bounds_device(hipStream_t s, const float4* pts, int64_t n, float inv, int* d_bounds, int h_bounds[6]) {
+int grid_bounds_device(hipStream_t s, const float4* pts, int64_t n, float invx, float inv, int* d_bounds,
+                       int h_bounds[6]) {
   const int init[6] = {INT_MAX, INT_MAX, INT_MAX, INT_MIN, INT_MIN, INT_MIN};
   if (hipMemcpyAsync(d_bounds, init, sizeof(init), hipMemcpyHostToDevice, s) != hipSuccess) return FBR_ERR_HIP;
   if (n > 0) {
     const int grid = (int)std::min<int64_t>((n + 255) / 256, 2048);
-    hipLaunchKernelGGL(k_grid_bounds, dim3(grid), dim3(256), 0, s, pts, n, inv, d_bounds);
+    hipLaunchKernelGGL(k_grid_bounds, dim3(grid), dim3(256), 0, s, pts, n, invx, inv, d_bounds);
   }
   if (hipMemcpyAsync(h_bounds, d_bounds, sizeof(int) * 6, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)

@@ -111,22 +111,22 @@ __device__ unsigned long long fbr_knn_stats[8];
 // distance to the previous iteration's 5 neighbours, 5 distinct candidates of the same crop box):
 // cells whose lower bound exceeds it cannot hold any of the 5 nearest, ties included, so they are
 // pruned from the start instead of only once 5 points have been inserted.
-template <int R>
+template <int R, int RX>
 __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
                           float bound, Knn5& r, unsigned* ks) {
-  constexpr int K = 2 * R + 1;
+  constexpr int K = 2 * R + 1;  // rows per side in y and z; RX = cells per side along x
 #pragma unroll
   for (int t = 0; t < 5; ++t) { r.d[t] = __int_as_float(0x7f800000); r.id[t] = 0x7fffffff; r.pos[t] = -1; }
-  const float inv = m.g.inv_cell, c = 1.0f / inv;
-  const float sx = qx * inv, sy = qy * inv, sz = qz * inv;
+  const float inv = m.g.inv_cell, c = 1.0f / inv, invx = m.g.inv_x, cxs = 1.0f / invx;
+  const float sx = qx * invx, sy = qy * inv, sz = qz * inv;
   const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
   if (!(fabsf(fx) < 1e7f && fabsf(fy) < 1e7f && fabsf(fz) < 1e7f)) return;
   const int cx = (int)fx - (int)m.g.origin[0], cy = (int)fy - (int)m.g.origin[1], cz = (int)fz - (int)m.g.origin[2];
   const int X = m.g.dims[0], Y = m.g.dims[1], Z = m.g.dims[2];
-  if (cx < -R || cy < -R || cz < -R || cx >= X + R || cy >= Y + R || cz >= Z + R) return;
+  if (cx < -RX || cy < -R || cz < -R || cx >= X + RX || cy >= Y + R || cz >= Z + R) return;
   const int sgy = (sy - fy) >= 0.5f ? 1 : -1, sgz = (sz - fz) >= 0.5f ? 1 : -1;
   // squared per-axis lower bounds: y/z by visit rank, x by offset (negative / positive side)
-  float ly2[K], lz2[K], lxm2[R + 1], lxp2[R + 1];
+  float ly2[K], lz2[K], lxm2[RX + 1], lxp2[RX + 1];
   int oyk[K], ozk[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -137,12 +137,12 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
     lz2[k] = lz * lz;
   }
 #pragma unroll
-  for (int o = 1; o <= R; ++o) {
-    const float a = axis_lb(qx, fx, -o, c), b = axis_lb(qx, fx, o, c);
+  for (int o = 1; o <= RX; ++o) {
+    const float a = axis_lb(qx, fx, -o, cxs), b = axis_lb(qx, fx, o, cxs);
     lxm2[o] = a * a;
     lxp2[o] = b * b;
   }
-  const float xlo = (fx - (float)R) * c, xhi = (fx + (float)(R + 1)) * c;  // row x extent (max)
+  const float xlo = (fx - (float)RX) * cxs, xhi = (fx + (float)(RX + 1)) * cxs;  // row x extent (max)
   const bool xin = xlo >= bmin[0] && xhi <= bmax[0];
 #pragma unroll
   for (int ksum = 0; ksum <= 2 * (K - 1); ++ksum) {
@@ -160,7 +160,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       int xa = 0, xb = 0;
       bool go_a = true, go_b = true;
 #pragma unroll
-      for (int o = 1; o <= R; ++o) {
+      for (int o = 1; o <= RX; ++o) {
         float ta = 0.0f, tb = 0.0f;
         ta += lxm2[o]; ta += ly2[ky]; ta += lz2[kz];
         tb += lxp2[o]; tb += ly2[ky]; tb += lz2[kz];
@@ -311,7 +311,7 @@ __global__ void k_gn_init(GnArgs a) {
 
 // kNN pass: one lane per query, writes the 5 neighbour positions (slot 0 = -1: no correspondence).
 // R = grid cells per side covering radius 1 (both map grids share one cell size).
-template <int R>
+template <int R, int RX>
 __global__ void __launch_bounds__(kResThreads)
 k_gn_knn(GnArgs a, int use_prev) {
   const int tid = threadIdx.x;
@@ -347,7 +347,7 @@ k_gn_knn(GnArgs a, int use_prev) {
     }
     Knn5 nn;
     unsigned ks[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-    knn5_grid<R>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
+    knn5_grid<R, RX>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
     const bool ok = nn.pos[4] >= 0 && nn.d[4] < 1.0f;
 #ifdef FBR_KNN_STATS
     ks[5] = ok;
@@ -599,12 +599,21 @@ void launch_export_records(hipStream_t s, int B, const float* pose_out, const fb
 }
 
 void launch_gn_init(hipStream_t s, const GnArgs& a) { hipLaunchKernelGGL(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
+template <int R>
+void launch_gn_knn_r(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
+  const float invx = a.mc.g.inv_x;  // == a.ms.g.inv_x
+  if (invx > 4.0f) hipLaunchKernelGGL((k_gn_knn<R, 8>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
+  else if (invx > 2.0f) hipLaunchKernelGGL((k_gn_knn<R, 4>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
+  else if (invx > 1.0f) hipLaunchKernelGGL((k_gn_knn<R, 2>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
+  else hipLaunchKernelGGL((k_gn_knn<R, 1>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
+}
+
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter) {
-  const float inv = a.mc.g.inv_cell;  // == a.ms.g.inv_cell (fbr_set_map)
+  const float inv = a.mc.g.inv_cell;  // == a.ms.g.inv_cell (fbr_set_map): y / z cells
   const int use_prev = iter > 0;      // nbr holds this launch's previous iteration
-  if (inv > 2.0f) hipLaunchKernelGGL((k_gn_knn<4>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.25 m
-  else if (inv > 1.0f) hipLaunchKernelGGL((k_gn_knn<2>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
-  else hipLaunchKernelGGL((k_gn_knn<1>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
+  if (inv > 2.0f) launch_gn_knn_r<4>(s, a, grid, use_prev);       // 0.25 m
+  else if (inv > 1.0f) launch_gn_knn_r<2>(s, a, grid, use_prev);  // 0.5 m
+  else launch_gn_knn_r<1>(s, a, grid, use_prev);                  // >= 1 m
 }
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
   hipLaunchKernelGGL(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);
