@@ -208,9 +208,12 @@ int check_params(const fbr_params* p) {
 // ---------------------------------------------------------------------------------------------
 // map grid (built once per fbr_set_map; see k_register.hip for why this replaces the KD-trees)
 // ---------------------------------------------------------------------------------------------
-// kNN grid cell sizes (powers of two, so cell coordinates and edges are exact): 1 m along y and
-// z, 0.25 m along x by default (FBR_KNN_CELL / FBR_KNN_CELL_X override; both maps share them).
-void grid_cell_sizes(float* inv_yz, float* inv_x) {
+// kNN grid cell sizes (powers of two, so cell coordinates and edges are exact), chosen from the
+// map density the mapping leaf implies (one point per leaf voxel at most): 1 m along y and z and
+// 0.25 m along x for surf leaves >= 0.3 m (the 0.4 m default), 0.5 m / 0.125 m for denser maps
+// (measured).  FBR_KNN_CELL / FBR_KNN_CELL_X override; both maps share them.
+void grid_cell_sizes(const fbr_params& P, float* inv_yz, float* inv_x) {
+  const bool sparse = P.mapping_surf_leaf_size >= 0.3f;
   auto pick = [](const char* name, float def, float lo, float hi) {
     float inv = def;
     if (const char* e = std::getenv(name)) {
@@ -219,8 +222,8 @@ void grid_cell_sizes(float* inv_yz, float* inv_x) {
     }
     return inv;
   };
-  *inv_yz = pick("FBR_KNN_CELL", 1.0f, 0.5f, 4.0f);  // 2 m .. 0.25 m
-  *inv_x = pick("FBR_KNN_CELL_X", 4.0f, 0.5f, 8.0f);  // 2 m .. 0.125 m
+  *inv_yz = pick("FBR_KNN_CELL", sparse ? 1.0f : 2.0f, 0.5f, 4.0f);  // 2 m .. 0.25 m
+  *inv_x = pick("FBR_KNN_CELL_X", sparse ? 4.0f : 8.0f, 0.5f, 8.0f);  // 2 m .. 0.125 m
 }
 
 // Host grid over host points (the start-up map): counting sort by cell, index order kept inside a
@@ -233,7 +236,7 @@ int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pt
   *d_cs = nullptr;
   const int64_t n = (int64_t)pts.size();
   float inv, invx;
-  grid_cell_sizes(&inv, &invx);
+  grid_cell_sizes(c->P, &inv, &invx);
   if (max) {
     inv = std::min(inv, max->inv_cell);
     invx = std::min(invx, max->inv_x);
@@ -435,6 +438,8 @@ int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode) {
   v.out = c->d_surf_ring + j0 * HW;
   v.stride_out = c->W;
   v.cnt_out = c->d_surf_ring_cnt + j0 * H;
+  v.dbg = std::getenv("FBR_VR_DBG") ? std::atoi(std::getenv("FBR_VR_DBG")) : 0;
+  v.stamps = a.stamps;
   TIMED_ON(c, sb.st, "voxel_ring", launch_voxel_ring(sb.st, v));
   TIMED_ON(c, sb.st, "concat",
            launch_concat(sb.st, sb.B, c->H, c->W, a.corner_slot, a.corner_cnt, v.out, v.cnt_out,
@@ -753,7 +758,7 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
   return rc;
 }
 
-// Device grid over a device-resident map (cell size as build_grid: 0.5 m, at most max_inv, halved
+// Device grid over a device-resident map (cell sizes as build_grid, at most max's, halved
 // until the dense grid has <= 2^26 cells).
 int build_grid_dev(fbr_ctx* c, const float4* d_src, int64_t n, float4** d_pts, int32_t** d_cs, GridDesc* g,
                    const GridDesc* max) {
@@ -763,7 +768,7 @@ int build_grid_dev(fbr_ctx* c, const float4* d_src, int64_t n, float4** d_pts, i
   *d_cs = nullptr;
   if (!c->d_bounds && dalloc(&c->d_bounds, 6)) return FBR_ERR_HIP;
   float inv, invx;
-  grid_cell_sizes(&inv, &invx);
+  grid_cell_sizes(c->P, &inv, &invx);
   if (max) {
     inv = std::min(inv, max->inv_cell);
     invx = std::min(invx, max->inv_x);

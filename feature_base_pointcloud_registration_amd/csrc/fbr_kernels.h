@@ -91,6 +91,8 @@ struct VgRing {
   float4* out;               // [B*H][stride_out]
   int64_t stride_out;
   int32_t* cnt_out;          // [B*H]
+  int dbg;                   // diagnostic phase cut (FBR_VR_DBG; 0 = full kernel)
+  unsigned long long* stamps;  // diagnostic builds (FBR_VR_STAMPS) only: [B*H][12]
 };
 void launch_voxel_ring(hipStream_t s, const VgRing& a);
 

@@ -47,39 +47,6 @@ __device__ __forceinline__ uint32_t spread3_10(uint32_t v) {  // 10 bits -> ever
   return v;
 }
 
-// Exclusive scan of nb (<= 512) LDS counters in place by a T-thread workgroup; returns nothing,
-// `wsum` is [T/64] scratch.  Must be called by all threads.
-template <int T>
-__device__ void block_exclusive_scan(uint32_t* arr, int nb, uint32_t* wsum) {
-  constexpr int PER = (512 + T - 1) / T;  // bins per thread (consecutive)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  uint32_t v[PER], loc = 0;
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int b = tid * PER + k;
-    v[k] = b < nb ? arr[b] : 0u;
-    loc += v[k];
-  }
-  uint32_t inc = loc;  // inclusive wave scan of per-thread sums
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o);
-    if (lane >= o) inc += y;
-  }
-  if (lane == 63) wsum[w] = inc;
-  __syncthreads();
-  uint32_t base = 0;
-  for (int ww = 0; ww < w; ++ww) base += wsum[ww];
-  uint32_t run = base + inc - loc;
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int b = tid * PER + k;
-    if (b < nb) arr[b] = run;
-    run += v[k];
-  }
-  __syncthreads();
-}
-
 // ---- shared pieces of the two VoxelGrid front ends ----
 
 // Block-wide float min / max (getMinMax3D) of per-thread partials; mm = [NW][6] LDS.
@@ -160,42 +127,55 @@ struct VgGrid {
 // ascending key order: out[v] = mean of in[vals of the run].  Returns the voxel count (all threads).
 template <int T, typename V, int MAXD = 9>
 __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, uint32_t* hist, uint32_t* wsum,
-                            const float4* in, float4* out) {
+                            const float4* in, float4* out, int dbg = 0, unsigned long long* t_sorted = nullptr) {
   constexpr int NW = T / 64, NB = 1 << MAXD;  // digits of <= MAXD bits; hist rows of NB counters
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int passes = (nbits + MAXD - 1) / MAXD;
-  const int dbits = (nbits + passes - 1) / passes;
+  const int passes = dbg == 1 ? 0 : (nbits + MAXD - 1) / MAXD;
+  const int dbits = passes > 0 ? (nbits + passes - 1) / passes : MAXD;
   const int nbins = 1 << dbits;
   const int chunk = (((n + NW - 1) / NW) + 63) & ~63;
   const int c0 = min(n, w * chunk), c1 = min(n, c0 + chunk);
-  uint32_t* hw = hist + w * NB;
+  // Counters live at hist[w * NB + d] (lanes of one wave hit distinct banks); the exclusive scan
+  // runs over them in digit-major, wave-minor order, which gives every (digit, wave) its output
+  // base (waves in chunk order -> stable)
+  constexpr int PER = NB * NW / T;
   int cur = 0;
   for (int pass = 0; pass < passes; ++pass) {
     const int shift = dbits * pass;
     const uint32_t dmask = (uint32_t)nbins - 1u;
+    const int tot = nbins * NW;
     const uint32_t* kin = kb[cur];
     const V* vin = vb[cur];
     uint32_t* kout = kb[cur ^ 1];
     V* vout = vb[cur ^ 1];
-    for (int b = tid; b < NW * NB; b += T) hist[b] = 0u;
+    for (int b = tid; b < tot; b += T) hist[(b % NW) * NB + b / NW] = 0u;
     __syncthreads();
-    for (int i = c0 + lane; i < c1; i += 64) atomicAdd(&hw[(kin[i] >> shift) & dmask], 1u);
+    for (int i = c0 + lane; i < c1; i += 64) atomicAdd(&hist[w * NB + ((kin[i] >> shift) & dmask)], 1u);
     __syncthreads();
-    // digit-major, wave-minor exclusive offsets: per digit over waves, then over digits
-    for (int d = tid; d < nbins; d += T) {
-      uint32_t run = 0;
-      for (int ww = 0; ww < NW; ++ww) {
-        const uint32_t t = hist[ww * NB + d];
-        hist[ww * NB + d] = run;
-        run += t;
+    {
+      uint32_t v[PER], loc = 0;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int idx = tid * PER + k;
+        v[k] = idx < tot ? hist[(idx % NW) * NB + idx / NW] : 0u;
+        loc += v[k];
       }
-      hist[NW * NB + d] = run;  // digit totals: the extra row NW
-    }
-    __syncthreads();
-    block_exclusive_scan<T>(hist + NW * NB, nbins, wsum);
-    for (int d = tid; d < nbins; d += T) {
-      const uint32_t base = hist[NW * NB + d];
-      for (int ww = 0; ww < NW; ++ww) hist[ww * NB + d] += base;
+      uint32_t inc = loc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+      }
+      if (lane == 63) wsum[w] = inc;
+      __syncthreads();
+      uint32_t run = inc - loc;
+      for (int ww = 0; ww < w; ++ww) run += wsum[ww];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int idx = tid * PER + k;
+        if (idx < tot) hist[(idx % NW) * NB + idx / NW] = run;
+        run += v[k];
+      }
     }
     __syncthreads();
     for (int i0 = c0; i0 < c1; i0 += 64) {
@@ -209,13 +189,14 @@ __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, u
         peers &= ((d >> b) & 1u) ? bal : ~bal;
       }
       const int rank = __popcll(peers & ((1ull << lane) - 1ull));
-      const uint32_t base = valid ? hw[d] : 0u;
+      uint32_t* hc = &hist[w * NB + d];
+      const uint32_t base = valid ? *hc : 0u;
       if (valid) {
         kout[base + rank] = key;
         vout[base + rank] = vin[i];
       }
       __builtin_amdgcn_wave_barrier();
-      if (valid && rank == 0) hw[d] = base + (uint32_t)__popcll(peers);
+      if (valid && rank == 0) *hc = base + (uint32_t)__popcll(peers);
       __builtin_amdgcn_wave_barrier();
     }
     cur ^= 1;
@@ -223,6 +204,8 @@ __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, u
   }
   const uint32_t* ks = kb[cur];
   const V* vs = vb[cur];
+  if (t_sorted && threadIdx.x == 0) *t_sorted = __builtin_amdgcn_s_memtime();
+  if (dbg == 2) return 0;
   // ---- voxels in ascending key order: heads of equal-key runs, centroid = float sum / count ----
   int nh = 0;
   for (int i0 = c0; i0 < c1; i0 += 64) {
@@ -235,26 +218,71 @@ __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, u
   for (int ww = 0; ww < w; ++ww) pos += (int)wsum[ww];
   int total = pos;
   for (int ww = w; ww < NW; ++ww) total += (int)wsum[ww];
-  for (int i0 = c0; i0 < c1; i0 += 64) {
+  // Runs of equal keys are summed in sorted order (the serial float sum of the reference) out of a
+  // per-wave LDS stage of the current 64-step (the digit histogram is free after the sort): every
+  // lane gathers its own sorted point (one parallel gather per step), a run's first lane adds the
+  // following staged points up to the next key break (independent LDS reads, no load chain), and
+  // a run still open at the end of the step is carried into the next step by lane 0 -- past c1 if
+  // it continues into the next wave's chunk.
+  float4* stg = reinterpret_cast<float4*>(hist) + w * 64;  // NW*1 KB <= (NW+1)*NB*4 B
+  bool carry_open = false;
+  float4 carry = make_float4(0.f, 0.f, 0.f, 0.f);
+  int carry_start = 0, carry_out = 0;
+  for (int i0 = c0; i0 < c1 || carry_open; i0 += 64) {
     const int i = i0 + lane;
-    const bool head = i < c1 && (i == 0 || ks[i] != ks[i - 1]);
-    const uint64_t bal = __ballot(head);
-    if (head) {
-      const uint32_t key = ks[i];
-      float4 c = in[vs[i]];
-      int j = i + 1;
-      while (j < n && ks[j] == key) {
-        const float4 p = in[vs[j]];
-        c.x += p.x;
-        c.y += p.y;
-        c.z += p.z;
-        c.w += p.w;
-        ++j;
-      }
-      const float cnt = (float)(j - i);
-      out[pos + __popcll(bal & ((1ull << lane) - 1ull))] = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
+    const bool valid = i < n;
+    const uint32_t key = valid ? ks[i] : 0u;
+    const bool brk_i = !valid || i == 0 || ks[i - 1] != key;  // a run starts here (or no point)
+    const bool head = valid && i < c1 && brk_i;
+    const bool cont = carry_open && lane == 0;  // continues the carried run (brk_i is false)
+    const uint64_t brk = __ballot(brk_i), hb = __ballot(head);
+    const float4 p = valid ? in[vs[i]] : make_float4(0.f, 0.f, 0.f, 0.f);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    stg[lane] = p;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t after = lane == 63 ? 0ull : (brk >> (lane + 1)) << (lane + 1);
+    const int nb = after ? __ffsll((unsigned long long)after) - 1 : 64;  // next break after this lane
+    float4 c = p;
+    if (cont) {
+      c.x = carry.x + p.x;
+      c.y = carry.y + p.y;
+      c.z = carry.z + p.z;
+      c.w = carry.w + p.w;
     }
-    pos += __popcll(bal);
+    const bool starter = head || cont;
+    if (starter)
+      for (int k = lane + 1; k < nb; k += 4) {  // four staged reads in flight, adds in order
+        float4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = stg[min(k + u, 63)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (k + u < nb) {
+            c.x += q[u].x;
+            c.y += q[u].y;
+            c.z += q[u].z;
+            c.w += q[u].w;
+          }
+      }
+    const bool spills = starter && nb == 64 && i0 + 64 < n && ks[i0 + 64] == key;
+    const int start = cont ? carry_start : i;
+    const int oidx = cont ? carry_out : pos + __popcll(hb & ((1ull << lane) - 1ull));
+    if (starter && !spills) {
+      const float cnt = (float)(i0 + nb - start);
+      out[oidx] = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
+    }
+    const uint64_t sp = __ballot(spills);
+    carry_open = sp != 0ull;
+    if (carry_open) {
+      const int src = __ffsll((unsigned long long)sp) - 1;
+      carry = make_float4(__shfl(c.x, src), __shfl(c.y, src), __shfl(c.z, src), __shfl(c.w, src));
+      carry_start = __shfl(start, src);
+      carry_out = __shfl(oidx, src);
+    }
+    pos += __popcll(hb);
   }
   return total;
 }
@@ -329,11 +357,20 @@ __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
 // index 4 may be stale across scans exactly as the reference's cloudLabel[4]).  One register
 // pass feeds min/max, the keys and the compaction; the sort runs in LDS (u16 ring offsets).
 template <int T, int KPT>
-__global__ void __launch_bounds__(T) k_voxel_ring(VgRing A) {
+__global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(KPT <= 4 ? 8 : 1)))
+k_voxel_ring(VgRing A) {
   constexpr int NW = T / 64, MAXD = 8;  // 8-bit digits: 3 passes cover the <= 24-bit ring keys
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int slot = blockIdx.x, job = slot / A.H;
+#ifdef FBR_VR_STAMPS  // diagnostic build only (tools/vr_stamps.py): phase boundaries of wave 0
+  unsigned long long ts[5] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0};
+#define VR_TS(i) (ts[i] = __builtin_amdgcn_s_memtime())
+#define VR_TS_PTR (&ts[3])
+#else
+#define VR_TS(i) ((void)0)
+#define VR_TS_PTR nullptr
+#endif
   uint32_t* hist = (uint32_t*)smem;
   uint32_t* wsum = hist + (NW + 1) * (1 << MAXD);
   float* mm = (float*)(wsum + NW);
@@ -352,7 +389,6 @@ __global__ void __launch_bounds__(T) k_voxel_ring(VgRing A) {
   }
   const float4* CL = A.cloud + (int64_t)job * A.HW + s;
   const int8_t* LB = A.label + (int64_t)job * A.HW;
-  float4 pt[KPT];
   bool cd[KPT];
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
 #pragma unroll
@@ -361,10 +397,12 @@ __global__ void __launch_bounds__(T) k_voxel_ring(VgRing A) {
     bool in = false;
 #pragma unroll
     for (int j = 0; j < 6; ++j) in |= sp6[j] < ep6[j] && k >= sp6[j] && k <= ep6[j];
-    cd[r] = in && LB[k] <= 0;
-    pt[r] = cd[r] ? CL[k - s] : make_float4(0.f, 0.f, 0.f, 0.f);
+    // label and point loads issued together (one round trip; the point's line is read anyway)
+    const int8_t lab = in ? LB[k] : (int8_t)1;
+    const float4 p = in ? CL[k - s] : make_float4(0.f, 0.f, 0.f, 0.f);
+    cd[r] = lab <= 0;
     if (cd[r]) {
-      const float v[3] = {pt[r].x, pt[r].y, pt[r].z};
+      const float v[3] = {p.x, p.y, p.z};
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
         mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
@@ -392,10 +430,11 @@ __global__ void __launch_bounds__(T) k_voxel_ring(VgRing A) {
     pos[r] = n + before + __popcll(bal[r] & ((1ull << lane) - 1ull));
     n += all;
   }
-  if (n == 0) {
+  if (n == 0 || A.dbg == 3) {
     if (tid == 0) A.cnt_out[slot] = 0;
     return;
   }
+  VR_TS(1);
   VgGrid G;
   G.init(mn, mx, A.leaf, false);
   unsigned char* q = (unsigned char*)(((uintptr_t)(cnts + KPT * NW) + 15) & ~(uintptr_t)15);
@@ -408,19 +447,27 @@ __global__ void __launch_bounds__(T) k_voxel_ring(VgRing A) {
   if (G.overflow) {  // output = input, in index order
 #pragma unroll
     for (int r = 0; r < KPT; ++r)
-      if (cd[r]) out[pos[r]] = pt[r];
+      if (cd[r]) out[pos[r]] = CL[r * T + tid];
     if (tid == 0) A.cnt_out[slot] = n;
     return;
   }
 #pragma unroll
   for (int r = 0; r < KPT; ++r)
     if (cd[r]) {
-      kb[0][pos[r]] = G.key(pt[r]);
+      kb[0][pos[r]] = G.key(CL[r * T + tid]);  // re-read (L2): no point registers live across the barrier
       vb[0][pos[r]] = (uint16_t)(r * T + tid);  // offset from the ring start s
     }
   __syncthreads();
-  const int total = vg_sort_emit<T, uint16_t, MAXD>(kb, vb, n, G.nbits, hist, wsum, CL, out);
+  VR_TS(2);
+  const int total = vg_sort_emit<T, uint16_t, MAXD>(kb, vb, n, G.nbits, hist, wsum, CL, out, A.dbg, VR_TS_PTR);
   if (tid == 0) A.cnt_out[slot] = total;
+#ifdef FBR_VR_STAMPS
+  VR_TS(4);
+  if (tid == 0 && A.stamps)
+    for (int i = 0; i < 5; ++i) A.stamps[(int64_t)slot * 12 + i] = ts[i];
+#endif
+#undef VR_TS
+#undef VR_TS_PTR
 }
 
 size_t voxel_ring_lds_bytes(const VgRing& a, int threads, int kpt) {

@@ -16,8 +16,8 @@ import sys
 from collections import defaultdict
 
 NAMES = {"gn_knn": r"k_gn_knn", "gn_residual": r"k_gn_residual", "features": r"k_features",
-         "voxel": r"k_voxel_grid", "project": r"k_project\b", "extract": r"k_compact|k_rowcount",
-         "gn_solve": r"k_gn_solve"}
+         "voxel_ring": r"k_voxel_ring", "voxel_scan": r"k_voxel_grid", "concat": r"k_concat",
+         "project": r"k_project\b", "extract": r"k_compact|k_rowcount", "gn_solve": r"k_gn_solve"}
 
 
 def per_launch(path, counter):
