@@ -36,15 +36,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 # Algorithmic bytes per unit for each kernel family (DESIGN.md "Kernels and rooflines").
 def kernel_bytes(name, tot):
-    n_in, n, Q, IQ, M = tot["n_in"], tot["n"], tot["Q"], tot["IQ"], tot["M"]
+    n_in, n, Q, IQ, M, F, S = tot["n_in"], tot["n"], tot["Q"], tot["IQ"], tot["M"], tot["F"], tot["S"]
     return {
         "gn_knn": 116.0 * IQ,                 # query 16 B + the 5 neighbours found 80 B + 5 positions out 20 B
         "gn_residual": 116.0 * IQ,            # query 16 B + 5 positions 20 B + 5 neighbour gathers 80 B
         "project": 24.0 * n_in + 4.0 * n,     # raw point read + owner claim
         "extract": 4.0 * 2 * n + 28.0 * n,    # owners, owning point, xyzi+col+range write
         "features": 41.0 * n,                 # range/col/cloud read, label + candidate write
-        "voxel_ring": 64.0 * n,               # candidates + sort passes (dominated by read/write)
-        "voxel_scan": 64.0 * Q,
+        "voxel_ring": 17.0 * n + 16.0 * S,    # label + candidate point read (<= n), per-ring DS write
+        "voxel_scan": 16.0 * F + 16.0 * Q,    # corner + surf clouds read, DS queries written
     }.get(name, 0.0)
 
 
@@ -128,7 +128,7 @@ def main():
     ctx.batch_wait()
     ctx.set_profiling(False)
     prof = {k: ctx.kernel_time(k) for k in kernels}
-    modelled = [k for k in kernels if kernel_bytes(k, {"n_in": 1, "n": 1, "Q": 1, "IQ": 1, "M": 1}) > 0]
+    modelled = [k for k in kernels if kernel_bytes(k, dict.fromkeys(["n_in", "n", "Q", "IQ", "M", "F", "S"], 1.0)) > 0]
     dom = max(modelled, key=lambda k: prof[k][0])
     if dist is not None:
         import torch
@@ -171,7 +171,8 @@ def main():
     tot = dict(n_in=float(sum(len(s) for s in scans)), n=float(stats["n_points"].sum()),
                Q=float((stats["n_corner_ds"] + stats["n_surf_ds"]).sum()),
                IQ=float(((stats["n_corner_ds"] + stats["n_surf_ds"]) * stats["iterations"]).sum()),
-               M=float((stats["n_corner_map"] + stats["n_surf_map"]).sum()))
+               M=float((stats["n_corner_map"] + stats["n_surf_map"]).sum()),
+               F=float((stats["n_corner"] + stats["n_surf"]).sum()), S=float(stats["n_surf"].sum()))
     if timed[dom][1] > 0:  # live events over the timed region
         dom_ms, dom_launches, steps_measured, live = timed[dom][0], timed[dom][1], args.steps, True
     else:                  # --profile off: the profiled step

@@ -374,7 +374,7 @@ k_features(FeatArgs a) {
   S.tmask = (uint64_t*)p;            p += sizeof(uint64_t) * 16;
   S.sstack = (SortFrame*)p;          p += sizeof(SortFrame) * kSortStack;
   S.cm = (uint32_t*)p;               p += sizeof(uint32_t) * segcap;
-  S.rb = (unsigned char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+  S.rb = smem + (((p - smem) + 15) & ~15);  // offset arithmetic: keeps the LDS address space (ds_*, not flat_*)
   {
     unsigned char* g = a.gscratch + (int64_t)slot * a.gslot_bytes;
     S.keys = (uint64_t*)g;           g += sizeof(uint64_t) * kseg;
@@ -382,7 +382,8 @@ k_features(FeatArgs a) {
     S.tmp = (SmoothEntry*)g;         g += sizeof(SmoothEntry) * segcap;
     S.sorder = (uint16_t*)g;         g += sizeof(uint16_t) * segcap;
     S.rankc = (uint16_t*)g;          g += sizeof(uint16_t) * segcap;
-    S.gcurv = (float*)(((uintptr_t)g + 15) & ~(uintptr_t)15);
+    unsigned char* g0 = a.gscratch + (int64_t)slot * a.gslot_bytes;
+    S.gcurv = (float*)(g0 + (((g - g0) + 15) & ~(int64_t)15));
   }
   S.sbase = 0;
 
@@ -395,23 +396,28 @@ k_features(FeatArgs a) {
   FBR_STAMP(0);
   // ---- phase 2: occlusion marks, column gaps, curvature, threshold bits (chunk c = 64 indices) ----
   // range / col are staged per group of 4 chunks: window [256g - 8, 256g + 264) in region B
+  // (the next group's window is loaded into registers while this group is processed)
   float* rw = (float*)S.rb;
   int16_t* cw = (int16_t*)(rw + kWin);
+  constexpr int kWq = (kWin + 63) / 64;
+  float rv[kWq];
+  int cv[kWq];
+  auto load_window = [&](int c) __attribute__((always_inline)) {
+    const int wb = 64 * c - 8;
+#pragma unroll
+    for (int q = 0; q < kWq; ++q) {
+      const int t = 64 * q + lane, idx = wb + t;
+      const bool in = t < kWin && idx >= 0 && idx < S.L;
+      rv[q] = in ? R[S.wlo + idx] : 0.0f;
+      cv[q] = in ? C[S.wlo + idx] : 0;
+    }
+  };
+  load_window(0);
   for (int c = 0; c < S.nw; ++c) {
     if ((c & 3) == 0) {
-      const int wb = 64 * c - 8;
-      float rv[(kWin + 63) / 64];
-      int cv[(kWin + 63) / 64];
-#pragma unroll
-      for (int q = 0; q < (kWin + 63) / 64; ++q) {
-        const int t = 64 * q + lane, idx = wb + t;
-        const bool in = t < kWin && idx >= 0 && idx < S.L;
-        rv[q] = in ? R[S.wlo + idx] : 0.0f;
-        cv[q] = in ? C[S.wlo + idx] : 0;
-      }
       __syncthreads();
 #pragma unroll
-      for (int q = 0; q < (kWin + 63) / 64; ++q) {
+      for (int q = 0; q < kWq; ++q) {
         const int t = 64 * q + lane;
         if (t < kWin) {
           rw[t] = rv[q];
@@ -419,32 +425,31 @@ k_features(FeatArgs a) {
         }
       }
       __syncthreads();
+      if (c + 4 < S.nw) load_window(c + 4);
     }
     const int i = 64 * c + lane;
     const int j = S.wlo + i;
     const int wo = 64 * (c & ~3) - 8;  // window origin of this chunk's group
-    bool fa = false, fb = false, fc = false, gp = true;
-    float curv = 0.0f;
-    if (i < S.L) {
-      if (i + 1 < S.L) gp = abs((int)cw[i + 1 - wo] - (int)cw[i - wo]) > 10;
-      if (j >= 5 && j < n - 6 && i >= 1 && i + 1 < S.L) {  // markOccludedPoints (:140-175)
-        const float depth1 = rw[i - wo], depth2 = rw[i + 1 - wo];
-        const int columnDiff = abs((int)cw[i + 1 - wo] - (int)cw[i - wo]);
-        if (columnDiff < 10) {
-          if ((double)(depth1 - depth2) > 0.3) fa = true;
-          else if ((double)(depth2 - depth1) > 0.3) fb = true;
-        }
-        const float diff1 = fabsf(rw[i - 1 - wo] - rw[i - wo]);
-        const float diff2 = fabsf(rw[i + 1 - wo] - rw[i - wo]);
-        fc = (double)diff1 > 0.02 * (double)rw[i - wo] && (double)diff2 > 0.02 * (double)rw[i - wo];
-      }
-      if (j >= 5 && j < n - 5 && i >= 5 && i + 5 < S.L) {  // calculateSmoothness (:113-122)
-        const float d = rw[i - 5 - wo] + rw[i - 4 - wo] + rw[i - 3 - wo] + rw[i - 2 - wo] + rw[i - 1 - wo] - rw[i - wo] * 10.0f +
-                        rw[i + 1 - wo] + rw[i + 2 - wo] + rw[i + 3 - wo] + rw[i + 4 - wo] + rw[i + 5 - wo];
-        curv = d * d;
-      }
-      S.gcurv[i] = curv;  // indices outside [5, n-5) keep the zero-initialised scratch value
-    }
+    // Branch-free: every window read is in bounds (t in [8, 264), margins of 8), values past the
+    // ring are masked by the conditions; the arithmetic is the reference's, in its order.
+    const int t = i - wo;
+    const float rm5 = rw[t - 5], rm4 = rw[t - 4], rm3 = rw[t - 3], rm2 = rw[t - 2], rm1 = rw[t - 1], r0 = rw[t];
+    const float rp1 = rw[t + 1], rp2 = rw[t + 2], rp3 = rw[t + 3], rp4 = rw[t + 4], rp5 = rw[t + 5];
+    const int c0 = cw[t], c1 = cw[t + 1];
+    const bool inL = i < S.L, has1 = i + 1 < S.L;
+    const int columnDiff = abs(c1 - c0);
+    const bool gp = !(inL & has1) | (columnDiff > 10);
+    const bool occ = inL & has1 & (j >= 5) & (j < n - 6) & (i >= 1);  // markOccludedPoints (:140-175)
+    const bool near = columnDiff < 10;
+    const bool a1 = (double)(r0 - rp1) > 0.3;  // depth1 - depth2
+    const bool fa = occ & near & a1;
+    const bool fb = occ & near & !a1 & ((double)(rp1 - r0) > 0.3);
+    const float diff1 = fabsf(rm1 - r0), diff2 = fabsf(rp1 - r0);
+    const bool fc = occ & ((double)diff1 > 0.02 * (double)r0) & ((double)diff2 > 0.02 * (double)r0);
+    const bool smooth_ok = inL & (j >= 5) & (j < n - 5) & (i >= 5) & (i + 5 < S.L);  // calculateSmoothness (:113-122)
+    const float d = rm5 + rm4 + rm3 + rm2 + rm1 - r0 * 10.0f + rp1 + rp2 + rp3 + rp4 + rp5;
+    const float curv = smooth_ok ? d * d : 0.0f;
+    if (inL) S.gcurv[i] = curv;  // indices outside [5, n-5) keep the zero-initialised scratch value
     const uint64_t ba = __ballot(fa), bb = __ballot(fb), bc = __ballot(fc), bg = __ballot(gp);
     const uint64_t be = __ballot(i < S.L && curv > a.edge_thr);
     const uint64_t bs = __ballot(i < S.L && curv < a.surf_thr);
@@ -478,6 +483,29 @@ k_features(FeatArgs a) {
   // ---- extractFeatures (:188-285) ----
   int corner_cnt = 0;
   float4* corner_out = a.corner_slot + (int64_t)slot * kCornerPerRing;
+  // The next non-empty segment's curvature window is loaded into registers during this segment's
+  // surf walk and written to LDS after it (windows up to 64 * kCq entries; longer ones, the first
+  // segment and the segment after a stale-slot one are staged on the spot).
+  constexpr int kCq = WMAX;  // 384 entries for W <= 2048
+  float cpf[kCq];
+  int pf_seg = -1, pf_next = -1, pf_len = 0;
+  auto prefetch_curv = [&](int j0) __attribute__((always_inline)) {
+    pf_next = -1;
+    for (int jj = j0; jj < 6; ++jj) {
+      const int psp = (s * (6 - jj) + e * jj) / 6, pep = (s * (5 - jj) + e * (jj + 1)) / 6 - 1;
+      if (psp >= pep) continue;
+      const int pb = max(psp - S.wlo - 6, 0), pl = min(pep - S.wlo + 7, S.L) - pb;
+      if (pl > 64 * kCq || pep - psp + 1 > segcap) return;
+#pragma unroll
+      for (int q = 0; q < kCq; ++q) {
+        const int t = 64 * q + lane;
+        cpf[q] = t < pl ? S.gcurv[pb + t] : 0.0f;
+      }
+      pf_next = jj;
+      pf_len = pl;
+      return;
+    }
+  };
   for (int j = 0; j < 6; j++) {
     const int sp = (s * (6 - j) + e * j) / 6;
     const int ep = (s * (5 - j) + e * (j + 1)) / 6 - 1;
@@ -490,7 +518,8 @@ k_features(FeatArgs a) {
     // stage this segment's curvature window [sp-6, ep+7) in LDS (members +-5 plus ep)
     S.sbase = max(sp - S.wlo - 6, 0);
     const int slen = min(ep - S.wlo + 7, S.L) - S.sbase;
-    for (int t = lane; t < slen; t += 64) S.scurv[t] = S.gcurv[S.sbase + t];
+    if (pf_seg != j)
+      for (int t = lane; t < slen; t += 64) S.scurv[t] = S.gcurv[S.sbase + t];
     __syncthreads();
 #ifdef FBR_FEAT_SKIP_STALE
     const bool has_stale = false;  // diagnostic ablation only
@@ -627,21 +656,19 @@ k_features(FeatArgs a) {
           const float vu = cv[5];
           uint32_t nb = 0, hc = 0;
 #pragma unroll
-          for (int d = 1; d <= 5; ++d) {
-            if (d <= f && u + d <= m) {  // u < m here
-              nb |= 1u << (4 + d);
-              const float vv = cv[5 + d];
-              if (u + d == m || vv > vu) hc |= 1u << (4 + d);
-              else if (!(vv < vu)) tf = true;
-            }
-            if (d <= b && u - d >= 0) {
-              nb |= 1u << (5 - d);
-              const float vv = cv[5 - d];
-              if (u != m) {  // ep outranks every neighbour
-                if (vv > vu) hc |= 1u << (5 - d);
-                else if (!(vv < vu)) tf = true;
-              }
-            }
+          for (int d = 1; d <= 5; ++d) {  // branch-free: masks from bitwise predicates
+            const bool fv = (d <= f) & (u + d <= m);  // u < m here
+            const float vf = cv[5 + d];
+            const bool fh = (u + d == m) | (vf > vu);
+            nb |= (uint32_t)fv << (4 + d);
+            hc |= (uint32_t)(fv & fh) << (4 + d);
+            tf |= fv & !fh & !(vf < vu);
+            const bool bv = (d <= b) & (u - d >= 0);
+            const float vb = cv[5 - d];
+            const bool notep = u != m;  // ep outranks every neighbour
+            nb |= (uint32_t)bv << (5 - d);
+            hc |= (uint32_t)(bv & notep & (vb > vu)) << (5 - d);
+            tf |= bv & notep & !(vb > vu) & !(vb < vu);
           }
           S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
         }
@@ -748,6 +775,7 @@ k_features(FeatArgs a) {
       corner_cnt += min(taken, kCornerPerSeg);
       __syncthreads();
       FBR_STAMP(5);
+      prefetch_curv(j + 1);  // scurv is not read again in this segment
       // -- surf walk: ascending, ep last -> higher priority = not higher corner priority --
 #pragma unroll
       for (int w = 0; w < WMAX; ++w) {
@@ -776,6 +804,12 @@ k_features(FeatArgs a) {
           atomicOr((unsigned long long*)&S.labneg.w[li >> 6], 1ull << (li & 63));
           or_range(S.picked, li - (int)((c >> 24) & 15u), li + (int)((c >> 20) & 15u));
         }
+      }
+      pf_seg = pf_next;
+      if (pf_seg >= 0) {
+#pragma unroll
+        for (int q = 0; q < kCq; ++q)
+          if (64 * q + lane < pf_len) S.scurv[64 * q + lane] = cpf[q];
       }
       __syncthreads();
     }

@@ -123,9 +123,18 @@ struct VgGrid {
   }
 };
 
+// LDS-mode buffers are accessed through address-space-3 pointers: the ping-pong selection by a
+// loop-carried index otherwise leaves generic pointers, i.e. flat_* instead of ds_* accesses.
+#define FBR_LDS_AS __attribute__((address_space(3)))
+template <bool L, typename X>
+__device__ __forceinline__ auto lds_if(X* p) {
+  if constexpr (L) return (FBR_LDS_AS X*)p;
+  else return p;
+}
+
 // Stable radix sort of kb[0]/vb[0] (n pairs), then one centroid per run of equal keys in
 // ascending key order: out[v] = mean of in[vals of the run].  Returns the voxel count (all threads).
-template <int T, typename V, int MAXD = 9>
+template <int T, typename V, int MAXD = 9, bool KV_LDS = true>
 __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, uint32_t* hist, uint32_t* wsum,
                             const float4* in, float4* out, int dbg = 0, unsigned long long* t_sorted = nullptr) {
   constexpr int NW = T / 64, NB = 1 << MAXD;  // digits of <= MAXD bits; hist rows of NB counters
@@ -144,10 +153,10 @@ __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, u
     const int shift = dbits * pass;
     const uint32_t dmask = (uint32_t)nbins - 1u;
     const int tot = nbins * NW;
-    const uint32_t* kin = kb[cur];
-    const V* vin = vb[cur];
-    uint32_t* kout = kb[cur ^ 1];
-    V* vout = vb[cur ^ 1];
+    const auto kin = lds_if<KV_LDS>(kb[cur]);
+    const auto vin = lds_if<KV_LDS>(vb[cur]);
+    const auto kout = lds_if<KV_LDS>(kb[cur ^ 1]);
+    const auto vout = lds_if<KV_LDS>(vb[cur ^ 1]);
     for (int b = tid; b < tot; b += T) hist[(b % NW) * NB + b / NW] = 0u;
     __syncthreads();
     for (int i = c0 + lane; i < c1; i += 64) atomicAdd(&hist[w * NB + ((kin[i] >> shift) & dmask)], 1u);
@@ -202,8 +211,8 @@ __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, u
     cur ^= 1;
     __syncthreads();
   }
-  const uint32_t* ks = kb[cur];
-  const V* vs = vb[cur];
+  const auto ks = lds_if<KV_LDS>(kb[cur]);
+  const auto vs = lds_if<KV_LDS>(vb[cur]);
   if (t_sorted && threadIdx.x == 0) *t_sorted = __builtin_amdgcn_s_memtime();
   if (dbg == 2) return 0;
   // ---- voxels in ascending key order: heads of equal-key runs, centroid = float sum / count ----
@@ -329,7 +338,7 @@ __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
   uint32_t* kb[2];
   V* vb[2];
   if constexpr (LDS) {
-    unsigned char* q = (unsigned char*)(((uintptr_t)(misc + 4) + 15) & ~(uintptr_t)15);
+    unsigned char* q = smem + ((((unsigned char*)(misc + 4) - smem) + 15) & ~15);  // keeps the LDS address space
     const int cap = (int)S.cap;
     kb[0] = (uint32_t*)q;
     kb[1] = kb[0] + cap;
@@ -347,7 +356,7 @@ __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
     vb[0][i] = (V)i;
   }
   __syncthreads();
-  const int total = vg_sort_emit<T, V>(kb, vb, n, G.nbits, hist, wsum, in, out);
+  const int total = vg_sort_emit<T, V, 9, LDS>(kb, vb, n, G.nbits, hist, wsum, in, out);
   if (tid == 0) S.cnt_out[seg] = total;
 }
 
@@ -437,7 +446,7 @@ k_voxel_ring(VgRing A) {
   VR_TS(1);
   VgGrid G;
   G.init(mn, mx, A.leaf, false);
-  unsigned char* q = (unsigned char*)(((uintptr_t)(cnts + KPT * NW) + 15) & ~(uintptr_t)15);
+  unsigned char* q = smem + ((((unsigned char*)(cnts + KPT * NW) - smem) + 15) & ~15);  // keeps the LDS address space
   uint32_t* kb[2];
   uint16_t* vb[2];
   kb[0] = (uint32_t*)q;
