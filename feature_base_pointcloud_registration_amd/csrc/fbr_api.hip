@@ -273,7 +273,8 @@ int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pt
     start[cell[i] + 1]++;
   }
   for (int64_t k = 0; k < ncell; ++k) start[k + 1] += start[k];
-  std::vector<float4> sorted(std::max<int64_t>(n, 1));
+  // [0, n): sorted by cell; [n, 2n): the same points in map-index order (MapGrid::by_id)
+  std::vector<float4> sorted(std::max<int64_t>(2 * n, 1));
   std::vector<int32_t> fill(start.begin(), start.end() - 1);
   for (int64_t i = 0; i < n; ++i) {  // counting sort, index order kept inside a cell
     const fbr_point_xyzi& p = pts[i];
@@ -281,9 +282,10 @@ int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pt
     int32_t ii = (int32_t)i;
     std::memcpy(&w, &ii, 4);
     sorted[fill[cell[i]]++] = make_float4(p.x, p.y, p.z, w);
+    sorted[n + i] = make_float4(p.x, p.y, p.z, w);
   }
-  if (dalloc(d_pts, std::max<int64_t>(n, 1)) || dalloc(d_cs, ncell + 1)) return FBR_ERR_HIP;
-  if (n) CK(hipMemcpy(*d_pts, sorted.data(), sizeof(float4) * n, hipMemcpyHostToDevice));
+  if (dalloc(d_pts, std::max<int64_t>(2 * n, 1)) || dalloc(d_cs, ncell + 1)) return FBR_ERR_HIP;
+  if (n) CK(hipMemcpy(*d_pts, sorted.data(), sizeof(float4) * 2 * n, hipMemcpyHostToDevice));
   CK(hipMemcpy(*d_cs, start.data(), sizeof(int32_t) * (ncell + 1), hipMemcpyHostToDevice));
   g->inv_cell = inv;
   g->inv_x = invx;
@@ -460,8 +462,8 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   a.surfDS = c->d_surfDS + j0 * HW;
   a.caps = HW;
   a.nsds = c->d_nsds + j0;
-  a.mc = MapGrid{c->d_map_c, c->d_cs_c, c->gc};
-  a.ms = MapGrid{c->d_map_s, c->d_cs_s, c->gs};
+  a.mc = MapGrid{c->d_map_c, c->d_cs_c, c->gc, c->d_map_c + c->gc.n_points};
+  a.ms = MapGrid{c->d_map_s, c->d_cs_s, c->gs, c->d_map_s + c->gs.n_points};
   a.gn = c->d_gn + j0;
   a.guess = c->d_guess + j0 * 6;
   a.items = c->d_items + ib;
@@ -793,7 +795,9 @@ int build_grid_dev(fbr_ctx* c, const float4* d_src, int64_t n, float4** d_pts, i
   }
   g->n_cells = (int32_t)(dims[0] * dims[1] * dims[2]);
   g->n_points = n;
-  if (dalloc(d_pts, std::max<int64_t>(n, 1)) || dalloc(d_cs, (int64_t)g->n_cells + 1)) return FBR_ERR_HIP;
+  // [0, n): sorted by cell; [n, 2n): the source points in map-index order (MapGrid::by_id)
+  if (dalloc(d_pts, std::max<int64_t>(2 * n, 1)) || dalloc(d_cs, (int64_t)g->n_cells + 1)) return FBR_ERR_HIP;
+  if (n) CK(hipMemcpyAsync(*d_pts + n, d_src, sizeof(float4) * n, hipMemcpyDeviceToDevice, c->stream));
   int rc = grid_fill_device(c->stream, d_src, n, *g, *d_cs, *d_pts);
   if (!rc) CK(hipStreamSynchronize(c->stream));
   return rc;

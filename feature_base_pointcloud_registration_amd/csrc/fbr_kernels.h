@@ -107,6 +107,7 @@ struct MapGrid {
   const float4* pts;          // sorted by cell; w = bit pattern of the map index
   const int32_t* cell_start;  // [n_cells+1]
   GridDesc g;
+  const float4* by_id;        // the same points in map-index order (neighbour gathers by index)
 };
 
 struct GnArgs {
@@ -131,7 +132,7 @@ struct GnArgs {
   float* pose_out;           // [B][6]
   fbr_reg_stats* stats;      // [B]
   float* trace;              // [B][max_iter][6] or null
-  int32_t* nbr;              // [max_items][5][256] kNN-5 map positions of each query (-1 = rejected)
+  int32_t* nbr;              // [max_items][5][256] kNN-5 map indices of each query (-1 = rejected)
   unsigned long long* iter_flags;  // host-mapped [max_iter]: (generation << 32) | jobs still active
   int32_t* iter_cnt;         // [max_iter][2] active-job count / finished workgroups (zeroed per solve)
   const int32_t* desk_mode;  // [B] kDesk* bits or null (transformUpdate's IMU slerp, :1447-1474)

@@ -55,26 +55,29 @@ __device__ void pose_to_T(const float* tr, float* T, float* trig) {
   trig[0] = D; trig[1] = C; trig[2] = B; trig[3] = A; trig[4] = F; trig[5] = E;
 }
 
+// The 5 nearest as sorted 64-bit keys (float bits of d2) << 32 | map index: d2 >= +0, so the
+// unsigned key order is exactly FLANN's (d2, index) order.  A key is built from a scanned point
+// without any instruction (hi = the distance register, lo = the w bit pattern).  Empty slots hold
+// kKnnEmpty = (bits(1.0f), 0): a point is only inserted with d2 < 1.0 (:1027, :1154).
+constexpr unsigned long long kKnnEmpty = (unsigned long long)0x3f800000u << 32;
+
 struct Knn5 {
-  float d[5];
-  int id[5];   // map index (tie-break of FLANN's sorted result)
-  int pos[5];  // position in the cell-sorted map array
+  unsigned long long k[5];
 };
 
-__device__ __forceinline__ bool knn_less(float d, int i, float d2, int i2) { return d < d2 || (d == d2 && i < i2); }
+__device__ __forceinline__ float knn_d(unsigned long long k) { return __int_as_float((int)(k >> 32)); }
+__device__ __forceinline__ int knn_id(unsigned long long k) { return (int)(unsigned)k; }
 
-// Insert by compare-swap down a sorted 5-slot list (compile-time indices: stays in registers).
-__device__ __forceinline__ void knn_insert(Knn5& r, float d, int id, int pos) {
-  if (!knn_less(d, id, r.d[4], r.id[4])) return;
+// Branch-free sorted insertion: the "less than slot t" flags are monotone over t, so every slot
+// takes its own key, its left neighbour's, or the new one (5 compares + 20 selects, no SALU mask
+// arithmetic and no serial compare-swap chain).
+__device__ __forceinline__ void knn_insert(Knn5& r, unsigned long long x) {
+  bool lt[5];
 #pragma unroll
-  for (int t = 0; t < 5; ++t) {
-    if (knn_less(d, id, r.d[t], r.id[t])) {
-      const float td = r.d[t];
-      const int ti = r.id[t], tp = r.pos[t];
-      r.d[t] = d; r.id[t] = id; r.pos[t] = pos;
-      d = td; id = ti; pos = tp;
-    }
-  }
+  for (int t = 0; t < 5; ++t) lt[t] = x < r.k[t];
+#pragma unroll
+  for (int t = 4; t > 0; --t) r.k[t] = lt[t] ? (lt[t - 1] ? r.k[t - 1] : x) : r.k[t];
+  r.k[0] = lt[0] ? x : r.k[0];
 }
 
 // Lower bound of |q - p| along one axis for a point p in the cell at offset o from q's cell
@@ -116,7 +119,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
                           float bound, Knn5& r, unsigned* ks) {
   constexpr int K = 2 * R + 1;  // rows per side in y and z; RX = cells per side along x
 #pragma unroll
-  for (int t = 0; t < 5; ++t) { r.d[t] = __int_as_float(0x7f800000); r.id[t] = 0x7fffffff; r.pos[t] = -1; }
+  for (int t = 0; t < 5; ++t) r.k[t] = kKnnEmpty;
   const float inv = m.g.inv_cell, c = 1.0f / inv, invx = m.g.inv_x, cxs = 1.0f / invx;
   const float sx = qx * invx, sy = qy * inv, sz = qz * inv;
   const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
@@ -155,7 +158,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       float lb = 0.0f;
       lb += ly2[ky];
       lb += lz2[kz];
-      const float cut = fminf(r.d[4], bound);
+      const float cut = fminf(knn_d(r.k[4]), bound);
       if (y < 0 || y >= Y || z < 0 || z >= Z || lb > cut || !(lb < 1.0f)) continue;
       int xa = 0, xb = 0;
       bool go_a = true, go_b = true;
@@ -188,10 +191,8 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         diff = qx - p.x; dist += diff * diff;                            // flann::L2_Simple
         diff = qy - p.y; dist += diff * diff;
         diff = qz - p.z; dist += diff * diff;
-        if (dist < 1.0f) {
-          FBR_KS(4, 1);
-          knn_insert(r, dist, __float_as_int(p.w), i);
-        }
+        FBR_KS(4, dist < knn_d(r.k[4]) ? 1 : 0);
+        knn_insert(r, ((unsigned long long)(unsigned)__float_as_int(dist) << 32) | (unsigned)__float_as_int(p.w));
       }
     }
   }
@@ -309,7 +310,7 @@ __global__ void k_gn_init(GnArgs a) {
   if (tid == 0) a.nitems[0] = min(base, a.max_items);
 }
 
-// kNN pass: one lane per query, writes the 5 neighbour positions (slot 0 = -1: no correspondence).
+// kNN pass: one lane per query, writes the 5 neighbour map indices (slot 0 = -1: no correspondence).
 // R = grid cells per side covering radius 1 (both map grids share one cell size).
 template <int R, int RX>
 __global__ void __launch_bounds__(kResThreads)
@@ -336,7 +337,7 @@ k_gn_knn(GnArgs a, int use_prev) {
       float mx = 0.0f;
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
-        const float4 q = mg.pts[o[k * kResThreads]];
+        const float4 q = mg.by_id[o[k * kResThreads]];
         float dist = 0.0f, diff;
         diff = x0 - q.x; dist += diff * diff;
         diff = y0 - q.y; dist += diff * diff;
@@ -348,7 +349,7 @@ k_gn_knn(GnArgs a, int use_prev) {
     Knn5 nn;
     unsigned ks[8] = {1, 0, 0, 0, 0, 0, 0, 0};
     knn5_grid<R, RX>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
-    const bool ok = nn.pos[4] >= 0 && nn.d[4] < 1.0f;
+    const bool ok = nn.k[4] < kKnnEmpty;
 #ifdef FBR_KNN_STATS
     ks[5] = ok;
     ks[6] = corner;
@@ -357,7 +358,7 @@ k_gn_knn(GnArgs a, int use_prev) {
     (void)ks;
 #endif
 #pragma unroll
-    for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? nn.pos[k] : -1;
+    for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? knn_id(nn.k[k]) : -1;
   }
 }
 
@@ -381,7 +382,7 @@ k_gn_residual(GnArgs a) {
       const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
       const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
       const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
-      const float4* mp = corner ? a.mc.pts : a.ms.pts;
+      const float4* mp = corner ? a.mc.by_id : a.ms.by_id;
       Nbr5 nn;
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
