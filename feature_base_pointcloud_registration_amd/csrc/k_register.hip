@@ -145,8 +145,10 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
     lxm2[o] = a * a;
     lxp2[o] = b * b;
   }
+  // the crop box in registers (per job: wave-uniform)
+  const float bx0 = bmin[0], by0 = bmin[1], bz0 = bmin[2], bx1 = bmax[0], by1 = bmax[1], bz1 = bmax[2];
   const float xlo = (fx - (float)RX) * cxs, xhi = (fx + (float)(RX + 1)) * cxs;  // row x extent (max)
-  const bool xin = xlo >= bmin[0] && xhi <= bmax[0];
+  const bool xin = xlo >= bx0 && xhi <= bx1;
 #pragma unroll
   for (int ksum = 0; ksum <= 2 * (K - 1); ++ksum) {
 #pragma unroll
@@ -180,19 +182,19 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       FBR_KS(3, e - b);
       // the whole row inside the crop box (pcl::CropBox, inclusive) -> no per-point test
       const float ylo = (fy + (float)oyk[ky]) * c, zlo = (fz + (float)ozk[kz]) * c;
-      const bool inside = xin && ylo >= bmin[1] && ylo + c <= bmax[1] && zlo >= bmin[2] && zlo + c <= bmax[2];
+      const bool inside = xin & (ylo >= by0) & (ylo + c <= by1) & (zlo >= bz0) & (zlo + c <= bz1);
       for (int i = b; i < e; ++i) {
         const float4 p = m.pts[i];
-        if (!inside) {
-          if (p.x < bmin[0] || p.y < bmin[1] || p.z < bmin[2]) continue;
-          if (p.x > bmax[0] || p.y > bmax[1] || p.z > bmax[2]) continue;
-        }
+        // pcl::CropBox (inclusive) as one mask: a point outside gets d2 = +inf (never inserted)
+        bool out = false;  // rows inside the box skip the test
+        if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
         float dist = 0.0f, diff;
         diff = qx - p.x; dist += diff * diff;                            // flann::L2_Simple
         diff = qy - p.y; dist += diff * diff;
         diff = qz - p.z; dist += diff * diff;
-        FBR_KS(4, dist < knn_d(r.k[4]) ? 1 : 0);
-        knn_insert(r, ((unsigned long long)(unsigned)__float_as_int(dist) << 32) | (unsigned)__float_as_int(p.w));
+        const unsigned hi = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
+        FBR_KS(4, __int_as_float((int)hi) < knn_d(r.k[4]) ? 1 : 0);
+        knn_insert(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
       }
     }
   }
