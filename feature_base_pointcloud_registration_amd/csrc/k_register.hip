@@ -364,6 +364,29 @@ k_gn_knn(GnArgs a, int use_prev) {
   }
 }
 
+// Normal-equation product k of one row: 0-20 the upper AtA triangle, 21-26 AtB, 27 the count,
+// 28-31 zero (compile-time k after unrolling).
+__device__ __forceinline__ double res_product(int k, const float* row, float b, bool ok) {
+  constexpr int kR[21] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 5};
+  constexpr int kC[21] = {0, 1, 2, 3, 4, 5, 1, 2, 3, 4, 5, 2, 3, 4, 5, 3, 4, 5, 4, 5, 5};
+  if (k < 21) return (double)row[kR[k]] * (double)row[kC[k]];
+  if (k < 27) return (double)row[k - 21] * (double)b;
+  if (k == 27) return ok ? 1.0 : 0.0;
+  return 0.0;
+}
+
+// One transposed-butterfly step: H values per lane -> H/2 (the lower lane of each OFF pair keeps
+// the first half, the upper lane the second).
+template <int H, int OFF>
+__device__ __forceinline__ void res_halve(double* v, int lane) {
+  const bool up = (lane & OFF) != 0;
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    const double lo = v[j], hi = v[j + H];
+    v[j] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, OFF);
+  }
+}
+
 __global__ void __launch_bounds__(kResThreads)
 k_gn_residual(GnArgs a) {
   __shared__ double red[kResThreads / 64][28];
@@ -411,17 +434,25 @@ k_gn_residual(GnArgs a) {
         b = -c.w;
       }
     }
-    // fp64 products (21 upper AtA entries, 6 AtB, count), each formed and wave-reduced in turn so
-    // that only a few doubles are live at once
+    // fp64 products (21 upper AtA entries, 6 AtB, count; 4 zero pads) reduced over the wave by a
+    // transposed butterfly: at each halving step a lane keeps half of its values and trades the
+    // other half with its partner, so 32 values cost 32 shuffles instead of 6 per value.  Lane l
+    // (bit 0 clear) ends with the wave sum of value res_index(l).
+    double v[16];
+    const bool up5 = (lane & 32) != 0;
 #pragma unroll
-    for (int k = 0; k < 28; ++k) {
-      constexpr int kR[21] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 5};
-      constexpr int kC[21] = {0, 1, 2, 3, 4, 5, 1, 2, 3, 4, 5, 2, 3, 4, 5, 3, 4, 5, 4, 5, 5};
-      const int rr = k < 21 ? kR[k] : 0, cc = k < 21 ? kC[k] : 0;  // upper-triangle (row, column)
-      double x = k < 21 ? (double)row[rr] * (double)row[cc] : (k < 27 ? (double)row[k - 21] * (double)b : (ok ? 1.0 : 0.0));
-      for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-      if (lane == 0) red[wave][k] = x;
+    for (int j = 0; j < 16; ++j) {
+      const double lo = res_product(j, row, b, ok), hi = res_product(j + 16, row, b, ok);
+      v[j] = (up5 ? hi : lo) + __shfl_xor(up5 ? lo : hi, 32);
     }
+    res_halve<8, 16>(v, lane);
+    res_halve<4, 8>(v, lane);
+    res_halve<2, 4>(v, lane);
+    res_halve<1, 2>(v, lane);
+    v[0] += __shfl_xor(v[0], 1);
+    const int ridx = ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 +
+                     ((lane >> 1) & 1);
+    if (!(lane & 1) && ridx < 28) red[wave][ridx] = v[0];
     __syncthreads();
     if (tid < 28) {
       double s = 0.0;
