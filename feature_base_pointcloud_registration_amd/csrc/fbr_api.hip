@@ -548,6 +548,15 @@ int gn_grid_cap() {
   return v;
 }
 
+// kNN and residual in one launch (FBR_GN_FUSED=0/1 overrides the default).
+bool gn_fused() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_GN_FUSED");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+
 // The Gauss-Newton iterations of one or two sub-batches.  Iterations run on the device without
 // host round trips; for each sub-batch the host stays kLag iterations ahead and stops enqueueing
 // once its k_gn_solve reports that no job is active (flags in host-mapped memory).
@@ -586,8 +595,12 @@ int register_iterate(fbr_ctx* c, const Sub* subs, int nsub, bool trace) {
         }
       }
       const int grid = std::max(1, std::min(a[k].max_items, gn_grid_cap()));
-      TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a[k], grid, it));
-      TIMED_ON(c, sb.st, "gn_residual", launch_gn_residual(sb.st, a[k], grid));
+      if (gn_fused()) {
+        TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a[k], grid, it, true));
+      } else {
+        TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a[k], grid, it, false));
+        TIMED_ON(c, sb.st, "gn_residual", launch_gn_residual(sb.st, a[k], grid));
+      }
       TIMED_ON(c, sb.st, "gn_solve", launch_gn_solve(sb.st, a[k], it, gen));
     }
   }

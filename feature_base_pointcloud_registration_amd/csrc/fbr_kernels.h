@@ -140,7 +140,8 @@ struct GnArgs {
   int nocrop;                // 1: keyframe local map, no CropBox (scan2MapOptimization on it)
 };
 void launch_gn_init(hipStream_t s, const GnArgs& a);
-void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter);
+// fused: kNN + residual row + item partial in one launch (launch_gn_residual is then skipped)
+void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fused);
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid);
 void launch_gn_solve(hipStream_t s, const GnArgs& a, int iter_idx, unsigned long long gen);
 void launch_gn_finalize(hipStream_t s, const GnArgs& a);

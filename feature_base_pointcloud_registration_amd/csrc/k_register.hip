@@ -312,58 +312,6 @@ __global__ void k_gn_init(GnArgs a) {
   if (tid == 0) a.nitems[0] = min(base, a.max_items);
 }
 
-// kNN pass: one lane per query, writes the 5 neighbour map indices (slot 0 = -1: no correspondence).
-// R = grid cells per side covering radius 1 (both map grids share one cell size).
-template <int R, int RX>
-__global__ void __launch_bounds__(kResThreads)
-k_gn_knn(GnArgs a, int use_prev) {
-  const int tid = threadIdx.x;
-  const int nitems = a.nitems[0];
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
-    const int4 item = a.items[it];
-    const int job = item.x;
-    const GnState& g = a.gn[job];
-    if (!g.active) continue;  // block-uniform
-    if (tid >= item.w) continue;
-    const bool corner = item.y == 0;
-    const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
-    const float* T = g.T;
-    // pointAssociateToMap (:397-403)
-    const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
-    const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
-    const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
-    const MapGrid& mg = corner ? a.mc : a.ms;
-    int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
-    float bound = __int_as_float(0x7f800000);
-    if (use_prev && o[0] >= 0) {  // warm start: the previous iteration's neighbours of this query
-      float mx = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const float4 q = mg.by_id[o[k * kResThreads]];
-        float dist = 0.0f, diff;
-        diff = x0 - q.x; dist += diff * diff;
-        diff = y0 - q.y; dist += diff * diff;
-        diff = z0 - q.z; dist += diff * diff;
-        mx = fmaxf(mx, dist);
-      }
-      bound = mx;
-    }
-    Knn5 nn;
-    unsigned ks[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-    knn5_grid<R, RX>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
-    const bool ok = nn.k[4] < kKnnEmpty;
-#ifdef FBR_KNN_STATS
-    ks[5] = ok;
-    ks[6] = corner;
-    for (int k = 0; k < 7; ++k) atomicAdd(&fbr_knn_stats[k], (unsigned long long)ks[k]);
-#else
-    (void)ks;
-#endif
-#pragma unroll
-    for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? knn_id(nn.k[k]) : -1;
-  }
-}
-
 // Normal-equation product k of one row: 0-20 the upper AtA triangle, 21-26 AtB, 27 the count,
 // 28-31 zero (compile-time k after unrolling).
 __device__ __forceinline__ double res_product(int k, const float* row, float b, bool ok) {
@@ -387,10 +335,74 @@ __device__ __forceinline__ void res_halve(double* v, int lane) {
   }
 }
 
+// cornerOptimization / surfOptimization + the LMOptimization row (:1286-1332) of one query whose 5
+// neighbours are the map points nb[0..4] (map indices); false when the correspondence is rejected.
+__device__ __forceinline__ bool res_row(const GnState& g, const float4* by_id, const int32_t* nb, int stride,
+                                        bool corner, const float4& p, float x0, float y0, float z0, float* row,
+                                        float& b) {
+  Nbr5 nn;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const float4 q = by_id[nb[k * stride]];
+    nn.x[k] = q.x; nn.y[k] = q.y; nn.z[k] = q.z;
+  }
+  float4 c;
+  const bool ok = corner ? corner_residual(nn, x0, y0, z0, c) : surf_residual(nn, x0, y0, z0, c);
+  if (ok) {
+    // camera-frame swap
+    const float srx = g.trig[0], crx = g.trig[1], sry = g.trig[2], cry = g.trig[3], srz = g.trig[4], crz = g.trig[5];
+    const float pox = p.y, poy = p.z, poz = p.x;
+    const float cox = c.y, coy = c.z, coz = c.x;
+    const float arx = (crx * sry * srz * pox + crx * crz * sry * poy - srx * sry * poz) * cox +
+                      (-srx * srz * pox - crz * srx * poy - crx * poz) * coy +
+                      (crx * cry * srz * pox + crx * cry * crz * poy - cry * srx * poz) * coz;
+    const float ary = ((cry * srx * srz - crz * sry) * pox + (sry * srz + cry * crz * srx) * poy + crx * cry * poz) * cox +
+                      ((-cry * crz - srx * sry * srz) * pox + (cry * srz - crz * srx * sry) * poy - crx * sry * poz) * coz;
+    const float arz = ((crz * srx * sry - cry * srz) * pox + (-cry * crz - srx * sry * srz) * poy) * cox +
+                      (crx * crz * pox - crx * srz * poy) * coy +
+                      ((sry * srz + cry * crz * srx) * pox + (crz * sry - cry * srx * srz) * poy) * coz;
+    row[0] = arz; row[1] = arx; row[2] = ary; row[3] = coz; row[4] = cox; row[5] = coy;
+    b = -c.w;
+  }
+  return ok;
+}
+
+// The item's fp64 normal-equation partial (21 upper AtA entries, 6 AtB, count; 4 zero pads):
+// every lane of the workgroup calls this with its row (zeros when it has none).  The wave sum is a
+// transposed butterfly: at each halving step a lane keeps half of its values and trades the other
+// half with its partner, so 32 values cost 32 shuffles instead of 6 per value.  Lane l (bit 0
+// clear) ends with the wave sum of value res_index(l); the 4 wave sums are added in LDS.
+__device__ __forceinline__ void res_reduce(double (*red)[28], int tid, const float* row, float b, bool ok,
+                                           double* out) {
+  const int lane = tid & 63, wave = tid >> 6;
+  double v[16];
+  const bool up5 = (lane & 32) != 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const double lo = res_product(j, row, b, ok), hi = res_product(j + 16, row, b, ok);
+    v[j] = (up5 ? hi : lo) + __shfl_xor(up5 ? lo : hi, 32);
+  }
+  res_halve<8, 16>(v, lane);
+  res_halve<4, 8>(v, lane);
+  res_halve<2, 4>(v, lane);
+  res_halve<1, 2>(v, lane);
+  v[0] += __shfl_xor(v[0], 1);
+  const int ridx = ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 +
+                   ((lane >> 1) & 1);
+  if (!(lane & 1) && ridx < 28) red[wave][ridx] = v[0];
+  __syncthreads();
+  if (tid < 28) {
+    double s = 0.0;
+    for (int w = 0; w < kResThreads / 64; ++w) s += red[w][tid];
+    out[tid] = s;
+  }
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(kResThreads)
 k_gn_residual(GnArgs a) {
   __shared__ double red[kResThreads / 64][28];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
   const int nitems = a.nitems[0];
   for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
     const int4 item = a.items[it];
@@ -407,59 +419,73 @@ k_gn_residual(GnArgs a) {
       const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
       const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
       const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
-      const float4* mp = corner ? a.mc.by_id : a.ms.by_id;
-      Nbr5 nn;
+      ok = res_row(g, corner ? a.mc.by_id : a.ms.by_id, nb, kResThreads, corner, p, x0, y0, z0, row, b);
+    }
+    res_reduce(red, tid, row, b, ok, a.partial + (int64_t)it * kPartial);
+  }
+}
+
+// kNN pass: one lane per query, writes the 5 neighbour map indices (slot 0 = -1: no correspondence).
+// R = grid cells per side covering radius 1 (both map grids share one cell size).  kFused: the
+// same lane goes on to its residual row and the workgroup reduces the item's normal-equation
+// partial (k_gn_residual's work, without re-reading the query and its neighbour indices).
+template <int R, int RX, bool kFused>
+__global__ void __launch_bounds__(kResThreads)
+k_gn_knn(GnArgs a, int use_prev) {
+  __shared__ double red[kResThreads / 64][28];
+  const int tid = threadIdx.x;
+  const int nitems = a.nitems[0];
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int4 item = a.items[it];
+    const int job = item.x;
+    const GnState& g = a.gn[job];
+    if (!g.active) continue;  // block-uniform
+    float row[6] = {0, 0, 0, 0, 0, 0}, b = 0.0f;
+    bool rok = false;
+    if (tid < item.w) {
+      const bool corner = item.y == 0;
+      const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
+      const float* T = g.T;
+      // pointAssociateToMap (:397-403)
+      const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
+      const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
+      const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
+      const MapGrid& mg = corner ? a.mc : a.ms;
+      int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
+      float bound = __int_as_float(0x7f800000);
+      if (use_prev && o[0] >= 0) {  // warm start: the previous iteration's neighbours of this query
+        float mx = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const float4 q = mg.by_id[o[k * kResThreads]];
+          float dist = 0.0f, diff;
+          diff = x0 - q.x; dist += diff * diff;
+          diff = y0 - q.y; dist += diff * diff;
+          diff = z0 - q.z; dist += diff * diff;
+          mx = fmaxf(mx, dist);
+        }
+        bound = mx;
+      }
+      Knn5 nn;
+      unsigned ks[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+      knn5_grid<R, RX>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
+      const bool ok = nn.k[4] < kKnnEmpty;
+#ifdef FBR_KNN_STATS
+      ks[5] = ok;
+      ks[6] = corner;
+      for (int k = 0; k < 7; ++k) atomicAdd(&fbr_knn_stats[k], (unsigned long long)ks[k]);
+#else
+      (void)ks;
+#endif
+      int32_t ids[5];
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
-        const float4 q = mp[nb[k * kResThreads]];
-        nn.x[k] = q.x; nn.y[k] = q.y; nn.z[k] = q.z;
+        ids[k] = knn_id(nn.k[k]);
+        o[k * kResThreads] = ok ? ids[k] : -1;
       }
-      float4 c;
-      ok = corner ? corner_residual(nn, x0, y0, z0, c) : surf_residual(nn, x0, y0, z0, c);
-      if (ok) {
-        // LMOptimization row (:1286-1332), camera-frame swap
-        const float srx = g.trig[0], crx = g.trig[1], sry = g.trig[2], cry = g.trig[3], srz = g.trig[4],
-                    crz = g.trig[5];
-        const float pox = p.y, poy = p.z, poz = p.x;
-        const float cox = c.y, coy = c.z, coz = c.x;
-        const float arx = (crx * sry * srz * pox + crx * crz * sry * poy - srx * sry * poz) * cox +
-                          (-srx * srz * pox - crz * srx * poy - crx * poz) * coy +
-                          (crx * cry * srz * pox + crx * cry * crz * poy - cry * srx * poz) * coz;
-        const float ary = ((cry * srx * srz - crz * sry) * pox + (sry * srz + cry * crz * srx) * poy + crx * cry * poz) * cox +
-                          ((-cry * crz - srx * sry * srz) * pox + (cry * srz - crz * srx * sry) * poy - crx * sry * poz) * coz;
-        const float arz = ((crz * srx * sry - cry * srz) * pox + (-cry * crz - srx * sry * srz) * poy) * cox +
-                          (crx * crz * pox - crx * srz * poy) * coy +
-                          ((sry * srz + cry * crz * srx) * pox + (crz * sry - cry * srx * srz) * poy) * coz;
-        row[0] = arz; row[1] = arx; row[2] = ary; row[3] = coz; row[4] = cox; row[5] = coy;
-        b = -c.w;
-      }
+      if (kFused && ok) rok = res_row(g, mg.by_id, ids, 1, corner, p, x0, y0, z0, row, b);
     }
-    // fp64 products (21 upper AtA entries, 6 AtB, count; 4 zero pads) reduced over the wave by a
-    // transposed butterfly: at each halving step a lane keeps half of its values and trades the
-    // other half with its partner, so 32 values cost 32 shuffles instead of 6 per value.  Lane l
-    // (bit 0 clear) ends with the wave sum of value res_index(l).
-    double v[16];
-    const bool up5 = (lane & 32) != 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const double lo = res_product(j, row, b, ok), hi = res_product(j + 16, row, b, ok);
-      v[j] = (up5 ? hi : lo) + __shfl_xor(up5 ? lo : hi, 32);
-    }
-    res_halve<8, 16>(v, lane);
-    res_halve<4, 8>(v, lane);
-    res_halve<2, 4>(v, lane);
-    res_halve<1, 2>(v, lane);
-    v[0] += __shfl_xor(v[0], 1);
-    const int ridx = ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 +
-                     ((lane >> 1) & 1);
-    if (!(lane & 1) && ridx < 28) red[wave][ridx] = v[0];
-    __syncthreads();
-    if (tid < 28) {
-      double s = 0.0;
-      for (int w = 0; w < kResThreads / 64; ++w) s += red[w][tid];
-      a.partial[(int64_t)it * kPartial + tid] = s;
-    }
-    __syncthreads();
+    if (kFused) res_reduce(red, tid, row, b, rok, a.partial + (int64_t)it * kPartial);
   }
 }
 
@@ -633,21 +659,27 @@ void launch_export_records(hipStream_t s, int B, const float* pose_out, const fb
 }
 
 void launch_gn_init(hipStream_t s, const GnArgs& a) { hipLaunchKernelGGL(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
-template <int R>
+template <int R, bool F>
 void launch_gn_knn_r(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
   const float invx = a.mc.g.inv_x;  // == a.ms.g.inv_x
-  if (invx > 4.0f) hipLaunchKernelGGL((k_gn_knn<R, 8>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
-  else if (invx > 2.0f) hipLaunchKernelGGL((k_gn_knn<R, 4>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
-  else if (invx > 1.0f) hipLaunchKernelGGL((k_gn_knn<R, 2>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
-  else hipLaunchKernelGGL((k_gn_knn<R, 1>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
+  if (invx > 4.0f) hipLaunchKernelGGL((k_gn_knn<R, 8, F>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
+  else if (invx > 2.0f) hipLaunchKernelGGL((k_gn_knn<R, 4, F>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
+  else if (invx > 1.0f) hipLaunchKernelGGL((k_gn_knn<R, 2, F>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
+  else hipLaunchKernelGGL((k_gn_knn<R, 1, F>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
 }
 
-void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter) {
+template <bool F>
+void launch_gn_knn_f(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
   const float inv = a.mc.g.inv_cell;  // == a.ms.g.inv_cell (fbr_set_map): y / z cells
-  const int use_prev = iter > 0;      // nbr holds this launch's previous iteration
-  if (inv > 2.0f) launch_gn_knn_r<4>(s, a, grid, use_prev);       // 0.25 m
-  else if (inv > 1.0f) launch_gn_knn_r<2>(s, a, grid, use_prev);  // 0.5 m
-  else launch_gn_knn_r<1>(s, a, grid, use_prev);                  // >= 1 m
+  if (inv > 2.0f) launch_gn_knn_r<4, F>(s, a, grid, use_prev);       // 0.25 m
+  else if (inv > 1.0f) launch_gn_knn_r<2, F>(s, a, grid, use_prev);  // 0.5 m
+  else launch_gn_knn_r<1, F>(s, a, grid, use_prev);                  // >= 1 m
+}
+
+void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fused) {
+  const int use_prev = iter > 0;  // nbr holds this launch's previous iteration
+  if (fused) launch_gn_knn_f<true>(s, a, grid, use_prev);
+  else launch_gn_knn_f<false>(s, a, grid, use_prev);
 }
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
   hipLaunchKernelGGL(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);
