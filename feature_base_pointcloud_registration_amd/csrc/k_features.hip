@@ -183,14 +183,22 @@ __device__ void greedy_rounds(int m, int lane, uint64_t (&und)[WMAX], uint64_t (
     for (int w = 0; w < WMAX; ++w) {
       if (w < nwm && und[w] != 0ull) {  // words whose candidates are all decided are skipped
         bool nt = false, tk = false;
-        if ((und[w] >> lane) & 1ull) {
+        const bool mine = (und[w] >> lane) & 1ull;
+        if (mine) {
           const uint32_t wt = win10(w > 0 ? tak[w - 1] : 0ull, tak[w], w + 1 < WMAX ? tak[w + 1] : 0ull, lane);
           const uint32_t wu = win10(w > 0 ? und[w - 1] : 0ull, und[w], w + 1 < WMAX ? und[w + 1] : 0ull, lane);
           if (wt & cmr[w]) nt = true;
           else if (!(wu & cmr[w])) tk = true;
         }
-        const uint64_t bt = __ballot(tk), bn = __ballot(nt);
+        const uint64_t bt = __ballot(tk);
         tak[w] |= bt;
+        // members suppressed by a member taken just now are decided in the same round (a
+        // monotone-priority run then resolves 6 members per round instead of 3)
+        if (bt != 0ull && mine && !tk && !nt) {
+          const uint32_t wt = win10(w > 0 ? tak[w - 1] : 0ull, tak[w], w + 1 < WMAX ? tak[w + 1] : 0ull, lane);
+          nt = (wt & cmr[w]) != 0u;
+        }
+        const uint64_t bn = __ballot(nt);
         und[w] &= ~(bt | bn);
         any |= und[w] != 0ull;
       }
