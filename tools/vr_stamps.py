@@ -10,7 +10,7 @@ R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, R)
 from feature_base_pointcloud_registration_amd import build  # noqa: E402
 
-diag = build.build_hip(defines=("FBR_VR_STAMPS",), name="libfbr_hip_vrdiag.so")
+diag = os.environ.get("FBR_DIAG_LIB") or build.build_hip(defines=("FBR_VR_STAMPS",), name="libfbr_hip_vrdiag.so")  # prebuilt diag lib (GPU box)
 os.environ["FBR_LIB"] = diag
 from feature_base_pointcloud_registration_amd import api, synth  # noqa: E402
 from feature_base_pointcloud_registration_amd.fbr_types import default_params  # noqa: E402
