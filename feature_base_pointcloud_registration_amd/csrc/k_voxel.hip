@@ -132,11 +132,11 @@ __device__ __forceinline__ auto lds_if(X* p) {
   else return p;
 }
 
-// Stable radix sort of kb[0]/vb[0] (n pairs), then one centroid per run of equal keys in
-// ascending key order: out[v] = mean of in[vals of the run].  Returns the voxel count (all threads).
+// Stable LSD radix sort of kb[0]/vb[0] (n pairs) over the low nbits key bits; returns the index
+// (0/1) of the buffers holding the sorted pairs.  Ends with a barrier.
 template <int T, typename V, int MAXD = 9, bool KV_LDS = true>
-__device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, uint32_t* hist, uint32_t* wsum,
-                            const float4* in, float4* out, int dbg = 0, unsigned long long* t_sorted = nullptr) {
+__device__ int vg_radix_sort(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, uint32_t* hist, uint32_t* wsum,
+                             int dbg = 0) {
   constexpr int NW = T / 64, NB = 1 << MAXD;  // digits of <= MAXD bits; hist rows of NB counters
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int passes = dbg == 1 ? 0 : (nbits + MAXD - 1) / MAXD;
@@ -211,6 +211,19 @@ __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, u
     cur ^= 1;
     __syncthreads();
   }
+  return cur;
+}
+
+// Stable radix sort of kb[0]/vb[0] (n pairs), then one centroid per run of equal keys in
+// ascending key order: out[v] = mean of in[vals of the run].  Returns the voxel count (all threads).
+template <int T, typename V, int MAXD = 9, bool KV_LDS = true>
+__device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, uint32_t* hist, uint32_t* wsum,
+                            const float4* in, float4* out, int dbg = 0, unsigned long long* t_sorted = nullptr) {
+  constexpr int NW = T / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int chunk = (((n + NW - 1) / NW) + 63) & ~63;
+  const int c0 = min(n, w * chunk), c1 = min(n, c0 + chunk);
+  const int cur = vg_radix_sort<T, V, MAXD, KV_LDS>(kb, vb, n, nbits, hist, wsum, dbg);
   const auto ks = lds_if<KV_LDS>(kb[cur]);
   const auto vs = lds_if<KV_LDS>(vb[cur]);
   if (t_sorted && threadIdx.x == 0) *t_sorted = __builtin_amdgcn_s_memtime();
@@ -447,12 +460,15 @@ k_voxel_ring(VgRing A) {
   VgGrid G;
   G.init(mn, mx, A.leaf, false);
   unsigned char* q = smem + ((((unsigned char*)(cnts + KPT * NW) - smem) + 15) & ~15);  // keeps the LDS address space
-  uint32_t* kb[2];
-  uint16_t* vb[2];
+  const int cap = (int)A.cap;
+  uint32_t* kb[2];   // [0]: candidate keys in index order, then run keys; sort ping-pong
+  uint16_t* vb[2];   // run ids; sort ping-pong
   kb[0] = (uint32_t*)q;
-  kb[1] = kb[0] + A.cap;
-  vb[0] = (uint16_t*)(kb[1] + A.cap);
-  vb[1] = vb[0] + A.cap;
+  kb[1] = kb[0] + cap;
+  vb[0] = (uint16_t*)(kb[1] + cap);
+  vb[1] = vb[0] + cap;
+  uint16_t* off = vb[1] + cap;  // [cap] ring offset of the t-th candidate
+  uint16_t* rst = off + cap;    // [cap + 1] first candidate of each run, rst[R] = n
   if (G.overflow) {  // output = input, in index order
 #pragma unroll
     for (int r = 0; r < KPT; ++r)
@@ -464,11 +480,119 @@ k_voxel_ring(VgRing A) {
   for (int r = 0; r < KPT; ++r)
     if (cd[r]) {
       kb[0][pos[r]] = G.key(CL[r * T + tid]);  // re-read (L2): no point registers live across the barrier
-      vb[0][pos[r]] = (uint16_t)(r * T + tid);  // offset from the ring start s
+      off[pos[r]] = (uint16_t)(r * T + tid);   // offset from the ring start s
     }
   __syncthreads();
   VR_TS(2);
-  const int total = vg_sort_emit<T, uint16_t, MAXD>(kb, vb, n, G.nbits, hist, wsum, CL, out, A.dbg, VR_TS_PTR);
+  // Runs of equal keys in index order (points adjacent along the ring share voxels: ~6.6
+  // candidates per run on C2, and nearly one run per voxel).  Only the runs are sorted; the
+  // stable sort keeps a voxel's runs in index order, so its points are still summed in index order.
+  const int chunk = (((n + NW - 1) / NW) + 63) & ~63;
+  const int c0 = min(n, w * chunk), c1 = min(n, c0 + chunk);
+  uint32_t rkey[KPT];
+  uint64_t hb[KPT];
+  int nrun = 0;
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int t = c0 + 64 * k + lane;
+    const bool valid = t < c1;
+    const uint32_t key = valid ? kb[0][t] : 0u;
+    hb[k] = __ballot(valid && (t == 0 || kb[0][t - 1] != key));
+    rkey[k] = key;
+    nrun += __popcll(hb[k]);
+  }
+  if (lane == 0) wsum[w] = (uint32_t)nrun;
+  __syncthreads();  // every candidate key is read before the run keys overwrite them
+  int rq = 0, R = 0;
+  for (int ww = 0; ww < NW; ++ww) {
+    const int cw = (int)wsum[ww];
+    rq += ww < w ? cw : 0;
+    R += cw;
+  }
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    if ((hb[k] >> lane) & 1ull) {
+      const int qq = rq + __popcll(hb[k] & ((1ull << lane) - 1ull));
+      kb[0][qq] = rkey[k];
+      vb[0][qq] = (uint16_t)qq;
+      rst[qq] = (uint16_t)(c0 + 64 * k + lane);
+    }
+    rq += __popcll(hb[k]);
+  }
+  if (tid == 0) rst[R] = (uint16_t)n;
+  __syncthreads();
+  const int cur = vg_radix_sort<T, uint16_t, MAXD>(kb, vb, R, G.nbits, hist, wsum, A.dbg);
+  VR_TS(3);
+  if (A.dbg == 2) {
+    if (tid == 0) A.cnt_out[slot] = 0;
+    return;
+  }
+  // voxels = groups of equal keys in sorted run order: voxel index of each group's first run and
+  // the next run of the same voxel, scattered by run id into the free ping-pong halves
+  const FBR_LDS_AS uint32_t* ks = (const FBR_LDS_AS uint32_t*)kb[cur];
+  const FBR_LDS_AS uint16_t* vs = (const FBR_LDS_AS uint16_t*)vb[cur];
+  FBR_LDS_AS int32_t* nxt = (FBR_LDS_AS int32_t*)kb[cur ^ 1];
+  FBR_LDS_AS uint16_t* vox = (FBR_LDS_AS uint16_t*)vb[cur ^ 1];
+  const int rchunk = (((R + NW - 1) / NW) + 63) & ~63;
+  const int r0 = min(R, w * rchunk), r1 = min(R, r0 + rchunk);
+  int nh = 0;
+  for (int i0 = r0; i0 < r1; i0 += 64) {
+    const int i = i0 + lane;
+    nh += __popcll(__ballot(i < r1 && (i == 0 || ks[i] != ks[i - 1])));
+  }
+  if (lane == 0) wsum[w] = (uint32_t)nh;
+  __syncthreads();
+  int vpos = 0, total = 0;
+  for (int ww = 0; ww < NW; ++ww) {
+    const int cw = (int)wsum[ww];
+    vpos += ww < w ? cw : 0;
+    total += cw;
+  }
+  for (int i0 = r0; i0 < r1; i0 += 64) {
+    const int i = i0 + lane;
+    const bool valid = i < r1;
+    const uint32_t key = valid ? ks[i] : 0u;
+    const bool head = valid && (i == 0 || ks[i - 1] != key);
+    const uint64_t bh = __ballot(head);
+    if (valid) {
+      const int rid = vs[i];
+      vox[rid] = head ? (uint16_t)(vpos + __popcll(bh & ((1ull << lane) - 1ull))) : (uint16_t)0xFFFFu;
+      nxt[rid] = (i + 1 < R && ks[i + 1] == key) ? (int32_t)vs[i + 1] : -1;
+    }
+    vpos += __popcll(bh);
+  }
+  __syncthreads();
+  // one lane per voxel (at its first run, in index order): the reference's serial float sum over
+  // the voxel's points in index order, four loads in flight
+  for (int rid = tid; rid < R; rid += T) {
+    const int v = vox[rid];
+    if (v == 0xFFFF) continue;
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    int cnt = 0;
+    for (int qq = rid; qq >= 0; qq = nxt[qq]) {
+      const int t0 = rst[qq], t1 = rst[qq + 1];
+      for (int t = t0; t < t1; t += 4) {
+        float4 pp[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pp[u] = CL[off[min(t + u, t1 - 1)]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (t + u < t1) {
+            if (cnt == 0) {
+              c = pp[u];
+            } else {
+              c.x += pp[u].x;
+              c.y += pp[u].y;
+              c.z += pp[u].z;
+              c.w += pp[u].w;
+            }
+            ++cnt;
+          }
+      }
+    }
+    const float fc = (float)cnt;
+    out[v] = make_float4(c.x / fc, c.y / fc, c.z / fc, c.w / fc);
+  }
   if (tid == 0) A.cnt_out[slot] = total;
 #ifdef FBR_VR_STAMPS
   VR_TS(4);
@@ -483,7 +607,8 @@ size_t voxel_ring_lds_bytes(const VgRing& a, int threads, int kpt) {
   const int nw = threads / 64;
   size_t b = sizeof(uint32_t) * ((size_t)(nw + 1) * 256 + nw) + sizeof(float) * nw * 6 + sizeof(int) * kpt * nw;
   b = (b + 15) & ~(size_t)15;
-  return b + (size_t)a.cap * 2 * (sizeof(uint32_t) + sizeof(uint16_t)) + 16;
+  // keys / run ids ping-pong + candidate offsets + run starts
+  return b + (size_t)a.cap * 2 * (sizeof(uint32_t) + sizeof(uint16_t)) + (size_t)(2 * a.cap + 1) * sizeof(uint16_t) + 16;
 }
 
 void launch_voxel_ring(hipStream_t s, const VgRing& a) {
