@@ -662,22 +662,23 @@ k_features(FeatArgs a) {
 #pragma unroll
           for (int d = 0; d < 11; ++d) cv[d] = S.scurv[max(li + d - 5, 0) - S.sbase];
           const float vu = cv[5];
-          uint32_t nb = 0, hc = 0;
+          // neighbour bits (bit 4+d forward, 5-d backward) as ranges: forward d <= min(f, m-u),
+          // backward d <= min(b, u); ep (member m) outranks every neighbour
+          const int lf = min(f, m - u), lb = min(b, u);
+          const uint32_t nbf = ((1u << lf) - 1u) << 5, nbb = ((1u << lb) - 1u) << (5 - lb);
+          const uint32_t epb = (m - u >= 1 && m - u <= 5) ? 1u << (4 + m - u) : 0u;
+          uint32_t gt = 0, eq = 0;
 #pragma unroll
-          for (int d = 1; d <= 5; ++d) {  // branch-free: masks from bitwise predicates
-            const bool fv = (d <= f) & (u + d <= m);  // u < m here
-            const float vf = cv[5 + d];
-            const bool fh = (u + d == m) | (vf > vu);
-            nb |= (uint32_t)fv << (4 + d);
-            hc |= (uint32_t)(fv & fh) << (4 + d);
-            tf |= fv & !fh & !(vf < vu);
-            const bool bv = (d <= b) & (u - d >= 0);
-            const float vb = cv[5 - d];
-            const bool notep = u != m;  // ep outranks every neighbour
-            nb |= (uint32_t)bv << (5 - d);
-            hc |= (uint32_t)(bv & notep & (vb > vu)) << (5 - d);
-            tf |= bv & notep & !(vb > vu) & !(vb < vu);
+          for (int d = 1; d <= 5; ++d) {
+            gt |= (cv[5 + d] > vu ? 1u : 0u) << (4 + d);
+            eq |= (!(cv[5 + d] < vu || cv[5 + d] > vu) ? 1u : 0u) << (4 + d);  // equal or NaN
+            gt |= (cv[5 - d] > vu ? 1u : 0u) << (5 - d);
+            eq |= (!(cv[5 - d] < vu || cv[5 - d] > vu) ? 1u : 0u) << (5 - d);
           }
+          const uint32_t notep = u != m ? ~0u : 0u;
+          const uint32_t nb = nbf | nbb;
+          const uint32_t hc = ((gt | epb) & nbf) | (gt & nbb & notep);
+          tf |= ((eq & ~epb & nbf) | (eq & nbb & notep)) != 0u;
           S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
         }
       }
