@@ -651,44 +651,46 @@ void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
   }
 }
 
-// One workgroup per job: ring-ordered concatenation of the per-ring corner picks and per-ring
-// surf DS outputs (cornerCloud / surfaceCloud of featureExtraction.h).
+// Ring-ordered concatenation of the per-ring corner picks and per-ring surf DS outputs
+// (cornerCloud / surfaceCloud of featureExtraction.h).  One wave per (job, ring), 4 rings per
+// workgroup: the wave sums the counts of the rings before its own (lanes over rings, a shuffle
+// reduction) and copies its ring's corner picks and surf DS points to their offsets; the last
+// ring's wave writes the job totals.
 __global__ void __launch_bounds__(256)
 k_concat(int H, int W, const float4* corner_slot, const int32_t* corner_cnt, const float4* surf_ring,
          const int32_t* surf_ring_cnt, float4* corner_all, int64_t capc, int32_t* n_corner, float4* surf_all,
          int64_t caps, int32_t* n_surf) {
-  extern __shared__ int32_t off[];  // [2][H+1]
-  const int job = blockIdx.x, tid = threadIdx.x;
+  const int lane = threadIdx.x & 63, rpj = (H + 3) / 4;
+  const int job = blockIdx.x / rpj, r = (blockIdx.x % rpj) * 4 + (threadIdx.x >> 6);
+  if (r >= H) return;
   const int32_t* cc = corner_cnt + job * H;
   const int32_t* sc = surf_ring_cnt + job * H;
-  if (tid == 0) {
-    int a = 0, b = 0;
-    for (int r = 0; r < H; ++r) {
-      off[r] = a;
-      off[H + 1 + r] = b;
-      a += cc[r];
-      b += sc[r];
-    }
-    off[H] = a;
-    off[2 * H + 1] = b;
-    n_corner[job] = a;
-    n_surf[job] = b;
+  int oc = 0, os = 0;
+  for (int k = lane; k < r; k += 64) {
+    oc += cc[k];
+    os += sc[k];
   }
-  __syncthreads();
-  for (int r = 0; r < H; ++r) {
-    const int nc = cc[r], ns = sc[r];
-    const float4* cs = corner_slot + ((int64_t)job * H + r) * kCornerPerRing;
-    const float4* ss = surf_ring + ((int64_t)job * H + r) * W;
-    for (int i = tid; i < nc; i += 256) corner_all[job * capc + off[r] + i] = cs[i];
-    for (int i = tid; i < ns; i += 256) surf_all[job * caps + off[H + 1 + r] + i] = ss[i];
+  for (int o = 32; o > 0; o >>= 1) {
+    oc += __shfl_xor(oc, o);
+    os += __shfl_xor(os, o);
   }
+  const int nc = cc[r], ns = sc[r];
+  if (r == H - 1 && lane == 0) {
+    n_corner[job] = oc + nc;
+    n_surf[job] = os + ns;
+  }
+  const float4* cs = corner_slot + ((int64_t)job * H + r) * kCornerPerRing;
+  const float4* ss = surf_ring + ((int64_t)job * H + r) * W;
+  for (int i = lane; i < nc; i += 64) corner_all[job * capc + oc + i] = cs[i];
+  for (int i = lane; i < ns; i += 64) surf_all[job * caps + os + i] = ss[i];
 }
 
 void launch_concat(hipStream_t s, int B, int H, int W, const float4* corner_slot, const int32_t* corner_cnt,
                    const float4* surf_ring, const int32_t* surf_ring_cnt, float4* corner_all, int64_t capc,
                    int32_t* n_corner, float4* surf_all, int64_t caps, int32_t* n_surf) {
-  hipLaunchKernelGGL(k_concat, dim3(B), dim3(256), sizeof(int32_t) * 2 * (H + 1), s, H, W, corner_slot,
-                     corner_cnt, surf_ring, surf_ring_cnt, corner_all, capc, n_corner, surf_all, caps, n_surf);
+  if (B <= 0 || H <= 0) return;
+  hipLaunchKernelGGL(k_concat, dim3(B * ((H + 3) / 4)), dim3(256), 0, s, H, W, corner_slot, corner_cnt, surf_ring,
+                     surf_ring_cnt, corner_all, capc, n_corner, surf_all, caps, n_surf);
 }
 
 
