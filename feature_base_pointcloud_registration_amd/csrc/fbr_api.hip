@@ -557,6 +557,18 @@ bool gn_fused() {
   return v;
 }
 
+// Tail mode: once at most 1/FBR_GN_TAIL of a sub-batch's jobs are still iterating (default 8),
+// its iterations run fused (kNN + residual in one launch) on a smaller grid: the few remaining
+// jobs' work is latency-bound, so one launch less per iteration and fewer idle workgroups
+// matter more than the fused kernel's register cost (0 disables).
+int gn_tail_div() {
+  static const int v = [] {
+    const char* e = std::getenv("FBR_GN_TAIL");
+    return e ? std::max(0, std::atoi(e)) : 8;
+  }();
+  return v;
+}
+
 // The Gauss-Newton iterations of one or two sub-batches.  Iterations run on the device without
 // host round trips; for each sub-batch the host stays kLag iterations ahead and stops enqueueing
 // once its k_gn_solve reports that no job is active (flags in host-mapped memory).
@@ -566,9 +578,11 @@ int register_iterate(fbr_ctx* c, const Sub* subs, int nsub, bool trace) {
   const int mi = std::max(1, c->P.max_iterations);
   GnArgs a[kMaxSub];
   bool live[kMaxSub] = {}, watch[kMaxSub] = {};
+  int active[kMaxSub] = {};  // jobs still iterating kLag iterations ago (an upper bound now)
   for (int k = 0; k < nsub; ++k) {
     a[k] = gn_args(c, subs[k], trace);
     live[k] = true;
+    active[k] = subs[k].B;
     watch[k] = c->h_iter_flags != nullptr;
   }
   for (int it = 0; it < c->P.max_iterations; ++it) {
@@ -589,13 +603,15 @@ int register_iterate(fbr_ctx* c, const Sub* subs, int nsub, bool trace) {
           }
           v = *f;
         }
-        if (watch[k] && (v & 0xFFFFFFFFull) == 0) {
+        if (watch[k]) active[k] = (int)(v & 0xFFFFFFFFull);
+        if (watch[k] && active[k] == 0) {
           live[k] = false;
           continue;
         }
       }
-      const int grid = std::max(1, std::min(a[k].max_items, gn_grid_cap()));
-      if (gn_fused()) {
+      const bool tail = gn_tail_div() > 0 && (int64_t)active[k] * gn_tail_div() <= sb.B;
+      const int grid = std::max(1, std::min(a[k].max_items, tail ? std::min(gn_grid_cap(), 1024) : gn_grid_cap()));
+      if (gn_fused() || tail) {
         TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a[k], grid, it, true));
       } else {
         TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a[k], grid, it, false));

@@ -21,10 +21,11 @@
 //     that provably never exceeds a member point's computed distance (see axis_lb).
 //   * k_gn_knn: one lane per query (corner and surf queries of every active job of the batch are
 //     packed into 256-query work items; the mapping-DS clouds are in Morton order, so a wave's
-//     queries are spatially compact); writes 5 neighbour positions per query.
+//     queries are spatially compact); writes the 5 neighbours' map indices per query.
 //   * k_gn_residual: gathers the 5 neighbours, residual and Jacobian row in float with the
 //     reference's operation order; the 21+6 normal-equation products are reduced in fp64
-//     (OpenCV's CV_32F gemm accumulates in double) by wave shuffles into one partial per item.
+//     (OpenCV's CV_32F gemm accumulates in double) by a transposed wave butterfly into one
+//     partial per item.  (k_gn_knn<.., true> does both in one launch: the GN tail mode.)
 //   * k_gn_solve: one lane per job sums its items in order (corner items, then surf items: the
 //     combineOptimizationCoeffs row order), rounds AtA/AtB to float and runs the reference's float
 //     QR solve / Jacobi / LU; the Gauss-Newton state never leaves the device.
