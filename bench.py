@@ -247,11 +247,15 @@ def main():
         S = min(args.cpu_sample, B)
         omap = O.Map(P, corner_map, surf_map)
         ref = np.zeros((S, 6), np.float32)
+        ref_iters, ref_nsel = np.zeros(S), np.zeros(S)
+        O.stage_ms(reset=True)
         t1 = time.perf_counter()
         for j in range(S):
             stream = O.Stream(P)  # independent job: fresh FeatureExtraction state
-            ref[j], _ = stream.process_scan(omap, scans[j], 0.0, guesses[j], n_threads=P.number_of_cores)
+            ref[j], st = stream.process_scan(omap, scans[j], 0.0, guesses[j], n_threads=P.number_of_cores)
+            ref_iters[j], ref_nsel[j] = st["iterations"], st["n_sel"]
         cpu_s = time.perf_counter() - t1
+        stage = O.stage_ms()
         dt = poses[:S, 3:] - ref[:, 3:]
         dr = np.angle(np.exp(1j * (poses[:S, :3].astype(np.float64) - ref[:, :3])))
         result["cpu_baseline"] = {
@@ -262,6 +266,10 @@ def main():
             "sample": f"first {S} of the {B} {cfg} jobs, whole path (projection, features, "
                       f"registration incl. per-scan KD-tree build), OpenMP {P.number_of_cores} threads "
                       f"(numberOfCores), host nproc={os.cpu_count()}",
+            # per-stage oracle time (A2/A4, A6-A9, A11, A12, A13 KD build, A13-A18 GN)
+            "stage_ms_per_scan": {k: round(v / S, 3) for k, v in stage.items()},
+            "mean_gn_iterations": float(ref_iters.mean()),
+            "mean_n_sel": float(ref_nsel.mean()),
         }
         result["pose_rmse_vs_ref"] = {
             "trans_m": float(np.sqrt(np.mean(np.sum(dt.astype(np.float64) ** 2, axis=1)))),

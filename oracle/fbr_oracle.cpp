@@ -21,7 +21,9 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
+#include <chrono>
 #include <climits>
 #include <cstdlib>
 #include <cmath>
@@ -914,6 +916,25 @@ static void crop(const std::vector<P4>& in, const float mn[3], const float mx[3]
   }
 }
 
+// Per-stage wall time accumulators for the CPU baseline report: A2/A4 projection,
+// A6-A9 features, A11 CropBox, A12 downsampleCurrentScan, A13 KD-tree builds, A13-A18 GN
+// iterations.  Relaxed atomics: the all-cores run calls process_scan from several threads.
+static std::atomic<int64_t> g_stage_ns[6];
+struct StageTimer {  // charges the time since the last lap to stage k; the destructor closes it
+  int k;
+  std::chrono::steady_clock::time_point t0;
+  explicit StageTimer(int k_) : k(k_), t0(std::chrono::steady_clock::now()) {}
+  void lap(int next) {
+    const auto t1 = std::chrono::steady_clock::now();
+    if (k >= 0)
+      g_stage_ns[k].fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count(),
+                              std::memory_order_relaxed);
+    k = next;
+    t0 = t1;
+  }
+  ~StageTimer() { lap(-1); }
+};
+
 static void registration_core(const fbr_params& P, const Map& map, const P4* cornerLast, int64_t ncl,
                               const P4* surfLast, int64_t nsl, float tr[6], RegResult& R, int nthreads,
                               const fbr_deskew_table* T = nullptr, bool no_crop = false) {
@@ -927,6 +948,7 @@ static void registration_core(const fbr_params& P, const Map& map, const P4* cor
     mn[i] = -P.crop_half[i] + origin[i];
     mx[i] = P.crop_half[i] + origin[i];
   }
+  StageTimer tm(2);
   std::vector<P4> cornerMap, surfMap;
   if (no_crop) {  // LIO-SAM path: scan2MapOptimization on laserCloud*FromMapDS as extracted
     cornerMap = map.corner;
@@ -937,6 +959,7 @@ static void registration_core(const fbr_params& P, const Map& map, const P4* cor
   }
   st.n_corner_map = (int)cornerMap.size();
   st.n_surf_map = (int)surfMap.size();
+  tm.lap(3);
   // downsampleCurrentScan (:981-993)
   std::vector<P4> cornerDS, surfDS;
   voxel_grid(cornerLast, ncl, P.mapping_corner_leaf_size, cornerDS);
@@ -945,6 +968,7 @@ static void registration_core(const fbr_params& P, const Map& map, const P4* cor
   st.n_corner_ds = Nc;
   st.n_surf_ds = Ns;
   // scan2MapOptimization (:1403-1442)
+  tm.lap(4);
   if (!(Nc > P.edge_feature_min_valid_num && Ns > P.surf_feature_min_valid_num)) {
     st.status = FBR_REG_NOT_ENOUGH_FEATURES;
     return;
@@ -952,6 +976,7 @@ static void registration_core(const fbr_params& P, const Map& map, const P4* cor
   KDTree kdc, kds;
   kdc.build(cornerMap.data(), (int)cornerMap.size());
   kds.build(surfMap.data(), (int)surfMap.size());
+  tm.lap(5);
   std::vector<P4> oriC(Nc), coeffC(Nc), oriS(Ns), coeffS(Ns);
   std::vector<char> flagC(Nc), flagS(Ns);
   bool isDegenerate = false;
@@ -1350,10 +1375,13 @@ int orc_register(const fbr_params* P, void* map, const fbr_point_xyzi* corner, i
 int orc_process_scan(void* s, void* map, const fbr_point_xyzirt* pts, int64_t n_in, double stamp, float pose[6],
                      fbr_reg_stats* st, int nthreads) {
   orc_stream* S = (orc_stream*)s;
+  StageTimer tm(0);
   Projection pr;
   project(S->P, pts, n_in, pr, S->table());
+  tm.lap(1);
   Features F;
   extract_features(S->P, S->fs, pr, F);
+  tm.lap(-1);
   RegResult R;
   std::memset(&R.st, 0, sizeof(R.st));
   if (stamp - S->timeLastProcessing >= S->P.mapping_process_interval) {
@@ -1528,5 +1556,15 @@ void orc_sort_smoothness(const float* values, int64_t n, int64_t* ind_out) {
   for (int64_t i = 0; i < n; ++i) ind_out[i] = (int64_t)v[i].ind;
 }
 int orc_num_threads_max(void) { return omp_get_max_threads(); }
+
+// Accumulated per-stage wall time (ms) of process_scan / register calls since the last reset:
+// [A2/A4 projection, A6-A9 features, A11 CropBox, A12 downsampleCurrentScan, A13 KD-tree builds,
+//  A13-A18 Gauss-Newton iterations].
+void orc_stage_ms(double out[6], int reset) {
+  for (int k = 0; k < 6; ++k) {
+    if (out) out[k] = (double)g_stage_ns[k].load(std::memory_order_relaxed) * 1e-6;
+    if (reset) g_stage_ns[k].store(0, std::memory_order_relaxed);
+  }
+}
 
 }  // extern "C"

@@ -66,6 +66,7 @@ def lib():
         L.orc_colpiv_solve.argtypes = [_VP, _VP, _VP]
         L.orc_knn5.argtypes = [_VP, _I64, _VP, _I64, _VP, _VP]
         L.orc_sort_smoothness.argtypes = [_VP, _I64, _VP]
+        L.orc_stage_ms.argtypes = [_VP, ctypes.c_int]
         _LIB = L
     return _LIB
 
@@ -176,6 +177,17 @@ class Map:
             lib().orc_map_destroy(self.h)
         except Exception:
             pass
+
+
+STAGES = ["A2_A4_projection", "A6_A9_features", "A11_cropbox", "A12_downsample", "A13_kdtree_build",
+          "A13_A18_gn_iterations"]
+
+
+def stage_ms(reset=False):
+    """Accumulated per-stage oracle wall time in ms since the last reset (dict by stage)."""
+    out = np.zeros(6, np.float64)
+    lib().orc_stage_ms(ptr(out), 1 if reset else 0)
+    return dict(zip(STAGES, out.tolist()))
 
 
 def affine_from_pose(pose):
