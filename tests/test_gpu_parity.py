@@ -277,6 +277,27 @@ def test_batch_matches_single_and_oracle(c2_map):
         assert_pose_close(poses[k], po)
 
 
+def test_batch_tail_mode_matches_oracle(c2_map):
+    """24 jobs = 3 sub-batches of 8: each sub-batch's last iterating job runs its final Gauss-Newton
+    iterations in tail mode (fused kNN + residual launch, fbr_api.hip gn_tail_div); every pose and
+    iteration count still matches the oracle."""
+    H, W = synth.CONFIGS["C2"][:2]
+    B = 24
+    P = default_params(H, W, max_batch=B)
+    jobs = synth.make_jobs("C2", B, base_seed=3000)
+    m = O.Map(P, *c2_map)
+    with api.Context(P) as ctx:
+        ctx.set_map(*c2_map)
+        poses, stats = ctx.process_batch([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
+    iters = []
+    for k, (pts, guess, gt) in enumerate(jobs):
+        po, so = O.Stream(P).process_scan(m, pts, 0.0, guess)
+        assert stats["status"][k] == 0 and stats["iterations"][k] == so["iterations"]
+        assert_pose_close(poses[k], po)
+        iters.append(so["iterations"])
+    assert max(iters) > min(iters)  # the sub-batches have stragglers, i.e. tail iterations
+
+
 def test_full_size_batch_properties(c2_map):
     """BASELINE sizes (C2, 64 jobs): every job registers, converges near ground truth."""
     H, W = synth.CONFIGS["C2"][:2]
