@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = [
     "fbr_register", "fbr_register_trace", "fbr_process_scan", "fbr_reset_stream",
     "fbr_process_batch", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
     "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
-    "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math",
+    "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math", "fbr_selftest_eigen6",
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
     "fbr_msg_to_points", "fbr_points_to_msg_data", "fbr_project_msg", "fbr_process_msg",
     "fbr_imu_convert", "fbr_imu_deskew_info", "fbr_set_deskew", "fbr_stream_copy_bandwidth",
@@ -89,6 +89,7 @@ def lib():
             "fbr_affine_from_pose": (None, [_VP, _VP]),
             "fbr_pose_from_affine": (None, [_VP, _VP]),
             "fbr_selftest_math": (ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP]),
+            "fbr_selftest_eigen6": (ctypes.c_int, [ctypes.c_int, _VP, _VP]),
             "fbr_load_map": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_char_p]),
             "fbr_pcd_read": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64, _VP]),
             "fbr_pcd_write_ascii": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64]),
@@ -138,6 +139,16 @@ def selftest_math(a, b):
     out = np.zeros((len(a), 4), np.float32)
     _check(lib().fbr_selftest_math(len(a), ptr(a), ptr(b), ptr(out)), "fbr_selftest_math")
     return out
+
+
+def selftest_eigen6(mats):
+    """cv::eigen of symmetric 6x6 float matrices on the device (see fbr_selftest_eigen6): returns
+    (single-lane (W, V), wave-parallel (W, V)), W (n, 6) descending, V (n, 6, 6) rows = vectors."""
+    a = np.ascontiguousarray(mats, np.float32).reshape(-1, 36)
+    out = np.zeros((len(a), 84), np.float32)
+    _check(lib().fbr_selftest_eigen6(len(a), ptr(a), ptr(out)), "fbr_selftest_eigen6")
+    n = len(a)
+    return ((out[:, :6], out[:, 6:42].reshape(n, 6, 6)), (out[:, 42:48], out[:, 48:].reshape(n, 6, 6)))
 
 
 def stream_copy_bandwidth(device=0, nbytes=2 << 30, iters=20):

@@ -301,6 +301,123 @@ __device__ void jacobi_eigen_lds(float* A, float* W, float* V, int* indR, int* i
 #undef C_
 }
 
+// LDS writes of this wave visible to all its lanes (no workgroup barrier: the other waves of the
+// workgroup do not take part).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// The same algorithm by one whole wave on shared arrays (A, V: N*N; W, indR, indC: N).  Every lane
+// finds the pivot (uniform LDS reads); the element pairs of one rotation are disjoint, so lane i
+// rotates the A pair and lane N+i the V pair of index i with the per-element operations of
+// jac_step; lanes 0 and 1 refresh the row / column maxima of k and l.  Same rotation sequence and
+// float results as jacobi_eigen<N> in a fraction of its dependent-instruction chain.
+template <int N>
+__device__ void jacobi_eigen_wave(float* A, float* W, float* V, int* indR, int* indC) {
+  static_assert(2 * N <= 64 && N * N <= 64, "one wave");
+  const int lane = threadIdx.x & 63;
+  const float eps = FLT_EPSILON;
+  if (lane < N * N) V[lane] = (lane / N == lane % N) ? 1.0f : 0.0f;
+  auto update_ind = [&](int idx) {
+    float mv;
+    if (idx < N - 1) {
+      int m = idx + 1;
+      mv = fabsf(A[N * idx + m]);
+      for (int i = idx + 2; i < N; i++) {
+        float val = fabsf(A[N * idx + i]);
+        if (mv < val) mv = val, m = i;
+      }
+      indR[idx] = m;
+    }
+    if (idx > 0) {
+      int m = 0;
+      mv = fabsf(A[idx]);
+      for (int i = 1; i < idx; i++) {
+        float val = fabsf(A[N * i + idx]);
+        if (mv < val) mv = val, m = i;
+      }
+      indC[idx] = m;
+    }
+  };
+  if (lane < N) {
+    W[lane] = A[(N + 1) * lane];
+    update_ind(lane);
+  }
+  wave_lds_sync();
+  const int maxIters = N * N * 30;
+  for (int iters = 0; iters < maxIters; iters++) {
+    int k = 0;
+    float mv = fabsf(A[indR[0]]);
+    for (int i = 1; i < N - 1; i++) {
+      float val = fabsf(A[N * i + indR[i]]);
+      if (mv < val) mv = val, k = i;
+    }
+    int l = indR[k];
+    for (int i = 1; i < N; i++) {
+      float val = fabsf(A[N * indC[i] + i]);
+      if (mv < val) mv = val, k = indC[i], l = i;
+    }
+    k = __builtin_amdgcn_readfirstlane(k);
+    l = __builtin_amdgcn_readfirstlane(l);
+    const float p = A[N * k + l];
+    if (fabsf(p) <= eps) break;
+    const float wl = W[l], wk = W[k];
+    float y = (float)((double)(wl - wk) * 0.5);
+    float t = fabsf(y) + cvhypot(p, y);
+    float s = cvhypot(p, t);
+    float c = t / s;
+    s = p / s;
+    t = (p / t) * p;
+    if (y < 0.0f) s = -s, t = -t;
+    wave_lds_sync();  // every lane has read the pivot row / column state
+    if (lane < N) {
+      const int i = lane;
+      int e0 = -1, e1 = -1;
+      if (i < k) e0 = N * i + k, e1 = N * i + l;
+      else if (i > k && i < l) e0 = N * k + i, e1 = N * i + l;
+      else if (i > l) e0 = N * k + i, e1 = N * l + i;
+      if (e0 >= 0) {
+        const float a0 = A[e0], b0 = A[e1];
+        A[e0] = a0 * c - b0 * s;
+        A[e1] = a0 * s + b0 * c;
+      }
+      if (i == 0) {
+        A[N * k + l] = 0.0f;
+        W[k] = wk - t;
+        W[l] = wl + t;
+      }
+    } else if (lane < 2 * N) {
+      const int i = lane - N;
+      const float a0 = V[N * k + i], b0 = V[N * l + i];
+      V[N * k + i] = a0 * c - b0 * s;
+      V[N * l + i] = a0 * s + b0 * c;
+    }
+    wave_lds_sync();
+    if (lane < 2) update_ind(lane == 0 ? k : l);
+    wave_lds_sync();
+  }
+  if (lane == 0) {
+    for (int k = 0; k < N - 1; k++) {
+      int m = k;
+      for (int i = k + 1; i < N; i++)
+        if (W[m] < W[i]) m = i;
+      if (k != m) {
+        float t = W[m];
+        W[m] = W[k];
+        W[k] = t;
+        for (int i = 0; i < N; i++) {
+          float u = V[N * m + i];
+          V[N * m + i] = V[N * k + i];
+          V[N * k + i] = u;
+        }
+      }
+    }
+  }
+  wave_lds_sync();
+}
+
 // OpenCV QRImpl (Householder) for a 6x6 system, eps = FLT_EPSILON*10; returns 0 if singular.
 __device__ int qr_solve6(float* A, float* b) {
   const int n = 6, m = 6;

@@ -40,6 +40,7 @@ namespace fbr {
 
 namespace {
 constexpr int kResThreads = 256;
+constexpr int kSolveThreads = 128;  // k_gn_solve: wave 0 sums + solves, wave 1 the iteration-0 degeneracy
 constexpr int kPartial = 32;  // doubles per item partial: 21 AtA upper + 6 AtB + count
 }
 
@@ -490,8 +491,68 @@ k_gn_knn(GnArgs a, int use_prev) {
   }
 }
 
-// One job's LMOptimization step on one lane (acc = the job's summed normal-equation products).
-__device__ void gn_solve_job(const GnArgs& a, int job, const double* acc) {
+// The normal equations of one job in float, as LMOptimization forms them (matAtA / matAtB).
+__device__ __forceinline__ void gn_normal_eq(const double* acc, float* AtA, float* X) {
+  int q = 0;
+  for (int r = 0; r < 6; ++r)
+    for (int c = r; c < 6; ++c) {
+      AtA[r * 6 + c] = (float)acc[q];
+      AtA[c * 6 + r] = (float)acc[q];
+      ++q;
+    }
+  for (int r = 0; r < 6; ++r) X[r] = (float)acc[21 + r];
+}
+
+// Iteration-0 degeneracy projection (:1280-1305): 6x6 Jacobi, eigenvalues < 100 zero rows of V2,
+// matP = V^-1 * V2 by LU.  It depends only on AtA, so the second wave of k_gn_solve computes it
+// (the Jacobi rotations spread over its lanes, jacobi_eigen_wave) while the first solves
+// AtA X = AtB.  All 64 lanes of the wave call it; matP / degenerate are written by lane 0.
+struct EigenLds {
+  float A[36], V[36], W[6];
+  int R[6], C[6];
+};
+__device__ void gn_degeneracy(const double* acc, EigenLds& e, float* matP, int* degenerate) {
+  const int lane = threadIdx.x & 63;
+  if (lane < 36) {
+    const int r = lane / 6, c = lane % 6, lo = r < c ? r : c, hi = r < c ? c : r;
+    e.A[lane] = (float)acc[lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];  // upper-triangle order
+  }
+  wave_lds_sync();
+  jacobi_eigen_wave<6>(e.A, e.W, e.V, e.R, e.C);
+  if (lane != 0) return;
+  float E[6], V[36], V2[36], Vi[36];
+  for (int k = 0; k < 6; ++k) E[k] = e.W[k];
+  for (int k = 0; k < 36; ++k) V[k] = e.V[k];
+  for (int k = 0; k < 36; ++k) V2[k] = V[k];
+  int deg = 0;
+  for (int i = 5; i >= 0; i--) {
+    if (E[i] < 100.0f) {
+      for (int j = 0; j < 6; j++) V2[i * 6 + j] = 0.0f;
+      deg = 1;
+    } else {
+      break;
+    }
+  }
+  *degenerate = deg;
+  if (!lu_inv6(V, Vi))
+    for (int k = 0; k < 36; ++k) Vi[k] = 0.0f;
+  float P[36];
+  for (int k = 0; k < 36; ++k) P[k] = 0.0f;
+  gemm_f32_acc64<6, 6, 6>(Vi, V2, P);
+  for (int k = 0; k < 36; ++k) matP[k] = P[k];
+}
+
+// matAtA X = matAtB by OpenCV's float Householder QR (:1276); X = 0 if singular.
+__device__ void gn_qr_step(const double* acc, float* X) {
+  float AtA[36];
+  gn_normal_eq(acc, AtA, X);
+  if (!qr_solve6(AtA, X))
+    for (int k = 0; k < 6; ++k) X[k] = 0.0f;
+}
+
+// One job's LMOptimization step on one lane (acc = the job's summed normal-equation products,
+// X = gn_qr_step's solution, matP0 / deg0 = gn_degeneracy's result at iteration 0).
+__device__ void gn_solve_job(const GnArgs& a, int job, const double* acc, float* X, const float* matP0, int deg0) {
   GnState& g = a.gn[job];
   const int iterCount = g.iter;
   g.iter = iterCount + 1;
@@ -505,45 +566,20 @@ __device__ void gn_solve_job(const GnArgs& a, int job, const double* acc) {
     if (g.iter >= a.max_iter) g.active = 0;
     return;
   }
-  float AtA[36], X[6], tmp[36];
-  {
-    int q = 0;
-    for (int r = 0; r < 6; ++r)
-      for (int c = r; c < 6; ++c) {
-        AtA[r * 6 + c] = (float)acc[q];
-        AtA[c * 6 + r] = (float)acc[q];
-        ++q;
-      }
-    for (int r = 0; r < 6; ++r) X[r] = (float)acc[21 + r];
-  }
-  for (int k = 0; k < 36; ++k) tmp[k] = AtA[k];
-  if (!qr_solve6(tmp, X))
-    for (int k = 0; k < 6; ++k) X[k] = 0.0f;
-  float matP[36];
-  for (int k = 0; k < 36; ++k) matP[k] = 0.0f;  // local cv::Mat matP (:1278)
-  if (iterCount == 0) {
-    float E[6], V[36], V2[36], Vi[36];
-    for (int k = 0; k < 36; ++k) tmp[k] = AtA[k];
-    jacobi_eigen<6>(tmp, E, V);  // register-resident; one job per wave, so no pivot divergence
-    for (int k = 0; k < 36; ++k) V2[k] = V[k];
-    int deg = 0;
-    for (int i = 5; i >= 0; i--) {
-      if (E[i] < 100.0f) {
-        for (int j = 0; j < 6; j++) V2[i * 6 + j] = 0.0f;
-        deg = 1;
-      } else {
-        break;
-      }
-    }
-    g.degenerate = deg;
-    if (!lu_inv6(V, Vi))
-      for (int k = 0; k < 36; ++k) Vi[k] = 0.0f;
-    gemm_f32_acc64<6, 6, 6>(Vi, V2, matP);
-  }
+  // the local cv::Mat matP (:1278) is zero after iteration 0
+  if (iterCount == 0) g.degenerate = deg0;
   if (g.degenerate) {
     float X2[6];
     for (int k = 0; k < 6; ++k) X2[k] = X[k];
-    gemm_f32_acc64<6, 6, 1>(matP, X2, X);
+    if (iterCount == 0) {
+      float P[36];
+      for (int k = 0; k < 36; ++k) P[k] = matP0[k];
+      gemm_f32_acc64<6, 6, 1>(P, X2, X);
+    } else {
+      float P[36];
+      for (int k = 0; k < 36; ++k) P[k] = 0.0f;
+      gemm_f32_acc64<6, 6, 1>(P, X2, X);
+    }
   }
   for (int k = 0; k < 6; ++k) g.pose[k] += X[k];
   if (a.trace)
@@ -561,26 +597,38 @@ __device__ void gn_solve_job(const GnArgs& a, int job, const double* acc) {
   pose_to_T(g.pose, g.T, g.trig);
 }
 
-// One wave per job: lanes 0..27 sum the job's item partials (each entry in item order, as before),
-// lane 0 runs the LMOptimization step.  The number of jobs still iterating is accumulated with
-// agent-scope atomics; the last workgroup to finish publishes it to host-mapped memory as
-// (generation << 32 | count) so the host stops enqueueing iterations once the batch converged.
-__global__ void __launch_bounds__(64) k_gn_solve(GnArgs a, int iter_idx, unsigned long long gen) {
+// Two waves per job: wave 0's lanes 0..27 sum the job's item partials (each entry in item order,
+// as before); then wave 0's lane 0 solves the normal equations while, at iteration 0, wave 1's
+// lane 0 computes the degeneracy projection (the two are independent; on one wave they would run
+// back to back); lane 0 then runs the rest of the LMOptimization step.  The number of jobs still
+// iterating is accumulated with agent-scope atomics; the last workgroup to finish publishes it to
+// host-mapped memory as (generation << 32 | count) so the host stops enqueueing iterations once
+// the batch converged.
+__global__ void __launch_bounds__(kSolveThreads) k_gn_solve(GnArgs a, int iter_idx, unsigned long long gen) {
   __shared__ double acc[28];
-  const int job = blockIdx.x, lane = threadIdx.x;
+  __shared__ float matP0[36];
+  __shared__ int deg0;
+  __shared__ EigenLds eig;
+  const int job = blockIdx.x, tid = threadIdx.x;
   GnState& g = a.gn[job];
-  if (g.active) {
-    if (lane < 28) {
+  if (g.active) {  // block-uniform
+    const int iter0 = g.iter == 0;  // read before lane 0 updates it (ordered by the barriers)
+    if (tid < 28) {
       double sum = 0.0;
       const int i0 = a.item_range[2 * job], i1 = a.item_range[2 * job + 1];
 #pragma unroll 8
-      for (int it = i0; it < i1; ++it) sum += a.partial[(int64_t)it * kPartial + lane];
-      acc[lane] = sum;
+      for (int it = i0; it < i1; ++it) sum += a.partial[(int64_t)it * kPartial + tid];
+      acc[tid] = sum;
     }
     __syncthreads();
-    if (lane == 0) gn_solve_job(a, job, acc);
+    float X[6];
+    const bool solve = (int)acc[27] >= 50;
+    if (tid >= 64 && iter0 && solve) gn_degeneracy(acc, eig, matP0, &deg0);
+    if (tid == 0 && solve) gn_qr_step(acc, X);
+    __syncthreads();
+    if (tid == 0) gn_solve_job(a, job, acc, X, matP0, deg0);
   }
-  if (lane == 0) {
+  if (tid == 0) {
     atomicAdd(&a.iter_cnt[2 * iter_idx], g.active);
     __threadfence();
     const int done = atomicAdd(&a.iter_cnt[2 * iter_idx + 1], 1);
@@ -686,7 +734,7 @@ void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
   hipLaunchKernelGGL(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);
 }
 void launch_gn_solve(hipStream_t s, const GnArgs& a, int iter_idx, unsigned long long gen) {
-  hipLaunchKernelGGL(k_gn_solve, dim3(a.B), dim3(64), 0, s, a, iter_idx, gen);
+  hipLaunchKernelGGL(k_gn_solve, dim3(a.B), dim3(kSolveThreads), 0, s, a, iter_idx, gen);
 }
 void launch_gn_finalize(hipStream_t s, const GnArgs& a) {
   hipLaunchKernelGGL(k_gn_finalize, dim3((a.B + 63) / 64), dim3(64), 0, s, a);

@@ -6,6 +6,7 @@
 // kernel and compares every output bit with the host.
 #include "fbr_common.h"
 #include "fbr_fdlibm.h"
+#include "fbr_solvers.h"
 
 namespace fbr {
 
@@ -17,6 +18,27 @@ __global__ void k_selftest_math(int n, const float* a, const float* b, float* ou
   out[4 * i + 1] = x / y;
   out[4 * i + 2] = fd_atan2f(x, y);
   out[4 * i + 3] = x * y + y * x - x;  // plain mul/add with contraction disabled
+}
+
+// One 64-lane workgroup per symmetric 6x6 matrix: the single-lane jacobi_eigen<6> (lane 0) and the
+// wave-parallel jacobi_eigen_wave<6>; out = 2 x (6 eigenvalues + 36 eigenvector entries).
+__global__ void __launch_bounds__(64) k_selftest_eigen6(const float* a, float* out) {
+  __shared__ float A[36], V[36], W[6];
+  __shared__ int R[6], C[6];
+  const int m = blockIdx.x, lane = threadIdx.x;
+  float* o = out + (int64_t)m * 84;
+  if (lane == 0) {
+    float Ar[36], Wr[6], Vr[36];
+    for (int k = 0; k < 36; ++k) Ar[k] = a[(int64_t)m * 36 + k];
+    jacobi_eigen<6>(Ar, Wr, Vr);
+    for (int k = 0; k < 6; ++k) o[k] = Wr[k];
+    for (int k = 0; k < 36; ++k) o[6 + k] = Vr[k];
+  }
+  if (lane < 36) A[lane] = a[(int64_t)m * 36 + lane];
+  __syncthreads();
+  jacobi_eigen_wave<6>(A, W, V, R, C);
+  if (lane < 6) o[42 + lane] = W[lane];
+  if (lane < 36) o[48 + lane] = V[lane];
 }
 
 }  // namespace fbr
@@ -37,6 +59,23 @@ extern "C" int fbr_selftest_math(int n, const float* a, const float* b, float* o
   }
   (void)hipFree(da);
   (void)hipFree(db);
+  (void)hipFree(dout);
+  return rc;
+}
+
+extern "C" int fbr_selftest_eigen6(int n, const float* a, float* out) {
+  if (n <= 0 || !a || !out) return FBR_ERR_INVALID_ARG;
+  float *da = nullptr, *dout = nullptr;
+  int rc = FBR_OK;
+  if (hipMalloc(&da, sizeof(float) * 36 * n) != hipSuccess || hipMalloc(&dout, sizeof(float) * 84 * n) != hipSuccess) {
+    rc = FBR_ERR_HIP;
+  } else if (hipMemcpy(da, a, sizeof(float) * 36 * n, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = FBR_ERR_HIP;
+  } else {
+    hipLaunchKernelGGL(fbr::k_selftest_eigen6, dim3(n), dim3(64), 0, 0, da, dout);
+    if (hipMemcpy(out, dout, sizeof(float) * 84 * n, hipMemcpyDeviceToHost) != hipSuccess) rc = FBR_ERR_HIP;
+  }
+  (void)hipFree(da);
   (void)hipFree(dout);
   return rc;
 }

@@ -371,6 +371,11 @@ int fbr_voxel_grid(fbr_ctx* ctx, const fbr_point_xyzi* in, int64_t n, float leaf
  * the host libm the reference uses). */
 int fbr_selftest_math(int n, const float* a, const float* b, float* out);
 
+/* Diagnostic: cv::eigen of n symmetric 6x6 float matrices a[36i..36i+35] (the degeneracy step,
+ * mapOptmization.h:1353) by the single-lane and the wave-parallel device Jacobi; out[84i..] =
+ * {6 eigenvalues, 36 eigenvector entries} of each (tests compare both with the host restatement). */
+int fbr_selftest_eigen6(int n, const float* a, float* out);
+
 /* Measurement helper: achievable HBM bandwidth of a device-wide float4 copy of `bytes` (read +
  * write counted), averaged over `iters` launches (the STREAM-copy figure bench.py reports next to
  * the 8 TB/s spec peak). */

@@ -74,6 +74,37 @@ def test_device_math_is_bit_exact():
     assert np.array_equal(out[idx, 2].view(np.int32), ref.view(np.int32))
 
 
+def test_degeneracy_eigen6_wave_matches_single_lane_and_oracle():
+    """cv::eigen of the 6x6 AtA (mapOptmization.h:1353): the wave-parallel Jacobi k_gn_solve runs at
+    iteration 0 gives the same bits as the single-lane restatement and the host oracle, on
+    normal-equation matrices of realistic scale, near-degenerate ones (eigenvalues around the
+    100 threshold), diagonal and rank-deficient ones."""
+    from feature_base_pointcloud_registration_amd.fbr_types import ptr
+    rng = np.random.default_rng(7)
+    mats = []
+    for t in range(600):
+        kind = t % 4
+        if kind == 3:
+            mats.append(np.diag(rng.uniform(0, 1e4, 6)).astype(np.float32))
+            continue
+        J = rng.standard_normal((int(rng.integers(50, 4000)), 6)).astype(np.float64)
+        J *= rng.uniform(0.05, 3.0, 6)
+        if kind == 1:
+            J[:, int(rng.integers(6))] *= rng.uniform(1e-3, 0.3)  # an eigenvalue near 100
+        if kind == 2:
+            J[:, 5] = J[:, 4]  # rank-deficient
+        mats.append((J.T @ J).astype(np.float32))
+    mats = np.stack(mats)
+    (w1, v1), (w2, v2) = api.selftest_eigen6(mats)
+    assert np.array_equal(bits(w1), bits(w2)) and np.array_equal(bits(v1), bits(v2))
+    for i in range(len(mats)):
+        a = mats[i].copy()
+        W = np.zeros(6, np.float32)
+        V = np.zeros((6, 6), np.float32)
+        O.lib().orc_jacobi(ptr(a), 6, ptr(W), ptr(V))
+        assert np.array_equal(bits(W), bits(w2[i])) and np.array_equal(bits(V), bits(v2[i])), i
+
+
 # ------------------------------------------------------------------------------- projection
 @pytest.mark.parametrize("cfg,seed", [("C1", 1), ("C1", 2), ("C2", 3), ("C2", 4), ("C3", 5)])
 def test_projection_bit_exact(cfg, seed):
