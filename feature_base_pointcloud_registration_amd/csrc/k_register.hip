@@ -78,7 +78,7 @@ __device__ __forceinline__ void knn_insert(Knn5& r, unsigned long long x) {
 #pragma unroll
   for (int t = 0; t < 5; ++t) lt[t] = x < r.k[t];
 #pragma unroll
-  for (int t = 4; t > 0; --t) r.k[t] = lt[t] ? (lt[t - 1] ? r.k[t - 1] : x) : r.k[t];
+  for (int t = 4; t > 0; --t) r.k[t] = lt[t - 1] ? r.k[t - 1] : (lt[t] ? x : r.k[t]);  // lt[t-1] implies lt[t]
   r.k[0] = lt[0] ? x : r.k[0];
 }
 
