@@ -62,6 +62,7 @@ __device__ void pose_to_T(const float* tr, float* T, float* trig) {
 // without any instruction (hi = the distance register, lo = the w bit pattern).  Empty slots hold
 // kKnnEmpty = (bits(1.0f), 0): a point is only inserted with d2 < 1.0 (:1027, :1154).
 constexpr unsigned long long kKnnEmpty = (unsigned long long)0x3f800000u << 32;
+constexpr float kBelowOne = 0.99999994f;  // nextafterf(1.0f, 0.0f)
 
 struct Knn5 {
   unsigned long long k[5];
@@ -162,8 +163,9 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       float lb = 0.0f;
       lb += ly2[ky];
       lb += lz2[kz];
-      const float cut = fminf(knn_d(r.k[4]), bound);
-      if (y < 0 || y >= Y || z < 0 || z >= Z || lb > cut || !(lb < 1.0f)) continue;
+      // "lb <= cut and lb < 1.0" as one compare: the largest float below 1.0 caps the cut
+      const float cut = fminf(fminf(knn_d(r.k[4]), bound), kBelowOne);
+      if (y < 0 || y >= Y || z < 0 || z >= Z || lb > cut) continue;
       int xa = 0, xb = 0;
       bool go_a = true, go_b = true;
 #pragma unroll
@@ -171,8 +173,8 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         float ta = 0.0f, tb = 0.0f;
         ta += lxm2[o]; ta += ly2[ky]; ta += lz2[kz];
         tb += lxp2[o]; tb += ly2[ky]; tb += lz2[kz];
-        go_a = go_a && !(ta > cut) && ta < 1.0f;
-        go_b = go_b && !(tb > cut) && tb < 1.0f;
+        go_a = go_a && !(ta > cut);
+        go_b = go_b && !(tb > cut);
         if (go_a) xa = -o;
         if (go_b) xb = o;
       }
