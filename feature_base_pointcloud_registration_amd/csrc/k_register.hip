@@ -31,6 +31,8 @@
 //     QR solve / Jacobi / LU; the Gauss-Newton state never leaves the device.
 // Roofline: HBM/L2 gather-bound.  Algorithmic bytes per query per iteration: 16 (query) +
 // 5 x 16 (neighbours) = 96 B.
+#include <cstdlib>
+
 #include "fbr_common.h"
 #include "fbr_imu.h"
 #include "fbr_kernels.h"
@@ -97,7 +99,7 @@ __device__ __forceinline__ int rank_offset(int k, int s) { return k == 0 ? 0 : (
 
 #ifdef FBR_KNN_STATS
 // Diagnostic builds only (tools/knn_stats.py): [queries, rows considered, rows scanned, points
-// scanned, points inserted, accepted queries]
+// scanned, points inserted, accepted queries, corner queries, wave iterations of the point loop]
 __device__ unsigned long long fbr_knn_stats[8];
 #define FBR_KS(i, v) ks[i] += (v)
 #else
@@ -117,9 +119,15 @@ __device__ unsigned long long fbr_knn_stats[8];
 // distance to the previous iteration's 5 neighbours, 5 distinct candidates of the same crop box):
 // cells whose lower bound exceeds it cannot hold any of the 5 nearest, ties included, so they are
 // pruned from the start instead of only once 5 points have been inserted.
-template <int R, int RX>
+// kFlat: the rows are pruned once up front with `bound` (the warm start, tight from iteration 1
+// on) and their point ranges queued in LDS (`rows`, stride kResThreads); one loop then walks a
+// lane's queued points across rows.  A wave then runs for its longest lane's total instead of the
+// sum over rows of each row's longest lane (lanes of a wave scan different rows: the per-row loop
+// kept ~30 % of the lanes busy).  Pruning with a larger cut only scans more cells, and the 5-NN
+// list is a function of the scanned set, so both forms give the same neighbours.
+template <int R, int RX, bool kFlat = false>
 __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
-                          float bound, Knn5& r, unsigned* ks) {
+                          float bound, Knn5& r, unsigned* ks, int2* rows = nullptr) {
   constexpr int K = 2 * R + 1;  // rows per side in y and z; RX = cells per side along x
 #pragma unroll
   for (int t = 0; t < 5; ++t) r.k[t] = kKnnEmpty;
@@ -152,6 +160,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
   const float bx0 = bmin[0], by0 = bmin[1], bz0 = bmin[2], bx1 = bmax[0], by1 = bmax[1], bz1 = bmax[2];
   const float xlo = (fx - (float)RX) * cxs, xhi = (fx + (float)(RX + 1)) * cxs;  // row x extent (max)
   const bool xin = xlo >= bx0 && xhi <= bx1;
+  int nrow = 0;  // kFlat: rows queued
 #pragma unroll
   for (int ksum = 0; ksum <= 2 * (K - 1); ++ksum) {
 #pragma unroll
@@ -187,6 +196,10 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       // the whole row inside the crop box (pcl::CropBox, inclusive) -> no per-point test
       const float ylo = (fy + (float)oyk[ky]) * c, zlo = (fz + (float)ozk[kz]) * c;
       const bool inside = xin & (ylo >= by0) & (ylo + c <= by1) & (zlo >= bz0) & (zlo + c <= bz1);
+      if constexpr (kFlat) {
+        if (e > b) rows[nrow++ * kResThreads] = make_int2(b, inside ? (int)((unsigned)e | 0x80000000u) : e);
+        continue;
+      }
       for (int i = b; i < e; ++i) {
         const float4 p = m.pts[i];
         // pcl::CropBox (inclusive) as one mask: a point outside gets d2 = +inf (never inserted)
@@ -198,8 +211,37 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         diff = qz - p.z; dist += diff * diff;
         const unsigned hi = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
         FBR_KS(4, __int_as_float((int)hi) < knn_d(r.k[4]) ? 1 : 0);
+#ifdef FBR_KNN_STATS
+        if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ks[7] += 1;  // one per wave iteration
+#endif
         knn_insert(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
       }
+    }
+  }
+  if constexpr (kFlat) {
+    int j = 0, i = 0, e = 0;
+    bool inside = true;
+    while (true) {
+      if (i >= e) {  // next queued row (every queued row is non-empty)
+        if (j >= nrow) break;
+        const int2 q = rows[j++ * kResThreads];
+        i = q.x;
+        e = q.y & 0x7fffffff;
+        inside = q.y < 0;
+      }
+      const float4 p = m.pts[i++];
+      bool out = false;
+      if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
+      float dist = 0.0f, diff;
+      diff = qx - p.x; dist += diff * diff;  // flann::L2_Simple
+      diff = qy - p.y; dist += diff * diff;
+      diff = qz - p.z; dist += diff * diff;
+      const unsigned hi = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
+      FBR_KS(4, __int_as_float((int)hi) < knn_d(r.k[4]) ? 1 : 0);
+#ifdef FBR_KNN_STATS
+      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ks[7] += 1;  // one per wave iteration
+#endif
+      knn_insert(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
     }
   }
 }
@@ -433,10 +475,11 @@ k_gn_residual(GnArgs a) {
 // R = grid cells per side covering radius 1 (both map grids share one cell size).  kFused: the
 // same lane goes on to its residual row and the workgroup reduces the item's normal-equation
 // partial (k_gn_residual's work, without re-reading the query and its neighbour indices).
-template <int R, int RX, bool kFused>
+template <int R, int RX, bool kFused, bool kFlat>
 __global__ void __launch_bounds__(kResThreads)
 k_gn_knn(GnArgs a, int use_prev) {
-  __shared__ double red[kResThreads / 64][28];
+  __shared__ double red[kFused ? kResThreads / 64 : 1][28];
+  __shared__ int2 rows[kFlat ? (2 * R + 1) * (2 * R + 1) : 1][kResThreads];
   const int tid = threadIdx.x;
   const int nitems = a.nitems[0];
   for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
@@ -472,12 +515,12 @@ k_gn_knn(GnArgs a, int use_prev) {
       }
       Knn5 nn;
       unsigned ks[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-      knn5_grid<R, RX>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
+      knn5_grid<R, RX, kFlat>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks, &rows[0][tid]);
       const bool ok = nn.k[4] < kKnnEmpty;
 #ifdef FBR_KNN_STATS
       ks[5] = ok;
       ks[6] = corner;
-      for (int k = 0; k < 7; ++k) atomicAdd(&fbr_knn_stats[k], (unsigned long long)ks[k]);
+      for (int k = 0; k < 8; ++k) atomicAdd(&fbr_knn_stats[k], (unsigned long long)ks[k]);
 #else
       (void)ks;
 #endif
@@ -710,13 +753,31 @@ void launch_export_records(hipStream_t s, int B, const float* pose_out, const fb
 }
 
 void launch_gn_init(hipStream_t s, const GnArgs& a) { hipLaunchKernelGGL(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
+template <int R, bool F, bool L>
+void launch_gn_knn_rl(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
+  const float invx = a.mc.g.inv_x;  // == a.ms.g.inv_x
+  if (invx > 4.0f) hipLaunchKernelGGL((k_gn_knn<R, 8, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
+  else if (invx > 2.0f) hipLaunchKernelGGL((k_gn_knn<R, 4, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
+  else if (invx > 1.0f) hipLaunchKernelGGL((k_gn_knn<R, 2, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
+  else hipLaunchKernelGGL((k_gn_knn<R, 1, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
+}
+
+// Flat row queue (FBR_KNN_FLAT=0 disables): from iteration 1 on (warm-start bound), 1 m y/z cells
+// (9 rows: the queue is 18 KB of LDS per workgroup), not in the fused tail launch.
+bool knn_flat() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_KNN_FLAT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 template <int R, bool F>
 void launch_gn_knn_r(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
-  const float invx = a.mc.g.inv_x;  // == a.ms.g.inv_x
-  if (invx > 4.0f) hipLaunchKernelGGL((k_gn_knn<R, 8, F>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
-  else if (invx > 2.0f) hipLaunchKernelGGL((k_gn_knn<R, 4, F>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
-  else if (invx > 1.0f) hipLaunchKernelGGL((k_gn_knn<R, 2, F>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
-  else hipLaunchKernelGGL((k_gn_knn<R, 1, F>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
+  if constexpr (R == 1 && !F) {
+    if (use_prev && knn_flat()) return launch_gn_knn_rl<R, F, true>(s, a, grid, use_prev);
+  }
+  launch_gn_knn_rl<R, F, false>(s, a, grid, use_prev);
 }
 
 template <bool F>

@@ -35,5 +35,6 @@ for cell in (sys.argv[2:] or ["0.5"]):
     q = float(st[0])
     print(f"cell {cell}: queries {int(q)} (corner {int(st[6])}) accepted {st[5] / q:.3f} | per query: rows considered "
           f"{st[1] / q:.1f}, rows scanned {st[2] / q:.1f}, points scanned {st[3] / q:.1f}, inserted {st[4] / q:.1f} | "
-          f"gn_knn ms {ctx.kernel_time('gn_knn')}")
+          f"gn_knn ms {ctx.kernel_time('gn_knn')} | point-loop lane efficiency "
+          f"{float(st[3]) / (64.0 * float(st[7])):.3f} (points scanned / (64 x wave iterations))")
     ctx.close()
