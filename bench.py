@@ -9,8 +9,10 @@ extraction, scan-to-map Gauss-Newton registration against a 100k-point local cor
 Inputs (raw scans, guesses, map grid) are resident in HBM before the timed region starts.
 
 Multi-GPU (launched by torch.distributed.run): every rank processes its own B jobs (weak scaling,
-no data-path collective); after each step the 32-byte pose records of all jobs are all-gathered
-over RCCL (the only collective of the path).
+the default) or a contiguous block of --total-jobs N (strong scaling: C4 = 1024 jobs over 8 GPUs,
+128 per GPU); there is no data-path collective.  After each step the 32-byte pose records of all
+jobs are all-gathered over RCCL (the only collective of the path) and, after the
+timed region, checked against every rank's own results.
 
 Rank 0 prints ONE JSON line with the metric, a roofline block for the dominant kernel (HIP events
 on the library's stream over the timed region) and a cpu_baseline block (the CPU oracle restating
@@ -35,18 +37,30 @@ WORKLOAD = {"C1": "VLP-16-style scans, local corner+surf map",
             "C5": "dense scans, ~5.8M-pt map inside the crop box (mapping leaves 0.05)"}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
-# Algorithmic bytes per unit for each kernel family (DESIGN.md "Kernels and rooflines").
+# Algorithmic bytes per unit for each kernel family: the minimal HBM traffic the kernel's job needs
+# (DESIGN.md §4 holds the same table).  Units per step: n_in raw points, HW range-image cells, n
+# valid points, C corner picks, S per-ring surf DS points, F = C + S feature points, Q DS queries,
+# IQ query-iterations.
 def kernel_bytes(name, tot):
-    n_in, n, Q, IQ, M, F, S = tot["n_in"], tot["n"], tot["Q"], tot["IQ"], tot["M"], tot["F"], tot["S"]
+    n_in, HW, n, C = tot["n_in"], tot["HW"], tot["n"], tot["C"]
+    S, F, Q, IQ = tot["S"], tot["F"], tot["Q"], tot["IQ"]
     return {
-        "gn_knn": 116.0 * IQ,                 # query 16 B + the 5 neighbours found 80 B + 5 positions out 20 B
-        "gn_residual": 116.0 * IQ,            # query 16 B + 5 positions 20 B + 5 neighbour gathers 80 B
-        "project": 24.0 * n_in + 4.0 * n,     # raw point read + owner claim
-        "extract": 4.0 * 2 * n + 28.0 * n,    # owners, owning point, xyzi+col+range write
-        "features": 41.0 * n,                 # range/col/cloud read, label + candidate write
-        "voxel_ring": 17.0 * n + 16.0 * S,    # label + candidate point read (<= n), per-ring DS write
-        "voxel_scan": 16.0 * F + 16.0 * Q,    # corner + surf clouds read, DS queries written
+        "project": 24.0 * n_in + 4.0 * n,        # raw point (24 B AoS) read + first-wins owner claim
+        "extract": 4.0 * HW + 24.0 * n + 24.0 * n,  # owner image read, owning raw point gather, xyzi+col+range write
+        "features": 24.0 * n + 1.0 * n + 16.0 * C,  # range+col+xyzi read, label write, corner picks write
+        "voxel_ring": 17.0 * n + 16.0 * S,       # label + candidate point read, per-ring DS write
+        "concat": 32.0 * F,                      # per-ring corner / surf outputs read + job clouds written
+        "voxel_scan": 16.0 * F + 16.0 * Q,       # corner + surf clouds read, DS queries written
+        "gn_knn": 116.0 * IQ,                    # query 16 B + the 5 neighbours found 80 B + 5 map indices out 20 B
+        "gn_residual": 116.0 * IQ,               # query 16 B + 5 map indices 20 B + 5 neighbour gathers 80 B
     }.get(name, 0.0)
+
+
+# rocprofv3 kernel symbols behind each launcher name (tools/roofline_check.py maps a profile's rows)
+KERNEL_SYMBOLS = {"project": ["k_project"], "extract": ["k_rowcount", "k_compact"], "features": ["k_features"],
+                  "voxel_ring": ["k_voxel_ring"], "concat": ["k_concat"], "voxel_scan": ["k_voxel_grid"],
+                  "gn_knn": ["k_gn_knn"], "gn_residual": ["k_gn_residual"], "gn_solve": ["k_gn_solve"],
+                  "gn_init": ["k_gn_init"], "gn_finalize": ["k_gn_finalize"], "crop": ["k_crop_count"]}
 
 
 def parse():
@@ -54,7 +68,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024, help="jobs per GPU per step")
+    ap.add_argument("--batch", type=int, default=1024, help="jobs per GPU per step (weak scaling)")
+    ap.add_argument("--total-jobs", type=int, default=0,
+                    help="strong scaling: N jobs per step split into contiguous per-rank blocks (C4: 1024)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend of the pose-record gather (gloo: host records, tests)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on device 0 (world-size > 1 rehearsal on a one-GPU box)")
+    ap.add_argument("--records-out", default=None, help="rank 0 writes the gathered records (.npy)")
     ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C5"])
     ap.add_argument("--cpu-sample", type=int, default=96, help="jobs timed on the CPU oracle (N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16,
@@ -64,9 +85,9 @@ def parse():
                     help="enable the IMU deskew path (SURVEY 8f row 3): one imuDeskewInfo table per job")
     ap.add_argument("--dist", action="store_true",
                     help="use the torch.distributed (RCCL) path even at world size 1 (tests)")
-    ap.add_argument("--profile", default="dominant", choices=["all", "dominant", "off"],
-                    help="HIP-event kernel timing inside the timed region: every kernel, only the roofline "
-                         "kernels (default), or none")
+    ap.add_argument("--profile", default="all", choices=["all", "dominant", "off"],
+                    help="kernel timing inside the timed region (dispatch start/end timestamps through HIP "
+                         "events): every kernel (default), only the roofline kernel, or none")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "hbm_traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from rocprofv3 PMC passes")
     return ap.parse_args()
@@ -78,25 +99,33 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    dev = 0 if args.same_device else local_rank
     if world > 1 or args.dist:
         import torch  # noqa: F401  (load torch's HIP runtime first; the library shares it)
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl", init_method="env://")
+        torch.cuda.set_device(dev)
+        dist.init_process_group(backend=args.backend, init_method="env://")
 
     from feature_base_pointcloud_registration_amd import api, shard, synth
 
     cfg = args.config
     H, W, *_ = synth.CONFIGS[cfg]
-    B = args.batch
+    if args.total_jobs:  # strong split (C4): rank r owns the contiguous block [j0, j1)
+        j0, j1 = shard.job_block(rank, world, args.total_jobs)
+        counts = [shard.job_block(r, world, args.total_jobs)[1] - shard.job_block(r, world, args.total_jobs)[0]
+                  for r in range(world)]
+    else:                # weak: every rank its own --batch jobs
+        j0, j1 = rank * args.batch, (rank + 1) * args.batch
+        counts = [args.batch] * world
+    B = j1 - j0
+    Bpad = max(counts)   # all-gather blocks are padded to the largest rank's
     P = synth.config_params(cfg, max_batch=B)
     corner_map, surf_map = synth.config_map(cfg)
-    jobs = synth.make_jobs(cfg, B, base_seed=1000 + rank * B)
+    jobs = synth.make_jobs(cfg, B, base_seed=1000 + j0)  # job j uses seed 1000 + j
     scans = [j[0] for j in jobs]
     guesses = np.stack([j[1] for j in jobs]).astype(np.float32)
     gts = np.stack([j[2] for j in jobs])
 
-    dev = local_rank if world > 1 else 0
     stream_gbps = api.stream_copy_bandwidth(dev) if rank == 0 else None  # achievable HBM copy rate
     ctx = api.Context(P, device=dev)
     ctx.set_map(corner_map, surf_map)
@@ -106,17 +135,30 @@ def main():
         ctx.set_deskew(tabs)
     ctx.batch_stage(scans, guesses)
 
-    gather_buf = None
+    gather_buf = lib_stream = None
     if dist is not None:
         import torch
-        gather_buf = torch.zeros(B * 8, dtype=torch.float32, device=f"cuda:{local_rank}")
+        if args.backend == "nccl":
+            gather_buf = torch.zeros(Bpad * shard.RECORD_FLOATS, dtype=torch.float32, device=f"cuda:{dev}")
+            lib_stream = torch.cuda.ExternalStream(ctx.stream_handle, device=f"cuda:{dev}")
+    gathered = [None]
 
     def step():
         ctx.batch_launch()
-        if dist is not None:
+        if dist is None:
+            return
+        if args.backend == "nccl":
+            # the export (library stream) must not overwrite gather_buf while the previous step's
+            # all_gather (torch's stream) still reads it, and the gather must see this export
+            lib_stream.wait_stream(torch.cuda.current_stream())
             ctx.batch_export(gather_buf.data_ptr())
-            ctx.batch_wait()
-            shard.gather_records(dist, gather_buf, world)
+            torch.cuda.current_stream().wait_stream(lib_stream)
+            gathered[0] = shard.gather_records(dist, gather_buf, world)
+        else:  # gloo: host records
+            poses_h, stats_h = ctx.batch_results()
+            rec = np.zeros(Bpad * shard.RECORD_FLOATS, np.float32)
+            rec[:B * shard.RECORD_FLOATS] = shard.encode_records(poses_h, stats_h["iterations"], stats_h["status"])
+            gathered[0] = shard.gather_records(dist, torch.from_numpy(rec), world)
 
     for _ in range(args.warmup):
         step()
@@ -129,13 +171,14 @@ def main():
     ctx.batch_wait()
     ctx.set_profiling(False)
     prof = {k: ctx.kernel_time(k) for k in kernels}
-    modelled = [k for k in kernels if kernel_bytes(k, dict.fromkeys(["n_in", "n", "Q", "IQ", "M", "F", "S"], 1.0)) > 0]
-    dom = max(modelled, key=lambda k: prof[k][0])
+    modelled = [k for k in kernels if kernel_bytes(k, dict.fromkeys(["n_in", "HW", "n", "C", "S", "F", "Q", "IQ"], 1.0)) > 0]
+    dom = max(modelled, key=lambda k: prof[k][0])  # largest total kernel time per step
     if dist is not None:
         import torch
         torch.cuda.synchronize()
         dist.barrier()
-    # timed region: HIP events only around the roofline kernel by default (--profile all: every kernel)
+    # timed region: every kernel's dispatches carry start / end events (--profile dominant: only the
+    # roofline kernel's, off: none)
     if args.profile == "all":
         ctx.set_profiling(True)
     elif args.profile == "dominant":
@@ -149,10 +192,23 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ctx.set_profiling(False)
+    records_check = None
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        tdev = f"cuda:{dev}" if args.backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # the last step's gathered records, rank-ordered, against every rank's own results
+        allrec = shard.unpad_records(gathered[0].cpu().numpy(), counts)
+        p_l, s_l = ctx.batch_results()
+        mine = shard.encode_records(p_l, s_l["iterations"], s_l["status"])
+        off = sum(counts[:rank]) * shard.RECORD_FLOATS
+        bad = int((allrec[off:off + len(mine)].view(np.int32) != mine.view(np.int32)).sum())
+        bt = torch.tensor([bad], dtype=torch.int64, device=tdev)
+        dist.all_reduce(bt)
+        records_check = {"jobs": int(sum(counts)), "mismatched_words": int(bt.item())}
+        if rank == 0 and args.records_out:
+            np.save(args.records_out, allrec)
 
     poses, stats = ctx.batch_results()
     tb, tg = ctx.batch_bytes()
@@ -165,23 +221,33 @@ def main():
             dist.destroy_process_group()
         return
 
-    total_jobs = world * B * args.steps
+    total_jobs = sum(counts) * args.steps
     value = total_jobs / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
     # per-step workload counts (identical every step: the same staged batch is re-registered)
-    tot = dict(n_in=float(sum(len(s) for s in scans)), n=float(stats["n_points"].sum()),
+    tot = dict(n_in=float(sum(len(s) for s in scans)), HW=float(B * H * W), n=float(stats["n_points"].sum()),
+               C=float(stats["n_corner"].sum()), S=float(stats["n_surf"].sum()),
+               F=float((stats["n_corner"] + stats["n_surf"]).sum()),
                Q=float((stats["n_corner_ds"] + stats["n_surf_ds"]).sum()),
                IQ=float(((stats["n_corner_ds"] + stats["n_surf_ds"]) * stats["iterations"]).sum()),
-               M=float((stats["n_corner_map"] + stats["n_surf_map"]).sum()),
-               F=float((stats["n_corner"] + stats["n_surf"]).sum()), S=float(stats["n_surf"].sum()))
-    if timed[dom][1] > 0:  # live events over the timed region
-        dom_ms, dom_launches, steps_measured, live = timed[dom][0], timed[dom][1], args.steps, True
-    else:                  # --profile off: the profiled step
-        dom_ms, dom_launches, steps_measured, live = prof[dom][0], prof[dom][1], 1, False
-    launches_per_step = dom_launches / max(steps_measured, 1)
-    bytes_per_launch = kernel_bytes(dom, tot) / max(launches_per_step, 1e-9)
-    avg_launch_s = dom_ms / 1000.0 / max(dom_launches, 1)
-    achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+               M=float((stats["n_corner_map"] + stats["n_surf_map"]).sum()))
+
+    def kernel_roofline(k):
+        if timed[k][1] > 0:  # live: the timed region's dispatches
+            ms, launches, steps_measured, live = timed[k][0], timed[k][1], args.steps, True
+        else:                # not timed live (--profile dominant/off): the profiled step
+            ms, launches, steps_measured, live = prof[k][0], prof[k][1], 1, False
+        lps = launches / max(steps_measured, 1)
+        bpl = kernel_bytes(k, tot) / max(lps, 1e-9)
+        avg_s = ms / 1000.0 / max(launches, 1)
+        ach = bpl / avg_s / 1e9 if avg_s > 0 else 0.0
+        return dict(bytes_per_launch=bpl, avg_launch_us=round(avg_s * 1e6, 3), launches_per_step=lps,
+                    achieved_GBps=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
+                    ms_per_step=round(ms / max(steps_measured, 1), 4), live=live)
+
+    kroof = {k: kernel_roofline(k) for k in modelled}
+    bytes_per_launch, launches_per_step = kroof[dom]["bytes_per_launch"], kroof[dom]["launches_per_step"]
+    avg_launch_s, achieved, live = kroof[dom]["avg_launch_us"] * 1e-6, kroof[dom]["achieved_GBps"], kroof[dom]["live"]
     traffic = None
     if os.path.exists(args.pmc_json):
         try:
@@ -203,19 +269,22 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.total_jobs else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": f"{cfg}: {H}x{W} {WORKLOAD[cfg]}; "
-                        f"{B} independent scan-to-map jobs per GPU per step (C4-style independent jobs)",
+            "workload": f"{cfg}: {H}x{W} {WORKLOAD[cfg]}; " + (
+                f"{args.total_jobs} independent scan-to-map jobs per step split over {world} GPU(s) (C4)"
+                if args.total_jobs else f"{B} independent scan-to-map jobs per GPU per step (C4-style independent jobs)"),
+            "jobs_per_step": int(sum(counts)),
             "jobs_per_gpu_per_step": B,
             "mean_points_per_scan": round(tot["n_in"] / B, 1),
             "mean_local_map_points": round(tot["M"] / B, 1),
             "mean_queries_per_scan": round(tot["Q"] / B, 1),
             "mean_gn_iterations": round(float(stats["iterations"].mean()), 3),
-            "parallelism": f"scan-shard x{world}, RCCL pose all-gather" if world > 1 else "single GPU",
+            "parallelism": (f"scan-shard x{world}, {'RCCL' if args.backend == 'nccl' else 'gloo'} pose all-gather"
+                            if world > 1 else "single GPU"),
             "imu_deskew": bool(args.deskew),
         },
         "roofline": {
@@ -231,8 +300,10 @@ def main():
             "bytes_per_launch": bytes_per_launch,
             "avg_launch_us": round(avg_launch_s * 1e6, 3),
             "launches_per_step": launches_per_step,
-            "timing": "HIP events on the library stream over the timed region" if live else
-                      "HIP events on the library stream, profiled untimed step",
+            "timing": ("kernel dispatch start/end timestamps (hipExtLaunchKernel events) over the timed region"
+                       if live else "kernel dispatch start/end timestamps, profiled untimed step"),
+            "rocprof_symbols": KERNEL_SYMBOLS[dom],
+            "kernels": {k: {kk: v for kk, v in r.items() if kk != "live"} for k, r in kroof.items()},
         },
         "kernel_ms_per_step": {k: round(v[0], 4) for k, v in prof.items()},  # profiled untimed step
         "path_bytes_per_step": tb,
@@ -241,6 +312,8 @@ def main():
         "max_abs_trans_err_vs_gt_m": float(err_gt),
         "registration_status_ok": int((stats["status"] == 0).sum()),
     }
+    if records_check is not None:
+        result["records_check"] = records_check
 
     if world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -271,6 +344,18 @@ def main():
             "stage_ms_per_scan": {k: round(v / S, 3) for k, v in stage.items()},
             "mean_gn_iterations": float(ref_iters.mean()),
             "mean_n_sel": float(ref_nsel.mean()),
+        }
+        # correspondence-level parity (SURVEY §7 hard part 3): a flipped gate (sqdist < 1, lambda ratio
+        # 3, s > 0.1, plane 0.2, degeneracy 100) in any iteration shows up as a different final n_sel,
+        # iteration count or pose bits
+        it_g, ns_g = stats["iterations"][:S], stats["n_sel"][:S]
+        result["parity_vs_ref"] = {
+            "n": S,
+            "iterations_equal": int((it_g == ref_iters).sum()),
+            "n_sel_equal": int((ns_g == ref_nsel).sum()),
+            "n_sel_absdiff_max": int(np.abs(ns_g - ref_nsel).max()),
+            "pose_bit_equal": int((poses[:S].view(np.int32) == ref.view(np.int32)).all(axis=1).sum()),
+            "iterations_hist": {int(k): int(v) for k, v in zip(*np.unique(it_g, return_counts=True))},
         }
         result["pose_rmse_vs_ref"] = {
             "trans_m": float(np.sqrt(np.mean(np.sum(dt.astype(np.float64) ** 2, axis=1)))),

@@ -133,10 +133,10 @@ def device_count():
 
 
 def selftest_math(a, b):
-    """Device sqrt(|a|), a/b, atan2f(a,b), a*b+b*a-a (see fbr_selftest_math)."""
+    """Device sqrt(|a|), a/b, atan2f(a,b), a*b+b*a-a, sinf(a), cosf(a) (see fbr_selftest_math)."""
     a = np.ascontiguousarray(a, np.float32)
     b = np.ascontiguousarray(b, np.float32)
-    out = np.zeros((len(a), 4), np.float32)
+    out = np.zeros((len(a), 6), np.float32)
     _check(lib().fbr_selftest_math(len(a), ptr(a), ptr(b), ptr(out)), "fbr_selftest_math")
     return out
 
@@ -401,6 +401,11 @@ class Context:
                                                        ctypes.byref(nc), ctypes.byref(ns), ctypes.byref(nf)),
                "fbr_extract_surrounding_keyframes")
         return nc.value, ns.value, nf.value
+
+    @property
+    def stream_handle(self):
+        """The context's primary hipStream_t (int address): batch results and exports are ordered on it."""
+        return lib().fbr_stream(self._h) or 0
 
     def reset_stream(self):
         _check(lib().fbr_reset_stream(self._h), "fbr_reset_stream")

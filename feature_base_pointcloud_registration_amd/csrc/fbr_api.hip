@@ -143,6 +143,7 @@ struct fbr_ctx {
   int64_t kf_segs_cap = 0;
   int* d_bounds = nullptr;
   bool map_nocrop = false;  // the registration map is a keyframe local map
+  int stream_degenerate = 0;  // mapOptimization::isDegenerate across single-scan registrations
 };
 
 namespace {
@@ -160,15 +161,22 @@ void timer_begin(fbr_ctx* c, hipStream_t st, const char* name, hipEvent_t* ev_en
     (void)hipEventCreate(&pr.first);
     (void)hipEventCreate(&pr.second);
   }
-  (void)hipEventRecord(pr.first, st);
   t.pending.push_back(pr);
   *ev_end = pr.second;
+  // the launcher's kernels carry the events in their dispatches (fbr_launch, fbr_kernels.h)
+  launch_timer() = LaunchTimer{pr.first, pr.second, 0};
 }
 void timer_end(hipStream_t st, hipEvent_t ev_end) {
-  if (ev_end) (void)hipEventRecord(ev_end, st);
+  if (!ev_end) return;
+  LaunchTimer& t = launch_timer();
+  if (!t.launched) {  // nothing dispatched (empty input): a zero-length interval on the stream
+    (void)hipEventRecord(t.start, st);
+    (void)hipEventRecord(t.stop, st);
+  }
+  t = LaunchTimer{};
 }
 
-// Kernel launch bracketed by HIP events on the stream it is launched on (when profiling).
+// Kernel launch timed by its dispatches' own start / end timestamps (when profiling).
 #define TIMED_ON(ctx, st, name, launch)   \
   do {                                    \
     hipEvent_t ev_;                       \
@@ -376,9 +384,12 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
 struct Sub {
   int j0, B, k;  // first job, job count, sub-batch index (< kMaxSub)
   hipStream_t st;
+  bool stream_mode = false;  // single-scan call (carries stream state) vs independent batch jobs
 };
 
-Sub single_sub(fbr_ctx* c) { return Sub{0, 1, 0, c->stream}; }
+// The single-scan sub-batch: job slot 0 on the primary stream, stream mode (the state the
+// reference's stage objects keep between scans is carried between calls).
+Sub single_sub(fbr_ctx* c) { return Sub{0, 1, 0, c->stream, true}; }
 
 int stage_project(fbr_ctx* c, const Sub& sb) {
   const int64_t j0 = sb.j0;
@@ -485,6 +496,7 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   a.desk_mode = c->desk_any ? c->d_desk_mode + j0 : nullptr;
   a.desk = c->desk_any ? c->d_desk + j0 : nullptr;
   a.nocrop = c->map_nocrop ? 1 : 0;
+  a.deg_carry = sb.stream_mode ? c->stream_degenerate : 0;
   return a;
 }
 
@@ -1119,6 +1131,7 @@ int fbr_register_trace(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corne
   fbr_reg_stats st;
   rc = copy_stats(c, 1, &st);
   if (rc) return rc;
+  c->stream_degenerate = st.degenerate;
   st.n_points = 0;
   st.n_corner = (int32_t)n_corner;
   st.n_surf = (int32_t)n_surf;
@@ -1169,6 +1182,7 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
     CK(hipMemcpyAsync(pose_inout, c->d_pose_out, sizeof(float) * 6, hipMemcpyDeviceToHost, c->stream));
     rc = copy_stats(c, 1, &st);
     if (rc) return rc;
+    c->stream_degenerate = st.degenerate;
   } else {
     int32_t nv = 0, nc = 0, ns = 0;
     CK(hipMemcpy(&nv, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -1194,6 +1208,7 @@ int fbr_reset_stream(fbr_ctx* c) {
   CK(hipStreamSynchronize(c->stream));
   c->time_last = -1.0;
   c->have_projection = false;
+  c->stream_degenerate = 0;
   return FBR_OK;
 }
 
@@ -1201,24 +1216,30 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
                     const float* poses_in) {
   if (!c || !scans || !n_in || !poses_in || n_jobs <= 0) return FBR_ERR_INVALID_ARG;
   if (n_jobs > c->Bcap) return FBR_ERR_CAPACITY;
-  CK(hipSetDevice(c->dev));
-  c->no_time_call = false;
+  // every job is validated before anything is copied: a rejected batch leaves the previous one's
+  // buffers untouched, and nothing stays staged after a failure
   for (int j = 0; j < n_jobs; ++j) {
     if (n_in[j] < 0 || n_in[j] > c->NMAX) return FBR_ERR_CAPACITY;
     if (n_in[j] && !scans[j]) return FBR_ERR_INVALID_ARG;
+  }
+  CK(hipSetDevice(c->dev));
+  drop_staged_batch(c);
+  c->no_time_call = false;
+  int rc = FBR_OK;
+  auto q = [&](hipError_t e) {
+    if (e != hipSuccess && !rc) rc = FBR_ERR_HIP;
+  };
+  for (int j = 0; j < n_jobs && !rc; ++j)
     if (n_in[j])
-      CK(hipMemcpyAsync(c->d_pts + j * c->NMAX, scans[j], sizeof(fbr_point_xyzirt) * n_in[j], hipMemcpyHostToDevice,
-                        c->stream));
-  }
-  CK(hipMemcpyAsync(c->d_nin, n_in, sizeof(int64_t) * n_jobs, hipMemcpyHostToDevice, c->stream));
-  CK(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * n_jobs, hipMemcpyHostToDevice, c->stream));
-  c->crop_cached = false;
-  if (c->has_map) {
-    const int rc = crop_stats(c, Sub{0, n_jobs, 0, c->stream});
-    if (rc) return rc;
-    c->crop_cached = true;
-  }
-  CK(hipStreamSynchronize(c->stream));
+      q(hipMemcpyAsync(c->d_pts + j * c->NMAX, scans[j], sizeof(fbr_point_xyzirt) * n_in[j], hipMemcpyHostToDevice,
+                       c->stream));
+  if (!rc) q(hipMemcpyAsync(c->d_nin, n_in, sizeof(int64_t) * n_jobs, hipMemcpyHostToDevice, c->stream));
+  if (!rc) q(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * n_jobs, hipMemcpyHostToDevice, c->stream));
+  if (!rc && c->has_map) rc = crop_stats(c, Sub{0, n_jobs, 0, c->stream});
+  // the caller's host buffers may be reused once this returns: drain the queued copies on every path
+  q(hipStreamSynchronize(c->stream));
+  if (rc) return rc;
+  c->crop_cached = c->has_map;
   c->staged_B = n_jobs;
   c->staged_nin.assign(n_in, n_in + n_jobs);
   return FBR_OK;
@@ -1408,11 +1429,12 @@ int fbr_kernel_time(fbr_ctx* c, const char* kernel, double* total_ms, int64_t* l
 
 void* fbr_stream(fbr_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
-// pcl::getTransformation(x, y, z, roll, pitch, yaw) (pcl/common/impl/eigen.hpp), float.
+// pcl::getTransformation(x, y, z, roll, pitch, yaw) (pcl/common/impl/eigen.hpp), float, with
+// glibc's sinf / cosf (fbr_sincosf.h).
 void fbr_affine_from_pose(const float pose[6], float m[16]) {
   const float roll = pose[0], pitch = pose[1], yaw = pose[2];
-  const float A = std::cos(yaw), B = std::sin(yaw), C = std::cos(pitch), D = std::sin(pitch), E = std::cos(roll),
-              F = std::sin(roll), DE = D * E, DF = D * F;
+  const float A = fbr::gl_cosf(yaw), B = fbr::gl_sinf(yaw), C = fbr::gl_cosf(pitch), D = fbr::gl_sinf(pitch),
+              E = fbr::gl_cosf(roll), F = fbr::gl_sinf(roll), DE = D * E, DF = D * F;
   m[0] = A * C; m[1] = A * DF - B * E; m[2] = B * F + A * DE; m[3] = pose[3];
   m[4] = B * C; m[5] = A * E + B * DF; m[6] = B * DE - A * F; m[7] = pose[4];
   m[8] = -D;    m[9] = C * F;          m[10] = C * E;         m[11] = pose[5];

@@ -12,14 +12,14 @@
 //                            (redux_novec_unroller splits 3 into 1 + 2)
 //   tf::Quaternion::setRPY / slerp / angleShortestPath, tf::Matrix3x3(q).getRPY
 //                            (tf/LinearMath/Quaternion.h, Matrix3x3.h; tfScalar = double)
-// Float sin/cos differ from the reference's glibc sinf/cosf (IFUNC-dispatched: FMA or SSE2
-// variant by host CPU) by an ulp or two on the device, so deskewed coordinates match the
-// reference to float rounding, not bit for bit.
+// Float sin/cos are glibc's sinf/cosf restated bit for bit (fbr_sincosf.h), on the host and the
+// device alike.
 #pragma once
 #include <math.h>
 #include <stdint.h>
 
 #include "fbr.h"
+#include "fbr_sincosf.h"
 
 #if defined(__HIPCC__)
 #define FBR_HD __host__ __device__
@@ -37,10 +37,9 @@ struct Rot3 {
   float m[3][3];
 };
 
-// sinf / cosf: glibc's on the host; on the device the ROCm f32 routines (within an ulp or two,
-// like glibc's IFUNC variants, and far cheaper than the double routines per deskewed point).
-FBR_HD inline float fsin(float x) { return sinf(x); }
-FBR_HD inline float fcos(float x) { return cosf(x); }
+// sinf / cosf as glibc 2.35 computes them on an FMA-capable x86-64 host (fbr_sincosf.h).
+FBR_HD inline float fsin(float x) { return gl_sinf(x); }
+FBR_HD inline float fcos(float x) { return gl_cosf(x); }
 
 // findRotation (:494-526)
 FBR_HD inline void find_rotation(const fbr_deskew_table& T, double pointTime, float* rx, float* ry, float* rz) {

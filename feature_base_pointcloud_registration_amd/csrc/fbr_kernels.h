@@ -1,11 +1,38 @@
 // fbr_kernels.h — argument blocks and host launchers of the device kernels.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "fbr_common.h"
 
 namespace fbr {
+
+// ---- kernel timing (fbr_set_profiling) ----
+// When a launcher runs under a kernel timer (fbr_api.hip TIMED_ON), its kernels are dispatched with
+// hipExtLaunchKernel and the timer's events: the first kernel's dispatch records the start event
+// with its own start timestamp and every kernel records the stop event with its end timestamp, so
+// the measured interval is the launcher's kernels' execution (the timestamps rocprofv3's kernel
+// trace reports), not the time the stream spends waiting for CUs the other streams hold.
+struct LaunchTimer {
+  hipEvent_t start = nullptr, stop = nullptr;
+  int launched = 0;
+};
+inline LaunchTimer& launch_timer() {
+  static thread_local LaunchTimer t;
+  return t;
+}
+
+template <typename F, typename... Args>
+inline void fbr_launch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, Args... args) {
+  LaunchTimer& t = launch_timer();
+  if (t.stop) {
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, t.launched ? nullptr : t.start, t.stop, 0, args...);
+    t.launched++;
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, shmem, s, args...);
+  }
+}
 
 // ---- A2+A4 (k_project.hip) ----
 // Device copy of the resolved PointCloud2 layout (fbr_msg.h): offsets x, y, z, intensity, ring,
@@ -138,6 +165,8 @@ struct GnArgs {
   const int32_t* desk_mode;  // [B] kDesk* bits or null (transformUpdate's IMU slerp, :1447-1474)
   const fbr_deskew_table* desk;  // [B]
   int nocrop;                // 1: keyframe local map, no CropBox (scan2MapOptimization on it)
+  int deg_carry;             // isDegenerate before the first LMOptimization (the member carried
+                             // across registration() calls, mapOptmization.h:137); 0 for batch jobs
 };
 void launch_gn_init(hipStream_t s, const GnArgs& a);
 // fused: kNN + residual row + item partial in one launch (launch_gn_residual is then skipped)

@@ -858,9 +858,9 @@ size_t features_gslot_bytes(const FeatArgs& a) {
 
 void launch_features(hipStream_t s, const FeatArgs& a) {
   if (a.segcap <= 6 * 64 && a.kseg <= 4 * 128)
-    hipLaunchKernelGGL((k_features<6, 4>), dim3(a.B * a.H), dim3(64), features_lds_bytes(a), s, a);
+    fbr_launch((k_features<6, 4>), dim3(a.B * a.H), dim3(64), features_lds_bytes(a), s, a);
   else
-    hipLaunchKernelGGL((k_features<12, 8>), dim3(a.B * a.H), dim3(64), features_lds_bytes(a), s, a);
+    fbr_launch((k_features<12, 8>), dim3(a.B * a.H), dim3(64), features_lds_bytes(a), s, a);
 }
 
 }  // namespace fbr

@@ -46,7 +46,7 @@ void launch_kf_transform(hipStream_t s, const float4* pool, const KfSeg* segs, i
   const int gx = (int)std::min<int64_t>((max_count + 255) / 256, 64);
   for (int s0 = 0; s0 < nseg; s0 += 65535) {
     const int n = std::min(65535, nseg - s0);
-    hipLaunchKernelGGL(k_kf_transform, dim3(gx, n), dim3(256), 0, s, pool, segs + s0, n, out);
+    fbr_launch(k_kf_transform, dim3(gx, n), dim3(256), 0, s, pool, segs + s0, n, out);
   }
 }
 
@@ -103,7 +103,7 @@ int grid_bounds_device(hipStream_t s, const float4* pts, int64_t n, float invx, 
   if (hipMemcpyAsync(d_bounds, init, sizeof(init), hipMemcpyHostToDevice, s) != hipSuccess) return FBR_ERR_HIP;
   if (n > 0) {
     const int grid = (int)std::min<int64_t>((n + 255) / 256, 2048);
-    hipLaunchKernelGGL(k_grid_bounds, dim3(grid), dim3(256), 0, s, pts, n, invx, inv, d_bounds);
+    fbr_launch(k_grid_bounds, dim3(grid), dim3(256), 0, s, pts, n, invx, inv, d_bounds);
   }
   if (hipMemcpyAsync(h_bounds, d_bounds, sizeof(int) * 6, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
@@ -120,7 +120,7 @@ int grid_fill_device(hipStream_t s, const float4* pts, int64_t n, const GridDesc
   if (hipMallocAsync((void**)&cnt, sizeof(int32_t) * (ncell + 1), s) != hipSuccess) return FBR_ERR_HIP;
   if (hipMemsetAsync(cnt, 0, sizeof(int32_t) * (ncell + 1), s) != hipSuccess) rc = FBR_ERR_HIP;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 2048));
-  if (!rc && n > 0) hipLaunchKernelGGL(k_grid_count, dim3(grid), dim3(256), 0, s, pts, n, g, cnt);
+  if (!rc && n > 0) fbr_launch(k_grid_count, dim3(grid), dim3(256), 0, s, pts, n, g, cnt);
   // cell_start = exclusive scan of the counts (ncell + 1 entries: the last is n)
   if (!rc && rocprim::exclusive_scan(nullptr, tmp_bytes, cnt, d_cs, 0, (size_t)(ncell + 1), rocprim::plus<int32_t>(), s) !=
                  hipSuccess)
@@ -131,7 +131,7 @@ int grid_fill_device(hipStream_t s, const float4* pts, int64_t n, const GridDesc
     rc = FBR_ERR_HIP;
   // reuse the counts as fill cursors
   if (!rc && hipMemcpyAsync(cnt, d_cs, sizeof(int32_t) * ncell, hipMemcpyDeviceToDevice, s) != hipSuccess) rc = FBR_ERR_HIP;
-  if (!rc && n > 0) hipLaunchKernelGGL(k_grid_scatter, dim3(grid), dim3(256), 0, s, pts, n, g, cnt, d_out);
+  if (!rc && n > 0) fbr_launch(k_grid_scatter, dim3(grid), dim3(256), 0, s, pts, n, g, cnt, d_out);
   if (tmp) (void)hipFreeAsync(tmp, s);
   (void)hipFreeAsync(cnt, s);
   return rc;

@@ -264,9 +264,9 @@ void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_
     if (L.off[k] >= 0) aligned = aligned && (L.off[k] % (k == 4 ? 2 : 4) == 0);
   const dim3 grid((unsigned)((L.n + 255) / 256));
   if (aligned)
-    hipLaunchKernelGGL(k_unpack_msg<true>, grid, dim3(256), 0, s, data, L, out);
+    fbr_launch(k_unpack_msg<true>, grid, dim3(256), 0, s, data, L, out);
   else
-    hipLaunchKernelGGL(k_unpack_msg<false>, grid, dim3(256), 0, s, data, L, out);
+    fbr_launch(k_unpack_msg<false>, grid, dim3(256), 0, s, data, L, out);
 }
 
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
@@ -277,19 +277,19 @@ void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* n
   int tile_log2 = 6;  // 64 columns, shrunk so the tile stays <= 32 KB
   while (tile_log2 > 3 && ((int64_t)H << tile_log2) > 8192) --tile_log2;
   const size_t lds = sizeof(int32_t) * ((size_t)H << tile_log2);
-  hipLaunchKernelGGL(k_project, dim3(blocks, B), dim3(kProjThreads), lds, s, pts, nin, nmax, H, W, tile_log2, owner);
+  fbr_launch(k_project, dim3(blocks, B), dim3(kProjThreads), lds, s, pts, nin, nmax, H, W, tile_log2, owner);
 }
 
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,
                     int W, int32_t* rowcnt, float4* cloud, int32_t* col, float* range, int32_t* start_ring,
                     int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk) {
-  hipLaunchKernelGGL(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, rowcnt, desk.mode ? desk.rowmin : nullptr);
+  fbr_launch(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, rowcnt, desk.mode ? desk.rowmin : nullptr);
   const int groups = (B + 7) / 8;
   if (desk.mode)
-    hipLaunchKernelGGL(k_compact<true>, dim3(groups * 8 * H), dim3(64), 0, s, pts, nmax, owner, rowcnt, B, H, W, cloud,
+    fbr_launch(k_compact<true>, dim3(groups * 8 * H), dim3(64), 0, s, pts, nmax, owner, rowcnt, B, H, W, cloud,
                        col, range, start_ring, end_ring, nvalid, desk);
   else
-    hipLaunchKernelGGL(k_compact<false>, dim3(groups * 8 * H), dim3(64), 0, s, pts, nmax, owner, rowcnt, B, H, W, cloud,
+    fbr_launch(k_compact<false>, dim3(groups * 8 * H), dim3(64), 0, s, pts, nmax, owner, rowcnt, B, H, W, cloud,
                        col, range, start_ring, end_ring, nvalid, desk);
 }
 

@@ -46,11 +46,12 @@ constexpr int kSolveThreads = 128;  // k_gn_solve: wave 0 sums + solves, wave 1 
 constexpr int kPartial = 32;  // doubles per item partial: 21 AtA upper + 6 AtB + count
 }
 
-// pcl::getTransformation (x,y,z,roll,pitch,yaw) in float, sin/cos rounded from double.
+// pcl::getTransformation (x,y,z,roll,pitch,yaw) in float with glibc's sinf / cosf
+// (fbr_sincosf.h: the FMA variant restated bit for bit).
 __device__ void pose_to_T(const float* tr, float* T, float* trig) {
   const float roll = tr[0], pitch = tr[1], yaw = tr[2];
-  const float A = (float)cos((double)yaw), B = (float)sin((double)yaw), C = (float)cos((double)pitch),
-              D = (float)sin((double)pitch), E = (float)cos((double)roll), F = (float)sin((double)roll);
+  const float A = gl_cosf(yaw), B = gl_sinf(yaw), C = gl_cosf(pitch), D = gl_sinf(pitch), E = gl_cosf(roll),
+              F = gl_sinf(roll);
   const float DE = D * E, DF = D * F;
   T[0] = A * C; T[1] = A * DF - B * E; T[2] = B * F + A * DE; T[3] = tr[3];
   T[4] = B * C; T[5] = A * E + B * DF; T[6] = B * DE - A * F; T[7] = tr[4];
@@ -321,7 +322,10 @@ __global__ void k_gn_init(GnArgs a) {
       }
       for (int k = 0; k < 36; ++k) g.matP[k] = 0.0f;
       const int nc = a.ncds[job], ns = a.nsds[job];
-      g.iter = 0; g.converged = 0; g.degenerate = 0; g.n_sel = 0;
+      g.iter = 0; g.converged = 0; g.n_sel = 0;
+      // isDegenerate is a class member: an iteration-0 early return (< 50 rows) keeps the previous
+      // scan's value (single-scan paths carry it; independent batch jobs start from false)
+      g.degenerate = a.deg_carry ? 1 : 0;
       if (nc > a.edge_min && ns > a.surf_min) {
         g.status = FBR_REG_OK;
         g.active = 1;
@@ -749,17 +753,17 @@ __global__ void k_export_records(int B, const float* pose_out, const fbr_reg_sta
 }
 
 void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, float* dst) {
-  hipLaunchKernelGGL(k_export_records, dim3((B + 63) / 64), dim3(64), 0, s, B, pose_out, stats, dst);
+  fbr_launch(k_export_records, dim3((B + 63) / 64), dim3(64), 0, s, B, pose_out, stats, dst);
 }
 
-void launch_gn_init(hipStream_t s, const GnArgs& a) { hipLaunchKernelGGL(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
+void launch_gn_init(hipStream_t s, const GnArgs& a) { fbr_launch(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
 template <int R, bool F, bool L>
 void launch_gn_knn_rl(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
   const float invx = a.mc.g.inv_x;  // == a.ms.g.inv_x
-  if (invx > 4.0f) hipLaunchKernelGGL((k_gn_knn<R, 8, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
-  else if (invx > 2.0f) hipLaunchKernelGGL((k_gn_knn<R, 4, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
-  else if (invx > 1.0f) hipLaunchKernelGGL((k_gn_knn<R, 2, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
-  else hipLaunchKernelGGL((k_gn_knn<R, 1, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
+  if (invx > 4.0f) fbr_launch((k_gn_knn<R, 8, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
+  else if (invx > 2.0f) fbr_launch((k_gn_knn<R, 4, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
+  else if (invx > 1.0f) fbr_launch((k_gn_knn<R, 2, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
+  else fbr_launch((k_gn_knn<R, 1, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
 }
 
 // Flat row queue (FBR_KNN_FLAT=0 disables): from iteration 1 on (warm-start bound), 1 m y/z cells
@@ -794,18 +798,18 @@ void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fuse
   else launch_gn_knn_f<false>(s, a, grid, use_prev);
 }
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
-  hipLaunchKernelGGL(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);
+  fbr_launch(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);
 }
 void launch_gn_solve(hipStream_t s, const GnArgs& a, int iter_idx, unsigned long long gen) {
-  hipLaunchKernelGGL(k_gn_solve, dim3(a.B), dim3(kSolveThreads), 0, s, a, iter_idx, gen);
+  fbr_launch(k_gn_solve, dim3(a.B), dim3(kSolveThreads), 0, s, a, iter_idx, gen);
 }
 void launch_gn_finalize(hipStream_t s, const GnArgs& a) {
-  hipLaunchKernelGGL(k_gn_finalize, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
+  fbr_launch(k_gn_finalize, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
 }
 void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* pts, int64_t n, int which, int32_t* counts) {
   if (n <= 0) return;
   int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
-  hipLaunchKernelGGL(k_crop_count, dim3(grid), dim3(256), sizeof(int32_t) * a.B, s, a, pts, n, which, counts);
+  fbr_launch(k_crop_count, dim3(grid), dim3(256), sizeof(int32_t) * a.B, s, a, pts, n, which, counts);
 }
 
 }  // namespace fbr

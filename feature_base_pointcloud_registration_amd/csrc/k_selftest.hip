@@ -1,23 +1,32 @@
 // k_selftest.hip — device numerics probe behind fbr_selftest_math (diagnostic entry point).
 //
 // The path's bit-exactness rests on a few device primitives matching the reference's host libm:
-// correctly rounded f32 sqrt and division (SSE sqrtss / divss) and glibc atan2f
-// (imageProjection.cpp:605,618).  tests/test_gpu_parity.py feeds random operands through this
+// correctly rounded f32 sqrt and division (SSE sqrtss / divss), glibc atan2f
+// (imageProjection.cpp:605,618) and glibc sinf / cosf (pcl::getTransformation, LMOptimization
+// mapOptmization.h:1259-1264).  tests/test_gpu_parity.py feeds random operands through this
 // kernel and compares every output bit with the host.
+#include <algorithm>
+
 #include "fbr_common.h"
 #include "fbr_fdlibm.h"
+#include "fbr_sincosf.h"
 #include "fbr_solvers.h"
 
 namespace fbr {
+
+constexpr int kSelftestMathOut = 6;
 
 __global__ void k_selftest_math(int n, const float* a, const float* b, float* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float x = a[i], y = b[i];
-  out[4 * i + 0] = sqrt_rn(x < 0.0f ? -x : x);
-  out[4 * i + 1] = x / y;
-  out[4 * i + 2] = fd_atan2f(x, y);
-  out[4 * i + 3] = x * y + y * x - x;  // plain mul/add with contraction disabled
+  float* o = out + (int64_t)kSelftestMathOut * i;
+  o[0] = sqrt_rn(x < 0.0f ? -x : x);
+  o[1] = x / y;
+  o[2] = fd_atan2f(x, y);
+  o[3] = x * y + y * x - x;  // plain mul/add with contraction disabled
+  o[4] = gl_sinf(x);
+  o[5] = gl_cosf(x);
 }
 
 // One 64-lane workgroup per symmetric 6x6 matrix: the single-lane jacobi_eigen<6> (lane 0) and the
@@ -48,14 +57,14 @@ extern "C" int fbr_selftest_math(int n, const float* a, const float* b, float* o
   float *da = nullptr, *db = nullptr, *dout = nullptr;
   int rc = FBR_OK;
   if (hipMalloc(&da, sizeof(float) * n) != hipSuccess || hipMalloc(&db, sizeof(float) * n) != hipSuccess ||
-      hipMalloc(&dout, sizeof(float) * 4 * n) != hipSuccess) {
+      hipMalloc(&dout, sizeof(float) * fbr::kSelftestMathOut * n) != hipSuccess) {
     rc = FBR_ERR_HIP;
   } else if (hipMemcpy(da, a, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess ||
              hipMemcpy(db, b, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) {
     rc = FBR_ERR_HIP;
   } else {
     hipLaunchKernelGGL(fbr::k_selftest_math, dim3((n + 255) / 256), dim3(256), 0, 0, n, da, db, dout);
-    if (hipMemcpy(out, dout, sizeof(float) * 4 * n, hipMemcpyDeviceToHost) != hipSuccess) rc = FBR_ERR_HIP;
+    if (hipMemcpy(out, dout, sizeof(float) * fbr::kSelftestMathOut * n, hipMemcpyDeviceToHost) != hipSuccess) rc = FBR_ERR_HIP;
   }
   (void)hipFree(da);
   (void)hipFree(db);
@@ -81,10 +90,33 @@ extern "C" int fbr_selftest_eigen6(int n, const float* a, float* out) {
 }
 
 // STREAM-copy probe (measurement helper, BASELINE.md "report vs measured STREAM-copy bandwidth"):
-// a grid-stride float4 copy of `bytes` per direction, timed with HIP events over `iters` launches.
+// float4 copies of `bytes` per direction, timed with HIP events over `iters` launches.  Three
+// shapes are timed and the best is reported: a grid-stride loop, one float4 per thread with one
+// workgroup per 4 KiB, and U float4 per thread (all loads issued before the stores, non-temporal
+// stores) with one workgroup per U * 4 KiB.
 namespace fbr {
 __global__ void __launch_bounds__(256) k_stream_copy(const float4* __restrict__ a, float4* __restrict__ b, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) b[i] = a[i];
+}
+template <int U>
+__global__ void __launch_bounds__(256) k_stream_copy_u(const float4* __restrict__ a, float4* __restrict__ b, int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+  float4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + (int64_t)u * 256;
+    v[u] = i < n ? a[i] : make_float4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + (int64_t)u * 256;
+    if (i < n) {
+      __builtin_nontemporal_store(v[u].x, &b[i].x);
+      __builtin_nontemporal_store(v[u].y, &b[i].y);
+      __builtin_nontemporal_store(v[u].z, &b[i].z);
+      __builtin_nontemporal_store(v[u].w, &b[i].w);
+    }
+  }
 }
 }  // namespace fbr
 
@@ -100,16 +132,26 @@ extern "C" int fbr_stream_copy_bandwidth(int hip_device, int64_t bytes, int iter
       hipEventCreate(&e1) != hipSuccess) {
     rc = FBR_ERR_HIP;
   } else {
-    const int grid = 256 * 8 * 4;  // 8 XCDs x 32 CUs, several workgroups per CU
-    hipLaunchKernelGGL(fbr::k_stream_copy, dim3(grid), dim3(256), 0, 0, a, b, n);  // warm-up
-    (void)hipEventRecord(e0, 0);
-    for (int k = 0; k < iters; ++k) hipLaunchKernelGGL(fbr::k_stream_copy, dim3(grid), dim3(256), 0, 0, a, b, n);
-    (void)hipEventRecord(e1, 0);
-    float ms = 0.0f;
-    if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess || ms <= 0.0f)
-      rc = FBR_ERR_HIP;
-    else
-      *gbps = 2.0 * 16.0 * (double)n * iters / (ms * 1e-3) / 1e9;  // read + write
+    *gbps = 0.0;
+    for (int variant = 0; variant < 3 && !rc; ++variant) {
+      auto launch = [&]() {
+        if (variant == 0)  // grid stride: 8 XCDs x 32 CUs, several workgroups per CU
+          hipLaunchKernelGGL(fbr::k_stream_copy, dim3(256 * 8 * 4), dim3(256), 0, 0, a, b, n);
+        else if (variant == 1)
+          hipLaunchKernelGGL(fbr::k_stream_copy_u<1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, a, b, n);
+        else
+          hipLaunchKernelGGL(fbr::k_stream_copy_u<4>, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, 0, a, b, n);
+      };
+      launch();  // warm-up
+      (void)hipEventRecord(e0, 0);
+      for (int k = 0; k < iters; ++k) launch();
+      (void)hipEventRecord(e1, 0);
+      float ms = 0.0f;
+      if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess || ms <= 0.0f)
+        rc = FBR_ERR_HIP;
+      else
+        *gbps = std::max(*gbps, 2.0 * 16.0 * (double)n * iters / (ms * 1e-3) / 1e9);  // read + write
+    }
   }
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);

@@ -617,11 +617,11 @@ void launch_voxel_ring(hipStream_t s, const VgRing& a) {
   // 512 threads, KPT = ceil(W / 512) points per thread (instances up to W = 4096)
   const int kpt = (int)((a.cap + 511) / 512);
   if (kpt <= 2)
-    hipLaunchKernelGGL((k_voxel_ring<512, 2>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 2), s, a);
+    fbr_launch((k_voxel_ring<512, 2>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 2), s, a);
   else if (kpt <= 4)
-    hipLaunchKernelGGL((k_voxel_ring<512, 4>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 4), s, a);
+    fbr_launch((k_voxel_ring<512, 4>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 4), s, a);
   else
-    hipLaunchKernelGGL((k_voxel_ring<512, 8>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 8), s, a);
+    fbr_launch((k_voxel_ring<512, 8>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 8), s, a);
 }
 
 size_t voxel_lds_bytes(const VgArgs& a, int threads, bool lds_mode) {
@@ -644,9 +644,9 @@ void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
   for (int k = 0; k < 2; ++k)
     if (a.s[k].nseg > 0) cap = std::max<int64_t>(cap, a.s[k].cap);
   if (cap <= kVgLdsCap) {
-    hipLaunchKernelGGL((k_voxel_grid<256, uint16_t, true>), dim3(nseg), dim3(256), voxel_lds_bytes(a, 256, true), s, a);
+    fbr_launch((k_voxel_grid<256, uint16_t, true>), dim3(nseg), dim3(256), voxel_lds_bytes(a, 256, true), s, a);
   } else {
-    hipLaunchKernelGGL((k_voxel_grid<1024, uint32_t, false>), dim3(nseg), dim3(1024), voxel_lds_bytes(a, 1024, false), s,
+    fbr_launch((k_voxel_grid<1024, uint32_t, false>), dim3(nseg), dim3(1024), voxel_lds_bytes(a, 1024, false), s,
                        a);
   }
 }
@@ -689,7 +689,7 @@ void launch_concat(hipStream_t s, int B, int H, int W, const float4* corner_slot
                    const float4* surf_ring, const int32_t* surf_ring_cnt, float4* corner_all, int64_t capc,
                    int32_t* n_corner, float4* surf_all, int64_t caps, int32_t* n_surf) {
   if (B <= 0 || H <= 0) return;
-  hipLaunchKernelGGL(k_concat, dim3(B * ((H + 3) / 4)), dim3(256), 0, s, H, W, corner_slot, corner_cnt, surf_ring,
+  fbr_launch(k_concat, dim3(B * ((H + 3) / 4)), dim3(256), 0, s, H, W, corner_slot, corner_cnt, surf_ring,
                      surf_ring_cnt, corner_all, capc, n_corner, surf_all, caps, n_surf);
 }
 
@@ -810,16 +810,16 @@ int voxel_grid_large(hipStream_t s, const float4* in, int64_t n, float leaf, int
       ok(hipMallocAsync((void**)&v0, 4 * N, s)) && ok(hipMallocAsync((void**)&v1, 4 * N, s)) &&
       ok(hipMallocAsync((void**)&vox, 4 * N, s)) &&
       ok(hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, s))) {
-    hipLaunchKernelGGL(k_vgl_minmax, dim3(grid), dim3(256), 0, s, in, n, mm);
-    hipLaunchKernelGGL(k_vgl_grid, dim3(1), dim3(1), 0, s, mm, leaf, morton, st);
-    hipLaunchKernelGGL(k_vgl_keys, dim3(grid), dim3(256), 0, s, in, n, st, k0, v0);
+    fbr_launch(k_vgl_minmax, dim3(grid), dim3(256), 0, s, in, n, mm);
+    fbr_launch(k_vgl_grid, dim3(1), dim3(1), 0, s, mm, leaf, morton, st);
+    fbr_launch(k_vgl_keys, dim3(grid), dim3(256), 0, s, in, n, st, k0, v0);
     if (ok(rocprim::radix_sort_pairs(nullptr, tb_sort, k0, k1, v0, v1, N, 0, 32, s)) &&
         ok(rocprim::exclusive_scan(nullptr, tb_scan, vox, vox, 0u, N, rocprim::plus<uint32_t>(), s)) &&
         ok(hipMallocAsync(&tmp, std::max<size_t>(std::max(tb_sort, tb_scan), 16), s)) &&
         ok(rocprim::radix_sort_pairs(tmp, tb_sort, k0, k1, v0, v1, N, 0, 32, s))) {
-      hipLaunchKernelGGL(k_vgl_heads, dim3(grid), dim3(256), 0, s, k1, n, vox);
+      fbr_launch(k_vgl_heads, dim3(grid), dim3(256), 0, s, k1, n, vox);
       if (ok(rocprim::exclusive_scan(tmp, tb_scan, vox, vox, 0u, N, rocprim::plus<uint32_t>(), s)))
-        hipLaunchKernelGGL(k_vgl_emit, dim3(grid), dim3(256), 0, s, in, n, st, k1, v1, vox, out, d_nout);
+        fbr_launch(k_vgl_emit, dim3(grid), dim3(256), 0, s, in, n, st, k1, v1, vox, out, d_nout);
     }
   }
   for (void* p : {(void*)mm, (void*)st, (void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)vox, tmp})

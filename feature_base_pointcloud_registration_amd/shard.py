@@ -17,6 +17,13 @@ def job_seeds(rank, world, per_rank, base=1000):
     return [base + rank * per_rank + j for j in range(per_rank)]
 
 
+def job_block(rank, world, total):
+    """Strong split of `total` jobs: rank r owns the contiguous block [j0, j1) (sizes differ by at
+    most one; the C4 config is 1024 jobs over 8 GPUs = 128 each)."""
+    assert 0 <= rank < world and total >= world
+    return total * rank // world, total * (rank + 1) // world
+
+
 def encode_records(poses, iterations, status):
     """numpy [B,6] f32 + [B] i32 + [B] i32 -> flat f32 [B*8] (the layout fbr_batch_export writes)."""
     B = len(poses)
@@ -38,3 +45,9 @@ def gather_records(dist, local, world):
     parts = [torch.empty_like(local) for _ in range(world)]
     dist.all_gather(parts, local)
     return torch.cat(parts)
+
+
+def unpad_records(gathered, counts):
+    """Rank-ordered records of a gather whose ranks padded their blocks to max(counts) jobs."""
+    flat = np.asarray(gathered, np.float32).reshape(len(counts), -1, RECORD_FLOATS)
+    return np.concatenate([flat[r, :c] for r, c in enumerate(counts)]).reshape(-1)

@@ -366,9 +366,9 @@ void* fbr_stream(fbr_ctx* ctx);
 int fbr_voxel_grid(fbr_ctx* ctx, const fbr_point_xyzi* in, int64_t n, float leaf,
                    fbr_point_xyzi* out, int64_t* n_out);
 
-/* Diagnostic: device numerics probe.  For i < n writes out[4i..4i+3] = {sqrtf(|a|), a/b,
- * atan2f(a,b), a*b+b*a-a} computed by the device kernels' primitives (tests compare the bits with
- * the host libm the reference uses). */
+/* Diagnostic: device numerics probe.  For i < n writes out[6i..6i+5] = {sqrtf(|a|), a/b,
+ * atan2f(a,b), a*b+b*a-a, sinf(a), cosf(a)} computed by the device kernels' primitives (tests
+ * compare the bits with the host libm the reference uses). */
 int fbr_selftest_math(int n, const float* a, const float* b, float* out);
 
 /* Diagnostic: cv::eigen of n symmetric 6x6 float matrices a[36i..36i+35] (the degeneracy step,

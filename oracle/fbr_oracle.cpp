@@ -937,9 +937,15 @@ struct StageTimer {  // charges the time since the last lap to stage k; the dest
 
 static void registration_core(const fbr_params& P, const Map& map, const P4* cornerLast, int64_t ncl,
                               const P4* surfLast, int64_t nsl, float tr[6], RegResult& R, int nthreads,
-                              const fbr_deskew_table* T = nullptr, bool no_crop = false) {
+                              const fbr_deskew_table* T = nullptr, bool no_crop = false,
+                              bool* deg_state = nullptr) {
   fbr_reg_stats& st = R.st;
   std::memset(&st, 0, sizeof(st));
+  // mapOptimization::isDegenerate is a class member (:137): LMOptimization only rewrites it at
+  // iteration 0 with >= 50 rows, so it carries across registration() calls (deg_state, when the
+  // caller keeps one; independent jobs start from false)
+  bool isDegenerate = deg_state ? *deg_state : false;
+  st.degenerate = isDegenerate ? 1 : 0;
   R.trace.clear();
   // CropBox around the guess translation (:284-304); origin/edges in float
   const float origin[3] = {tr[3], tr[4], tr[5]};
@@ -973,13 +979,19 @@ static void registration_core(const fbr_params& P, const Map& map, const P4* cor
     st.status = FBR_REG_NOT_ENOUGH_FEATURES;
     return;
   }
+  struct DegSave {  // write the member back on every return below
+    bool* state;
+    const bool& v;
+    ~DegSave() {
+      if (state) *state = v;
+    }
+  } deg_save{deg_state, isDegenerate};
   KDTree kdc, kds;
   kdc.build(cornerMap.data(), (int)cornerMap.size());
   kds.build(surfMap.data(), (int)surfMap.size());
   tm.lap(5);
   std::vector<P4> oriC(Nc), coeffC(Nc), oriS(Ns), coeffS(Ns);
   std::vector<char> flagC(Nc), flagS(Ns);
-  bool isDegenerate = false;
   for (int iterCount = 0; iterCount < P.max_iterations; iterCount++) {
     const Affine T = trans2affine(tr);  // updatePointAssociateToMap (:995-1000)
     std::fill(flagC.begin(), flagC.end(), 0);
@@ -1198,6 +1210,7 @@ struct orc_stream {
   fbr_params P;
   FeatState fs;
   double timeLastProcessing = -1;
+  bool isDegenerate = false;  // mapOptimization::isDegenerate (carried between scans)
   bool has_desk = false;  // deskewInfo() enabled for the next scans (orc_stream_set_deskew)
   fbr_deskew_table desk;
   const fbr_deskew_table* table() const { return has_desk ? &desk : nullptr; }
@@ -1242,6 +1255,7 @@ void orc_stream_reset(void* s) {
   orc_stream* st = (orc_stream*)s;
   st->fs.init(st->P.n_scan, st->P.horizon_scan);
   st->timeLastProcessing = -1;
+  st->isDegenerate = false;
 }
 
 // Projection + FeatureExtraction on one scan (stream state carried in `s`).
@@ -1361,11 +1375,15 @@ int orc_map_get(void* mp, int64_t* nc, int64_t* ns, fbr_point_xyzi* corner, fbr_
   return 0;
 }
 
+// degenerate_inout: the isDegenerate member before / after the call (null: a fresh matcher, false)
 int orc_register(const fbr_params* P, void* map, const fbr_point_xyzi* corner, int64_t nc, const fbr_point_xyzi* surf,
                  int64_t ns, float pose[6], fbr_reg_stats* st, float* trace, int nthreads,
-                 const fbr_deskew_table* desk, int no_crop) {
+                 const fbr_deskew_table* desk, int no_crop, int32_t* degenerate_inout) {
   RegResult R;
-  registration_core(*P, *(Map*)map, corner, nc, surf, ns, pose, R, nthreads, desk, no_crop != 0);
+  bool deg = degenerate_inout ? *degenerate_inout != 0 : false;
+  registration_core(*P, *(Map*)map, corner, nc, surf, ns, pose, R, nthreads, desk, no_crop != 0,
+                    degenerate_inout ? &deg : nullptr);
+  if (degenerate_inout) *degenerate_inout = deg ? 1 : 0;
   if (st) *st = R.st;
   if (trace) std::memcpy(trace, R.trace.data(), sizeof(float) * R.trace.size());
   return 0;
@@ -1387,7 +1405,7 @@ int orc_process_scan(void* s, void* map, const fbr_point_xyzirt* pts, int64_t n_
   if (stamp - S->timeLastProcessing >= S->P.mapping_process_interval) {
     S->timeLastProcessing = stamp;
     registration_core(S->P, *(Map*)map, F.corner.data(), (int64_t)F.corner.size(), F.surf.data(),
-                      (int64_t)F.surf.size(), pose, R, nthreads, S->table());
+                      (int64_t)F.surf.size(), pose, R, nthreads, S->table(), false, &S->isDegenerate);
   } else {
     R.st.status = FBR_REG_SKIPPED_INTERVAL;
   }

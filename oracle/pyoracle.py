@@ -53,7 +53,8 @@ def lib():
         L.orc_map_create.argtypes = [_VP, _VP, _I64, _VP, _I64]
         L.orc_map_destroy.argtypes = [_VP]
         L.orc_map_get.argtypes = [_VP, _VP, _VP, _VP, _VP]
-        L.orc_register.argtypes = [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP, ctypes.c_int, _VP, ctypes.c_int]
+        L.orc_register.argtypes = [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP, ctypes.c_int, _VP, ctypes.c_int,
+                                   _VP]
         L.orc_map_create_raw.restype = _VP
         L.orc_map_create_raw.argtypes = [_VP, _I64, _VP, _I64]
         L.orc_kf_extract.argtypes = [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_double, _VP, _VP,
@@ -161,14 +162,17 @@ class Map:
         lib().orc_map_get(self.h, None, None, ptr(c), ptr(s))
         return c[:nc.value].copy(), s[:ns.value].copy()
 
-    def register(self, corner, surf, pose, n_threads=4, deskew=None):
-        """registration() core: returns (pose, stats dict, per-iteration pose trace)."""
+    def register(self, corner, surf, pose, n_threads=4, deskew=None, degenerate=None):
+        """registration() core: returns (pose, stats dict, per-iteration pose trace).
+        degenerate: optional int32 array [1], the matcher's isDegenerate member before the call,
+        updated in place (None: a fresh matcher, false)."""
         tab = _table(deskew)
         pose = np.ascontiguousarray(pose, dtype=np.float32).copy()
         st = FbrRegStats()
         trace = np.zeros((self.params.max_iterations, 6), np.float32)
         lib().orc_register(ctypes.byref(self.params), self.h, ptr(corner), len(corner), ptr(surf),
-                           len(surf), ptr(pose), ctypes.byref(st), ptr(trace), n_threads, ptr(tab), int(self.raw))
+                           len(surf), ptr(pose), ctypes.byref(st), ptr(trace), n_threads, ptr(tab), int(self.raw),
+                           ptr(degenerate) if degenerate is not None else None)
         d = st.as_dict()
         return pose, d, trace[:d["iterations"]].copy()
 

@@ -52,6 +52,22 @@ def test_gloo_world2_shard_and_gather():
     assert status.tolist() == [0] * 5 + [1] * 5
 
 
+def test_job_block_strong_split_and_unpad():
+    from feature_base_pointcloud_registration_amd import shard
+    blocks = [shard.job_block(r, 8, 1024) for r in range(8)]  # C4: 1024 jobs over 8 GPUs
+    assert blocks == [(128 * r, 128 * (r + 1)) for r in range(8)]
+    blocks = [shard.job_block(r, 3, 10) for r in range(3)]
+    assert blocks[0][0] == 0 and blocks[-1][1] == 10 and all(a[1] == b[0] for a, b in zip(blocks, blocks[1:]))
+    counts = [b - a for a, b in blocks]
+    assert sorted(counts) == [3, 3, 4]
+    pad = max(counts)
+    g = np.full((3, pad, shard.RECORD_FLOATS), -1.0, np.float32)
+    for r, (a, b) in enumerate(blocks):
+        g[r, :b - a, 0] = np.arange(a, b)
+    flat = shard.unpad_records(g.reshape(-1), counts)
+    assert flat.reshape(-1, shard.RECORD_FLOATS)[:, 0].tolist() == list(range(10))
+
+
 def test_record_roundtrip():
     from feature_base_pointcloud_registration_amd import shard
     p = np.random.default_rng(0).standard_normal((7, 6)).astype(np.float32)
@@ -59,6 +75,38 @@ def test_record_roundtrip():
     st = np.array([0, 1, 0, 2, 0, 0, 1], np.int32)
     p2, it2, st2 = shard.decode_records(shard.encode_records(p, it, st))
     assert np.array_equal(p, p2) and np.array_equal(it, it2) and np.array_equal(st, st2)
+
+
+def _run_bench(nproc, extra, tmp_path, tag):
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = str(tmp_path / f"records_{tag}.npy")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(repo, "bench.py"),
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dist", "--records-out", out, *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=repo)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    return json.loads(line), np.load(out)
+
+
+@pytest.mark.gpu
+def test_bench_world2_strong_split_matches_world1(tmp_path):
+    """C4's sharded path with two registering ranks (both on the box's one GPU, gloo process group):
+    a strong split of 24 jobs into two contiguous blocks gathers records bit-identical to one rank
+    running all 24 (the jobs are independent; sub-batching differs between the runs)."""
+    r2, rec2 = _run_bench(2, ["--total-jobs", "24", "--backend", "gloo", "--same-device"], tmp_path, "w2")
+    r1, rec1 = _run_bench(1, ["--total-jobs", "24", "--backend", "gloo"], tmp_path, "w1")
+    assert r2["n_gpus"] == 2 and r2["scaling"] == "strong" and r2["config"]["jobs_per_step"] == 24
+    assert r2["records_check"] == {"jobs": 24, "mismatched_words": 0}
+    assert r1["records_check"] == {"jobs": 24, "mismatched_words": 0}
+    assert rec1.shape == rec2.shape == (24 * 8,)
+    assert np.array_equal(rec1.view(np.int32), rec2.view(np.int32))
+    _, _, status = __import__("feature_base_pointcloud_registration_amd.shard", fromlist=["x"]).decode_records(rec1)
+    assert (status == 0).all()
 
 
 @pytest.mark.gpu
@@ -83,3 +131,4 @@ def test_bench_rccl_path_one_rank(tmp_path):
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     res = json.loads(line)
     assert res["n_gpus"] == 1 and res["value"] > 0 and res["registration_status_ok"] == 16
+    assert res["records_check"] == {"jobs": 16, "mismatched_words": 0}

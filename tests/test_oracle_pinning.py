@@ -47,6 +47,21 @@ def test_fdlibm_atan2f_port_matches_glibc_bitwise(probe_lib):
     assert same.all(), f"{(~same).sum()} mismatches"
 
 
+def test_glibc_sincosf_port_matches_glibc(probe_lib):
+    """fbr_sincosf.h (the device's sinf / cosf in pcl::getTransformation and LMOptimization,
+    mapOptmization.h:444-448, 1259-1264) equals the host glibc bit for bit: exhaustively for every
+    float below 8 in magnitude (all pose angles; both reduction paths up to 120 are sampled too),
+    and on a 1/97 stride over the whole 32-bit range (large-argument reduction, inf, NaN)."""
+    import os
+    probe_lib.probe_sincosf_range.restype = ctypes.c_uint64
+    probe_lib.probe_sincosf_range.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_int]
+    th = min(8, os.cpu_count() or 1)
+    eight = int(np.float32(8.0).view(np.uint32))
+    assert probe_lib.probe_sincosf_range(0, eight, 1, th) == 0
+    assert probe_lib.probe_sincosf_range(0x80000000, 0x80000000 + eight, 1, th) == 0
+    assert probe_lib.probe_sincosf_range(0, 1 << 32, 97, th) == 0
+
+
 @pytest.mark.parametrize("nvals", [1, 2, 3, 7, 50, 10_000_000])
 def test_sort_emulation_matches_libstdcxx(probe_lib, nvals):
     rng = np.random.default_rng(nvals)

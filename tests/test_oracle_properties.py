@@ -134,6 +134,18 @@ def test_registration_degenerate_case_projects_update():
     assert st["degenerate"] == 1
     assert st["iterations"] == 2 and st["converged"] == 1
     assert np.array_equal(trace[0], trace[1])
+    # isDegenerate is a member of the matcher (mapOptmization.h:137): a registration whose every
+    # LMOptimization returns early (< 50 rows, :1268) keeps the previous scan's value
+    state = np.zeros(1, np.int32)
+    m.register(corner, surf, guess, degenerate=state)
+    assert state[0] == 1
+    far = guess.copy()
+    far[3] += 500.0  # nothing of the map within 1 m of any query
+    pf, sf, _ = m.register(corner, surf, far, degenerate=state)
+    assert sf["status"] == 0 and sf["n_sel"] == 0 and sf["iterations"] == P.max_iterations
+    assert np.array_equal(pf, far) and sf["degenerate"] == 1 and state[0] == 1
+    _, s0, _ = m.register(corner, surf, far)  # a fresh matcher starts from false
+    assert s0["degenerate"] == 0
 
 
 @pytest.mark.parametrize("n", [3, 6])

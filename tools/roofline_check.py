@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Recompute bench.py's roofline fractions from a rocprofv3 --stats kernel summary.
+
+bench.py times every kernel family with the dispatches' own start / end timestamps; rocprofv3's
+kernel trace reports the same per-dispatch durations.  This script takes a committed
+`*_kernel_stats.csv` and the bench JSON line of the same command and prints, per kernel family,
+the bench's average launch time next to rocprofv3's and the HBM fraction each gives for the
+bench's algorithmic bytes per launch (bench.py kernel_bytes / DESIGN.md §4).
+
+usage: roofline_check.py KERNEL_STATS.csv BENCH.json [--peak 8000]
+"""
+import argparse
+import csv
+import json
+
+
+def rocprof_avg_us(rows, symbols):
+    """Mean duration of one launcher call: all rows matching any symbol, summed, over the launches
+    of the most-called symbol (a launcher of two kernels, e.g. extract = k_rowcount + k_compact,
+    counts as one launch of both)."""
+    total_ns, calls = 0.0, 0
+    for sym in symbols:
+        c = 0
+        for r in rows:
+            if sym in r["Name"]:
+                total_ns += float(r["TotalDurationNs"])
+                c += int(r["Calls"])
+        calls = max(calls, c)
+    return (total_ns / calls / 1e3, calls) if calls else (None, 0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("stats_csv")
+    ap.add_argument("bench_json")
+    ap.add_argument("--peak", type=float, default=8000.0, help="GB/s (MI355X HBM3E spec)")
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.stats_csv)))
+    with open(a.bench_json) as f:
+        line = [l for l in f.read().splitlines() if l.strip().startswith("{")][-1]
+    res = json.loads(line)
+    roof = res["roofline"]
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import KERNEL_SYMBOLS as symbols
+    print(f"{'kernel':12s} {'bytes/launch':>14s} {'bench us':>10s} {'rocprof us':>11s} {'calls':>6s} "
+          f"{'bench frac':>10s} {'rocprof frac':>12s}")
+    for k, r in roof["kernels"].items():
+        avg, calls = rocprof_avg_us(rows, symbols.get(k, [k]))
+        bpl = r["bytes_per_launch"]
+        rf = bpl / (avg * 1e-6) / 1e9 / a.peak if avg else float("nan")
+        mark = " <- roofline kernel" if k == roof["kernel"] else ""
+        print(f"{k:12s} {bpl:14.4g} {r['avg_launch_us']:10.1f} {avg if avg else float('nan'):11.1f} {calls:6d} "
+              f"{r['frac']:10.4f} {rf:12.4f}{mark}")
+    print(f"bench line: kernel {roof['kernel']} frac {roof['frac']}")
+
+
+if __name__ == "__main__":
+    main()
