@@ -27,6 +27,7 @@
 #include "fbr_kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace fbr {
 
@@ -214,20 +215,101 @@ __device__ int vg_radix_sort(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, 
   return cur;
 }
 
+// Stable in-place LSD radix sort of an LDS-resident segment (n <= T * KPL pairs): every wave keeps
+// its chunk (KPL 64-element steps) in registers, so a pass reads the whole chunk before the barrier
+// and scatters straight into the same LDS arrays after it -- no ping-pong buffer, no global scratch.
+// The ranking is vg_radix_sort's (wave chunks in order, ballot peer masks), so the sort is stable.
+// 8-bit digits (hist holds (NW + 1) * 256 counters).  Ends with a barrier.
+template <int T, int KPL>
+__device__ void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint16_t* vals, int n, int nbits,
+                                      uint32_t* hist, uint32_t* wsum) {
+  constexpr int NW = T / 64, NB = 256, PER = NB * NW / T;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int passes = (nbits + 7) / 8;
+  const int dbits = passes > 0 ? (nbits + passes - 1) / passes : 8;
+  const uint32_t dmask = (1u << dbits) - 1u;
+  const int nbins = 1 << dbits, tot = nbins * NW;
+  const int chunk = (((n + NW - 1) / NW) + 63) & ~63;
+  const int c0 = min(n, w * chunk), c1 = min(n, c0 + chunk);
+  uint32_t kr[KPL], vr[KPL];
+  for (int pass = 0; pass < passes; ++pass) {
+    const int shift = dbits * pass;
+#pragma unroll
+    for (int k = 0; k < KPL; ++k) {
+      const int i = c0 + 64 * k + lane;
+      kr[k] = i < c1 ? keys[i] : 0u;
+      vr[k] = i < c1 ? vals[i] : 0u;
+    }
+    for (int b = tid; b < tot; b += T) hist[(b % NW) * NB + b / NW] = 0u;
+    __syncthreads();  // every wave holds its chunk: the scatter below may overwrite any position
+#pragma unroll
+    for (int k = 0; k < KPL; ++k)
+      if (c0 + 64 * k + lane < c1) atomicAdd(&hist[w * NB + ((kr[k] >> shift) & dmask)], 1u);
+    __syncthreads();
+    {
+      uint32_t v[PER], loc = 0;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int idx = tid * PER + k;
+        v[k] = idx < tot ? hist[(idx % NW) * NB + idx / NW] : 0u;
+        loc += v[k];
+      }
+      uint32_t inc = loc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+      }
+      if (lane == 63) wsum[w] = inc;
+      __syncthreads();
+      uint32_t run = inc - loc;
+      for (int ww = 0; ww < w; ++ww) run += wsum[ww];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int idx = tid * PER + k;
+        if (idx < tot) hist[(idx % NW) * NB + idx / NW] = run;
+        run += v[k];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < KPL; ++k) {
+      const bool valid = c0 + 64 * k + lane < c1;
+      const uint32_t d = (kr[k] >> shift) & dmask;
+      uint64_t peers = __ballot(valid);
+      for (int b = 0; b < dbits; ++b) {
+        const uint64_t bal = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? bal : ~bal;
+      }
+      const int rank = __popcll(peers & ((1ull << lane) - 1ull));
+      uint32_t* hc = &hist[w * NB + d];
+      const uint32_t base = valid ? *hc : 0u;
+      if (valid) {
+        keys[base + rank] = kr[k];
+        vals[base + rank] = (uint16_t)vr[k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (valid && rank == 0) *hc = base + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+  }
+}
+
 // Stable radix sort of kb[0]/vb[0] (n pairs), then one centroid per run of equal keys in
 // ascending key order: out[v] = mean of in[vals of the run].  Returns the voxel count (all threads).
 template <int T, typename V, int MAXD = 9, bool KV_LDS = true>
 __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, uint32_t* hist, uint32_t* wsum,
-                            const float4* in, float4* out, int dbg = 0, unsigned long long* t_sorted = nullptr) {
+                            const float4* in, float4* out, int dbg = 0, unsigned long long* t_sorted = nullptr);
+
+// One centroid per run of equal keys of the sorted pairs ks / vs (n), in ascending key order.
+// hist must hold NW KB (the per-wave point stage).  Returns the voxel count (all threads).
+template <int T, typename KP, typename VP>
+__device__ int vg_emit(KP ks, VP vs, int n, uint32_t* hist, uint32_t* wsum, const float4* in, float4* out) {
   constexpr int NW = T / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int chunk = (((n + NW - 1) / NW) + 63) & ~63;
   const int c0 = min(n, w * chunk), c1 = min(n, c0 + chunk);
-  const int cur = vg_radix_sort<T, V, MAXD, KV_LDS>(kb, vb, n, nbits, hist, wsum, dbg);
-  const auto ks = lds_if<KV_LDS>(kb[cur]);
-  const auto vs = lds_if<KV_LDS>(vb[cur]);
-  if (t_sorted && threadIdx.x == 0) *t_sorted = __builtin_amdgcn_s_memtime();
-  if (dbg == 2) return 0;
   // ---- voxels in ascending key order: heads of equal-key runs, centroid = float sum / count ----
   int nh = 0;
   for (int i0 = c0; i0 < c1; i0 += 64) {
@@ -309,6 +391,15 @@ __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, u
   return total;
 }
 
+template <int T, typename V, int MAXD, bool KV_LDS>
+__device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, uint32_t* hist, uint32_t* wsum,
+                            const float4* in, float4* out, int dbg, unsigned long long* t_sorted) {
+  const int cur = vg_radix_sort<T, V, MAXD, KV_LDS>(kb, vb, n, nbits, hist, wsum, dbg);
+  if (t_sorted && threadIdx.x == 0) *t_sorted = __builtin_amdgcn_s_memtime();
+  if (dbg == 2) return 0;
+  return vg_emit<T>(lds_if<KV_LDS>(kb[cur]), lds_if<KV_LDS>(vb[cur]), n, hist, wsum, in, out);
+}
+
 // Generic front end: segments of a VgArgs (per-job mapping DS, start-up map filter, fbr_voxel_grid).
 template <int T, typename V, bool LDS>
 __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
@@ -370,6 +461,74 @@ __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
   }
   __syncthreads();
   const int total = vg_sort_emit<T, V, 9, LDS>(kb, vb, n, G.nbits, hist, wsum, in, out);
+  if (tid == 0) S.cnt_out[seg] = total;
+}
+
+// Mapping-DS front end (downsampleCurrentScan, one 1024-thread workgroup per job cloud): segments
+// of up to T * KPL points sort in place in LDS (keys u32 + u16 indices, vg_radix_sort_inplace), so
+// the only global writes are the centroids; larger segments take the global-scratch ping-pong of
+// k_voxel_grid.  Same semantics and output as k_voxel_grid.
+template <int T, int KPL>
+__global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
+  constexpr int NW = T / 64, LCAP = T * KPL;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  int seg = blockIdx.x;
+  const bool second = seg >= A.s[0].nseg;
+  const VgSet S = second ? A.s[1] : A.s[0];
+  if (second) seg -= A.s[0].nseg;
+  uint32_t* hist = (uint32_t*)smem;  // [NW + 1][512] (global path) / [NW + 1][256] (in place)
+  uint32_t* wsum = hist + (NW + 1) * 512;
+  float* mm = (float*)(wsum + NW);
+  int* misc = (int*)(mm + NW * 6);
+  const int n = (int)min((int64_t)S.cnt_in[seg], S.cap);
+  const float4* in = S.in + (int64_t)seg * S.stride_in;
+  float4* out = S.out + (int64_t)seg * S.stride_out;
+  if (n <= 0) {
+    if (tid == 0) S.cnt_out[seg] = 0;
+    return;
+  }
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int i = tid; i < n; i += T) {
+    const float4 p = in[i];
+    const float v[3] = {p.x, p.y, p.z};
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
+      mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
+    }
+  }
+  vg_block_minmax<T>(mn, mx, mm);
+  VgGrid G;
+  G.init(mn, mx, S.leaf, S.morton != 0);
+  if (G.overflow) {
+    for (int i = tid; i < n; i += T) out[i] = in[i];
+    if (tid == 0) S.cnt_out[seg] = n;
+    return;
+  }
+  int total;
+  if (n <= LCAP) {
+    unsigned char* q = smem + ((((unsigned char*)(misc + 4) - smem) + 15) & ~15);
+    FBR_LDS_AS uint32_t* keys = (FBR_LDS_AS uint32_t*)q;
+    FBR_LDS_AS uint16_t* vals = (FBR_LDS_AS uint16_t*)((FBR_LDS_AS uint32_t*)q + LCAP);
+    for (int i = tid; i < n; i += T) {
+      keys[i] = G.key(in[i]);
+      vals[i] = (uint16_t)i;
+    }
+    __syncthreads();
+    vg_radix_sort_inplace<T, KPL>(keys, vals, n, G.nbits, hist, wsum);
+    total = vg_emit<T>(keys, vals, n, hist, wsum, in, out);
+  } else {
+    uint32_t* sc = S.scratch + (int64_t)seg * 4 * S.cap;
+    uint32_t* kb[2] = {sc, sc + S.cap};
+    uint32_t* vb[2] = {sc + 2 * S.cap, sc + 3 * S.cap};
+    for (int i = tid; i < n; i += T) {
+      kb[0][i] = G.key(in[i]);
+      vb[0][i] = (uint32_t)i;
+    }
+    __syncthreads();
+    total = vg_sort_emit<T, uint32_t, 9, false>(kb, vb, n, G.nbits, hist, wsum, in, out);
+  }
   if (tid == 0) S.cnt_out[seg] = total;
 }
 
@@ -624,6 +783,15 @@ void launch_voxel_ring(hipStream_t s, const VgRing& a) {
     fbr_launch((k_voxel_ring<512, 8>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 8), s, a);
 }
 
+// In-place LDS sort of the mapping-DS segments (FBR_VG_INPLACE=0: the global-scratch kernel).
+bool vg_inplace() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_VG_INPLACE");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 size_t voxel_lds_bytes(const VgArgs& a, int threads, bool lds_mode) {
   const int nw = threads / 64;
   size_t b = sizeof(uint32_t) * ((size_t)(nw + 1) * 512 + nw) + sizeof(float) * nw * 6 + sizeof(int) * 4;
@@ -637,6 +805,8 @@ size_t voxel_lds_bytes(const VgArgs& a, int threads, bool lds_mode) {
   return b;
 }
 
+constexpr int kVgIpKpl = 18;  // k_voxel_grid_ip: segments up to 1024 * 18 points sort in LDS
+
 void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
   const int nseg = a.s[0].nseg + a.s[1].nseg;
   if (nseg <= 0) return;
@@ -645,6 +815,9 @@ void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
     if (a.s[k].nseg > 0) cap = std::max<int64_t>(cap, a.s[k].cap);
   if (cap <= kVgLdsCap) {
     fbr_launch((k_voxel_grid<256, uint16_t, true>), dim3(nseg), dim3(256), voxel_lds_bytes(a, 256, true), s, a);
+  } else if (vg_inplace()) {
+    const size_t lds = voxel_lds_bytes(a, 1024, false) + (size_t)1024 * kVgIpKpl * (sizeof(uint32_t) + sizeof(uint16_t));
+    fbr_launch((k_voxel_grid_ip<1024, kVgIpKpl>), dim3(nseg), dim3(1024), lds, s, a);
   } else {
     fbr_launch((k_voxel_grid<1024, uint32_t, false>), dim3(nseg), dim3(1024), voxel_lds_bytes(a, 1024, false), s,
                        a);

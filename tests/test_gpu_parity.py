@@ -463,3 +463,40 @@ def test_voxel_grid_large_cloud_kernel():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=env, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout == a.tobytes()
+
+
+def test_voxel_grid_inplace_lds_sort_matches_global_scratch_kernel():
+    """The mapping-DS VoxelGrid sorts segments of up to 1024 * 18 points in place in LDS
+    (k_voxel_grid_ip); larger ones take the global-scratch ping-pong.  Both give the bytes of the
+    global-scratch kernel (FBR_VG_INPLACE=0, child process) on either side of the LDS capacity, and
+    the oracle's voxels (mapOptmization.h:981-993)."""
+    import subprocess
+    import sys
+    rng = np.random.default_rng(21)
+    outs = {}
+    clouds = {}
+    for n in (6000, 18432, 18433, 30000):
+        pts = np.zeros(n, POINT_XYZI)
+        pts["x"], pts["y"] = rng.uniform(-30, 30, n), rng.uniform(-30, 30, n)
+        pts["z"] = rng.normal(0, 0.4, n) + (rng.random(n) < 0.3) * rng.uniform(0, 6, n)
+        pts["intensity"] = rng.uniform(0, 255, n)
+        clouds[n] = pts
+    with api.Context(default_params(16, 900)) as ctx:
+        for n, pts in clouds.items():
+            outs[n] = ctx.voxel_grid(pts, 0.4)
+            ref = O.voxel_grid(pts, 0.4)
+            assert len(outs[n]) == len(ref)
+            a, b = outs[n].view(np.float32).reshape(-1, 4), ref.view(np.float32).reshape(-1, 4)
+            assert np.array_equal(np.floor(a[:, :3] * np.float32(2.5)), np.floor(b[:, :3] * np.float32(2.5)))
+            assert_ulps_close(a, b, SURF_ULPS)
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_vg_ip_in.npz")
+    np.savez(path, **{str(n): p for n, p in clouds.items()})
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api; "
+            "from feature_base_pointcloud_registration_amd.fbr_types import default_params; "
+            "c = api.Context(default_params(16, 900)); d = np.load(%r); "
+            "sys.stdout.buffer.write(b''.join(c.voxel_grid(d[k], 0.4).tobytes() for k in %r))"
+            % (REPO, path, [str(n) for n in clouds]))
+    env = dict(os.environ, FBR_VG_INPLACE="0")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout == b"".join(outs[n].tobytes() for n in clouds)
