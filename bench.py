@@ -76,6 +76,12 @@ def parse():
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on device 0 (world-size > 1 rehearsal on a one-GPU box)")
     ap.add_argument("--records-out", default=None, help="rank 0 writes the gathered records (.npy)")
+    ap.add_argument("--latency", type=int, default=0,
+                    help="single-stream line: N pose-chained scans through fbr_process_scan (the reference's "
+                         "operating mode, imageProjection.cpp:206-218), rank 0 at N=1; 0 disables")
+    ap.add_argument("--ingest", type=int, default=2,
+                    help="ingest-inclusive line: REPS x B jobs from host memory through fbr_process_batch "
+                         "(pinned double-buffered staging), rank 0 at N=1; 0 disables")
     ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C5"])
     ap.add_argument("--cpu-sample", type=int, default=96, help="jobs timed on the CPU oracle (N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16,
@@ -91,6 +97,83 @@ def parse():
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "hbm_traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from rocprofv3 PMC passes")
     return ap.parse_args()
+
+
+def ingest_line(ctx, scans, guesses, resident_poses, reps, B):
+    """Scans/s with the raw scans starting in host memory: reps x B jobs through fbr_process_batch
+    (pinned staging + copy stream, batch k+1's upload overlapping batch k's compute), next to the
+    pageable path (fbr_batch_stage's synchronous copies, then the batch) for one batch."""
+    ctx.process_batch(scans[:min(B, 8)], guesses[:min(B, 8)])  # allocates the staging ring
+    t0 = time.perf_counter()
+    p, st = ctx.process_batch(scans * reps, np.tile(guesses, (reps, 1)))
+    t_pipe = time.perf_counter() - t0
+    h2d = ctx.ingest_bytes()
+    same = bool((p[:B].view(np.int32) == resident_poses.view(np.int32)).all())
+    t1 = time.perf_counter()
+    ctx.batch_stage(scans, guesses)
+    ctx.batch_launch()
+    ctx.batch_wait()
+    ctx.batch_results()
+    t_page = time.perf_counter() - t1
+    return {
+        "value": round(reps * B / t_pipe, 3), "unit": "scans/s",
+        "jobs": reps * B, "path": "fbr_process_batch: pinned staging ring, copy stream, double-buffered inputs",
+        "h2d_bytes_per_scan": round(h2d / (reps * B), 1),
+        "h2d_GBps": round(h2d / t_pipe / 1e9, 2),
+        "pageable_one_batch_scans_per_s": round(B / t_page, 3),
+        "poses_equal_resident": same,
+    }
+
+
+def latency_line(cfg, corner_map, surf_map, n, cpu_scans=0):
+    """The reference's operating mode: one scan at a time, each registration starting from the
+    previous result (imageProjection.cpp:206-218), host scan in, pose out.  Reports wall ms per
+    scan (host upload to pose back), kernel launches / blocking host syncs / GN flag polls per scan,
+    and the oracle's per-scan time and pose on the same chain for the first cpu_scans scans."""
+    from feature_base_pointcloud_registration_amd import api, synth
+    H, W, *_ = synth.CONFIGS[cfg]
+    P = synth.config_params(cfg, max_batch=1)
+    traj = synth.trajectory(7, n + 3)
+    scans = [synth.scan(p, H, W, seed=500 + k) for k, p in enumerate(traj)]
+    _, guess0 = synth.job(7)
+    ms = []
+    poses = []
+    with api.Context(P) as c:
+        c.set_map(corner_map, surf_map)
+        pose = guess0.copy()
+        for k in range(3):  # warm-up (first-call allocations, code loading)
+            pose, _ = c.process_scan(scans[k], 0.2 * k, pose)
+        warm_pose = pose.copy()
+        api.debug_counters(reset=True)
+        for k in range(3, n + 3):
+            t = time.perf_counter()
+            pose, st = c.process_scan(scans[k], 0.2 * k, pose)
+            ms.append(1e3 * (time.perf_counter() - t))
+            poses.append(pose.copy())
+        launches, syncs, polls = api.debug_counters()
+    ms = np.array(ms)
+    out = {"scans": n, "ms_per_scan_mean": round(float(ms.mean()), 4), "ms_per_scan_p50": round(float(np.median(ms)), 4),
+           "ms_per_scan_p99": round(float(np.percentile(ms, 99)), 4),
+           "launches_per_scan": round(launches / n, 2), "host_syncs_per_scan": round(syncs / n, 2),
+           "gn_flag_polls_per_scan": round(polls / n, 2),
+           "path": "fbr_process_scan (host scan -> HBM, projection, features, registration, pose back)"}
+    if cpu_scans:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import pyoracle as O
+        st = O.Stream(P)
+        omap = O.Map(P, corner_map, surf_map)
+        po = guess0.copy()
+        for k in range(3):
+            po, _ = st.process_scan(omap, scans[k], 0.2 * k, po, n_threads=P.number_of_cores)
+        t = time.perf_counter()
+        dmax = float(np.abs(po.astype(np.float64) - warm_pose).max())
+        for k in range(3, 3 + cpu_scans):
+            po, _ = st.process_scan(omap, scans[k], 0.2 * k, po, n_threads=P.number_of_cores)
+            dmax = max(dmax, float(np.abs(po.astype(np.float64) - poses[k - 3]).max()))
+        out["cpu_oracle_ms_per_scan"] = round(1e3 * (time.perf_counter() - t) / cpu_scans, 3)
+        out["cpu_oracle_threads"] = int(P.number_of_cores)
+        out["chain_max_abs_pose_diff_vs_oracle"] = dmax
+    return out
 
 
 def main():
@@ -314,6 +397,13 @@ def main():
     }
     if records_check is not None:
         result["records_check"] = records_check
+
+    if world == 1 and args.latency > 0:
+        result["latency"] = latency_line(cfg, corner_map, surf_map, args.latency,
+                                         cpu_scans=0 if args.no_cpu_baseline else 10)
+
+    if world == 1 and args.ingest > 0:
+        result["ingest"] = ingest_line(ctx, scans, guesses, poses, args.ingest, B)
 
     if world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "oracle"))

@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = [
     "fbr_params_default", "fbr_strerror", "fbr_abi_version", "fbr_device_count", "fbr_create",
     "fbr_destroy", "fbr_set_map", "fbr_get_map", "fbr_project", "fbr_extract_features",
     "fbr_register", "fbr_register_trace", "fbr_process_scan", "fbr_reset_stream",
-    "fbr_process_batch", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
+    "fbr_process_batch", "fbr_ingest_bytes", "fbr_debug_counters", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
     "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
     "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math", "fbr_selftest_eigen6",
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
@@ -75,6 +75,8 @@ def lib():
             "fbr_process_scan": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_double, _VP, _VP]),
             "fbr_reset_stream": (ctypes.c_int, [_VP]),
             "fbr_process_batch": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, _VP, _VP]),
+            "fbr_ingest_bytes": (ctypes.c_int, [_VP, _VP]),
+            "fbr_debug_counters": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int]),
             "fbr_batch_stage": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, _VP]),
             "fbr_batch_launch": (ctypes.c_int, [_VP]),
             "fbr_batch_wait": (ctypes.c_int, [_VP]),
@@ -130,6 +132,13 @@ def device_count():
     n = ctypes.c_int(0)
     _check(lib().fbr_device_count(ctypes.byref(n)), "fbr_device_count")
     return n.value
+
+
+def debug_counters(reset=False):
+    """(kernel launches, blocking host syncs, GN flag polls) since the last reset (process-wide)."""
+    v = [ctypes.c_longlong() for _ in range(3)]
+    _check(lib().fbr_debug_counters(*[ctypes.byref(x) for x in v], int(reset)), "fbr_debug_counters")
+    return tuple(x.value for x in v)
 
 
 def selftest_math(a, b):
@@ -424,6 +433,12 @@ class Context:
         _check(lib().fbr_process_batch(self._h, arr, ptr(n_in), len(keep), ptr(poses), ptr(stats)),
                "fbr_process_batch")
         return poses, stats
+
+    def ingest_bytes(self):
+        """Host-to-device scan bytes of the last process_batch."""
+        v = ctypes.c_double()
+        _check(lib().fbr_ingest_bytes(self._h, ctypes.byref(v)), "fbr_ingest_bytes")
+        return v.value
 
     def batch_stage(self, scans, guesses):
         keep, arr, n_in = self._scan_ptrs(scans)

@@ -18,6 +18,7 @@
 #include <map>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fbr_common.h"
@@ -38,6 +39,16 @@ using namespace fbr;
 
 namespace {
 
+// Blocking host synchronisations, counted (fbr_debug_counters).
+hipError_t fbr_sync(hipStream_t s) {
+  debug_counters().host_syncs.fetch_add(1, std::memory_order_relaxed);
+  return hipStreamSynchronize(s);
+}
+hipError_t fbr_memcpy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  debug_counters().host_syncs.fetch_add(1, std::memory_order_relaxed);
+  return hipMemcpy(dst, src, bytes, kind);
+}
+
 struct KernelTimer {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
@@ -56,6 +67,23 @@ int dalloc(T** p, size_t count) {
 }  // namespace
 
 constexpr int kMaxSub = 4;
+
+// Host ingest of fbr_process_batch: the caller's (pageable) scans are packed into a ring of pinned
+// staging chunks by host threads and copied to HBM on a copy stream, into the input slot the
+// running device batch does not read; batch k+1's upload overlaps batch k's compute.
+struct Ingest {
+  static constexpr int kChunks = 4;
+  hipStream_t cstream = nullptr;
+  hipEvent_t up_ev[2] = {};          // the upload of input slot s is complete (on cstream)
+  hipEvent_t chunk_ev[kChunks] = {};  // the copies out of chunk k are complete
+  bool chunk_used[kChunks] = {};
+  int next_chunk = 0;
+  uint8_t* h_stage = nullptr;        // kChunks x chunk_bytes, pinned
+  int64_t chunk_bytes = 0;
+  fbr_point_xyzirt* d_pts_slot[2] = {};  // slot 0 = the context's scan buffer, slot 1 allocated here
+  int nthreads = 8;                  // packing threads per chunk
+  double h2d_bytes = 0.0;            // bytes copied host -> device by the last fbr_process_batch
+};
 
 struct fbr_ctx {
   fbr_params P;
@@ -144,6 +172,7 @@ struct fbr_ctx {
   int* d_bounds = nullptr;
   bool map_nocrop = false;  // the registration map is a keyframe local map
   int stream_degenerate = 0;  // mapOptimization::isDegenerate across single-scan registrations
+  Ingest ing;                 // fbr_process_batch host ingest (allocated on first use)
 };
 
 namespace {
@@ -293,8 +322,8 @@ int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pt
     sorted[n + i] = make_float4(p.x, p.y, p.z, w);
   }
   if (dalloc(d_pts, std::max<int64_t>(2 * n, 1)) || dalloc(d_cs, ncell + 1)) return FBR_ERR_HIP;
-  if (n) CK(hipMemcpy(*d_pts, sorted.data(), sizeof(float4) * 2 * n, hipMemcpyHostToDevice));
-  CK(hipMemcpy(*d_cs, start.data(), sizeof(int32_t) * (ncell + 1), hipMemcpyHostToDevice));
+  if (n) CK(fbr_memcpy_sync(*d_pts, sorted.data(), sizeof(float4) * 2 * n, hipMemcpyHostToDevice));
+  CK(fbr_memcpy_sync(*d_cs, start.data(), sizeof(int32_t) * (ncell + 1), hipMemcpyHostToDevice));
   g->inv_cell = inv;
   g->inv_x = invx;
   for (int d = 0; d < 3; ++d) {
@@ -337,11 +366,11 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
       rc = voxel_grid_large(c->stream, d_in, n, leaf, 0, d_out, d_cnt + 1);
       int32_t nout = 0;
       if (!rc && (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-                  hipStreamSynchronize(c->stream) != hipSuccess))
+                  fbr_sync(c->stream) != hipSuccess))
         rc = FBR_ERR_HIP;
       if (!rc) {
         out.resize(nout);
-        if (nout && hipMemcpy(out.data(), d_out, sizeof(float4) * nout, hipMemcpyDeviceToHost) != hipSuccess)
+        if (nout && fbr_memcpy_sync(out.data(), d_out, sizeof(float4) * nout, hipMemcpyDeviceToHost) != hipSuccess)
           rc = FBR_ERR_HIP;
       }
     } else {
@@ -359,11 +388,11 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
       launch_voxel_grid(c->stream, a);
       int32_t nout = 0;
       if (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-          hipStreamSynchronize(c->stream) != hipSuccess) {
+          fbr_sync(c->stream) != hipSuccess) {
         rc = FBR_ERR_HIP;
       } else {
         out.resize(nout);
-        if (nout && hipMemcpy(out.data(), d_out, sizeof(float4) * nout, hipMemcpyDeviceToHost) != hipSuccess)
+        if (nout && fbr_memcpy_sync(out.data(), d_out, sizeof(float4) * nout, hipMemcpyDeviceToHost) != hipSuccess)
           rc = FBR_ERR_HIP;
       }
     }
@@ -518,7 +547,7 @@ int crop_stats(fbr_ctx* c, const Sub& sb) {
       v[2 * j + 1] = (int32_t)c->gs.n_points;
     }
     CK(hipMemcpyAsync(cnt, v.data(), sizeof(int32_t) * 2 * sb.B, hipMemcpyHostToDevice, sb.st));
-    CK(hipStreamSynchronize(sb.st));
+    CK(fbr_sync(sb.st));
     return FBR_OK;
   }
   CK(hipMemsetAsync(cnt, 0, sizeof(int32_t) * 2 * sb.B, sb.st));
@@ -615,6 +644,7 @@ int register_iterate(fbr_ctx* c, const Sub* subs, int nsub, bool trace) {
           }
           v = *f;
         }
+        debug_counters().flag_polls.fetch_add(1, std::memory_order_relaxed);
         if (watch[k]) active[k] = (int)(v & 0xFFFFFFFFull);
         if (watch[k] && active[k] == 0) {
           live[k] = false;
@@ -651,7 +681,7 @@ int copy_stats(fbr_ctx* c, int B, fbr_reg_stats* stats) {
   CK(hipMemcpyAsync(nv.data(), c->d_nvalid, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
   CK(hipMemcpyAsync(nc.data(), c->d_ncorner, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
   CK(hipMemcpyAsync(ns.data(), c->d_nsurf, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
-  CK(hipStreamSynchronize(c->stream));
+  CK(fbr_sync(c->stream));
   c->last_iters.resize(B);
   c->last_q.resize(B);
   c->last_n.resize(B);
@@ -676,7 +706,7 @@ int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n) {
   c->no_time_call = false;
   if (n) CK(hipMemcpyAsync(c->d_pts + job * c->NMAX, pts, sizeof(fbr_point_xyzirt) * n, hipMemcpyHostToDevice, c->stream));
   CK(hipMemcpyAsync(c->d_nin + job, &n, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-  CK(hipStreamSynchronize(c->stream));  // n lives on the caller's stack
+  CK(fbr_sync(c->stream));  // n lives on the caller's stack
   return FBR_OK;
 }
 
@@ -688,7 +718,7 @@ int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags) {
   if (rc) return rc;
   if (L.n > c->NMAX) return FBR_ERR_CAPACITY;
   if (L.bytes > c->msg_cap) {
-    CK(hipStreamSynchronize(c->stream));
+    CK(fbr_sync(c->stream));
     if (c->d_msg) CK(hipFree(c->d_msg));
     c->d_msg = nullptr;
     c->msg_cap = 0;
@@ -705,7 +735,7 @@ int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags) {
   TIMED(c, "unpack_msg", launch_unpack_msg(c->stream, c->d_msg, D, c->d_pts));
   const int64_t n = L.n;
   CK(hipMemcpyAsync(c->d_nin, &n, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-  CK(hipStreamSynchronize(c->stream));  // n lives on this stack; msg->data is the caller's
+  CK(fbr_sync(c->stream));  // n lives on this stack; msg->data is the caller's
   if (msg_flags) *msg_flags = L.flags;
   c->no_time_call = (L.flags & FBR_MSG_NO_TIME) != 0;
   return FBR_OK;
@@ -714,7 +744,7 @@ int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags) {
 int check_err(fbr_ctx* c, int B) {
   std::vector<int32_t> e(B);
   CK(hipMemcpyAsync(e.data(), c->d_err, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
-  CK(hipStreamSynchronize(c->stream));
+  CK(fbr_sync(c->stream));
   for (int j = 0; j < B; ++j)
     if (e[j]) return FBR_ERR_UNSUPPORTED;
   return FBR_OK;
@@ -726,7 +756,7 @@ int upload_cloud(fbr_ctx* c, float4* dst, int32_t* dcnt, const fbr_point_xyzi* s
   if (n) CK(hipMemcpyAsync(dst, src, sizeof(float4) * n, hipMemcpyHostToDevice, c->stream));
   int32_t nn = (int32_t)n;
   CK(hipMemcpyAsync(dcnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
-  CK(hipStreamSynchronize(c->stream));
+  CK(fbr_sync(c->stream));
   return FBR_OK;
 }
 
@@ -745,7 +775,7 @@ int grow(T** p, int64_t* cap, int64_t need, int64_t keep, hipStream_t st) {
   T* q = nullptr;
   CK(hipMalloc((void**)&q, sizeof(T) * ncap));
   if (*p && keep > 0) CK(hipMemcpyAsync(q, *p, sizeof(T) * keep, hipMemcpyDeviceToDevice, st));
-  CK(hipStreamSynchronize(st));
+  CK(fbr_sync(st));
   if (*p) CK(hipFree(*p));
   *p = q;
   *cap = ncap;
@@ -765,7 +795,7 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
     if (dalloc(&d_cnt, 1)) return FBR_ERR_HIP;
     rc = voxel_grid_large(c->stream, d_in, n, leaf, 0, d_out, d_cnt);
     if (!rc && (hipMemcpyAsync(&nout, d_cnt, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-                hipStreamSynchronize(c->stream) != hipSuccess))
+                fbr_sync(c->stream) != hipSuccess))
       rc = FBR_ERR_HIP;
     *n_out = nout;
     (void)hipFree(d_cnt);
@@ -791,7 +821,7 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
     } else {
       launch_voxel_grid(c->stream, a);
       if (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-          hipStreamSynchronize(c->stream) != hipSuccess)
+          fbr_sync(c->stream) != hipSuccess)
         rc = FBR_ERR_HIP;
       *n_out = nout;
     }
@@ -840,7 +870,7 @@ int build_grid_dev(fbr_ctx* c, const float4* d_src, int64_t n, float4** d_pts, i
   if (dalloc(d_pts, std::max<int64_t>(2 * n, 1)) || dalloc(d_cs, (int64_t)g->n_cells + 1)) return FBR_ERR_HIP;
   if (n) CK(hipMemcpyAsync(*d_pts + n, d_src, sizeof(float4) * n, hipMemcpyDeviceToDevice, c->stream));
   int rc = grid_fill_device(c->stream, d_src, n, *g, *d_cs, *d_pts);
-  if (!rc) CK(hipStreamSynchronize(c->stream));
+  if (!rc) CK(fbr_sync(c->stream));
   return rc;
 }
 
@@ -975,9 +1005,9 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
 int fbr_destroy(fbr_ctx* c) {
   if (!c) return FBR_ERR_INVALID_ARG;
   (void)hipSetDevice(c->dev);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->stream) (void)fbr_sync(c->stream);
   for (int k = 1; k < kMaxSub; ++k)
-    if (c->xstream[k]) (void)hipStreamSynchronize(c->xstream[k]);
+    if (c->xstream[k]) (void)fbr_sync(c->xstream[k]);
   void* ptrs[] = {c->d_pts, c->d_nin, c->d_guess, c->d_owner, c->d_rowcnt, c->d_col, c->d_start, c->d_end,
                   c->d_nvalid, c->d_cloud, c->d_range, c->d_sstate, c->d_sstream, c->d_label, c->d_label_stream,
                   c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring, c->d_surf_ring_cnt,
@@ -990,6 +1020,14 @@ int fbr_destroy(fbr_ctx* c) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);
+  if (c->ing.cstream) (void)fbr_sync(c->ing.cstream);
+  if (c->ing.h_stage) (void)hipHostFree(c->ing.h_stage);
+  if (c->ing.d_pts_slot[1]) (void)hipFree(c->ing.d_pts_slot[1]);
+  for (auto& e : c->ing.up_ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->ing.chunk_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->ing.cstream) (void)hipStreamDestroy(c->ing.cstream);
   for (auto& kv : c->timers) {
     for (auto& pr : kv.second.pending) {
       (void)hipEventDestroy(pr.first);
@@ -1033,8 +1071,8 @@ int fbr_get_map(fbr_ctx* c, int64_t* n_corner, int64_t* n_surf, fbr_point_xyzi* 
     CK(hipSetDevice(c->dev));
     if (n_corner) *n_corner = c->kds_c_n;
     if (n_surf) *n_surf = c->kds_s_n;
-    if (corner && c->kds_c_n) CK(hipMemcpy(corner, c->d_kds_c, sizeof(float4) * c->kds_c_n, hipMemcpyDeviceToHost));
-    if (surf && c->kds_s_n) CK(hipMemcpy(surf, c->d_kds_s, sizeof(float4) * c->kds_s_n, hipMemcpyDeviceToHost));
+    if (corner && c->kds_c_n) CK(fbr_memcpy_sync(corner, c->d_kds_c, sizeof(float4) * c->kds_c_n, hipMemcpyDeviceToHost));
+    if (surf && c->kds_s_n) CK(fbr_memcpy_sync(surf, c->d_kds_s, sizeof(float4) * c->kds_s_n, hipMemcpyDeviceToHost));
     return FBR_OK;
   }
   if (n_corner) *n_corner = (int64_t)c->map_c_host.size();
@@ -1079,12 +1117,12 @@ int project_uploaded(fbr_ctx* c, int32_t* start_ring, int32_t* end_ring, int32_t
   if (rc) return rc;
   int32_t n = 0;
   CK(hipMemcpyAsync(&n, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  CK(hipStreamSynchronize(c->stream));
-  if (start_ring) CK(hipMemcpy(start_ring, c->d_start, sizeof(int32_t) * c->H, hipMemcpyDeviceToHost));
-  if (end_ring) CK(hipMemcpy(end_ring, c->d_end, sizeof(int32_t) * c->H, hipMemcpyDeviceToHost));
-  if (col_ind && n) CK(hipMemcpy(col_ind, c->d_col, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
-  if (range && n) CK(hipMemcpy(range, c->d_range, sizeof(float) * n, hipMemcpyDeviceToHost));
-  if (cloud && n) CK(hipMemcpy(cloud, c->d_cloud, sizeof(float4) * n, hipMemcpyDeviceToHost));
+  CK(fbr_sync(c->stream));
+  if (start_ring) CK(fbr_memcpy_sync(start_ring, c->d_start, sizeof(int32_t) * c->H, hipMemcpyDeviceToHost));
+  if (end_ring) CK(fbr_memcpy_sync(end_ring, c->d_end, sizeof(int32_t) * c->H, hipMemcpyDeviceToHost));
+  if (col_ind && n) CK(fbr_memcpy_sync(col_ind, c->d_col, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  if (range && n) CK(fbr_memcpy_sync(range, c->d_range, sizeof(float) * n, hipMemcpyDeviceToHost));
+  if (cloud && n) CK(fbr_memcpy_sync(cloud, c->d_cloud, sizeof(float4) * n, hipMemcpyDeviceToHost));
   if (n_out) *n_out = n;
   c->have_projection = true;
   return FBR_OK;
@@ -1101,12 +1139,12 @@ int fbr_extract_features(fbr_ctx* c, int8_t* label, fbr_point_xyzi* corner, int6
   rc = check_err(c, 1);
   if (rc) return rc;
   int32_t n = 0, nc = 0, ns = 0;
-  CK(hipMemcpy(&n, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost));
-  CK(hipMemcpy(&nc, c->d_ncorner, sizeof(int32_t), hipMemcpyDeviceToHost));
-  CK(hipMemcpy(&ns, c->d_nsurf, sizeof(int32_t), hipMemcpyDeviceToHost));
-  if (label && n) CK(hipMemcpy(label, c->d_label_stream, (size_t)n, hipMemcpyDeviceToHost));
-  if (corner && nc) CK(hipMemcpy(corner, c->d_corner_all, sizeof(float4) * nc, hipMemcpyDeviceToHost));
-  if (surf && ns) CK(hipMemcpy(surf, c->d_surf_all, sizeof(float4) * ns, hipMemcpyDeviceToHost));
+  CK(fbr_memcpy_sync(&n, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost));
+  CK(fbr_memcpy_sync(&nc, c->d_ncorner, sizeof(int32_t), hipMemcpyDeviceToHost));
+  CK(fbr_memcpy_sync(&ns, c->d_nsurf, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (label && n) CK(fbr_memcpy_sync(label, c->d_label_stream, (size_t)n, hipMemcpyDeviceToHost));
+  if (corner && nc) CK(fbr_memcpy_sync(corner, c->d_corner_all, sizeof(float4) * nc, hipMemcpyDeviceToHost));
+  if (surf && ns) CK(fbr_memcpy_sync(surf, c->d_surf_all, sizeof(float4) * ns, hipMemcpyDeviceToHost));
   if (n_corner) *n_corner = nc;
   if (n_surf) *n_surf = ns;
   return FBR_OK;
@@ -1185,9 +1223,9 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
     c->stream_degenerate = st.degenerate;
   } else {
     int32_t nv = 0, nc = 0, ns = 0;
-    CK(hipMemcpy(&nv, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost));
-    CK(hipMemcpy(&nc, c->d_ncorner, sizeof(int32_t), hipMemcpyDeviceToHost));
-    CK(hipMemcpy(&ns, c->d_nsurf, sizeof(int32_t), hipMemcpyDeviceToHost));
+    CK(fbr_memcpy_sync(&nv, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost));
+    CK(fbr_memcpy_sync(&nc, c->d_ncorner, sizeof(int32_t), hipMemcpyDeviceToHost));
+    CK(fbr_memcpy_sync(&ns, c->d_nsurf, sizeof(int32_t), hipMemcpyDeviceToHost));
     st.status = FBR_REG_SKIPPED_INTERVAL;
     st.n_points = nv;
     st.n_corner = nc;
@@ -1205,7 +1243,7 @@ int fbr_reset_stream(fbr_ctx* c) {
   CK(hipMemsetAsync(c->d_label_stream, 0, c->HW, c->stream));
   CK(hipMemsetAsync(c->d_col, 0, sizeof(int32_t) * c->HW, c->stream));
   CK(hipMemsetAsync(c->d_range, 0, sizeof(float) * c->HW, c->stream));
-  CK(hipStreamSynchronize(c->stream));
+  CK(fbr_sync(c->stream));
   c->time_last = -1.0;
   c->have_projection = false;
   c->stream_degenerate = 0;
@@ -1237,7 +1275,7 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
   if (!rc) q(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * n_jobs, hipMemcpyHostToDevice, c->stream));
   if (!rc && c->has_map) rc = crop_stats(c, Sub{0, n_jobs, 0, c->stream});
   // the caller's host buffers may be reused once this returns: drain the queued copies on every path
-  q(hipStreamSynchronize(c->stream));
+  q(fbr_sync(c->stream));
   if (rc) return rc;
   c->crop_cached = c->has_map;
   c->staged_B = n_jobs;
@@ -1259,9 +1297,9 @@ int fbr_set_deskew(fbr_ctx* c, const fbr_deskew_table* tables, int n_tables) {
     any = any || mode[j] != 0;
   }
   if (any && !c->d_desk) CK(hipMalloc((void**)&c->d_desk, sizeof(fbr_deskew_table) * c->Bcap));
-  CK(hipStreamSynchronize(c->stream));
-  if (any) CK(hipMemcpy(c->d_desk, tables, sizeof(fbr_deskew_table) * n_tables, hipMemcpyHostToDevice));
-  CK(hipMemcpy(c->d_desk_mode, mode.data(), sizeof(int32_t) * c->Bcap, hipMemcpyHostToDevice));
+  CK(fbr_sync(c->stream));
+  if (any) CK(fbr_memcpy_sync(c->d_desk, tables, sizeof(fbr_deskew_table) * n_tables, hipMemcpyHostToDevice));
+  CK(fbr_memcpy_sync(c->d_desk_mode, mode.data(), sizeof(int32_t) * c->Bcap, hipMemcpyHostToDevice));
   c->desk_any = any;
   return FBR_OK;
 }
@@ -1301,7 +1339,7 @@ int fbr_batch_launch(fbr_ctx* c) {
 int fbr_batch_wait(fbr_ctx* c) {
   if (!c) return FBR_ERR_INVALID_ARG;
   CK(hipSetDevice(c->dev));
-  CK(hipStreamSynchronize(c->stream));
+  CK(fbr_sync(c->stream));
   return FBR_OK;
 }
 
@@ -1341,17 +1379,145 @@ int fbr_batch_bytes(fbr_ctx* c, double* bytes_total, double* bytes_gn) {
   return FBR_OK;
 }
 
+namespace {
+
+int ingest_init(fbr_ctx* c) {
+  Ingest& g = c->ing;
+  if (g.cstream) return FBR_OK;
+  int64_t mb = 64;
+  if (const char* e = std::getenv("FBR_STAGE_MB")) mb = std::max<int64_t>(1, std::atoll(e));
+  g.chunk_bytes = std::max<int64_t>(mb << 20, c->NMAX * (int64_t)sizeof(fbr_point_xyzirt));
+  g.nthreads = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  if (const char* e = std::getenv("FBR_STAGE_THREADS")) g.nthreads = std::max(1, std::atoi(e));
+  CK(hipStreamCreateWithFlags(&g.cstream, hipStreamNonBlocking));
+  for (auto& e : g.up_ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : g.chunk_ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  CK(hipHostMalloc((void**)&g.h_stage, (size_t)g.chunk_bytes * Ingest::kChunks, hipHostMallocDefault));
+  g.d_pts_slot[0] = c->d_pts;
+  if (dalloc(&g.d_pts_slot[1], (int64_t)c->Bcap * c->NMAX)) return FBR_ERR_HIP;
+  return FBR_OK;
+}
+
+// Upload B scans into input slot `slot`: pack them into free pinned chunks (host threads), queue
+// one H2D copy per scan on the copy stream, then record up_ev[slot].  Runs on a worker thread
+// while the previous device batch computes.
+int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, const int64_t* n_in, int B) {
+  CK(hipSetDevice(c->dev));
+  Ingest& g = c->ing;
+  fbr_point_xyzirt* dst = g.d_pts_slot[slot];
+  std::vector<int64_t> off;
+  for (int j = 0; j < B;) {
+    const int k = g.next_chunk;
+    g.next_chunk = (k + 1) % Ingest::kChunks;
+    if (g.chunk_used[k]) CK(hipEventSynchronize(g.chunk_ev[k]));  // its previous copies are done
+    uint8_t* base = g.h_stage + (int64_t)k * g.chunk_bytes;
+    int j1 = j;
+    int64_t used = 0;
+    off.clear();
+    while (j1 < B && used + n_in[j1] * (int64_t)sizeof(fbr_point_xyzirt) <= g.chunk_bytes) {
+      off.push_back(used);
+      used += n_in[j1] * (int64_t)sizeof(fbr_point_xyzirt);
+      ++j1;
+    }
+    if (j1 == j) return FBR_ERR_CAPACITY;  // (chunk_bytes >= NMAX * 24: not reached)
+    const int nt = std::max(1, std::min(g.nthreads, j1 - j));
+    auto pack = [&](int t) {
+      for (int jj = j + t; jj < j1; jj += nt)
+        if (n_in[jj]) std::memcpy(base + off[jj - j], scans[jj], n_in[jj] * sizeof(fbr_point_xyzirt));
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(pack, t);
+    pack(0);
+    for (auto& x : th) x.join();
+    for (int jj = j; jj < j1; ++jj)
+      if (n_in[jj])
+        CK(hipMemcpyAsync(dst + (int64_t)jj * c->NMAX, base + off[jj - j], n_in[jj] * sizeof(fbr_point_xyzirt),
+                          hipMemcpyHostToDevice, g.cstream));
+    CK(hipEventRecord(g.chunk_ev[k], g.cstream));
+    g.chunk_used[k] = true;
+    g.h2d_bytes += (double)used;
+    j = j1;
+  }
+  CK(hipEventRecord(g.up_ev[slot], g.cstream));
+  return FBR_OK;
+}
+
+// Stage device batch `slot` whose scans ingest_upload queued: job metadata on the primary stream,
+// which then waits for the slot's upload.
+int ingest_stage(fbr_ctx* c, int slot, const int64_t* n_in, int B, const float* poses_in) {
+  drop_staged_batch(c);
+  c->no_time_call = false;
+  c->d_pts = c->ing.d_pts_slot[slot];
+  CK(hipMemcpyAsync(c->d_nin, n_in, sizeof(int64_t) * B, hipMemcpyHostToDevice, c->stream));
+  CK(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * B, hipMemcpyHostToDevice, c->stream));
+  CK(hipStreamWaitEvent(c->stream, c->ing.up_ev[slot], 0));
+  if (c->has_map) {
+    const int rc = crop_stats(c, Sub{0, B, 0, c->stream});
+    if (rc) return rc;
+  }
+  CK(fbr_sync(c->stream));  // n_in / poses_in are the caller's
+  c->crop_cached = c->has_map;
+  c->staged_B = B;
+  c->staged_nin.assign(n_in, n_in + B);
+  return FBR_OK;
+}
+
+}  // namespace
+
+// Independent jobs in device batches of max_batch.  The scans go through pinned staging on a copy
+// stream, double-buffered: batch k+1 is packed and copied while batch k computes.
 int fbr_process_batch(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int64_t* n_in, int n_jobs,
                       float* poses_inout, fbr_reg_stats* stats) {
   if (!c || !scans || !n_in || !poses_inout || n_jobs < 0) return FBR_ERR_INVALID_ARG;
-  for (int j0 = 0; j0 < n_jobs; j0 += c->Bcap) {
-    const int B = std::min(c->Bcap, n_jobs - j0);
-    int rc = fbr_batch_stage(c, scans + j0, n_in + j0, B, poses_inout + 6 * j0);
+  for (int j = 0; j < n_jobs; ++j) {  // validated before anything is copied
+    if (n_in[j] < 0 || n_in[j] > c->NMAX) return FBR_ERR_CAPACITY;
+    if (n_in[j] && !scans[j]) return FBR_ERR_INVALID_ARG;
+  }
+  if (n_jobs == 0) return FBR_OK;
+  if (!c->has_map) return FBR_ERR_NO_MAP;
+  CK(hipSetDevice(c->dev));
+  int rc = ingest_init(c);
+  if (rc) return rc;
+  c->ing.h2d_bytes = 0.0;
+  const int nb = (n_jobs + c->Bcap - 1) / c->Bcap;
+  auto first = [&](int b) { return b * c->Bcap; };
+  auto count = [&](int b) { return std::min(c->Bcap, n_jobs - b * c->Bcap); };
+  rc = ingest_upload(c, 0, scans, n_in, count(0));
+  for (int b = 0; b < nb && !rc; ++b) {
+    const int slot = b & 1, j0 = first(b), B = count(b);
+    int up_rc = FBR_OK;
+    std::thread up;
+    if (b + 1 < nb)  // the other slot is free: batch b - 1 finished before its results were read
+      up = std::thread([&, b] { up_rc = ingest_upload(c, slot ^ 1, scans + first(b + 1), n_in + first(b + 1), count(b + 1)); });
+    rc = ingest_stage(c, slot, n_in + j0, B, poses_inout + 6 * j0);
     if (!rc) rc = fbr_batch_launch(c);
     if (!rc) rc = fbr_batch_wait(c);
     if (!rc) rc = fbr_batch_results(c, poses_inout + 6 * j0, stats ? stats + j0 : nullptr);
-    if (rc) return rc;
+    if (up.joinable()) up.join();
+    if (!rc) rc = up_rc;
   }
+  (void)fbr_sync(c->ing.cstream);
+  c->d_pts = c->ing.d_pts_slot[0];
+  if (rc) drop_staged_batch(c);
+  return rc;
+}
+
+int fbr_debug_counters(long long* launches, long long* host_syncs, long long* flag_polls, int reset) {
+  DebugCounters& d = debug_counters();
+  if (launches) *launches = d.launches.load();
+  if (host_syncs) *host_syncs = d.host_syncs.load();
+  if (flag_polls) *flag_polls = d.flag_polls.load();
+  if (reset) {
+    d.launches = 0;
+    d.host_syncs = 0;
+    d.flag_polls = 0;
+  }
+  return FBR_OK;
+}
+
+int fbr_ingest_bytes(fbr_ctx* c, double* h2d_bytes) {
+  if (!c || !h2d_bytes) return FBR_ERR_INVALID_ARG;
+  *h2d_bytes = c->ing.h2d_bytes;
   return FBR_OK;
 }
 
@@ -1376,7 +1542,7 @@ extern "C" int fbr_diag_feature_stamps(fbr_ctx* c, unsigned long long* out /* [m
     CK(hipMemset(c->d_feat_stamps, 0, sizeof(unsigned long long) * n));
     return FBR_OK;
   }
-  if (out) CK(hipMemcpy(out, c->d_feat_stamps, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
+  if (out) CK(fbr_memcpy_sync(out, c->d_feat_stamps, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
   return FBR_OK;
 }
 
@@ -1472,7 +1638,7 @@ int fbr_keyframes_add(fbr_ctx* c, const fbr_keypose* pose, const fbr_point_xyzi*
   if (n_corner)
     CK(hipMemcpyAsync(c->d_kf_c + c->kf_c_used, corner, sizeof(float4) * n_corner, hipMemcpyHostToDevice, c->stream));
   if (n_surf) CK(hipMemcpyAsync(c->d_kf_s + c->kf_s_used, surf, sizeof(float4) * n_surf, hipMemcpyHostToDevice, c->stream));
-  CK(hipStreamSynchronize(c->stream));
+  CK(fbr_sync(c->stream));
   fbr_keypose p = *pose;
   p.intensity = (float)c->kf_poses.size();  // "this can be used as index" (:1687, :1694)
   c->kf_poses.push_back(p);

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "fbr_common.h"
 
 namespace fbr {
@@ -23,8 +25,19 @@ inline LaunchTimer& launch_timer() {
   return t;
 }
 
+// Diagnostic counters (fbr_debug_counters): kernel launches, blocking host synchronisations
+// (stream syncs and synchronous copies of the boundary code) and Gauss-Newton flag polls.
+struct DebugCounters {
+  std::atomic<long long> launches{0}, host_syncs{0}, flag_polls{0};
+};
+inline DebugCounters& debug_counters() {
+  static DebugCounters c;
+  return c;
+}
+
 template <typename F, typename... Args>
 inline void fbr_launch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, Args... args) {
+  debug_counters().launches.fetch_add(1, std::memory_order_relaxed);
   LaunchTimer& t = launch_timer();
   if (t.stop) {
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, t.launched ? nullptr : t.start, t.stop, 0, args...);

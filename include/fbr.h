@@ -330,10 +330,18 @@ int fbr_process_scan(fbr_ctx* ctx, const fbr_point_xyzirt* points, int64_t n_in,
 int fbr_reset_stream(fbr_ctx* ctx);
 
 /* Independent jobs (config C4): each job is one scan registered from its own guess against the
- * shared map, with fresh FeatureExtraction state.  Processed in device batches of max_batch. */
+ * shared map, with fresh FeatureExtraction state.  Processed in device batches of max_batch; the
+ * host scans are packed into pinned staging and copied on a second stream, double-buffered, so
+ * batch k+1's host-to-device copy overlaps batch k's compute.  The caller's buffers may be reused
+ * once the call returns. */
 int fbr_process_batch(fbr_ctx* ctx, const fbr_point_xyzirt* const* scans, const int64_t* n_in,
                       int n_jobs, float* poses_inout /* [n_jobs][6] */,
                       fbr_reg_stats* stats /* [n_jobs] or NULL */);
+/* Host-to-device scan bytes copied by the last fbr_process_batch (ingest measurement). */
+int fbr_ingest_bytes(fbr_ctx* ctx, double* h2d_bytes);
+/* Diagnostic process-wide counters: kernel launches, blocking host synchronisations of the
+ * boundary code, and host polls of the device Gauss-Newton flags; reset != 0 zeroes them. */
+int fbr_debug_counters(long long* launches, long long* host_syncs, long long* flag_polls, int reset);
 
 /* Device-resident batch (throughput measurement): stage copies the scans and guesses to HBM (and
  * computes the per-job CropBox map statistics, which depend only on the guesses); launch enqueues
