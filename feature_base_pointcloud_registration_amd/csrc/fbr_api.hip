@@ -172,6 +172,12 @@ struct fbr_ctx {
   int* d_bounds = nullptr;
   bool map_nocrop = false;  // the registration map is a keyframe local map
   int stream_degenerate = 0;  // mapOptimization::isDegenerate across single-scan registrations
+  JobResult* d_result = nullptr;          // [Bcap] packed per-job results
+  JobResult* h_result = nullptr;          // [Bcap] pinned
+  fbr_point_xyzirt* h_scan = nullptr;     // [NMAX] pinned staging of single-scan uploads
+  int64_t* h_nin = nullptr;               // pinned scalar
+  uint8_t* h_msg = nullptr;               // pinned staging of raw PointCloud2 bytes (grown on demand)
+  uint64_t h_msg_cap = 0;
   Ingest ing;                 // fbr_process_batch host ingest (allocated on first use)
 };
 
@@ -673,40 +679,85 @@ int stage_register(fbr_ctx* c, const Sub& sb, bool trace) {
   return rc;
 }
 
-int copy_stats(fbr_ctx* c, int B, fbr_reg_stats* stats) {
-  std::vector<fbr_reg_stats> st(B);
-  std::vector<int32_t> crop(2 * B), nv(B), nc(B), ns(B);
-  CK(hipMemcpyAsync(st.data(), c->d_stats, sizeof(fbr_reg_stats) * B, hipMemcpyDeviceToHost, c->stream));
-  CK(hipMemcpyAsync(crop.data(), c->d_cropcnt, sizeof(int32_t) * 2 * B, hipMemcpyDeviceToHost, c->stream));
-  CK(hipMemcpyAsync(nv.data(), c->d_nvalid, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
-  CK(hipMemcpyAsync(nc.data(), c->d_ncorner, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
-  CK(hipMemcpyAsync(ns.data(), c->d_nsurf, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
+// Per-job results of the last B jobs, packed on the device and returned by one copy (then one
+// host synchronisation): poses (when poses_out), stats, and the features' capacity errors
+// (FBR_ERR_UNSUPPORTED if any job has one).  with_reg = false: the registration was gated off.
+int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool with_reg = true) {
+  launch_pack_results(c->stream, B, with_reg ? 1 : 0, c->d_pose_out, c->d_stats, c->d_nvalid, c->d_ncorner, c->d_nsurf,
+                      c->d_cropcnt, c->d_err, c->d_result);
+  CK(hipMemcpyAsync(c->h_result, c->d_result, sizeof(JobResult) * B, hipMemcpyDeviceToHost, c->stream));
   CK(fbr_sync(c->stream));
-  c->last_iters.resize(B);
-  c->last_q.resize(B);
-  c->last_n.resize(B);
-  c->last_m.resize(B);
-  for (int j = 0; j < B; ++j) {
-    st[j].n_corner_map = crop[2 * j];
-    st[j].n_surf_map = crop[2 * j + 1];
-    st[j].n_points = nv[j];
-    st[j].n_corner = nc[j];
-    st[j].n_surf = ns[j];
-    c->last_iters[j] = st[j].iterations;
-    c->last_q[j] = st[j].n_corner_ds + st[j].n_surf_ds;
-    c->last_n[j] = nv[j];
-    c->last_m[j] = crop[2 * j] + crop[2 * j + 1];
-    if (stats) stats[j] = st[j];
+  int rc = FBR_OK;
+  if (with_reg) {
+    c->last_iters.resize(B);
+    c->last_q.resize(B);
+    c->last_n.resize(B);
+    c->last_m.resize(B);
   }
-  return FBR_OK;
+  for (int j = 0; j < B; ++j) {
+    const JobResult& r = c->h_result[j];
+    if (r.err) rc = FBR_ERR_UNSUPPORTED;
+    if (with_reg) {
+      c->last_iters[j] = r.st.iterations;
+      c->last_q[j] = r.st.n_corner_ds + r.st.n_surf_ds;
+      c->last_n[j] = r.st.n_points;
+      c->last_m[j] = r.st.n_corner_map + r.st.n_surf_map;
+    }
+    if (stats) stats[j] = r.st;
+    if (poses_out && with_reg)
+      for (int k = 0; k < 6; ++k) poses_out[6 * j + k] = r.pose[k];
+  }
+  return rc;
 }
 
+int copy_stats(fbr_ctx* c, int B, fbr_reg_stats* stats) { return copy_results(c, B, stats, nullptr, true); }
+
+// Host copy into pinned staging, split over threads for large scans (a 64x1800 scan is 2.6 MB).
+void pinned_copy(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kPart = 1 << 20;
+  const int nt = (int)std::min<size_t>(4, (bytes + kPart - 1) / kPart);
+  if (nt <= 1) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  const size_t part = (bytes + nt - 1) / nt;
+  auto one = [&](int t) {
+    const size_t b = (size_t)t * part, e = std::min(bytes, b + part);
+    if (e > b) std::memcpy((uint8_t*)dst + b, (const uint8_t*)src + b, e - b);
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(one, t);
+  one(0);
+  for (auto& x : th) x.join();
+}
+
+// Single-scan uploads stage through our own pinned buffer with a threaded host copy (default;
+// 1.00 vs 1.07 ms per pose-chained C2 scan) or hand the caller's pageable buffer to the runtime's
+// staging copy (FBR_PINNED_UPLOAD=0).
+bool pinned_upload() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_PINNED_UPLOAD");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+// A single scan into job slot `job` with no host synchronisation of its own: a copy from pageable
+// memory returns once the runtime has staged the source, and the pinned staging buffer is only
+// rewritten by the next call, after this call's results came back.
 int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n) {
   if (n < 0 || n > c->NMAX) return FBR_ERR_CAPACITY;
   c->no_time_call = false;
-  if (n) CK(hipMemcpyAsync(c->d_pts + job * c->NMAX, pts, sizeof(fbr_point_xyzirt) * n, hipMemcpyHostToDevice, c->stream));
-  CK(hipMemcpyAsync(c->d_nin + job, &n, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-  CK(fbr_sync(c->stream));  // n lives on the caller's stack
+  if (n && pinned_upload()) {
+    CK(fbr_sync(c->stream));  // staging free (a no-op after the previous call's result copy)
+    pinned_copy(c->h_scan, pts, sizeof(fbr_point_xyzirt) * n);
+    CK(hipMemcpyAsync(c->d_pts + job * c->NMAX, c->h_scan, sizeof(fbr_point_xyzirt) * n, hipMemcpyHostToDevice,
+                      c->stream));
+  } else if (n) {
+    CK(hipMemcpyAsync(c->d_pts + job * c->NMAX, pts, sizeof(fbr_point_xyzirt) * n, hipMemcpyHostToDevice, c->stream));
+  }
+  *c->h_nin = n;
+  CK(hipMemcpyAsync(c->d_nin + job, c->h_nin, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
   return FBR_OK;
 }
 
@@ -717,15 +768,25 @@ int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags) {
   int rc = resolve_msg(msg, &L);
   if (rc) return rc;
   if (L.n > c->NMAX) return FBR_ERR_CAPACITY;
+  CK(fbr_sync(c->stream));  // staging free (a no-op after the previous call's result copy)
   if (L.bytes > c->msg_cap) {
-    CK(fbr_sync(c->stream));
     if (c->d_msg) CK(hipFree(c->d_msg));
     c->d_msg = nullptr;
     c->msg_cap = 0;
     CK(hipMalloc(&c->d_msg, L.bytes));
     c->msg_cap = L.bytes;
   }
-  if (L.bytes) CK(hipMemcpyAsync(c->d_msg, msg->data, L.bytes, hipMemcpyHostToDevice, c->stream));
+  if (L.bytes > c->h_msg_cap) {
+    if (c->h_msg) CK(hipHostFree(c->h_msg));
+    c->h_msg = nullptr;
+    c->h_msg_cap = 0;
+    CK(hipHostMalloc((void**)&c->h_msg, L.bytes, hipHostMallocDefault));
+    c->h_msg_cap = L.bytes;
+  }
+  if (L.bytes) {
+    pinned_copy(c->h_msg, msg->data, L.bytes);
+    CK(hipMemcpyAsync(c->d_msg, c->h_msg, L.bytes, hipMemcpyHostToDevice, c->stream));
+  }
   MsgDev D;
   D.n = L.n;
   D.width = L.width;
@@ -733,9 +794,8 @@ int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags) {
   D.point_step = L.point_step;
   for (int k = 0; k < kMsgFields; ++k) D.off[k] = L.off[k];
   TIMED(c, "unpack_msg", launch_unpack_msg(c->stream, c->d_msg, D, c->d_pts));
-  const int64_t n = L.n;
-  CK(hipMemcpyAsync(c->d_nin, &n, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-  CK(fbr_sync(c->stream));  // n lives on this stack; msg->data is the caller's
+  *c->h_nin = L.n;
+  CK(hipMemcpyAsync(c->d_nin, c->h_nin, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
   if (msg_flags) *msg_flags = L.flags;
   c->no_time_call = (L.flags & FBR_MSG_NO_TIME) != 0;
   return FBR_OK;
@@ -985,7 +1045,11 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
                             hipHostMallocMapped) != hipSuccess ||
               hipHostGetDevicePointer((void**)&c->d_iter_flags, c->h_iter_flags, 0) != hipSuccess || dalloc(&c->d_pose_out, B * 6) ||
               dalloc(&c->d_stats, B) || dalloc(&c->d_trace, B * p->max_iterations * 6) ||
-              dalloc(&c->d_desk_mode, B) || dalloc(&c->d_rowmin, B * H);
+              dalloc(&c->d_desk_mode, B) || dalloc(&c->d_rowmin, B * H) || dalloc(&c->d_result, B) ||
+              hipHostMalloc((void**)&c->h_result, sizeof(JobResult) * B, hipHostMallocDefault) != hipSuccess ||
+              hipHostMalloc((void**)&c->h_scan, sizeof(fbr_point_xyzirt) * std::max<int64_t>(c->NMAX, 1),
+                            hipHostMallocDefault) != hipSuccess ||
+              hipHostMalloc((void**)&c->h_nin, sizeof(int64_t), hipHostMallocDefault) != hipSuccess;
   if (fail) {
     fbr_destroy(c);
     return FBR_ERR_HIP;
@@ -1020,6 +1084,9 @@ int fbr_destroy(fbr_ctx* c) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);
+  for (void* h : {(void*)c->h_result, (void*)c->h_scan, (void*)c->h_nin, (void*)c->h_msg})
+    if (h) (void)hipHostFree(h);
+  if (c->d_result) (void)hipFree(c->d_result);
   if (c->ing.cstream) (void)fbr_sync(c->ing.cstream);
   if (c->ing.h_stage) (void)hipHostFree(c->ing.h_stage);
   if (c->ing.d_pts_slot[1]) (void)hipFree(c->ing.d_pts_slot[1]);
@@ -1161,6 +1228,7 @@ int fbr_register_trace(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corne
   if (rc) return rc;
   CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->stream));
   CK(hipMemsetAsync(c->d_nvalid, 0, sizeof(int32_t), c->stream));
+  CK(hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream));  // no feature stage in this call
   rc = stage_register(c, single_sub(c), trace != nullptr);
   if (rc) return rc;
   CK(hipMemcpyAsync(pose_inout, c->d_pose_out, sizeof(float) * 6, hipMemcpyDeviceToHost, c->stream));
@@ -1203,33 +1271,30 @@ int fbr_process_msg(fbr_ctx* c, const fbr_pointcloud2* msg, double stamp, float 
 }
 
 namespace {
+// The scan is already queued into job slot 0.  Everything up to the pose runs on the stream with
+// no host round trip (the features' capacity error is checked with the results); one packed copy
+// and one synchronisation return pose and stats.
 int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stats* stats) {
   int rc = stage_project(c, single_sub(c));
   if (!rc) rc = stage_features(c, single_sub(c), true);
-  if (!rc) rc = check_err(c, 1);
   if (rc) return rc;
   c->have_projection = true;
   fbr_reg_stats st;
   std::memset(&st, 0, sizeof(st));
-  if (stamp - c->time_last >= c->P.mapping_process_interval) {  // mapOptmization.h:279
-    if (!c->has_map) return FBR_ERR_NO_MAP;
-    c->time_last = stamp;
+  const bool run = stamp - c->time_last >= c->P.mapping_process_interval;  // mapOptmization.h:279
+  if (run && !c->has_map) return FBR_ERR_NO_MAP;
+  float pose[6];
+  if (run) {
     CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->stream));
     rc = stage_register(c, single_sub(c), false);
     if (rc) return rc;
-    CK(hipMemcpyAsync(pose_inout, c->d_pose_out, sizeof(float) * 6, hipMemcpyDeviceToHost, c->stream));
-    rc = copy_stats(c, 1, &st);
-    if (rc) return rc;
+  }
+  rc = copy_results(c, 1, &st, pose, run);
+  if (rc) return rc;  // capacity error: the pose stays the guess, the time gate is not consumed
+  if (run) {
+    c->time_last = stamp;
+    for (int k = 0; k < 6; ++k) pose_inout[k] = pose[k];
     c->stream_degenerate = st.degenerate;
-  } else {
-    int32_t nv = 0, nc = 0, ns = 0;
-    CK(fbr_memcpy_sync(&nv, c->d_nvalid, sizeof(int32_t), hipMemcpyDeviceToHost));
-    CK(fbr_memcpy_sync(&nc, c->d_ncorner, sizeof(int32_t), hipMemcpyDeviceToHost));
-    CK(fbr_memcpy_sync(&ns, c->d_nsurf, sizeof(int32_t), hipMemcpyDeviceToHost));
-    st.status = FBR_REG_SKIPPED_INTERVAL;
-    st.n_points = nv;
-    st.n_corner = nc;
-    st.n_surf = ns;
   }
   if (stats) *stats = st;
   return FBR_OK;
@@ -1347,11 +1412,7 @@ int fbr_batch_results(fbr_ctx* c, float* poses_out, fbr_reg_stats* stats) {
   if (!c) return FBR_ERR_INVALID_ARG;
   if (c->staged_B <= 0) return FBR_ERR_STATE;
   CK(hipSetDevice(c->dev));
-  const int B = c->staged_B;
-  int rc = check_err(c, B);
-  if (rc) return rc;
-  if (poses_out) CK(hipMemcpyAsync(poses_out, c->d_pose_out, sizeof(float) * 6 * B, hipMemcpyDeviceToHost, c->stream));
-  return copy_stats(c, B, stats);
+  return copy_results(c, c->staged_B, stats, poses_out, true);
 }
 
 int fbr_batch_export(fbr_ctx* c, void* device_dst) {

@@ -187,6 +187,17 @@ void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fuse
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid);
 void launch_gn_solve(hipStream_t s, const GnArgs& a, int iter_idx, unsigned long long gen);
 void launch_gn_finalize(hipStream_t s, const GnArgs& a);
+// Everything the host reads back per job, packed by one kernel so a single copy returns it.
+struct JobResult {
+  float pose[6];
+  fbr_reg_stats st;
+  int32_t err;  // k_features capacity error of the job
+  int32_t pad;
+};
+// with_reg = 0: the registration did not run (interval gate): stats hold only the cloud counts
+void launch_pack_results(hipStream_t s, int B, int with_reg, const float* pose_out, const fbr_reg_stats* stats,
+                         const int32_t* nvalid, const int32_t* ncorner, const int32_t* nsurf, const int32_t* cropcnt,
+                         const int32_t* err, JobResult* out);
 // laserCloud{Corner,Surf}FromMapDSNum: CropBox counts of the global map per job.
 void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, float* dst);
 void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* map_pts, int64_t n, int which,

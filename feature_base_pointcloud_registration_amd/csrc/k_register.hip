@@ -752,6 +752,37 @@ __global__ void k_export_records(int B, const float* pose_out, const fbr_reg_sta
   dst[8 * j + 7] = __int_as_float(stats[j].status);
 }
 
+__global__ void k_pack_results(int B, int with_reg, const float* pose_out, const fbr_reg_stats* stats,
+                               const int32_t* nvalid, const int32_t* ncorner, const int32_t* nsurf,
+                               const int32_t* cropcnt, const int32_t* err, JobResult* out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= B) return;
+  JobResult r;
+  if (with_reg) {
+    for (int k = 0; k < 6; ++k) r.pose[k] = pose_out[6 * j + k];
+    r.st = stats[j];
+    r.st.n_corner_map = cropcnt[2 * j];
+    r.st.n_surf_map = cropcnt[2 * j + 1];
+  } else {
+    for (int k = 0; k < 6; ++k) r.pose[k] = 0.0f;
+    r.st = fbr_reg_stats{};
+    r.st.status = FBR_REG_SKIPPED_INTERVAL;
+  }
+  r.st.n_points = nvalid[j];
+  r.st.n_corner = ncorner[j];
+  r.st.n_surf = nsurf[j];
+  r.err = err[j];
+  r.pad = 0;
+  out[j] = r;
+}
+
+void launch_pack_results(hipStream_t s, int B, int with_reg, const float* pose_out, const fbr_reg_stats* stats,
+                         const int32_t* nvalid, const int32_t* ncorner, const int32_t* nsurf, const int32_t* cropcnt,
+                         const int32_t* err, JobResult* out) {
+  fbr_launch(k_pack_results, dim3((B + 63) / 64), dim3(64), 0, s, B, with_reg, pose_out, stats, nvalid, ncorner, nsurf,
+             cropcnt, err, out);
+}
+
 void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, float* dst) {
   fbr_launch(k_export_records, dim3((B + 63) / 64), dim3(64), 0, s, B, pose_out, stats, dst);
 }
