@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = [
     "fbr_params_default", "fbr_strerror", "fbr_abi_version", "fbr_device_count", "fbr_create",
     "fbr_destroy", "fbr_set_map", "fbr_get_map", "fbr_project", "fbr_extract_features",
     "fbr_register", "fbr_register_trace", "fbr_process_scan", "fbr_reset_stream",
-    "fbr_process_batch", "fbr_ingest_bytes", "fbr_debug_counters", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
+    "fbr_process_batch", "fbr_ingest_bytes", "fbr_debug_counters", "fbr_map_grid_info", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
     "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
     "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math", "fbr_selftest_eigen6",
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
@@ -76,6 +76,7 @@ def lib():
             "fbr_reset_stream": (ctypes.c_int, [_VP]),
             "fbr_process_batch": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, _VP, _VP]),
             "fbr_ingest_bytes": (ctypes.c_int, [_VP, _VP]),
+            "fbr_map_grid_info": (ctypes.c_int, [_VP, _VP]),
             "fbr_debug_counters": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int]),
             "fbr_batch_stage": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, _VP]),
             "fbr_batch_launch": (ctypes.c_int, [_VP]),
@@ -433,6 +434,13 @@ class Context:
         _check(lib().fbr_process_batch(self._h, arr, ptr(n_in), len(keep), ptr(poses), ptr(stats)),
                "fbr_process_batch")
         return poses, stats
+
+    def map_grid_info(self):
+        """The map's kNN grid: dict(sparse, dims, box_cells, stored, n_corner, n_surf)."""
+        v = np.zeros(8, np.int64)
+        _check(lib().fbr_map_grid_info(self._h, ptr(v)), "fbr_map_grid_info")
+        return dict(sparse=bool(v[0]), dims=tuple(int(x) for x in v[1:4]), box_cells=int(v[4]), stored=int(v[5]),
+                    n_corner=int(v[6]), n_surf=int(v[7]))
 
     def ingest_bytes(self):
         """Host-to-device scan bytes of the last process_batch."""

@@ -139,9 +139,7 @@ struct fbr_ctx {
   float* d_trace = nullptr;
   // map
   bool has_map = false;
-  float4 *d_map_c = nullptr, *d_map_s = nullptr;
-  int32_t *d_cs_c = nullptr, *d_cs_s = nullptr;
-  GridDesc gc{}, gs{};
+  DevGrid grid_c, grid_s;  // kNN grids of the corner / surf maps (k_grid.hip)
   std::vector<fbr_point_xyzi> map_c_host, map_s_host;
   // state
   bool have_projection = false;
@@ -267,78 +265,6 @@ void grid_cell_sizes(const fbr_params& P, float* inv_yz, float* inv_x) {
   };
   *inv_yz = pick("FBR_KNN_CELL", sparse ? 1.0f : 2.0f, 0.5f, 4.0f);  // 2 m .. 0.25 m
   *inv_x = pick("FBR_KNN_CELL_X", sparse ? 4.0f : 8.0f, 0.5f, 8.0f);  // 2 m .. 0.125 m
-}
-
-// Host grid over host points (the start-up map): counting sort by cell, index order kept inside a
-// cell; `max` caps both inverse cell sizes (the second map follows the first one's cells).
-int build_grid(fbr_ctx* c, const std::vector<fbr_point_xyzi>& pts, float4** d_pts, int32_t** d_cs, GridDesc* g,
-               const GridDesc* max) {
-  if (*d_pts) (void)hipFree(*d_pts);
-  if (*d_cs) (void)hipFree(*d_cs);
-  *d_pts = nullptr;
-  *d_cs = nullptr;
-  const int64_t n = (int64_t)pts.size();
-  float inv, invx;
-  grid_cell_sizes(c->P, &inv, &invx);
-  if (max) {
-    inv = std::min(inv, max->inv_cell);
-    invx = std::min(invx, max->inv_x);
-  }
-  int64_t lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0}, dims[3] = {1, 1, 1};
-  for (int attempt = 0; attempt < 12; ++attempt) {
-    const float iv[3] = {invx, inv, inv};
-    for (int d = 0; d < 3; ++d) {
-      lo[d] = INT64_MAX;
-      hi[d] = INT64_MIN;
-    }
-    for (const auto& p : pts) {
-      const float v[3] = {p.x, p.y, p.z};
-      for (int d = 0; d < 3; ++d) {
-        const int64_t cidx = (int64_t)std::floor(v[d] * iv[d]);
-        lo[d] = std::min(lo[d], cidx);
-        hi[d] = std::max(hi[d], cidx);
-      }
-    }
-    if (n == 0)
-      for (int d = 0; d < 3; ++d) lo[d] = hi[d] = 0;
-    for (int d = 0; d < 3; ++d) dims[d] = hi[d] - lo[d] + 1;
-    if (dims[0] * dims[1] * dims[2] <= (int64_t)1 << 26) break;
-    inv *= 0.5f;
-    invx *= 0.5f;
-  }
-  const int64_t ncell = dims[0] * dims[1] * dims[2];
-  std::vector<int32_t> cell(n), start(ncell + 1, 0);
-  for (int64_t i = 0; i < n; ++i) {
-    const fbr_point_xyzi& p = pts[i];
-    const int64_t cx = (int64_t)std::floor(p.x * invx) - lo[0], cy = (int64_t)std::floor(p.y * inv) - lo[1],
-                  cz = (int64_t)std::floor(p.z * inv) - lo[2];
-    cell[i] = (int32_t)((cz * dims[1] + cy) * dims[0] + cx);
-    start[cell[i] + 1]++;
-  }
-  for (int64_t k = 0; k < ncell; ++k) start[k + 1] += start[k];
-  // [0, n): sorted by cell; [n, 2n): the same points in map-index order (MapGrid::by_id)
-  std::vector<float4> sorted(std::max<int64_t>(2 * n, 1));
-  std::vector<int32_t> fill(start.begin(), start.end() - 1);
-  for (int64_t i = 0; i < n; ++i) {  // counting sort, index order kept inside a cell
-    const fbr_point_xyzi& p = pts[i];
-    float w;
-    int32_t ii = (int32_t)i;
-    std::memcpy(&w, &ii, 4);
-    sorted[fill[cell[i]]++] = make_float4(p.x, p.y, p.z, w);
-    sorted[n + i] = make_float4(p.x, p.y, p.z, w);
-  }
-  if (dalloc(d_pts, std::max<int64_t>(2 * n, 1)) || dalloc(d_cs, ncell + 1)) return FBR_ERR_HIP;
-  if (n) CK(fbr_memcpy_sync(*d_pts, sorted.data(), sizeof(float4) * 2 * n, hipMemcpyHostToDevice));
-  CK(fbr_memcpy_sync(*d_cs, start.data(), sizeof(int32_t) * (ncell + 1), hipMemcpyHostToDevice));
-  g->inv_cell = inv;
-  g->inv_x = invx;
-  for (int d = 0; d < 3; ++d) {
-    g->origin[d] = (float)lo[d];
-    g->dims[d] = (int32_t)dims[d];
-  }
-  g->n_cells = (int32_t)ncell;
-  g->n_points = n;
-  return FBR_OK;
 }
 
 // Clouds at least this large take the device-wide VoxelGrid (FBR_VG_LARGE_MIN overrides; tests
@@ -508,8 +434,8 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   a.surfDS = c->d_surfDS + j0 * HW;
   a.caps = HW;
   a.nsds = c->d_nsds + j0;
-  a.mc = MapGrid{c->d_map_c, c->d_cs_c, c->gc, c->d_map_c + c->gc.n_points};
-  a.ms = MapGrid{c->d_map_s, c->d_cs_s, c->gs, c->d_map_s + c->gs.n_points};
+  a.mc = c->grid_c.view();
+  a.ms = c->grid_s.view();
   a.gn = c->d_gn + j0;
   a.guess = c->d_guess + j0 * 6;
   a.items = c->d_items + ib;
@@ -549,16 +475,16 @@ int crop_stats(fbr_ctx* c, const Sub& sb) {
   if (c->map_nocrop) {  // keyframe local map: laserCloud*FromMapDSNum = the whole DS map
     std::vector<int32_t> v(2 * sb.B);
     for (int j = 0; j < sb.B; ++j) {
-      v[2 * j] = (int32_t)c->gc.n_points;
-      v[2 * j + 1] = (int32_t)c->gs.n_points;
+      v[2 * j] = (int32_t)c->grid_c.g.n_points;
+      v[2 * j + 1] = (int32_t)c->grid_s.g.n_points;
     }
     CK(hipMemcpyAsync(cnt, v.data(), sizeof(int32_t) * 2 * sb.B, hipMemcpyHostToDevice, sb.st));
     CK(fbr_sync(sb.st));
     return FBR_OK;
   }
   CK(hipMemsetAsync(cnt, 0, sizeof(int32_t) * 2 * sb.B, sb.st));
-  TIMED_ON(c, sb.st, "crop", launch_crop_count(sb.st, a, c->d_map_c, c->gc.n_points, 0, cnt));
-  TIMED_ON(c, sb.st, "crop", launch_crop_count(sb.st, a, c->d_map_s, c->gs.n_points, 1, cnt));
+  TIMED_ON(c, sb.st, "crop", launch_crop_count(sb.st, a, c->grid_c.pts, c->grid_c.g.n_points, 0, cnt));
+  TIMED_ON(c, sb.st, "crop", launch_crop_count(sb.st, a, c->grid_s.pts, c->grid_s.g.n_points, 1, cnt));
   return FBR_OK;
 }
 
@@ -891,46 +817,16 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
   return rc;
 }
 
-// Device grid over a device-resident map (cell sizes as build_grid, at most max's, halved
-// until the dense grid has <= 2^26 cells).
-int build_grid_dev(fbr_ctx* c, const float4* d_src, int64_t n, float4** d_pts, int32_t** d_cs, GridDesc* g,
-                   const GridDesc* max) {
-  if (*d_pts) (void)hipFree(*d_pts);
-  if (*d_cs) (void)hipFree(*d_cs);
-  *d_pts = nullptr;
-  *d_cs = nullptr;
-  if (!c->d_bounds && dalloc(&c->d_bounds, 6)) return FBR_ERR_HIP;
+// Both kNN grids of a map (corner, surf) on the device, with one cell size and one layout (the
+// kNN kernel is specialised on both): the shared cell sizes of grid_cell_sizes, dense unless a
+// map's occupied box is too large, then hashed chunks for both.
+int build_map_grids(fbr_ctx* c, const float4* d_corner, int64_t nc, const float4* d_surf, int64_t ns) {
   float inv, invx;
   grid_cell_sizes(c->P, &inv, &invx);
-  if (max) {
-    inv = std::min(inv, max->inv_cell);
-    invx = std::min(invx, max->inv_x);
-  }
-  int64_t dims[3] = {1, 1, 1};
-  int b[6] = {0, 0, 0, 0, 0, 0};
-  for (int attempt = 0; attempt < 12; ++attempt) {
-    const int rc = grid_bounds_device(c->stream, d_src, n, invx, inv, c->d_bounds, b);
-    if (rc) return rc;
-    if (n == 0)
-      for (int d = 0; d < 6; ++d) b[d] = 0;
-    for (int d = 0; d < 3; ++d) dims[d] = (int64_t)b[3 + d] - b[d] + 1;
-    if (dims[0] * dims[1] * dims[2] <= (int64_t)1 << 26) break;
-    inv *= 0.5f;
-    invx *= 0.5f;
-  }
-  g->inv_cell = inv;
-  g->inv_x = invx;
-  for (int d = 0; d < 3; ++d) {
-    g->origin[d] = (float)b[d];
-    g->dims[d] = (int32_t)dims[d];
-  }
-  g->n_cells = (int32_t)(dims[0] * dims[1] * dims[2]);
-  g->n_points = n;
-  // [0, n): sorted by cell; [n, 2n): the source points in map-index order (MapGrid::by_id)
-  if (dalloc(d_pts, std::max<int64_t>(2 * n, 1)) || dalloc(d_cs, (int64_t)g->n_cells + 1)) return FBR_ERR_HIP;
-  if (n) CK(hipMemcpyAsync(*d_pts + n, d_src, sizeof(float4) * n, hipMemcpyDeviceToDevice, c->stream));
-  int rc = grid_fill_device(c->stream, d_src, n, *g, *d_cs, *d_pts);
-  if (!rc) CK(fbr_sync(c->stream));
+  int rc = grid_build_device(c->stream, d_corner, nc, invx, inv, false, c->grid_c);
+  if (!rc) rc = grid_build_device(c->stream, d_surf, ns, invx, inv, c->grid_c.g.sparse != 0, c->grid_s);
+  if (!rc && c->grid_s.g.sparse && !c->grid_c.g.sparse)
+    rc = grid_build_device(c->stream, d_corner, nc, invx, inv, true, c->grid_c);
   return rc;
 }
 
@@ -1077,13 +973,14 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring, c->d_surf_ring_cnt,
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
-                  c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_map_c,
-                  c->d_map_s, c->d_cs_c, c->d_cs_s, c->d_nbr, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
+                  c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
                   c->d_desk, c->d_desk_mode, c->d_rowmin,
                   c->d_kf_c, c->d_kf_s, c->d_kraw_c, c->d_kraw_s, c->d_kds_c, c->d_kds_s, c->d_kf_segs, c->d_bounds};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);
+  free_grid(c->grid_c);
+  free_grid(c->grid_s);
   for (void* h : {(void*)c->h_result, (void*)c->h_scan, (void*)c->h_nin, (void*)c->h_msg})
     if (h) (void)hipHostFree(h);
   if (c->d_result) (void)hipFree(c->d_result);
@@ -1122,13 +1019,34 @@ int fbr_set_map(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corner, cons
   c->map_nocrop = false;
   int rc = voxel_grid_once(c, corner, n_corner, c->P.mapping_corner_leaf_size, c->map_c_host);
   if (!rc) rc = voxel_grid_once(c, surf, n_surf, c->P.mapping_surf_leaf_size, c->map_s_host);
-  // both grids share one (power-of-two) cell size: the kNN kernel is specialised on it
-  if (!rc) rc = build_grid(c, c->map_c_host, &c->d_map_c, &c->d_cs_c, &c->gc, nullptr);
-  if (!rc) rc = build_grid(c, c->map_s_host, &c->d_map_s, &c->d_cs_s, &c->gs, &c->gc);
-  if (!rc && (c->gs.inv_cell < c->gc.inv_cell || c->gs.inv_x < c->gc.inv_x))
-    rc = build_grid(c, c->map_c_host, &c->d_map_c, &c->d_cs_c, &c->gc, &c->gs);
+  // the DS maps (map-index order) go to HBM once; the grids are built there
+  float4 *d_c = nullptr, *d_s = nullptr;
+  const int64_t nc = (int64_t)c->map_c_host.size(), ns = (int64_t)c->map_s_host.size();
+  if (!rc && (dalloc(&d_c, std::max<int64_t>(nc, 1)) || dalloc(&d_s, std::max<int64_t>(ns, 1)))) rc = FBR_ERR_HIP;
+  if (!rc && nc && hipMemcpy(d_c, c->map_c_host.data(), sizeof(float4) * nc, hipMemcpyHostToDevice) != hipSuccess)
+    rc = FBR_ERR_HIP;
+  if (!rc && ns && hipMemcpy(d_s, c->map_s_host.data(), sizeof(float4) * ns, hipMemcpyHostToDevice) != hipSuccess)
+    rc = FBR_ERR_HIP;
+  if (!rc) rc = build_map_grids(c, d_c, nc, d_s, ns);
+  if (d_c) (void)hipFree(d_c);
+  if (d_s) (void)hipFree(d_s);
   c->has_map = rc == FBR_OK;
   return rc;
+}
+
+int fbr_map_grid_info(fbr_ctx* c, int64_t info[8]) {
+  if (!c || !info) return FBR_ERR_INVALID_ARG;
+  if (!c->has_map) return FBR_ERR_NO_MAP;
+  const GridDesc& g = c->grid_s.g;
+  info[0] = g.sparse;
+  info[1] = g.dims[0];
+  info[2] = g.dims[1];
+  info[3] = g.dims[2];
+  info[4] = (int64_t)g.dims[0] * g.dims[1] * g.dims[2];  // cells of the occupied box
+  info[5] = g.sparse ? (int64_t)c->grid_c.g.n_cells + g.n_cells : info[4];  // chunks (sparse) / cells
+  info[6] = c->grid_c.g.n_points;
+  info[7] = g.n_points;
+  return FBR_OK;
 }
 
 int fbr_get_map(fbr_ctx* c, int64_t* n_corner, int64_t* n_surf, fbr_point_xyzi* corner, fbr_point_xyzi* surf) {
@@ -1843,10 +1761,7 @@ int fbr_extract_surrounding_keyframes(fbr_ctx* c, double stamp, const fbr_keyfra
   rc = voxel_grid_dev(c, c->d_kraw_c, tot_c, c->P.mapping_corner_leaf_size, c->d_kds_c, &c->kds_c_n);
   if (!rc) rc = voxel_grid_dev(c, c->d_kraw_s, tot_s, c->P.mapping_surf_leaf_size, c->d_kds_s, &c->kds_s_n);
   // the kNN grids (both maps share one cell size, as in fbr_set_map)
-  if (!rc) rc = build_grid_dev(c, c->d_kds_c, c->kds_c_n, &c->d_map_c, &c->d_cs_c, &c->gc, nullptr);
-  if (!rc) rc = build_grid_dev(c, c->d_kds_s, c->kds_s_n, &c->d_map_s, &c->d_cs_s, &c->gs, &c->gc);
-  if (!rc && (c->gs.inv_cell < c->gc.inv_cell || c->gs.inv_x < c->gc.inv_x))
-    rc = build_grid_dev(c, c->d_kds_c, c->kds_c_n, &c->d_map_c, &c->d_cs_c, &c->gc, &c->gs);
+  if (!rc) rc = build_map_grids(c, c->d_kds_c, c->kds_c_n, c->d_kds_s, c->kds_s_n);
   c->has_map = rc == FBR_OK;
   c->map_nocrop = rc == FBR_OK;
   c->crop_cached = false;

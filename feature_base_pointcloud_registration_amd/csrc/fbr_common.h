@@ -67,14 +67,28 @@ struct GnState {
   int32_t pad[2];
 };
 
-struct GridDesc {        // dense 3D grid over a map (cell indices, not metres, in origin)
+struct GridDesc {        // 3D grid over a map (cell indices, not metres, in origin)
   float origin[3];       // cell index of cell (0,0,0) per axis
   float inv_cell;        // 1 / cell size along y and z (a power of two)
   float inv_x;           // 1 / cell size along x (a power of two): cells may be shorter in x, the
                          // axis a grid row runs along, so rows scanned stay few and short
-  int32_t dims[3];
-  int32_t n_cells;
+  int32_t dims[3];       // bounding box of the occupied cells
+  int32_t n_cells;       // dense: dims product; sparse: occupied chunks
   int64_t n_points;
+  int32_t sparse;        // 0: dense cell_start over the box; 1: hashed chunks of kChunkX cells in x
+  uint32_t hmask;        // sparse: hash table size - 1
 };
+
+// Sparse grids: a row of cells (fixed y, z) is split into chunks of kChunkX cells along x; each
+// occupied chunk stores kChunkX + 1 point offsets and is found through an open-addressing hash of
+// its (z, y, x / kChunkX) key.  A kNN row range spans at most 2 chunks (<= 2 * 8 + 1 cells).
+constexpr int kChunkX = 16;
+constexpr unsigned long long kChunkEmpty = ~0ull;
+__host__ __device__ inline unsigned long long chunk_key(int z, int y, int xc) {
+  return ((unsigned long long)(unsigned)z << 48) | ((unsigned long long)(unsigned)y << 24) | (unsigned long long)(unsigned)xc;
+}
+__host__ __device__ inline uint32_t chunk_hash(unsigned long long k) {
+  return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 32);
+}
 
 }  // namespace fbr

@@ -145,10 +145,29 @@ void launch_concat(hipStream_t s, int B, int H, int W, const float4* corner_slot
 // ---- A10-A18 (k_register.hip) ----
 struct MapGrid {
   const float4* pts;          // sorted by cell; w = bit pattern of the map index
-  const int32_t* cell_start;  // [n_cells+1]
+  const int32_t* cell_start;  // dense: [n_cells+1]; sparse: [chunks][kChunkX + 1]
   GridDesc g;
   const float4* by_id;        // the same points in map-index order (neighbour gathers by index)
+  const unsigned long long* hkeys;  // sparse: [hmask + 1] chunk keys (kChunkEmpty = free)
+  const int32_t* hvals;             // sparse: [hmask + 1] chunk ids
 };
+
+// A map's kNN grid in HBM (fbr_set_map, the keyframe local map): built on the device from the
+// map points in map-index order.  Dense when the occupied box has at most kDenseGridCells cells,
+// hashed chunks otherwise (or when FBR_GRID_SPARSE=1).
+struct DevGrid {
+  float4* pts = nullptr;              // [0, n): sorted by cell; [n, 2n): by map index
+  int32_t* cs = nullptr;
+  unsigned long long* hkeys = nullptr;
+  int32_t* hvals = nullptr;
+  GridDesc g{};
+  MapGrid view() const { return MapGrid{pts, cs, g, pts + g.n_points, hkeys, hvals}; }
+};
+constexpr int64_t kDenseGridCells = (int64_t)1 << 26;
+void free_grid(DevGrid& d);
+// Build `out` over n points (device, map-index order) with cells of 1/invx (x) and 1/inv (y, z).
+int grid_build_device(hipStream_t s, const float4* pts, int64_t n, float invx, float inv, bool force_sparse,
+                      DevGrid& out);
 
 struct GnArgs {
   int B, max_iter;
@@ -209,10 +228,5 @@ struct KfSeg {               // one selected keyframe cloud: pool[src .. src+cou
   float T[12];               // pcl::getTransformation of the key pose, row-major 3x4
 };
 void launch_kf_transform(hipStream_t s, const float4* pool, const KfSeg* segs, int nseg, int64_t max_count, float4* out);
-// Device kNN grid build: cell bounds of pts at 1/inv cells (h_bounds = lo xyz, hi xyz), then the
-// per-cell counts, exclusive scan into d_cs [n_cells + 1] and the scatter into d_out.
-int grid_bounds_device(hipStream_t s, const float4* pts, int64_t n, float invx, float inv, int* d_bounds,
-                       int h_bounds[6]);
-int grid_fill_device(hipStream_t s, const float4* pts, int64_t n, const GridDesc& g, int32_t* d_cs, float4* d_out);
 
 }  // namespace fbr

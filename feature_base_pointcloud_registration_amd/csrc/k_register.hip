@@ -98,6 +98,41 @@ __device__ __forceinline__ float axis_lb(float q, float fcell, int o, float c) {
 
 __device__ __forceinline__ int rank_offset(int k, int s) { return k == 0 ? 0 : ((k & 1) ? s * ((k + 1) >> 1) : -s * (k >> 1)); }
 
+// Sparse grids (k_grid.hip): the chunk of (z, y, x / kChunkX), or -1.  The table is at most half
+// full, so a free slot ends every probe sequence.
+__device__ __forceinline__ int chunk_find(const MapGrid& m, int z, int y, int xc) {
+  const unsigned long long key = chunk_key(z, y, xc);
+  uint32_t h = chunk_hash(key) & m.g.hmask;
+  for (uint32_t probe = 0; probe <= m.g.hmask; ++probe) {
+    const unsigned long long k = m.hkeys[h];
+    if (k == key) return m.hvals[h];
+    if (k == kChunkEmpty) break;
+    h = (h + 1) & m.g.hmask;
+  }
+  return -1;
+}
+
+// Point range [b, e) of the cells x0..x1 (x1 - x0 < 2 * kChunkX) of row (y, z).  The two chunks
+// are adjacent in the (z, y, x) sort, so their points form one contiguous range.
+template <bool kSparse>
+__device__ __forceinline__ bool row_range(const MapGrid& m, int y, int z, int x0, int x1, int& b, int& e) {
+  if constexpr (!kSparse) {
+    const int rowbase = (z * m.g.dims[1] + y) * m.g.dims[0];
+    b = m.cell_start[rowbase + x0];
+    e = m.cell_start[rowbase + x1 + 1];
+    return true;
+  } else {
+    const int ca = x0 / kChunkX, cb = x1 / kChunkX;
+    const int ia = chunk_find(m, z, y, ca);
+    const int ib = cb == ca ? ia : chunk_find(m, z, y, cb);
+    if (ia < 0 && ib < 0) return false;
+    constexpr int S = kChunkX + 1;
+    b = ia >= 0 ? m.cell_start[ia * S + (x0 - ca * kChunkX)] : m.cell_start[ib * S];
+    e = ib >= 0 ? m.cell_start[ib * S + (x1 - cb * kChunkX) + 1] : m.cell_start[ia * S + kChunkX];
+    return true;
+  }
+}
+
 #ifdef FBR_KNN_STATS
 // Diagnostic builds only (tools/knn_stats.py): [queries, rows considered, rows scanned, points
 // scanned, points inserted, accepted queries, corner queries, wave iterations of the point loop]
@@ -126,7 +161,7 @@ __device__ unsigned long long fbr_knn_stats[8];
 // sum over rows of each row's longest lane (lanes of a wave scan different rows: the per-row loop
 // kept ~30 % of the lanes busy).  Pruning with a larger cut only scans more cells, and the 5-NN
 // list is a function of the scanned set, so both forms give the same neighbours.
-template <int R, int RX, bool kFlat = false>
+template <int R, int RX, bool kFlat = false, bool kSparse = false>
 __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
                           float bound, Knn5& r, unsigned* ks, int2* rows = nullptr) {
   constexpr int K = 2 * R + 1;  // rows per side in y and z; RX = cells per side along x
@@ -190,8 +225,8 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       }
       const int x0 = max(cx + xa, 0), x1 = min(cx + xb, X - 1);
       if (x0 > x1) continue;
-      const int rowbase = (z * Y + y) * X;
-      const int b = m.cell_start[rowbase + x0], e = m.cell_start[rowbase + x1 + 1];
+      int b, e;
+      if (!row_range<kSparse>(m, y, z, x0, x1, b, e)) continue;
       FBR_KS(2, 1);
       FBR_KS(3, e - b);
       // the whole row inside the crop box (pcl::CropBox, inclusive) -> no per-point test
@@ -479,7 +514,7 @@ k_gn_residual(GnArgs a) {
 // R = grid cells per side covering radius 1 (both map grids share one cell size).  kFused: the
 // same lane goes on to its residual row and the workgroup reduces the item's normal-equation
 // partial (k_gn_residual's work, without re-reading the query and its neighbour indices).
-template <int R, int RX, bool kFused, bool kFlat>
+template <int R, int RX, bool kFused, bool kFlat, bool kSparse>
 __global__ void __launch_bounds__(kResThreads)
 k_gn_knn(GnArgs a, int use_prev) {
   __shared__ double red[kFused ? kResThreads / 64 : 1][28];
@@ -519,7 +554,7 @@ k_gn_knn(GnArgs a, int use_prev) {
       }
       Knn5 nn;
       unsigned ks[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-      knn5_grid<R, RX, kFlat>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks, &rows[0][tid]);
+      knn5_grid<R, RX, kFlat, kSparse>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks, &rows[0][tid]);
       const bool ok = nn.k[4] < kKnnEmpty;
 #ifdef FBR_KNN_STATS
       ks[5] = ok;
@@ -788,13 +823,19 @@ void launch_export_records(hipStream_t s, int B, const float* pose_out, const fb
 }
 
 void launch_gn_init(hipStream_t s, const GnArgs& a) { fbr_launch(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
+template <int R, bool F, bool L, bool S>
+void launch_gn_knn_rls(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
+  const float invx = a.mc.g.inv_x;  // == a.ms.g.inv_x
+  if (invx > 4.0f) fbr_launch((k_gn_knn<R, 8, F, L, S>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
+  else if (invx > 2.0f) fbr_launch((k_gn_knn<R, 4, F, L, S>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
+  else if (invx > 1.0f) fbr_launch((k_gn_knn<R, 2, F, L, S>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
+  else fbr_launch((k_gn_knn<R, 1, F, L, S>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
+}
+// Dense or hashed-chunk map grids (one flag for both maps: fbr_set_map builds them alike).
 template <int R, bool F, bool L>
 void launch_gn_knn_rl(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
-  const float invx = a.mc.g.inv_x;  // == a.ms.g.inv_x
-  if (invx > 4.0f) fbr_launch((k_gn_knn<R, 8, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
-  else if (invx > 2.0f) fbr_launch((k_gn_knn<R, 4, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
-  else if (invx > 1.0f) fbr_launch((k_gn_knn<R, 2, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
-  else fbr_launch((k_gn_knn<R, 1, F, L>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
+  if (a.mc.g.sparse || a.ms.g.sparse) launch_gn_knn_rls<R, F, L, true>(s, a, grid, use_prev);
+  else launch_gn_knn_rls<R, F, L, false>(s, a, grid, use_prev);
 }
 
 // Flat row queue (FBR_KNN_FLAT=0 disables): from iteration 1 on (warm-start bound), 1 m y/z cells

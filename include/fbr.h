@@ -337,6 +337,9 @@ int fbr_reset_stream(fbr_ctx* ctx);
 int fbr_process_batch(fbr_ctx* ctx, const fbr_point_xyzirt* const* scans, const int64_t* n_in,
                       int n_jobs, float* poses_inout /* [n_jobs][6] */,
                       fbr_reg_stats* stats /* [n_jobs] or NULL */);
+/* Diagnostic: the kNN grid of the current map: {sparse (hashed chunks) 0/1, surf-grid box dims
+ * x, y, z, box cells, stored chunks (sparse) or cells (dense), corner points, surf points}. */
+int fbr_map_grid_info(fbr_ctx* ctx, int64_t info[8]);
 /* Host-to-device scan bytes copied by the last fbr_process_batch (ingest measurement). */
 int fbr_ingest_bytes(fbr_ctx* ctx, double* h2d_bytes);
 /* Diagnostic process-wide counters: kernel launches, blocking host synchronisations of the

@@ -143,11 +143,13 @@ class Stream:
 class Map:
     """Global prior map after the start-up VoxelGrid (mapOptmization.h:245-260)."""
 
-    def __init__(self, params, corner, surf, raw=False):
+    def __init__(self, params, corner, surf, raw=False, crop=None):
         """raw=False: the prior map after the start-up VoxelGrid; raw=True: the clouds as given (a
-        keyframe local map from kf_extract), registered without the CropBox."""
+        keyframe local map from kf_extract), registered without the CropBox unless crop=True (an
+        already down-sampled prior map)."""
         self.params = params
         self.raw = raw
+        self.no_crop = raw if crop is None else not crop
         if raw:
             self.h = lib().orc_map_create_raw(ptr(corner), len(corner), ptr(surf), len(surf))
         else:
@@ -171,7 +173,7 @@ class Map:
         st = FbrRegStats()
         trace = np.zeros((self.params.max_iterations, 6), np.float32)
         lib().orc_register(ctypes.byref(self.params), self.h, ptr(corner), len(corner), ptr(surf),
-                           len(surf), ptr(pose), ctypes.byref(st), ptr(trace), n_threads, ptr(tab), int(self.raw),
+                           len(surf), ptr(pose), ctypes.byref(st), ptr(trace), n_threads, ptr(tab), int(self.no_crop),
                            ptr(degenerate) if degenerate is not None else None)
         d = st.as_dict()
         return pose, d, trace[:d["iterations"]].copy()

@@ -500,3 +500,73 @@ def test_voxel_grid_inplace_lds_sort_matches_global_scratch_kernel():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=env, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout == b"".join(outs[n].tobytes() for n in clouds)
+
+
+# ------------------------------------------------------------------------------- map grids
+def test_sparse_grid_registration_is_bit_identical_to_dense(c2_map):
+    """The hashed-chunk kNN grid (k_grid.hip, used when a map's occupied box exceeds 2^26 dense
+    cells) forced on the C2 map (FBR_GRID_SPARSE=1, child process) returns the dense grid's poses
+    and stats bit for bit: both give the kNN the same candidate sets."""
+    import subprocess
+    import sys
+    jobs = synth.make_jobs("C2", 12, base_seed=600)
+    H, W = synth.CONFIGS["C2"][:2]
+    P = default_params(H, W, max_batch=12)
+    with api.Context(P) as ctx:
+        ctx.set_map(*c2_map)
+        assert not ctx.map_grid_info()["sparse"]
+        poses, stats = ctx.process_batch([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_sparse_jobs.npz")
+    np.savez(path, *[j[0] for j in jobs], guesses=np.stack([j[1] for j in jobs]))
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api, synth; "
+            "from feature_base_pointcloud_registration_amd.fbr_types import default_params; "
+            "d = np.load(%r); scans = [d['arr_%%d' %% k] for k in range(12)]; "
+            "c = api.Context(default_params(%d, %d, max_batch=12)); c.set_map(*synth.config_map('C2')); "
+            "assert c.map_grid_info()['sparse']; p, s = c.process_batch(scans, d['guesses']); "
+            "sys.stdout.buffer.write(p.tobytes() + s.tobytes())" % (REPO, path, H, W))
+    env = dict(os.environ, FBR_GRID_SPARSE="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout == poses.tobytes() + stats.tobytes()
+
+
+def test_kilometre_prior_map_uses_sparse_grid_and_matches_oracle(c2_map):
+    """A 1.1 x 1.1 km prior map (11 x 11 translated copies of the C2 map, 11.6M points: a dense
+    grid of its box would need > 2^26 cells) registers jobs anywhere on it: hashed-chunk grid,
+    pose / iterations / n_sel against the oracle's CropBox + KD-tree (mapOptmization.h:245-304)."""
+    cm, sm = c2_map
+    tiles = [(i, j) for i in range(-5, 6) for j in range(-5, 6)]
+
+    def tile(m):
+        out = np.concatenate([m] * len(tiles))
+        for k, (i, j) in enumerate(tiles):
+            out["x"][k * len(m):(k + 1) * len(m)] += np.float32(100.0 * i)
+            out["y"][k * len(m):(k + 1) * len(m)] += np.float32(100.0 * j)
+        return out
+
+    big_c, big_s = tile(cm), tile(sm)
+    H, W = synth.CONFIGS["C2"][:2]
+    P = default_params(H, W)
+    with api.Context(P) as ctx:
+        ctx.set_map(big_c, big_s)
+        info = ctx.map_grid_info()
+        assert info["sparse"] and info["box_cells"] > (1 << 26)
+        # the start-up DS (mapOptmization.h:251-257) keeps the oracle's voxels; its centroids may
+        # differ in the last bits (PCL sums a voxel in std::sort order), so the registrations below
+        # run the oracle on the device's DS map to compare the search itself
+        dc, ds = ctx.get_map()
+        rc_, rs_ = O.Map(P, big_c, big_s).arrays()
+        assert (len(dc), len(ds)) == (len(rc_), len(rs_))
+        m = O.Map(P, dc, ds, raw=True, crop=True)
+        for seed, (i, j) in zip([71, 72, 73], [(0, 0), (3, -2), (-5, 5)]):
+            gt, guess = synth.job(seed)
+            f = O.Stream(P).features(synth.scan(gt, H, W, seed=seed))
+            g = guess.copy()
+            g[3] += np.float32(100.0 * i)
+            g[4] += np.float32(100.0 * j)
+            po, so, _ = m.register(f["corner"], f["surf"], g)
+            pg, sg, _ = ctx.register(f["corner"], f["surf"], g, trace=True)
+            assert_pose_close(pg, po)
+            assert (sg["iterations"], sg["n_sel"], sg["status"]) == (so["iterations"], so["n_sel"], so["status"])
+            assert (sg["n_corner_map"], sg["n_surf_map"]) == (so["n_corner_map"], so["n_surf_map"])
+            assert np.abs(pg[3:5] - (gt[3:5] + [100.0 * i, 100.0 * j])).max() < 0.05
