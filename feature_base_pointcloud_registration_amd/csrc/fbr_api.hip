@@ -124,6 +124,9 @@ struct fbr_ctx {
   int32_t *d_nitems = nullptr, *d_item_range = nullptr, *d_cropcnt = nullptr;
   double* d_partial = nullptr;
   int32_t* d_nbr = nullptr;
+  float* d_fitc = nullptr;     // [max_items][6][256] per-query fit cache (k_gn_residual)
+  int8_t* d_fits = nullptr;    // [max_items][256]
+  int8_t* d_nsame = nullptr;   // [max_items][256]
   unsigned long long* h_iter_flags = nullptr;  // host-mapped, written by k_gn_solve
   unsigned long long* d_iter_flags = nullptr;  // its device address
   unsigned long long gn_gen = 0;
@@ -452,6 +455,14 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   a.stats = c->d_stats + j0;
   a.trace = trace ? c->d_trace + j0 * c->P.max_iterations * 6 : nullptr;
   a.nbr = c->d_nbr + ib * 5 * 256;
+  a.fitc = c->d_fitc + ib * 6 * 256;
+  a.fits = c->d_fits + ib * 256;
+  a.nsame = c->d_nsame + ib * 256;
+  static const int fit_cache = [] {
+    const char* e = std::getenv("FBR_FIT_CACHE");
+    return e ? std::atoi(e) : 1;
+  }();
+  a.fit_cache = fit_cache;
   a.iter_flags = c->d_iter_flags + (int64_t)sb.k * mi;
   a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 2 * mi;
   a.desk_mode = c->desk_any ? c->d_desk_mode + j0 : nullptr;
@@ -935,6 +946,8 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_item_range, 2 * B) || dalloc(&c->d_cropcnt, 2 * B) ||
               dalloc(&c->d_partial, (int64_t)c->max_items * 32) ||
               dalloc(&c->d_nbr, (int64_t)c->max_items * 5 * 256) ||
+              dalloc(&c->d_fitc, (int64_t)c->max_items * 6 * 256) || dalloc(&c->d_fits, (int64_t)c->max_items * 256) ||
+              dalloc(&c->d_nsame, (int64_t)c->max_items * 256) ||
               dalloc(&c->d_iter_cnt, kMaxSub * 2 * std::max(1, p->max_iterations)) ||
               dalloc(&c->d_feat_scratch, (int64_t)B * H * feat_slot_bytes(c->W)) ||
               hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * kMaxSub * std::max(1, p->max_iterations),
@@ -973,7 +986,7 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring, c->d_surf_ring_cnt,
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
-                  c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
+                  c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_fitc, c->d_fits, c->d_nsame, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
                   c->d_desk, c->d_desk_mode, c->d_rowmin,
                   c->d_kf_c, c->d_kf_s, c->d_kraw_c, c->d_kraw_s, c->d_kds_c, c->d_kds_s, c->d_kf_segs, c->d_bounds};
   for (void* p : ptrs)

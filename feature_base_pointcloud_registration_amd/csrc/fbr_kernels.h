@@ -192,6 +192,10 @@ struct GnArgs {
   fbr_reg_stats* stats;      // [B]
   float* trace;              // [B][max_iter][6] or null
   int32_t* nbr;              // [max_items][5][256] kNN-5 map indices of each query (-1 = rejected)
+  float* fitc;               // [max_items][6][256] fit cache: line / plane of each query's neighbours
+  int8_t* fits;              // [max_items][256] fit cache state (0 none, 1 fitted, 2 rejected)
+  int8_t* nsame;             // [max_items][256] 1: this iteration's neighbours equal the previous ones
+  int fit_cache;             // reuse cached fits (FBR_FIT_CACHE, default 1)
   unsigned long long* iter_flags;  // host-mapped [max_iter]: (generation << 32) | jobs still active
   int32_t* iter_cnt;         // [max_iter][2] active-job count / finished workgroups (zeroed per solve)
   const int32_t* desk_mode;  // [B] kDesk* bits or null (transformUpdate's IMU slerp, :1447-1474)

@@ -135,8 +135,9 @@ __device__ __forceinline__ bool row_range(const MapGrid& m, int y, int z, int x0
 
 #ifdef FBR_KNN_STATS
 // Diagnostic builds only (tools/knn_stats.py): [queries, rows considered, rows scanned, points
-// scanned, points inserted, accepted queries, corner queries, wave iterations of the point loop]
-__device__ unsigned long long fbr_knn_stats[8];
+// scanned, points inserted, accepted queries, corner queries, wave iterations of the point loop,
+// warm-started queries, queries whose neighbours equal the previous iteration's]
+__device__ unsigned long long fbr_knn_stats[10];
 #define FBR_KS(i, v) ks[i] += (v)
 #else
 #define FBR_KS(i, v) \
@@ -287,7 +288,12 @@ struct Nbr5 {
   float x[5], y[5], z[5];
 };
 
-__device__ bool corner_residual(const Nbr5& nn, float x0, float y0, float z0, float4& coeff) {
+// The part of a correspondence that depends only on its 5 map neighbours: the corner line (two
+// points 0.1 along the principal axis through the mean, after the eigenvalue-ratio gate) or the
+// plane (pa, pb, pc, pd after the 0.2 m check).  A query whose kNN returns the same 5 neighbours as
+// in the previous Gauss-Newton iteration reuses it (bit-identical: same inputs, same operations);
+// only the query-dependent residual below is recomputed.  f[0..5]; false = rejected.
+__device__ bool corner_fit(const Nbr5& nn, float* f) {
   float cx = 0, cy = 0, cz = 0;
   for (int j = 0; j < 5; j++) { cx += nn.x[j]; cy += nn.y[j]; cz += nn.z[j]; }
   cx /= 5.0f; cy /= 5.0f; cz /= 5.0f;
@@ -303,10 +309,18 @@ __device__ bool corner_residual(const Nbr5& nn, float x0, float y0, float z0, fl
   float D1[3], V1[9];
   jacobi_eigen<3>(A1, D1, V1);
   if (!(D1[0] > 3.0f * D1[1])) return false;
-  const float x1 = (float)((double)cx + 0.1 * (double)V1[0]), y1 = (float)((double)cy + 0.1 * (double)V1[1]),
-              z1 = (float)((double)cz + 0.1 * (double)V1[2]);
-  const float x2 = (float)((double)cx - 0.1 * (double)V1[0]), y2 = (float)((double)cy - 0.1 * (double)V1[1]),
-              z2 = (float)((double)cz - 0.1 * (double)V1[2]);
+  f[0] = (float)((double)cx + 0.1 * (double)V1[0]);
+  f[1] = (float)((double)cy + 0.1 * (double)V1[1]);
+  f[2] = (float)((double)cz + 0.1 * (double)V1[2]);
+  f[3] = (float)((double)cx - 0.1 * (double)V1[0]);
+  f[4] = (float)((double)cy - 0.1 * (double)V1[1]);
+  f[5] = (float)((double)cz - 0.1 * (double)V1[2]);
+  return true;
+}
+
+// cornerOptimization's residual (:1083-1112) of query (x0, y0, z0) against the fitted line.
+__device__ bool corner_apply(const float* f, float x0, float y0, float z0, float4& coeff) {
+  const float x1 = f[0], y1 = f[1], z1 = f[2], x2 = f[3], y2 = f[4], z2 = f[5];
   const float a012 = sqrt_rn(((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) +
                                 ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) +
                                 ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1)) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1)));
@@ -323,8 +337,9 @@ __device__ bool corner_residual(const Nbr5& nn, float x0, float y0, float z0, fl
   return (double)s > 0.1;
 }
 
-// surfOptimization body (:1145-1211).
-__device__ bool surf_residual(const Nbr5& nn, float x0, float y0, float z0, float4& coeff) {
+// surfOptimization's plane (:1145-1186): f[0..3] = (pa, pb, pc, pd); false when a neighbour is
+// more than 0.2 from it.
+__device__ bool surf_fit(const Nbr5& nn, float* f) {
   float A0[5][3], B0[5], X0[3];
   for (int j = 0; j < 5; j++) { A0[j][0] = nn.x[j]; A0[j][1] = nn.y[j]; A0[j][2] = nn.z[j]; B0[j] = -1.0f; }
   colpiv_solve53(A0, B0, X0);
@@ -333,6 +348,13 @@ __device__ bool surf_residual(const Nbr5& nn, float x0, float y0, float z0, floa
   pa /= ps; pb /= ps; pc /= ps; pd /= ps;
   for (int j = 0; j < 5; j++)
     if ((double)fabsf(pa * nn.x[j] + pb * nn.y[j] + pc * nn.z[j] + pd) > 0.2) return false;
+  f[0] = pa; f[1] = pb; f[2] = pc; f[3] = pd;
+  return true;
+}
+
+// surfOptimization's residual (:1198-1211) of query (x0, y0, z0) against the plane.
+__device__ bool surf_apply(const float* f, float x0, float y0, float z0, float4& coeff) {
+  const float pa = f[0], pb = f[1], pc = f[2], pd = f[3];
   const float pd2 = pa * x0 + pb * y0 + pc * z0 + pd;
   const float s = (float)(1.0 - 0.9 * (double)fabsf(pd2) /
                                     (double)sqrt_rn(sqrt_rn(x0 * x0 + y0 * y0 + z0 * z0)));
@@ -422,17 +444,38 @@ __device__ __forceinline__ void res_halve(double* v, int lane) {
 
 // cornerOptimization / surfOptimization + the LMOptimization row (:1286-1332) of one query whose 5
 // neighbours are the map points nb[0..4] (map indices); false when the correspondence is rejected.
+// fc / fs: the query's fit cache (fit floats at stride kResThreads, state 0 none / 1 fitted /
+// 2 rejected); same: the neighbours equal the previous iteration's, whose fit the cache holds.
 __device__ __forceinline__ bool res_row(const GnState& g, const float4* by_id, const int32_t* nb, int stride,
                                         bool corner, const float4& p, float x0, float y0, float z0, float* row,
-                                        float& b) {
-  Nbr5 nn;
+                                        float& b, float* fc, int8_t* fs, bool same) {
+  float fit[6];
+  bool fit_ok;
+  const int8_t st = same ? *fs : (int8_t)0;
+  if (st != 0) {
+    fit_ok = st == 1;
+    if (fit_ok) {
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const float4 q = by_id[nb[k * stride]];
-    nn.x[k] = q.x; nn.y[k] = q.y; nn.z[k] = q.z;
+      for (int k = 0; k < 6; ++k) fit[k] = fc[k * kResThreads];
+    }
+  } else {
+    Nbr5 nn;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const float4 q = by_id[nb[k * stride]];
+      nn.x[k] = q.x; nn.y[k] = q.y; nn.z[k] = q.z;
+    }
+    fit_ok = corner ? corner_fit(nn, fit) : surf_fit(nn, fit);
+    *fs = fit_ok ? 1 : 2;
+    if (fit_ok) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        if (corner || k < 4) fc[k * kResThreads] = fit[k];
+    }
   }
+  if (!fit_ok) return false;
   float4 c;
-  const bool ok = corner ? corner_residual(nn, x0, y0, z0, c) : surf_residual(nn, x0, y0, z0, c);
+  const bool ok = corner ? corner_apply(fit, x0, y0, z0, c) : surf_apply(fit, x0, y0, z0, c);
   if (ok) {
     // camera-frame swap
     const float srx = g.trig[0], crx = g.trig[1], sry = g.trig[2], cry = g.trig[3], srz = g.trig[4], crz = g.trig[5];
@@ -504,7 +547,9 @@ k_gn_residual(GnArgs a) {
       const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
       const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
       const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
-      ok = res_row(g, corner ? a.mc.by_id : a.ms.by_id, nb, kResThreads, corner, p, x0, y0, z0, row, b);
+      const int64_t q = (int64_t)it * kResThreads + tid;
+      ok = res_row(g, corner ? a.mc.by_id : a.ms.by_id, nb, kResThreads, corner, p, x0, y0, z0, row, b,
+                   a.fitc + (int64_t)it * 6 * kResThreads + tid, a.fits + q, a.nsame[q] != 0);
     }
     res_reduce(red, tid, row, b, ok, a.partial + (int64_t)it * kPartial);
   }
@@ -539,11 +584,15 @@ k_gn_knn(GnArgs a, int use_prev) {
       const MapGrid& mg = corner ? a.mc : a.ms;
       int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
       float bound = __int_as_float(0x7f800000);
-      if (use_prev && o[0] >= 0) {  // warm start: the previous iteration's neighbours of this query
+      int32_t oid[5] = {-1, -1, -1, -1, -1};
+      const bool have_prev = use_prev && o[0] >= 0;
+      if (have_prev) {  // warm start: the previous iteration's neighbours of this query
         float mx = 0.0f;
 #pragma unroll
+        for (int k = 0; k < 5; ++k) oid[k] = o[k * kResThreads];
+#pragma unroll
         for (int k = 0; k < 5; ++k) {
-          const float4 q = mg.by_id[o[k * kResThreads]];
+          const float4 q = mg.by_id[oid[k]];
           float dist = 0.0f, diff;
           diff = x0 - q.x; dist += diff * diff;
           diff = y0 - q.y; dist += diff * diff;
@@ -553,23 +602,30 @@ k_gn_knn(GnArgs a, int use_prev) {
         bound = mx;
       }
       Knn5 nn;
-      unsigned ks[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+      unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       knn5_grid<R, RX, kFlat, kSparse>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks, &rows[0][tid]);
       const bool ok = nn.k[4] < kKnnEmpty;
-#ifdef FBR_KNN_STATS
-      ks[5] = ok;
-      ks[6] = corner;
-      for (int k = 0; k < 8; ++k) atomicAdd(&fbr_knn_stats[k], (unsigned long long)ks[k]);
-#else
       (void)ks;
-#endif
       int32_t ids[5];
+      bool same = have_prev && ok && a.fit_cache;
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
         ids[k] = knn_id(nn.k[k]);
+        same = same && ids[k] == oid[k];
         o[k * kResThreads] = ok ? ids[k] : -1;
       }
-      if (kFused && ok) rok = res_row(g, mg.by_id, ids, 1, corner, p, x0, y0, z0, row, b);
+      const int64_t q = (int64_t)it * kResThreads + tid;
+      if (!kFused) a.nsame[q] = same ? 1 : 0;
+#ifdef FBR_KNN_STATS
+      ks[5] = ok;
+      ks[6] = corner;
+      ks[8] = have_prev;
+      ks[9] = same;
+      for (int k = 0; k < 10; ++k) atomicAdd(&fbr_knn_stats[k], (unsigned long long)ks[k]);
+#endif
+      if (kFused && ok)
+        rok = res_row(g, mg.by_id, ids, 1, corner, p, x0, y0, z0, row, b, a.fitc + (int64_t)it * 6 * kResThreads + tid,
+                      a.fits + q, same);
     }
     if (kFused) res_reduce(red, tid, row, b, rok, a.partial + (int64_t)it * kPartial);
   }
@@ -889,10 +945,10 @@ void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* pts, int64_
 #ifdef FBR_KNN_STATS
 // Diagnostic builds only: read (and optionally reset) the kNN counters of k_gn_knn.
 extern "C" int fbr_diag_knn_stats(unsigned long long* out, int reset) {
-  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(fbr::fbr_knn_stats), sizeof(unsigned long long) * 8) != hipSuccess)
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(fbr::fbr_knn_stats), sizeof(unsigned long long) * 10) != hipSuccess)
     return FBR_ERR_HIP;
   if (reset) {
-    unsigned long long z[8] = {0};
+    unsigned long long z[10] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(fbr::fbr_knn_stats), z, sizeof(z)) != hipSuccess) return FBR_ERR_HIP;
   }
   return FBR_OK;

@@ -30,11 +30,13 @@ for cell in (sys.argv[2:] or ["0.5"]):
     L.fbr_diag_knn_stats(None, 1)
     ctx.set_profiling(True)
     ctx.batch_launch(); ctx.batch_wait()
-    st = np.zeros(8, np.uint64)
+    st = np.zeros(10, np.uint64)
     L.fbr_diag_knn_stats(st.ctypes.data, 0)
     q = float(st[0])
     print(f"cell {cell}: queries {int(q)} (corner {int(st[6])}) accepted {st[5] / q:.3f} | per query: rows considered "
           f"{st[1] / q:.1f}, rows scanned {st[2] / q:.1f}, points scanned {st[3] / q:.1f}, inserted {st[4] / q:.1f} | "
           f"gn_knn ms {ctx.kernel_time('gn_knn')} | point-loop lane efficiency "
-          f"{float(st[3]) / (64.0 * float(st[7])):.3f} (points scanned / (64 x wave iterations))")
+          f"{float(st[3]) / (64.0 * float(st[7])):.3f} (points scanned / (64 x wave iterations)) | "
+          f"neighbours unchanged from the previous iteration: {float(st[9]) / max(float(st[8]), 1.0):.3f} "
+          f"of {int(st[8])} warm-started queries")
     ctx.close()
