@@ -33,8 +33,11 @@ __device__ __forceinline__ bool project_point(const fbr_point_xyzirt& q, int H, 
   int columnIdn = x86_cvt(-round(((double)horizonAngle - 90.0) / (double)ang_res_x) + (double)(W / 2));
   if (columnIdn >= W) columnIdn -= W;
   if (columnIdn < 0 || columnIdn >= W) return false;
-  float range = sqrt_rn(q.x * q.x + q.y * q.y + q.z * q.z);
-  if (range < 1.0f) return false;
+  // range = sqrtf(x^2 + y^2 + z^2) < 1.0 (:618-621): a correctly rounded sqrt is below 1 exactly
+  // when its argument is (the largest float below 1 has a square root that rounds below 1; a NaN
+  // is not below 1 either way), so the test needs no square root here (k_compact recomputes the
+  // stored range)
+  if (q.x * q.x + q.y * q.y + q.z * q.z < 1.0f) return false;
   row = rowIdn;
   colo = columnIdn;
   return true;

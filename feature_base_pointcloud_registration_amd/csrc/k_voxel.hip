@@ -570,14 +570,23 @@ k_voxel_ring(VgRing A) {
   }
   const float4* CL = A.cloud + (int64_t)job * A.HW + s;
   const int8_t* LB = A.label + (int64_t)job * A.HW;
+  // segment j is [sp_j, sp_{j+1} - 1] (ep_j = sp_{j+1} - 1, ep_5 = e - 1): when all six are
+  // non-empty (sp < ep) they tile [s, e - 1]
+  bool all6 = true;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) all6 = all6 && sp6[j] < ep6[j];
   bool cd[KPT];
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
 #pragma unroll
   for (int r = 0; r < KPT; ++r) {
     const int k = s + r * T + tid;
     bool in = false;
+    if (all6) {
+      in = k <= ep6[5];
+    } else {
 #pragma unroll
-    for (int j = 0; j < 6; ++j) in |= sp6[j] < ep6[j] && k >= sp6[j] && k <= ep6[j];
+      for (int j = 0; j < 6; ++j) in |= sp6[j] < ep6[j] && k >= sp6[j] && k <= ep6[j];
+    }
     // label and point loads issued together (one round trip; the point's line is read anyway)
     const int8_t lab = in ? LB[k] : (int8_t)1;
     const float4 p = in ? CL[k - s] : make_float4(0.f, 0.f, 0.f, 0.f);

@@ -62,6 +62,16 @@ def test_glibc_sincosf_port_matches_glibc(probe_lib):
     assert probe_lib.probe_sincosf_range(0, 1 << 32, 97, th) == 0
 
 
+def test_range_gate_without_square_root():
+    """k_project tests range < 1.0 (imageProjection.cpp:618-621) on the squared sum: a correctly
+    rounded float sqrt is below 1 exactly when its argument is, NaN and inf included."""
+    lo, hi = np.float32(0.98).view(np.uint32), np.float32(1.02).view(np.uint32)
+    s = np.arange(lo, hi, dtype=np.uint32).view(np.float32)
+    s = np.concatenate([s, np.array([0.0, 1e-45, 1.0, np.inf, np.nan, 3.4e38], np.float32)])
+    with np.errstate(invalid="ignore"):
+        assert np.array_equal(np.sqrt(s) < np.float32(1.0), s < np.float32(1.0))
+
+
 @pytest.mark.parametrize("nvals", [1, 2, 3, 7, 50, 10_000_000])
 def test_sort_emulation_matches_libstdcxx(probe_lib, nvals):
     rng = np.random.default_rng(nvals)
