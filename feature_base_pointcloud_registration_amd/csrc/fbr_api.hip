@@ -157,6 +157,8 @@ struct fbr_ctx {
   fbr_deskew_table* d_desk = nullptr;  // [Bcap] tables (allocated on first use)
   int32_t* d_desk_mode = nullptr;      // [Bcap] kDesk* bits per job
   int32_t* d_rowmin = nullptr;         // [Bcap][H] minimum owner per row
+  int32_t* d_choff = nullptr;          // [Bcap][H][W / 32 + 1] compaction tile offsets
+  DevArena arena;                      // scratch of the set-up paths (map VoxelGrid, grid builds)
   bool desk_any = false;               // some job has a non-zero mode
   bool no_time_call = false;           // the current call's PointCloud2 has no "time" field
   // LIO-SAM keyframe store (fbr_keyframes_*) and the local map built from it
@@ -298,7 +300,7 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
         hipMemcpyAsync(d_cnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
       rc = FBR_ERR_HIP;
     } else if (large) {
-      rc = voxel_grid_large(c->stream, d_in, n, leaf, 0, d_out, d_cnt + 1);
+      rc = voxel_grid_large(c->stream, c->arena, d_in, n, leaf, 0, d_out, d_cnt + 1);
       int32_t nout = 0;
       if (!rc && (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
                   fbr_sync(c->stream) != hipSuccess))
@@ -366,6 +368,7 @@ int stage_project(fbr_ctx* c, const Sub& sb) {
                                                c->W, owner));
   TIMED_ON(c, sb.st, "extract",
            launch_extract(sb.st, c->d_pts + j0 * c->NMAX, c->NMAX, owner, sb.B, c->H, c->W, c->d_rowcnt + j0 * c->H,
+                          c->d_choff + j0 * c->H * (c->W / 32 + 1),
                           c->d_cloud + j0 * c->HW, c->d_col + j0 * c->HW, c->d_range + j0 * c->HW,
                           c->d_start + j0 * c->H, c->d_end + j0 * c->H, c->d_nvalid + j0, desk));
   return FBR_OK;
@@ -790,7 +793,7 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
   if (n >= vg_large_min()) {
     int32_t nout = 0;
     if (dalloc(&d_cnt, 1)) return FBR_ERR_HIP;
-    rc = voxel_grid_large(c->stream, d_in, n, leaf, 0, d_out, d_cnt);
+    rc = voxel_grid_large(c->stream, c->arena, d_in, n, leaf, 0, d_out, d_cnt);
     if (!rc && (hipMemcpyAsync(&nout, d_cnt, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
                 fbr_sync(c->stream) != hipSuccess))
       rc = FBR_ERR_HIP;
@@ -834,10 +837,10 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
 int build_map_grids(fbr_ctx* c, const float4* d_corner, int64_t nc, const float4* d_surf, int64_t ns) {
   float inv, invx;
   grid_cell_sizes(c->P, &inv, &invx);
-  int rc = grid_build_device(c->stream, d_corner, nc, invx, inv, false, c->grid_c);
-  if (!rc) rc = grid_build_device(c->stream, d_surf, ns, invx, inv, c->grid_c.g.sparse != 0, c->grid_s);
+  int rc = grid_build_device(c->stream, c->arena, d_corner, nc, invx, inv, false, c->grid_c);
+  if (!rc) rc = grid_build_device(c->stream, c->arena, d_surf, ns, invx, inv, c->grid_c.g.sparse != 0, c->grid_s);
   if (!rc && c->grid_s.g.sparse && !c->grid_c.g.sparse)
-    rc = grid_build_device(c->stream, d_corner, nc, invx, inv, true, c->grid_c);
+    rc = grid_build_device(c->stream, c->arena, d_corner, nc, invx, inv, true, c->grid_c);
   return rc;
 }
 
@@ -955,6 +958,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               hipHostGetDevicePointer((void**)&c->d_iter_flags, c->h_iter_flags, 0) != hipSuccess || dalloc(&c->d_pose_out, B * 6) ||
               dalloc(&c->d_stats, B) || dalloc(&c->d_trace, B * p->max_iterations * 6) ||
               dalloc(&c->d_desk_mode, B) || dalloc(&c->d_rowmin, B * H) || dalloc(&c->d_result, B) ||
+              dalloc(&c->d_choff, B * H * (c->W / 32 + 1)) ||
               hipHostMalloc((void**)&c->h_result, sizeof(JobResult) * B, hipHostMallocDefault) != hipSuccess ||
               hipHostMalloc((void**)&c->h_scan, sizeof(fbr_point_xyzirt) * std::max<int64_t>(c->NMAX, 1),
                             hipHostMallocDefault) != hipSuccess ||
@@ -987,13 +991,14 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_fitc, c->d_fits, c->d_nsame, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
-                  c->d_desk, c->d_desk_mode, c->d_rowmin,
+                  c->d_desk, c->d_desk_mode, c->d_rowmin, c->d_choff,
                   c->d_kf_c, c->d_kf_s, c->d_kraw_c, c->d_kraw_s, c->d_kds_c, c->d_kds_s, c->d_kf_segs, c->d_bounds};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);
   free_grid(c->grid_c);
   free_grid(c->grid_s);
+  arena_free(c->arena);
   for (void* h : {(void*)c->h_result, (void*)c->h_scan, (void*)c->h_nin, (void*)c->h_msg})
     if (h) (void)hipHostFree(h);
   if (c->d_result) (void)hipFree(c->d_result);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <atomic>
 
 #include "fbr_common.h"
@@ -65,9 +66,10 @@ struct DeskArgs {
   const fbr_deskew_table* table;
   int32_t* rowmin;
 };
+// choff: [B][H][ceil(W / 32)] scratch (claimed cells of a row before each compaction tile)
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,
-                    int W, int32_t* rowcnt, float4* cloud, int32_t* col, float* range, int32_t* start_ring,
-                    int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk);
+                    int W, int32_t* rowcnt, int32_t* choff, float4* cloud, int32_t* col, float* range,
+                    int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk);
 
 // ---- A6-A8 (k_features.hip) ----
 struct FeatArgs {
@@ -114,9 +116,47 @@ struct VgArgs {
 };
 constexpr int64_t kVgLdsCap = 4096;  // segments up to this size sort entirely in LDS
 void launch_voxel_grid(hipStream_t s, const VgArgs& a);
+
+// Device scratch of the set-up paths (map VoxelGrid, kNN grid builds): one hipMalloc'd block per
+// context, grown when a call needs more (after draining the stream that used it) and carved by a
+// bump allocator.  Every user runs on the context's stream, so a call that fits reuses the block
+// in stream order without a host synchronisation.
+struct DevArena {
+  char* base = nullptr;
+  size_t cap = 0, used = 0;
+};
+inline size_t arena_bytes(size_t b) { return (std::max<size_t>(b, 1) + 255) & ~(size_t)255; }
+// Room for `bytes` (the sum of arena_bytes of every slice the call takes); carving restarts at 0.
+inline hipError_t arena_reserve(DevArena& a, size_t bytes, hipStream_t s) {
+  a.used = 0;
+  if (bytes <= a.cap) return hipSuccess;
+  hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  if (a.base) (void)hipFree(a.base);
+  a.base = nullptr;
+  a.cap = 0;
+  const size_t nc = std::max(bytes + bytes / 4, (size_t)1 << 20);
+  e = hipMalloc((void**)&a.base, nc);
+  if (e == hipSuccess) a.cap = nc;
+  return e;
+}
+template <typename T>
+T* arena_take(DevArena& a, size_t bytes) {
+  const size_t b = arena_bytes(bytes);
+  if (!a.base || a.used + b > a.cap) return nullptr;
+  T* p = reinterpret_cast<T*>(a.base + a.used);
+  a.used += b;
+  return p;
+}
+inline void arena_free(DevArena& a) {
+  if (a.base) (void)hipFree(a.base);
+  a = DevArena{};
+}
+
 // One large cloud on the whole device (rocprim stable radix sort); *d_nout gets the voxel count.
 constexpr int64_t kVgLargeMin = 32768;  // below this the one-workgroup kernel is faster
-int voxel_grid_large(hipStream_t s, const float4* in, int64_t n, float leaf, int morton, float4* out, int32_t* d_nout);
+int voxel_grid_large(hipStream_t s, DevArena& ar, const float4* in, int64_t n, float leaf, int morton, float4* out,
+                     int32_t* d_nout);
 
 // Per-ring surf filter reading the projected cloud + label mask directly (no candidate copy).
 struct VgRing {
@@ -166,8 +206,8 @@ struct DevGrid {
 constexpr int64_t kDenseGridCells = (int64_t)1 << 26;
 void free_grid(DevGrid& d);
 // Build `out` over n points (device, map-index order) with cells of 1/invx (x) and 1/inv (y, z).
-int grid_build_device(hipStream_t s, const float4* pts, int64_t n, float invx, float inv, bool force_sparse,
-                      DevGrid& out);
+int grid_build_device(hipStream_t s, DevArena& ar, const float4* pts, int64_t n, float invx, float inv,
+                      bool force_sparse, DevGrid& out);
 
 struct GnArgs {
   int B, max_iter;

@@ -158,8 +158,8 @@ bool force_sparse_env() {
 }
 }  // namespace
 
-int grid_build_device(hipStream_t s, const float4* src, int64_t n, float invx, float inv, bool force_sparse,
-                      DevGrid& out) {
+int grid_build_device(hipStream_t s, DevArena& ar, const float4* src, int64_t n, float invx, float inv,
+                      bool force_sparse, DevGrid& out) {
   free_grid(out);
   if (n > (int64_t)INT32_MAX / 2) return FBR_ERR_CAPACITY;
   int rc = FBR_OK;
@@ -168,16 +168,16 @@ int grid_build_device(hipStream_t s, const float4* src, int64_t n, float invx, f
     return rc == FBR_OK;
   };
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 2048));
-  int* d_bounds = nullptr;
+  // cell bounds (min x, y, z, max x, y, z), read back once
   int b[6] = {0, 0, 0, 0, 0, 0};
-  const int init[6] = {INT_MAX, INT_MAX, INT_MAX, INT_MIN, INT_MIN, INT_MIN};
-  if (!ok(hipMallocAsync((void**)&d_bounds, sizeof(init), s)) ||
-      !ok(hipMemcpyAsync(d_bounds, init, sizeof(init), hipMemcpyHostToDevice, s)))
+  if (!ok(arena_reserve(ar, arena_bytes(sizeof(b)), s))) return rc;
+  int* d_bounds = arena_take<int>(ar, sizeof(b));
+  if (!ok(hipMemsetD32Async((hipDeviceptr_t)d_bounds, (unsigned)INT_MAX, 3, s)) ||
+      !ok(hipMemsetD32Async((hipDeviceptr_t)(d_bounds + 3), (unsigned)INT_MIN, 3, s)))
     return rc;
   if (n > 0) fbr_launch(k_grid_bounds, dim3(grid), dim3(256), 0, s, src, n, invx, inv, d_bounds);
   ok(hipMemcpyAsync(b, d_bounds, sizeof(b), hipMemcpyDeviceToHost, s));
   ok(hipStreamSynchronize(s));
-  (void)hipFree(d_bounds);
   if (rc) return rc;
   if (n == 0)
     for (int d = 0; d < 6; ++d) b[d] = 0;
@@ -200,41 +200,46 @@ int grid_build_device(hipStream_t s, const float4* src, int64_t n, float invx, f
     g.sparse = 0;
     g.hmask = 0;
     g.n_cells = (int32_t)ncell;
-    int32_t* cnt = nullptr;
-    void* tmp = nullptr;
     size_t tb = 0;
-    if (ok(hipMalloc((void**)&out.cs, sizeof(int32_t) * (ncell + 1))) &&
-        ok(hipMallocAsync((void**)&cnt, sizeof(int32_t) * (ncell + 1), s)) &&
-        ok(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (ncell + 1), s))) {
-      if (n > 0) fbr_launch(k_grid_count, dim3(grid), dim3(256), 0, s, src, n, g, cnt);
-      // cell_start = exclusive scan of the counts (ncell + 1 entries: the last is n)
-      if (ok(rocprim::exclusive_scan(nullptr, tb, cnt, out.cs, 0, (size_t)(ncell + 1), rocprim::plus<int32_t>(), s)) &&
-          ok(hipMallocAsync(&tmp, std::max<size_t>(tb, 16), s)) &&
-          ok(rocprim::exclusive_scan(tmp, tb, cnt, out.cs, 0, (size_t)(ncell + 1), rocprim::plus<int32_t>(), s)) &&
-          ok(hipMemcpyAsync(cnt, out.cs, sizeof(int32_t) * ncell, hipMemcpyDeviceToDevice, s)) && n > 0)
-        fbr_launch(k_grid_scatter, dim3(grid), dim3(256), 0, s, src, n, g, cnt, out.pts);
+    int32_t* null32 = nullptr;
+    if (ok(rocprim::exclusive_scan(nullptr, tb, null32, null32, 0, (size_t)(ncell + 1), rocprim::plus<int32_t>(), s)) &&
+        ok(arena_reserve(ar, arena_bytes(sizeof(int32_t) * (ncell + 1)) + arena_bytes(tb), s)) &&
+        ok(hipMalloc((void**)&out.cs, sizeof(int32_t) * (ncell + 1)))) {
+      int32_t* cnt = arena_take<int32_t>(ar, sizeof(int32_t) * (ncell + 1));
+      void* tmp = arena_take<void>(ar, tb);
+      if (ok(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (ncell + 1), s))) {
+        if (n > 0) fbr_launch(k_grid_count, dim3(grid), dim3(256), 0, s, src, n, g, cnt);
+        // cell_start = exclusive scan of the counts (ncell + 1 entries: the last is n)
+        if (ok(rocprim::exclusive_scan(tmp, tb, cnt, out.cs, 0, (size_t)(ncell + 1), rocprim::plus<int32_t>(), s)) &&
+            ok(hipMemcpyAsync(cnt, out.cs, sizeof(int32_t) * ncell, hipMemcpyDeviceToDevice, s)) && n > 0)
+          fbr_launch(k_grid_scatter, dim3(grid), dim3(256), 0, s, src, n, g, cnt, out.pts);
+      }
     }
-    if (tmp) (void)hipFreeAsync(tmp, s);
-    if (cnt) (void)hipFreeAsync(cnt, s);
     ok(hipStreamSynchronize(s));
     return rc;
   }
   // ---- sparse ----
   g.sparse = 1;
-  unsigned long long *k0 = nullptr, *k1 = nullptr, *ckey = nullptr;
-  uint32_t *v0 = nullptr, *v1 = nullptr, *head = nullptr, *cid = nullptr;
-  void* tmp = nullptr;
-  size_t tb_sort = 0, tb_scan = 0;
   const size_t N = (size_t)std::max<int64_t>(n, 1);
+  size_t tb_sort = 0, tb_scan = 0;
+  unsigned long long* null64 = nullptr;
+  uint32_t* nullu = nullptr;
+  if (!ok(rocprim::radix_sort_pairs(nullptr, tb_sort, null64, null64, nullu, nullu, N, 0, 64, s)) ||
+      !ok(rocprim::exclusive_scan(nullptr, tb_scan, nullu, nullu, 0u, N, rocprim::plus<uint32_t>(), s)) ||
+      !ok(arena_reserve(ar, 3 * arena_bytes(8 * N) + 4 * arena_bytes(4 * N) + arena_bytes(std::max(tb_sort, tb_scan)), s)))
+    return rc;
+  unsigned long long* k0 = arena_take<unsigned long long>(ar, 8 * N);
+  unsigned long long* k1 = arena_take<unsigned long long>(ar, 8 * N);
+  unsigned long long* ckey = arena_take<unsigned long long>(ar, 8 * N);  // nchunks <= n
+  uint32_t* v0 = arena_take<uint32_t>(ar, 4 * N);
+  uint32_t* v1 = arena_take<uint32_t>(ar, 4 * N);
+  uint32_t* head = arena_take<uint32_t>(ar, 4 * N);
+  uint32_t* cid = arena_take<uint32_t>(ar, 4 * N);
+  void* tmp = arena_take<void>(ar, std::max(tb_sort, tb_scan));
   uint32_t nchunks = 0;
-  if (ok(hipMallocAsync((void**)&k0, 8 * N, s)) && ok(hipMallocAsync((void**)&k1, 8 * N, s)) &&
-      ok(hipMallocAsync((void**)&v0, 4 * N, s)) && ok(hipMallocAsync((void**)&v1, 4 * N, s)) &&
-      ok(hipMallocAsync((void**)&head, 4 * N, s)) && ok(hipMallocAsync((void**)&cid, 4 * N, s)) && n > 0) {
+  if (n > 0) {
     fbr_launch(k_chunk_keys, dim3(grid), dim3(256), 0, s, src, n, g, k0, v0);
-    if (ok(rocprim::radix_sort_pairs(nullptr, tb_sort, k0, k1, v0, v1, (size_t)n, 0, 64, s)) &&
-        ok(rocprim::exclusive_scan(nullptr, tb_scan, head, cid, 0u, (size_t)n, rocprim::plus<uint32_t>(), s)) &&
-        ok(hipMallocAsync(&tmp, std::max<size_t>(std::max(tb_sort, tb_scan), 16), s)) &&
-        ok(rocprim::radix_sort_pairs(tmp, tb_sort, k0, k1, v0, v1, (size_t)n, 0, 64, s))) {
+    if (ok(rocprim::radix_sort_pairs(tmp, tb_sort, k0, k1, v0, v1, (size_t)n, 0, 64, s))) {
       fbr_launch(k_chunk_scatter, dim3(grid), dim3(256), 0, s, src, n, k1, v1, out.pts, head);
       uint32_t last[2] = {0, 0};
       if (ok(rocprim::exclusive_scan(tmp, tb_scan, head, cid, 0u, (size_t)n, rocprim::plus<uint32_t>(), s)) &&
@@ -250,7 +255,6 @@ int grid_build_device(hipStream_t s, const float4* src, int64_t n, float invx, f
   if (!rc && ok(hipMalloc((void**)&out.cs, sizeof(int32_t) * (kChunkX + 1) * std::max<uint32_t>(nchunks, 1))) &&
       ok(hipMalloc((void**)&out.hkeys, sizeof(unsigned long long) * hsize)) &&
       ok(hipMalloc((void**)&out.hvals, sizeof(int32_t) * hsize)) &&
-      ok(hipMallocAsync((void**)&ckey, sizeof(unsigned long long) * std::max<uint32_t>(nchunks, 1), s)) &&
       ok(hipMemsetAsync(out.cs, 0xFF, sizeof(int32_t) * (kChunkX + 1) * std::max<uint32_t>(nchunks, 1), s)) &&
       ok(hipMemsetAsync(out.hkeys, 0xFF, sizeof(unsigned long long) * hsize, s)) && nchunks > 0) {
     fbr_launch(k_chunk_cells, dim3(grid), dim3(256), 0, s, n, k1, cid, head, out.cs, ckey);
@@ -258,8 +262,6 @@ int grid_build_device(hipStream_t s, const float4* src, int64_t n, float invx, f
     fbr_launch(k_chunk_finish, dim3(cg), dim3(256), 0, s, (int64_t)nchunks, out.cs, ckey, out.hkeys, out.hvals,
                g.hmask);
   }
-  for (void* p : {(void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)head, (void*)cid, (void*)ckey, tmp})
-    if (p) (void)hipFreeAsync(p, s);
   ok(hipStreamSynchronize(s));
   return rc;
 }

@@ -118,23 +118,41 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
   }
 }
 
-// One wave per (job,row): number of claimed cells in the row (and, for deskew, its minimum owner).
+// Compaction tiles (k_compact): HB = min(H, 64) rows x CG columns, HB * CG <= 2048 cells, CG a
+// power of two in [32, 256].
+__host__ __device__ inline int compact_hb(int H) { return H < 64 ? H : 64; }
+__host__ __device__ inline int compact_cg(int H) {
+  int cg = 32;
+  while (cg < 256 && 2 * cg * compact_hb(H) <= 2048) cg *= 2;
+  return cg;
+}
+__host__ __device__ inline int compact_nchunk(int H, int W) { return (W + compact_cg(H) - 1) / compact_cg(H); }
+
+// One wave per (job, row): number of claimed cells in the row, the claimed cells of the row before
+// each CG-column chunk (choff [job][row][chunk]), and, for deskew, the row's minimum owner.
 __global__ void k_rowcount(const int32_t* __restrict__ owner, int H, int W, int32_t* __restrict__ rowcnt,
-                           int32_t* __restrict__ rowmin) {
+                           int32_t* __restrict__ rowmin, int32_t* __restrict__ choff) {
   const int row = blockIdx.x, job = blockIdx.y, lane = threadIdx.x;
   const int32_t* O = owner + ((int64_t)job * H + row) * W;
-  int cnt = 0, mn = kEmptyOwner;
-  for (int c = lane; c < W; c += 64) {
-    const int32_t o = O[c];
-    cnt += (o != kEmptyOwner);
+  const int cg = compact_cg(H), nch = compact_nchunk(H, W);
+  int32_t* CH = choff + ((int64_t)job * H + row) * nch;
+  int run = 0, mn = kEmptyOwner;
+  for (int c0 = 0; c0 < W; c0 += 64) {
+    const int c = c0 + lane;
+    const int32_t o = c < W ? O[c] : kEmptyOwner;
     mn = min(mn, o);
+    const uint64_t m = __ballot(o != kEmptyOwner);
+    // chunk starts inside this 64-column step (cg is a multiple of 32)
+    if (lane == 0) {
+      if (c0 % cg == 0) CH[c0 / cg] = run;
+      if ((c0 + 32) % cg == 0 && c0 + 32 < W) CH[(c0 + 32) / cg] = run + __popcll(m & 0xFFFFFFFFull);
+    }
+    run += __popcll(m);
   }
-  for (int off = 32; off > 0; off >>= 1) {
-    cnt += __shfl_xor(cnt, off);
-    if (rowmin) mn = min(mn, __shfl_xor(mn, off));
-  }
+  if (rowmin)
+    for (int off = 32; off > 0; off >>= 1) mn = min(mn, __shfl_xor(mn, off));
   if (lane == 0) {
-    rowcnt[job * H + row] = cnt;
+    rowcnt[job * H + row] = run;
     if (rowmin) rowmin[job * H + row] = mn;
   }
 }
@@ -152,35 +170,74 @@ __device__ __forceinline__ float4 deskew_point(const fbr_point_xyzirt& q, const 
   return make_float4(o[0], o[1], o[2], q.intensity);
 }
 
-// Blocks are dealt round-robin over the 8 XCDs (b, b+8, ... share one); the (job, row) mapping
-// keeps every row of a job on one XCD so the owner gathers of the job's raw points hit that
-// XCD's L2 (speed only: correctness never depends on placement).
+// One workgroup per (job, HB-row block, CG-column chunk) tile.  The owner tile is read row by row
+// (coalesced), the owning raw points are gathered column by column (in the sensor's firing order
+// consecutive rings of one column are consecutive raw points, so a wave's gather is one contiguous
+// span instead of 64 lines 1.5 KB apart), staged in LDS, and written out row by row at
+// rowoff + choff + rank: ring-major (ring, column) order as cloudExtraction (:642-670).  Tiles of
+// a job are dealt to one XCD (b % 8), so its raw points stay in that XCD's L2 (speed only).
 template <bool kDesk>
-__global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, const int32_t* __restrict__ owner,
-                          const int32_t* __restrict__ rowcnt, int B, int H, int W, float4* __restrict__ cloud,
-                          int32_t* __restrict__ col, float* __restrict__ range, int32_t* __restrict__ start_ring,
-                          int32_t* __restrict__ end_ring, int32_t* __restrict__ nvalid, DeskArgs desk) {
-  const int b = blockIdx.x, lane = threadIdx.x;
-  const int g = b / (8 * H), x = b % 8;  // job group of 8, XCD slot
-  const int job = g * 8 + x, row = (b / 8) % H;
+__global__ void __launch_bounds__(256)
+k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, const int32_t* __restrict__ owner,
+          const int32_t* __restrict__ rowcnt, const int32_t* __restrict__ choff, int B, int H, int W,
+          float4* __restrict__ cloud, int32_t* __restrict__ col, float* __restrict__ range,
+          int32_t* __restrict__ start_ring, int32_t* __restrict__ end_ring, int32_t* __restrict__ nvalid,
+          DeskArgs desk) {
+  __shared__ int32_t own[2048];     // [HB][CG] owners of the tile
+  __shared__ float4 pxyz[2048];     // [HB][CG] gathered xyzi
+  __shared__ float prng[2048];      // [HB][CG] range
+  __shared__ int32_t rowoff[64];    // output offset of each tile row before this chunk
+  __shared__ int32_t scan[256];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int HB = compact_hb(H), CG = compact_cg(H), nch = compact_nchunk(H, W);
+  const int nrb = (H + HB - 1) / HB;
+  const int tiles = nrb * nch;  // tiles per job
+  // XCD-aware deal: job groups of 8, tile t of job (g*8 + x) at block (g*tiles + t)*8 + x
+  const int b = blockIdx.x, x = b % 8, rest = b / 8, g = rest / tiles, t = rest % tiles;
+  const int job = g * 8 + x;
   if (job >= B) return;
+  const int rb = t / nch, ch = t % nch;
+  const int r0 = rb * HB, c0 = ch * CG;
+  const int nr = min(HB, H - r0), ncl = min(CG, W - c0);
   const int64_t HW = (int64_t)H * W;
   const int32_t* RC = rowcnt + job * H;
-  int off = 0;
-  for (int r = lane; r < row; r += 64) off += RC[r];
-  for (int s = 32; s > 0; s >>= 1) off += __shfl_xor(off, s);
-  const int cnt = RC[row];
-  if (lane == 0) {
-    start_ring[job * H + row] = off - 1 + 5;        // imageProjection.cpp:650
-    end_ring[job * H + row] = off + cnt - 1 - 5;    // :668
-    if (row == H - 1) nvalid[job] = off + cnt;
+  // prefix of the row counts: rows before r0 (block reduction), then the tile rows
+  int before = 0;
+  for (int r = tid; r < r0; r += 256) before += RC[r];
+  scan[tid] = before;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) scan[tid] += scan[tid + s];
+    __syncthreads();
   }
-  const int32_t* O = owner + job * HW + (int64_t)row * W;
-  const fbr_point_xyzirt* P = pts + (int64_t)job * nmax;
-  float4* C = cloud + job * HW;
-  int32_t* CI = col + job * HW;
-  float* R = range + job * HW;
+  const int base = scan[0];
+  if (tid < 64) {
+    // inclusive prefix of the tile rows' counts (lane r of wave 0), plus this chunk's offset
+    int v = tid < nr ? RC[r0 + tid] : 0;
+    int inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(inc, o);
+      if (lane >= o) inc += y;
+    }
+    if (tid < nr) {
+      const int roff = base + inc - v;
+      rowoff[tid] = roff + choff[((int64_t)job * H + r0 + tid) * nch + ch];
+      if (ch == 0) {
+        start_ring[job * H + r0 + tid] = roff - 1 + 5;   // imageProjection.cpp:650
+        end_ring[job * H + r0 + tid] = roff + v - 1 - 5;  // :668
+        if (r0 + tid == H - 1) nvalid[job] = roff + v;
+      }
+    }
+  }
+  // owners, row by row (coalesced)
+  const int32_t* O = owner + job * HW;
+  for (int i = tid; i < HB * CG; i += 256) {
+    const int r = i / CG, c = i % CG;
+    own[i] = (r < nr && c < ncl) ? O[(int64_t)(r0 + r) * W + c0 + c] : kEmptyOwner;
+  }
+  __syncthreads();
   // deskew: transStartInverse from the scan's first deskewed point (the minimum owner)
+  const fbr_point_xyzirt* P = pts + (int64_t)job * nmax;
   const bool dsk = kDesk && (desk.mode[job] & kDeskPoints);
   const fbr_deskew_table* DT = dsk ? desk.table + job : nullptr;
   Rot3 Ls;
@@ -193,34 +250,50 @@ __global__ void k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax
     if (mn != kEmptyOwner) find_rotation(*DT, DT->time_scan_cur + (double)P[mn].time, &rx, &ry, &rz);
     affine_inverse(rot_rpy(rx, ry, rz), Ls, ts);
   }
-  int base = off;
-  // kCC 64-column chunks per step: all their owner loads, then all their point gathers, are in
-  // flight together (the gather depends on the owner load)
-  constexpr int kCC = 4;
-  for (int c0 = 0; c0 < W; c0 += 64 * kCC) {
-    int32_t ow[kCC];
-    uint64_t mk[kCC];
-    fbr_point_xyzirt q[kCC];
-#pragma unroll
-    for (int k = 0; k < kCC; ++k) {
-      const int cc = c0 + 64 * k + lane;
-      ow[k] = cc < W ? O[cc] : kEmptyOwner;
+  // gather, column by column (consecutive threads = consecutive rings of one column)
+  for (int i = tid; i < HB * CG; i += 256) {
+    const int c = i / HB, r = i % HB, k = r * CG + c;
+    const int32_t o = own[k];
+    if (o != kEmptyOwner) {
+      const fbr_point_xyzirt q = P[o];
+      pxyz[k] = dsk ? deskew_point(q, *DT, Ls, ts) : make_float4(q.x, q.y, q.z, q.intensity);
+      prng[k] = sqrt_rn(q.x * q.x + q.y * q.y + q.z * q.z);
     }
-#pragma unroll
-    for (int k = 0; k < kCC; ++k) {
-      mk[k] = __ballot(ow[k] != kEmptyOwner);
-      if (ow[k] != kEmptyOwner) q[k] = P[ow[k]];
+  }
+  __syncthreads();
+  // write out row by row: rank of each claimed cell among the row's claimed cells of the tile
+  float4* C = cloud + job * HW;
+  int32_t* CI = col + job * HW;
+  float* R = range + job * HW;
+  const int rpp = 256 / CG;                          // rows per pass, CG threads per row
+  const int passes = (nr + rpp - 1) / rpp;             // the same for every thread (barriers below)
+  for (int p = 0; p < passes; ++p) {
+    const int r = p * rpp + tid / CG;
+    int rank = 0;
+    const int c = tid % CG;
+    const int k = r * CG + c;
+    const bool v = r < nr && own[k] != kEmptyOwner;
+    // prefix over the CG cells of the row: ballots over the wave's 64 lanes (CG = 32: two rows per
+    // wave; CG >= 64: a row spans CG / 64 waves, combined through LDS)
+    const uint64_t m = __ballot(v);
+    if (CG <= 32) {
+      const int sh = lane & ~31;  // the row's half of the wave
+      const uint64_t mm = (m >> sh) & 0xFFFFFFFFull;
+      rank = __popcll(mm & ((1ull << (lane & 31)) - 1ull));
+    } else {
+      const int wv = tid >> 6, wrow = (tid % CG) >> 6;  // wave index inside the row
+      scan[wv] = __popcll(m);
+      __syncthreads();
+      int prev = 0;
+      for (int q = 0; q < wrow; ++q) prev += scan[wv - wrow + q];
+      rank = prev + __popcll(m & ((1ull << lane) - 1ull));
+      __syncthreads();
     }
-#pragma unroll
-    for (int k = 0; k < kCC; ++k) {
-      if (ow[k] != kEmptyOwner) {
-        const int dst = base + __popcll(mk[k] & ((1ull << lane) - 1ull));
-        const fbr_point_xyzirt& qq = q[k];
-        C[dst] = dsk ? deskew_point(qq, *DT, Ls, ts) : make_float4(qq.x, qq.y, qq.z, qq.intensity);
-        CI[dst] = c0 + 64 * k + lane;
-        R[dst] = sqrt_rn(qq.x * qq.x + qq.y * qq.y + qq.z * qq.z);
-      }
-      base += __popcll(mk[k]);
+    if (v) {
+      const int dst = rowoff[r] + rank;
+      C[dst] = pxyz[k];
+      CI[dst] = c0 + c;
+      R[dst] = prng[k];
     }
   }
 }
@@ -284,16 +357,18 @@ void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* n
 }
 
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,
-                    int W, int32_t* rowcnt, float4* cloud, int32_t* col, float* range, int32_t* start_ring,
-                    int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk) {
-  fbr_launch(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, rowcnt, desk.mode ? desk.rowmin : nullptr);
+                    int W, int32_t* rowcnt, int32_t* choff, float4* cloud, int32_t* col, float* range,
+                    int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk) {
+  fbr_launch(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, rowcnt, desk.mode ? desk.rowmin : nullptr, choff);
+  const int tiles = ((H + compact_hb(H) - 1) / compact_hb(H)) * compact_nchunk(H, W);
   const int groups = (B + 7) / 8;
+  const dim3 grid((unsigned)(groups * 8 * tiles));
   if (desk.mode)
-    fbr_launch(k_compact<true>, dim3(groups * 8 * H), dim3(64), 0, s, pts, nmax, owner, rowcnt, B, H, W, cloud,
-                       col, range, start_ring, end_ring, nvalid, desk);
+    fbr_launch(k_compact<true>, grid, dim3(256), 0, s, pts, nmax, owner, rowcnt, choff, B, H, W, cloud, col, range,
+               start_ring, end_ring, nvalid, desk);
   else
-    fbr_launch(k_compact<false>, dim3(groups * 8 * H), dim3(64), 0, s, pts, nmax, owner, rowcnt, B, H, W, cloud,
-                       col, range, start_ring, end_ring, nvalid, desk);
+    fbr_launch(k_compact<false>, grid, dim3(256), 0, s, pts, nmax, owner, rowcnt, choff, B, H, W, cloud, col, range,
+               start_ring, end_ring, nvalid, desk);
 }
 
 }  // namespace fbr

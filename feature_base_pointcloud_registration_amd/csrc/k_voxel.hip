@@ -972,40 +972,47 @@ k_vgl_emit(const float4* __restrict__ in, int64_t n, const VglState* __restrict_
   }
 }
 
-int voxel_grid_large(hipStream_t s, const float4* in, int64_t n, float leaf, int morton, float4* out, int32_t* d_nout) {
+int voxel_grid_large(hipStream_t s, DevArena& ar, const float4* in, int64_t n, float leaf, int morton, float4* out,
+                     int32_t* d_nout) {
   if (n <= 0) return hipMemsetAsync(d_nout, 0, sizeof(int32_t), s) == hipSuccess ? FBR_OK : FBR_ERR_HIP;
   if (n > (int64_t)INT32_MAX) return FBR_ERR_CAPACITY;
-  uint32_t *mm = nullptr, *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *vox = nullptr;
-  VglState* st = nullptr;
-  void* tmp = nullptr;
+  const size_t N = (size_t)n;
   size_t tb_sort = 0, tb_scan = 0;
+  uint32_t* null32 = nullptr;
+  if (rocprim::radix_sort_pairs(nullptr, tb_sort, null32, null32, null32, null32, N, 0, 32, s) != hipSuccess ||
+      rocprim::exclusive_scan(nullptr, tb_scan, null32, null32, 0u, N, rocprim::plus<uint32_t>(), s) != hipSuccess)
+    return FBR_ERR_HIP;
+  const size_t tb = std::max<size_t>(std::max(tb_sort, tb_scan), 16);
+  if (arena_reserve(ar, arena_bytes(6 * sizeof(uint32_t)) + arena_bytes(sizeof(VglState)) + 6 * arena_bytes(4 * N) +
+                            arena_bytes(tb), s) != hipSuccess)
+    return FBR_ERR_HIP;
+  uint32_t* mm = arena_take<uint32_t>(ar, 6 * sizeof(uint32_t));
+  VglState* st = arena_take<VglState>(ar, sizeof(VglState));
+  uint32_t* k0 = arena_take<uint32_t>(ar, 4 * N);
+  uint32_t* k1 = arena_take<uint32_t>(ar, 4 * N);
+  uint32_t* v0 = arena_take<uint32_t>(ar, 4 * N);
+  uint32_t* v1 = arena_take<uint32_t>(ar, 4 * N);
+  uint32_t* head = arena_take<uint32_t>(ar, 4 * N);
+  uint32_t* vox = arena_take<uint32_t>(ar, 4 * N);
+  void* tmp = arena_take<void>(ar, tb);
   int rc = FBR_OK;
   auto ok = [&](hipError_t e) {
     if (e != hipSuccess) rc = FBR_ERR_HIP;
     return rc == FBR_OK;
   };
-  const size_t N = (size_t)n;
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
-  const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
-  if (ok(hipMallocAsync((void**)&mm, sizeof(init), s)) && ok(hipMallocAsync((void**)&st, sizeof(VglState), s)) &&
-      ok(hipMallocAsync((void**)&k0, 4 * N, s)) && ok(hipMallocAsync((void**)&k1, 4 * N, s)) &&
-      ok(hipMallocAsync((void**)&v0, 4 * N, s)) && ok(hipMallocAsync((void**)&v1, 4 * N, s)) &&
-      ok(hipMallocAsync((void**)&vox, 4 * N, s)) &&
-      ok(hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, s))) {
+  // min / max accumulators: ordered-uint encodings of +inf-like (all ones) and -inf-like (0)
+  if (ok(hipMemsetD32Async((hipDeviceptr_t)mm, 0xFFFFFFFFu, 3, s)) && ok(hipMemsetD32Async((hipDeviceptr_t)(mm + 3), 0u, 3, s))) {
     fbr_launch(k_vgl_minmax, dim3(grid), dim3(256), 0, s, in, n, mm);
     fbr_launch(k_vgl_grid, dim3(1), dim3(1), 0, s, mm, leaf, morton, st);
     fbr_launch(k_vgl_keys, dim3(grid), dim3(256), 0, s, in, n, st, k0, v0);
-    if (ok(rocprim::radix_sort_pairs(nullptr, tb_sort, k0, k1, v0, v1, N, 0, 32, s)) &&
-        ok(rocprim::exclusive_scan(nullptr, tb_scan, vox, vox, 0u, N, rocprim::plus<uint32_t>(), s)) &&
-        ok(hipMallocAsync(&tmp, std::max<size_t>(std::max(tb_sort, tb_scan), 16), s)) &&
-        ok(rocprim::radix_sort_pairs(tmp, tb_sort, k0, k1, v0, v1, N, 0, 32, s))) {
-      fbr_launch(k_vgl_heads, dim3(grid), dim3(256), 0, s, k1, n, vox);
-      if (ok(rocprim::exclusive_scan(tmp, tb_scan, vox, vox, 0u, N, rocprim::plus<uint32_t>(), s)))
+    if (ok(rocprim::radix_sort_pairs(tmp, tb_sort, k0, k1, v0, v1, N, 0, 32, s))) {
+      fbr_launch(k_vgl_heads, dim3(grid), dim3(256), 0, s, k1, n, head);
+      // head flags -> voxel index (out of place)
+      if (ok(rocprim::exclusive_scan(tmp, tb_scan, head, vox, 0u, N, rocprim::plus<uint32_t>(), s)))
         fbr_launch(k_vgl_emit, dim3(grid), dim3(256), 0, s, in, n, st, k1, v1, vox, out, d_nout);
     }
   }
-  for (void* p : {(void*)mm, (void*)st, (void*)k0, (void*)k1, (void*)v0, (void*)v1, (void*)vox, tmp})
-    if (p) (void)hipFreeAsync(p, s);
   return rc;
 }
 
