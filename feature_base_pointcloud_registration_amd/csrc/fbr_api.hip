@@ -627,7 +627,10 @@ int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool
                       c->d_cropcnt, c->d_err, c->d_result);
   CK(hipMemcpyAsync(c->h_result, c->d_result, sizeof(JobResult) * B, hipMemcpyDeviceToHost, c->stream));
   CK(fbr_sync(c->stream));
-  int rc = FBR_OK;
+  // A capacity error in any job (features truncated) fails the call before anything is written:
+  // poses_inout keeps the caller's guesses, as the reference leaves the pose on a failed scan.
+  for (int j = 0; j < B; ++j)
+    if (c->h_result[j].err) return FBR_ERR_UNSUPPORTED;
   if (with_reg) {
     c->last_iters.resize(B);
     c->last_q.resize(B);
@@ -636,7 +639,6 @@ int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool
   }
   for (int j = 0; j < B; ++j) {
     const JobResult& r = c->h_result[j];
-    if (r.err) rc = FBR_ERR_UNSUPPORTED;
     if (with_reg) {
       c->last_iters[j] = r.st.iterations;
       c->last_q[j] = r.st.n_corner_ds + r.st.n_surf_ds;
@@ -647,7 +649,7 @@ int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool
     if (poses_out && with_reg)
       for (int k = 0; k < 6; ++k) poses_out[6 * j + k] = r.pose[k];
   }
-  return rc;
+  return FBR_OK;
 }
 
 int copy_stats(fbr_ctx* c, int B, fbr_reg_stats* stats) { return copy_results(c, B, stats, nullptr, true); }
@@ -1774,7 +1776,10 @@ int fbr_extract_surrounding_keyframes(fbr_ctx* c, double stamp, const fbr_keyfra
   if (c->d_kds_c) CK(hipFree(c->d_kds_c));
   if (c->d_kds_s) CK(hipFree(c->d_kds_s));
   c->d_kds_c = c->d_kds_s = nullptr;
-  if (dalloc(&c->d_kds_c, std::max<int64_t>(tot_c, 1)) || dalloc(&c->d_kds_s, std::max<int64_t>(tot_s, 1))) return FBR_ERR_HIP;
+  if (dalloc(&c->d_kds_c, std::max<int64_t>(tot_c, 1)) || dalloc(&c->d_kds_s, std::max<int64_t>(tot_s, 1))) {
+    (void)fbr_sync(c->stream);  // the pageable copy of `segs` must finish before it goes out of scope
+    return FBR_ERR_HIP;
+  }
   // downSizeFilterCorner / downSizeFilterSurf (:946-954)
   rc = voxel_grid_dev(c, c->d_kraw_c, tot_c, c->P.mapping_corner_leaf_size, c->d_kds_c, &c->kds_c_n);
   if (!rc) rc = voxel_grid_dev(c, c->d_kraw_s, tot_s, c->P.mapping_surf_leaf_size, c->d_kds_s, &c->kds_s_n);

@@ -172,6 +172,7 @@ int grid_build_device(hipStream_t s, DevArena& ar, const float4* src, int64_t n,
   int b[6] = {0, 0, 0, 0, 0, 0};
   if (!ok(arena_reserve(ar, arena_bytes(sizeof(b)), s))) return rc;
   int* d_bounds = arena_take<int>(ar, sizeof(b));
+  if (!d_bounds) return FBR_ERR_HIP;
   if (!ok(hipMemsetD32Async((hipDeviceptr_t)d_bounds, (unsigned)INT_MAX, 3, s)) ||
       !ok(hipMemsetD32Async((hipDeviceptr_t)(d_bounds + 3), (unsigned)INT_MIN, 3, s)))
     return rc;
@@ -188,7 +189,11 @@ int grid_build_device(hipStream_t s, DevArena& ar, const float4* src, int64_t n,
   g.inv_x = invx;
   for (int d = 0; d < 3; ++d) g.origin[d] = (float)b[d];
   g.n_points = n;
-  const bool sparse = force_sparse || force_sparse_env() || dims[0] * dims[1] * dims[2] > kDenseGridCells;
+  // dense only when the box has at most kDenseGridCells cells; each factor is checked before the
+  // product so that far outliers on every axis cannot overflow it
+  const bool too_big = dims[0] > kDenseGridCells || dims[1] > kDenseGridCells / dims[0] ||
+                       dims[2] > kDenseGridCells / (dims[0] * dims[1]);
+  const bool sparse = force_sparse || force_sparse_env() || too_big;
   if (sparse && (dims[0] > ((int64_t)1 << 28) || dims[1] > ((int64_t)1 << 24) || dims[2] > ((int64_t)1 << 12)))
     return FBR_ERR_CAPACITY;
   for (int d = 0; d < 3; ++d) g.dims[d] = (int32_t)std::min<int64_t>(dims[d], INT32_MAX);
@@ -207,7 +212,8 @@ int grid_build_device(hipStream_t s, DevArena& ar, const float4* src, int64_t n,
         ok(hipMalloc((void**)&out.cs, sizeof(int32_t) * (ncell + 1)))) {
       int32_t* cnt = arena_take<int32_t>(ar, sizeof(int32_t) * (ncell + 1));
       void* tmp = arena_take<void>(ar, tb);
-      if (ok(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (ncell + 1), s))) {
+      if (!cnt || !tmp) rc = FBR_ERR_HIP;
+      if (!rc && ok(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (ncell + 1), s))) {
         if (n > 0) fbr_launch(k_grid_count, dim3(grid), dim3(256), 0, s, src, n, g, cnt);
         // cell_start = exclusive scan of the counts (ncell + 1 entries: the last is n)
         if (ok(rocprim::exclusive_scan(tmp, tb, cnt, out.cs, 0, (size_t)(ncell + 1), rocprim::plus<int32_t>(), s)) &&
@@ -236,6 +242,7 @@ int grid_build_device(hipStream_t s, DevArena& ar, const float4* src, int64_t n,
   uint32_t* head = arena_take<uint32_t>(ar, 4 * N);
   uint32_t* cid = arena_take<uint32_t>(ar, 4 * N);
   void* tmp = arena_take<void>(ar, std::max(tb_sort, tb_scan));
+  if (!k0 || !k1 || !ckey || !v0 || !v1 || !head || !cid || !tmp) return FBR_ERR_HIP;
   uint32_t nchunks = 0;
   if (n > 0) {
     fbr_launch(k_chunk_keys, dim3(grid), dim3(256), 0, s, src, n, g, k0, v0);

@@ -995,6 +995,7 @@ int voxel_grid_large(hipStream_t s, DevArena& ar, const float4* in, int64_t n, f
   uint32_t* head = arena_take<uint32_t>(ar, 4 * N);
   uint32_t* vox = arena_take<uint32_t>(ar, 4 * N);
   void* tmp = arena_take<void>(ar, tb);
+  if (!mm || !st || !k0 || !k1 || !v0 || !v1 || !head || !vox || !tmp) return FBR_ERR_HIP;  // arena sizing slip
   int rc = FBR_OK;
   auto ok = [&](hipError_t e) {
     if (e != hipSuccess) rc = FBR_ERR_HIP;

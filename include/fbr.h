@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FBR_ABI_VERSION 1
+#define FBR_ABI_VERSION 2  /* 2: fbr_selftest_math writes 6 floats per element (was 4) */
 
 /* ---- status codes ------------------------------------------------------------------------- */
 #define FBR_OK 0
