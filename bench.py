@@ -51,10 +51,21 @@ def kernel_bytes(name, tot):
         "voxel_ring": 17.0 * n + 16.0 * S,       # label + candidate point read, per-ring DS write
         "concat": 32.0 * F,                      # per-ring corner / surf outputs read + job clouds written
         "voxel_scan": 16.0 * F + 16.0 * Q,       # corner + surf clouds read, DS queries written
-        "gn_knn": 116.0 * IQ,                    # query 16 B + the 5 neighbours found 80 B + 5 map indices out 20 B
+        "gn_knn": 96.0 * IQ,                     # query 16 B + the 5 neighbours found 80 B
         "gn_residual": 116.0 * IQ,               # query 16 B + 5 map indices 20 B + 5 neighbour gathers 80 B
     }.get(name, 0.0)
 
+
+BYTE_MODEL = {
+    "project": "24 B per raw point + 4 B owner claim per valid point",
+    "extract": "4 B per range-image cell + 24 B raw-point gather + 24 B written per valid point",
+    "features": "24 B read + 1 B label per valid point + 16 B per corner pick",
+    "voxel_ring": "17 B per valid point + 16 B per per-ring DS point",
+    "concat": "32 B per feature point",
+    "voxel_scan": "16 B per feature point + 16 B per DS query",
+    "gn_knn": "96 B per query-iteration (SURVEY 8d: query 16 B + 5 neighbours 80 B)",
+    "gn_residual": "116 B per query-iteration (query 16 B + 5 indices 20 B + 5 neighbour gathers 80 B)",
+}
 
 # rocprofv3 kernel symbols behind each launcher name (tools/roofline_check.py maps a profile's rows)
 KERNEL_SYMBOLS = {"project": ["k_project"], "extract": ["k_rowcount", "k_compact"], "features": ["k_features"],
@@ -76,7 +87,7 @@ def parse():
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on device 0 (world-size > 1 rehearsal on a one-GPU box)")
     ap.add_argument("--records-out", default=None, help="rank 0 writes the gathered records (.npy)")
-    ap.add_argument("--latency", type=int, default=0,
+    ap.add_argument("--latency", type=int, default=50,
                     help="single-stream line: N pose-chained scans through fbr_process_scan (the reference's "
                          "operating mode, imageProjection.cpp:206-218), rank 0 at N=1; 0 disables")
     ap.add_argument("--ingest", type=int, default=2,
@@ -255,7 +266,7 @@ def main():
     ctx.set_profiling(False)
     prof = {k: ctx.kernel_time(k) for k in kernels}
     modelled = [k for k in kernels if kernel_bytes(k, dict.fromkeys(["n_in", "HW", "n", "C", "S", "F", "Q", "IQ"], 1.0)) > 0]
-    dom = max(modelled, key=lambda k: prof[k][0])  # largest total kernel time per step
+    dom = max(modelled, key=lambda k: prof[k][0])  # provisional (the profiled step); final pick below
     if dist is not None:
         import torch
         torch.cuda.synchronize()
@@ -297,6 +308,8 @@ def main():
     tb, tg = ctx.batch_bytes()
     ktot = {k: ctx.kernel_time(k) for k in kernels}
     timed = {k: (ktot[k][0] - prof[k][0], ktot[k][1] - prof[k][1]) for k in kernels}  # timed region only
+    if args.profile == "all":  # the roofline kernel: largest total kernel time inside the timed region
+        dom = max(modelled, key=lambda k: timed[k][0])
 
     if rank != 0:
         ctx.close()
@@ -386,6 +399,7 @@ def main():
             "timing": ("kernel dispatch start/end timestamps (hipExtLaunchKernel events) over the timed region"
                        if live else "kernel dispatch start/end timestamps, profiled untimed step"),
             "rocprof_symbols": KERNEL_SYMBOLS[dom],
+            "byte_model": BYTE_MODEL[dom],
             "kernels": {k: {kk: v for kk, v in r.items() if kk != "live"} for k, r in kroof.items()},
         },
         "kernel_ms_per_step": {k: round(v[0], 4) for k, v in prof.items()},  # profiled untimed step

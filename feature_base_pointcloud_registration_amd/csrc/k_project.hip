@@ -18,6 +18,9 @@
 //                 in input order that passes every check always wins its cell).
 // Roofline: HBM-bound.  Algorithmic bytes: 24 B per raw point read (K1), 4 B/cell owner
 // write+read, 24 B per valid point written (xyzi 16 + col 4 + range 4).
+#include <algorithm>
+#include <cstdlib>
+
 #include "fbr_common.h"
 #include "fbr_fdlibm.h"
 #include "fbr_imu.h"
@@ -118,23 +121,27 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
   }
 }
 
-// Compaction tiles (k_compact): HB = min(H, 64) rows x CG columns, HB * CG <= 2048 cells, CG a
-// power of two in [32, 256].
-__host__ __device__ inline int compact_hb(int H) { return H < 64 ? H : 64; }
-__host__ __device__ inline int compact_cg(int H) {
-  int cg = 32;
-  while (cg < 256 && 2 * cg * compact_hb(H) <= 2048) cg *= 2;
-  return cg;
+// Compaction tiles (k_compact): HB rows x CG columns, HB * CG <= cells (1024 or 2048, FBR_COMPACT_CELLS),
+// HB <= 64, CG a power of two in [32, 256].  Chosen on the host and passed to both kernels.
+struct CompactTile {
+  int hb, cg;
+};
+inline CompactTile compact_tile(int H, int cells) {
+  CompactTile t;
+  t.hb = std::min(std::min(H, 64), cells / 32);
+  t.cg = 32;
+  while (t.cg < 256 && 2 * t.cg * t.hb <= cells) t.cg *= 2;
+  return t;
 }
-__host__ __device__ inline int compact_nchunk(int H, int W) { return (W + compact_cg(H) - 1) / compact_cg(H); }
+__host__ __device__ inline int compact_nchunk(int cg, int W) { return (W + cg - 1) / cg; }
 
 // One wave per (job, row): number of claimed cells in the row, the claimed cells of the row before
 // each CG-column chunk (choff [job][row][chunk]), and, for deskew, the row's minimum owner.
-__global__ void k_rowcount(const int32_t* __restrict__ owner, int H, int W, int32_t* __restrict__ rowcnt,
+__global__ void k_rowcount(const int32_t* __restrict__ owner, int H, int W, int cg, int32_t* __restrict__ rowcnt,
                            int32_t* __restrict__ rowmin, int32_t* __restrict__ choff) {
   const int row = blockIdx.x, job = blockIdx.y, lane = threadIdx.x;
   const int32_t* O = owner + ((int64_t)job * H + row) * W;
-  const int cg = compact_cg(H), nch = compact_nchunk(H, W);
+  const int nch = compact_nchunk(cg, W);
   int32_t* CH = choff + ((int64_t)job * H + row) * nch;
   int run = 0, mn = kEmptyOwner;
   for (int c0 = 0; c0 < W; c0 += 64) {
@@ -176,20 +183,24 @@ __device__ __forceinline__ float4 deskew_point(const fbr_point_xyzirt& q, const 
 // span instead of 64 lines 1.5 KB apart), staged in LDS, and written out row by row at
 // rowoff + choff + rank: ring-major (ring, column) order as cloudExtraction (:642-670).  Tiles of
 // a job are dealt to one XCD (b % 8), so its raw points stay in that XCD's L2 (speed only).
+// LDS (dynamic): xyzi [HB*CG] float4, owners [HB*CG] int32, and with deskew the raw ranges
+// [HB*CG] float (without deskew the staged point is the raw point and the range is recomputed
+// from it at the write, same expression, same bits): 20 KB per 1024-cell tile.
 template <bool kDesk>
 __global__ void __launch_bounds__(256)
 k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, const int32_t* __restrict__ owner,
-          const int32_t* __restrict__ rowcnt, const int32_t* __restrict__ choff, int B, int H, int W,
+          const int32_t* __restrict__ rowcnt, const int32_t* __restrict__ choff, int B, int H, int W, int HB, int CG,
           float4* __restrict__ cloud, int32_t* __restrict__ col, float* __restrict__ range,
           int32_t* __restrict__ start_ring, int32_t* __restrict__ end_ring, int32_t* __restrict__ nvalid,
           DeskArgs desk) {
-  __shared__ int32_t own[2048];     // [HB][CG] owners of the tile
-  __shared__ float4 pxyz[2048];     // [HB][CG] gathered xyzi
-  __shared__ float prng[2048];      // [HB][CG] range
+  extern __shared__ float4 lds_c[];
+  float4* pxyz = lds_c;                                    // [HB][CG] gathered xyzi
+  int32_t* own = reinterpret_cast<int32_t*>(pxyz + HB * CG);  // [HB][CG] owners of the tile
+  float* prng = reinterpret_cast<float*>(own + HB * CG);   // [HB][CG] range (deskew only)
   __shared__ int32_t rowoff[64];    // output offset of each tile row before this chunk
   __shared__ int32_t scan[256];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int HB = compact_hb(H), CG = compact_cg(H), nch = compact_nchunk(H, W);
+  const int nch = compact_nchunk(CG, W);
   const int nrb = (H + HB - 1) / HB;
   const int tiles = nrb * nch;  // tiles per job
   // XCD-aware deal: job groups of 8, tile t of job (g*8 + x) at block (g*tiles + t)*8 + x
@@ -256,8 +267,12 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, const int32_t*
     const int32_t o = own[k];
     if (o != kEmptyOwner) {
       const fbr_point_xyzirt q = P[o];
-      pxyz[k] = dsk ? deskew_point(q, *DT, Ls, ts) : make_float4(q.x, q.y, q.z, q.intensity);
-      prng[k] = sqrt_rn(q.x * q.x + q.y * q.y + q.z * q.z);
+      if (kDesk) {
+        pxyz[k] = dsk ? deskew_point(q, *DT, Ls, ts) : make_float4(q.x, q.y, q.z, q.intensity);
+        prng[k] = sqrt_rn(q.x * q.x + q.y * q.y + q.z * q.z);
+      } else {
+        pxyz[k] = make_float4(q.x, q.y, q.z, q.intensity);
+      }
     }
   }
   __syncthreads();
@@ -291,9 +306,10 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, const int32_t*
     }
     if (v) {
       const int dst = rowoff[r] + rank;
-      C[dst] = pxyz[k];
+      const float4 p = pxyz[k];
+      C[dst] = p;
       CI[dst] = c0 + c;
-      R[dst] = prng[k];
+      R[dst] = kDesk ? prng[k] : sqrt_rn(p.x * p.x + p.y * p.y + p.z * p.z);
     }
   }
 }
@@ -356,19 +372,32 @@ void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* n
   fbr_launch(k_project, dim3(blocks, B), dim3(kProjThreads), lds, s, pts, nin, nmax, H, W, tile_log2, owner);
 }
 
+// Compaction tile size in cells (FBR_COMPACT_CELLS: 1024 or 2048).
+int compact_cells() {
+  static const int v = [] {
+    const char* e = std::getenv("FBR_COMPACT_CELLS");
+    const int c = e ? std::atoi(e) : 1024;
+    return c >= 2048 ? 2048 : 1024;
+  }();
+  return v;
+}
+
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,
                     int W, int32_t* rowcnt, int32_t* choff, float4* cloud, int32_t* col, float* range,
                     int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk) {
-  fbr_launch(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, rowcnt, desk.mode ? desk.rowmin : nullptr, choff);
-  const int tiles = ((H + compact_hb(H) - 1) / compact_hb(H)) * compact_nchunk(H, W);
+  const CompactTile T = compact_tile(H, compact_cells());
+  fbr_launch(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, T.cg, rowcnt, desk.mode ? desk.rowmin : nullptr,
+             choff);
+  const int tiles = ((H + T.hb - 1) / T.hb) * compact_nchunk(T.cg, W);
   const int groups = (B + 7) / 8;
   const dim3 grid((unsigned)(groups * 8 * tiles));
+  const size_t cells = (size_t)T.hb * T.cg;
   if (desk.mode)
-    fbr_launch(k_compact<true>, grid, dim3(256), 0, s, pts, nmax, owner, rowcnt, choff, B, H, W, cloud, col, range,
-               start_ring, end_ring, nvalid, desk);
+    fbr_launch(k_compact<true>, grid, dim3(256), (uint32_t)(cells * 24), s, pts, nmax, owner, rowcnt, choff, B, H, W,
+               T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk);
   else
-    fbr_launch(k_compact<false>, grid, dim3(256), 0, s, pts, nmax, owner, rowcnt, choff, B, H, W, cloud, col, range,
-               start_ring, end_ring, nvalid, desk);
+    fbr_launch(k_compact<false>, grid, dim3(256), (uint32_t)(cells * 20), s, pts, nmax, owner, rowcnt, choff, B, H,
+               W, T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk);
 }
 
 }  // namespace fbr

@@ -15,24 +15,22 @@ import numpy as np
 import pytest
 
 
-def compact_hb(H):
-    return H if H < 64 else 64
-
-
-def compact_cg(H):
+def compact_tile(H, cells):
+    """k_project.hip compact_tile: (HB, CG) for a tile of at most `cells` cells."""
+    hb = min(H, 64, cells // 32)
     cg = 32
-    while cg < 256 and 2 * cg * compact_hb(H) <= 2048:
+    while cg < 256 and 2 * cg * hb <= cells:
         cg *= 2
-    return cg
+    return hb, cg
 
 
-def compact_nchunk(H, W):
-    return (W + compact_cg(H) - 1) // compact_cg(H)
+def compact_nchunk(cg, W):
+    return (W + cg - 1) // cg
 
 
-def rowcount(claimed, H, W):
+def rowcount(claimed, H, W, cg):
     """k_rowcount for one job: per-row counts and the chunk offsets it writes (-1 = never written)."""
-    cg, nch = compact_cg(H), compact_nchunk(H, W)
+    nch = compact_nchunk(cg, W)
     choff = np.full((H, nch), -1, np.int64)
     cnt = np.zeros(H, np.int64)
     for row in range(H):
@@ -48,15 +46,16 @@ def rowcount(claimed, H, W):
     return cnt, choff
 
 
-def compact_destinations(claimed_jobs, H, W):
+def compact_destinations(claimed_jobs, H, W, cells):
     """k_compact over B jobs: {(job, row, col): dst} for every claimed cell, tiles dealt as launched."""
     B = len(claimed_jobs)
-    HB, CG, nch = compact_hb(H), compact_cg(H), compact_nchunk(H, W)
-    assert HB * CG <= 2048 and CG in (32, 64, 128, 256)
+    HB, CG = compact_tile(H, cells)
+    nch = compact_nchunk(CG, W)
+    assert HB * CG <= cells and CG in (32, 64, 128, 256)
     nrb = (H + HB - 1) // HB
     tiles = nrb * nch
     groups = (B + 7) // 8
-    per_job = [rowcount(cl, H, W) for cl in claimed_jobs]
+    per_job = [rowcount(cl, H, W, CG) for cl in claimed_jobs]
     out = {}
     seen_tiles = set()
     for b in range(groups * 8 * tiles):  # launch_extract's grid
@@ -88,21 +87,24 @@ def compact_destinations(claimed_jobs, H, W):
                                  (32, 1024), (40, 77), (48, 2048), (64, 1800), (65, 200), (100, 96), (128, 2048),
                                  (129, 64), (16, 4096)])
 @pytest.mark.parametrize("density", [0.0, 0.3, 1.0])
-def test_compaction_index_model(H, W, density):
+@pytest.mark.parametrize("cells", [1024, 2048])
+def test_compaction_index_model(H, W, density, cells):
     rng = np.random.default_rng(H * 10007 + W)
     B = 3 if H * W <= 4096 else 2  # job groups of 8 with a partial last group
     if H * W * B > 300_000:
         B = 1
     jobs = [rng.random((H, W)) < density for _ in range(B)]
-    dst = compact_destinations(jobs, H, W)
+    dst = compact_destinations(jobs, H, W, cells)
     for j, cl in enumerate(jobs):
         rows, cols = np.nonzero(cl)  # row-major order = cloudExtraction's order
         got = np.array([dst[(j, r, c)] for r, c in zip(rows, cols)], np.int64)
         assert np.array_equal(got, np.arange(len(rows)))
 
 
-def test_tile_shapes_fit_lds():
+@pytest.mark.parametrize("cells", [1024, 2048])
+def test_tile_shapes_fit_lds(cells):
     for H in range(1, 257):
-        HB, CG = compact_hb(H), compact_cg(H)
-        assert HB * CG <= 2048 and 256 % CG == 0 and CG >= 32
+        HB, CG = compact_tile(H, cells)
+        assert HB * CG <= cells and 256 % CG == 0 and CG >= 32
         assert HB <= 64  # rowoff[64] in LDS
+        assert 24 * HB * CG <= 48 * 1024  # dynamic LDS of the deskew variant
