@@ -121,7 +121,7 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
   }
 }
 
-// Compaction tiles (k_compact): HB rows x CG columns, HB * CG <= cells (1024 or 2048, FBR_COMPACT_CELLS),
+// Compaction tiles (k_compact): HB rows x CG columns, HB * CG <= cells (512, 1024 or 2048, FBR_COMPACT_CELLS),
 // HB <= 64, CG a power of two in [32, 256].  Chosen on the host and passed to both kernels.
 struct CompactTile {
   int hb, cg;
@@ -372,12 +372,12 @@ void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* n
   fbr_launch(k_project, dim3(blocks, B), dim3(kProjThreads), lds, s, pts, nin, nmax, H, W, tile_log2, owner);
 }
 
-// Compaction tile size in cells (FBR_COMPACT_CELLS: 1024 or 2048).
+// Compaction tile size in cells (FBR_COMPACT_CELLS: 512, 1024 or 2048).
 int compact_cells() {
   static const int v = [] {
     const char* e = std::getenv("FBR_COMPACT_CELLS");
     const int c = e ? std::atoi(e) : 1024;
-    return c >= 2048 ? 2048 : 1024;
+    return c >= 2048 ? 2048 : c >= 1024 ? 1024 : 512;
   }();
   return v;
 }

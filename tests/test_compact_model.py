@@ -87,7 +87,7 @@ def compact_destinations(claimed_jobs, H, W, cells):
                                  (32, 1024), (40, 77), (48, 2048), (64, 1800), (65, 200), (100, 96), (128, 2048),
                                  (129, 64), (16, 4096)])
 @pytest.mark.parametrize("density", [0.0, 0.3, 1.0])
-@pytest.mark.parametrize("cells", [1024, 2048])
+@pytest.mark.parametrize("cells", [512, 1024, 2048])
 def test_compaction_index_model(H, W, density, cells):
     rng = np.random.default_rng(H * 10007 + W)
     B = 3 if H * W <= 4096 else 2  # job groups of 8 with a partial last group
@@ -101,7 +101,7 @@ def test_compaction_index_model(H, W, density, cells):
         assert np.array_equal(got, np.arange(len(rows)))
 
 
-@pytest.mark.parametrize("cells", [1024, 2048])
+@pytest.mark.parametrize("cells", [512, 1024, 2048])
 def test_tile_shapes_fit_lds(cells):
     for H in range(1, 257):
         HB, CG = compact_tile(H, cells)

@@ -7,7 +7,7 @@ TAG=${1:-r01}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-CMD="bench.py --steps 10 --warmup 3"
+CMD="bench.py --steps 10 --warmup 3 --latency 0 --ingest 0"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- python3 $CMD --no-cpu-baseline > $OUT/bench_trace.log 2>&1 || exit 11
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o bench --output-format csv -- python3 $CMD --no-cpu-baseline > $OUT/bench_fetch.log 2>&1 || exit 12
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o bench --output-format csv -- python3 $CMD --no-cpu-baseline > $OUT/bench_write.log 2>&1 || exit 13
