@@ -15,20 +15,26 @@ import re
 import sys
 from collections import defaultdict
 
-NAMES = {"gn_knn": r"k_gn_knn", "gn_residual": r"k_gn_residual", "features": r"k_features",
-         "voxel_ring": r"k_voxel_ring", "voxel_scan": r"k_voxel_grid", "concat": r"k_concat",
-         "project": r"k_project\b", "extract": r"k_compact|k_rowcount", "gn_solve": r"k_gn_solve"}
+NAMES = {"gn_knn": [r"k_gn_knn"], "gn_residual": [r"k_gn_residual"], "features": [r"k_features"],
+         "voxel_ring": [r"k_voxel_ring"], "voxel_scan": [r"k_voxel_grid"], "concat": [r"k_concat"],
+         "project": [r"k_project\b"], "extract": [r"k_compact", r"k_rowcount"], "gn_solve": [r"k_gn_solve"]}
 
 
 def per_launch(path, counter):
-    acc = defaultdict(list)
+    """Bytes per launcher call: a launcher of several kernels (extract = k_rowcount + k_compact)
+    counts each call once, so its dispatches are summed and divided by the most-called kernel's
+    dispatch count."""
+    acc = defaultdict(float)
+    calls = defaultdict(lambda: defaultdict(int))
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        for key, rx in NAMES.items():
-            if re.search(rx, r["Kernel_Name"]):
-                acc[key].append(float(r["Counter_Value"]) * 1024.0)
-    return acc
+        for key, rxs in NAMES.items():
+            for i, rx in enumerate(rxs):
+                if re.search(rx, r["Kernel_Name"]):
+                    acc[key] += float(r["Counter_Value"]) * 1024.0
+                    calls[key][i] += 1
+    return {k: (acc[k], max(calls[k].values())) for k in acc}
 
 
 def main():
@@ -38,11 +44,11 @@ def main():
     w = per_launch(write_csv, "WRITE_SIZE")
     kernels = {}
     for k in NAMES:
-        if f.get(k) and w.get(k):
-            fb = sum(f[k]) / len(f[k])
-            wb = sum(w[k]) / len(w[k])
+        if k in f and k in w:
+            fb = f[k][0] / f[k][1]
+            wb = w[k][0] / w[k][1]
             kernels[k] = {"hbm_bytes_per_launch": 2.0 * fb + wb, "fetch_bytes_raw": fb, "write_bytes": wb,
-                          "launches_sampled": len(f[k])}
+                          "launches_sampled": f[k][1]}
     res = {"config": cfg, "batch": int(batch), "kernels": kernels,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of bench.py; "
                      "bytes = 2*FETCH_SIZE (gfx950 64-B tally of 128-B requests) + WRITE_SIZE, mean per launch",
