@@ -93,7 +93,7 @@ struct FeatArgs {
   int64_t gslot_bytes;
   unsigned long long* stamps;  // diagnostic builds only: [B*H][12] phase cycle sums
 };
-size_t features_lds_bytes(const FeatArgs& a);
+size_t features_lds_bytes(const FeatArgs& a, int nwv);  // nwv: waves per ring
 size_t features_gslot_bytes(const FeatArgs& a);
 void launch_features(hipStream_t s, const FeatArgs& a);
 

@@ -35,12 +35,23 @@
 #include "fbr_sort.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace fbr {
+
+// Synchronisation of code that one wave runs on its own (the single-wave kernel, or wave 0 of the
+// multi-wave kernel while the helper waves wait at the next workgroup barrier): a workgroup-scope
+// fence (every earlier LDS / global access of the wave has completed) and a wave barrier (no code
+// motion across it).  For a one-wave workgroup this is what __syncthreads amounts to.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
 
 namespace {
 constexpr uint64_t kPadKey = ~0ull;
 constexpr int kWin = 256 + 16;  // phase-2 window: 4 chunks + 8 on each side
+constexpr int kWinBytes = kWin * (sizeof(float) + sizeof(int16_t));  // 1632 B per wave (16-B multiple)
 }  // namespace
 
 // Window bit-words (index i of the window <-> bit i&63 of word i>>6).
@@ -236,7 +247,7 @@ __device__ int wave_partition(SmoothEntry* a, int lo, int hi, float p, int* posL
     if (isR) posR[cntR + __popcll(br & ((1ull << lane) - 1ull))] = i;
     cntR += __popcll(br);
   }
-  __syncthreads();
+  wsync();
   const int mn = min(cntL, cntR);
   int K1 = 0;  // swaps performed = number of k with g_k < r_k (a prefix of k)
   for (int k0 = 0; k0 < mn; k0 += 64) {
@@ -253,7 +264,7 @@ __device__ int wave_partition(SmoothEntry* a, int lo, int hi, float p, int* posL
   }
   int cut = K1 < cntL ? posL[K1] : INT_MAX;
   if (K1 > 0) cut = min(cut, posR[K1 - 1]);
-  __syncthreads();
+  wsync();
   return min(cut, hi);
 }
 
@@ -267,19 +278,19 @@ __device__ void wave_introsort_partitions(SmoothEntry* a, int n, SortFrame* stac
     while (last - first > 16) {
       if (depth == 0) {  // std::partial_sort(first, last, last)
         if (lane == 0) sm_heap_sort(a, first, last);
-        __syncthreads();
+        wsync();
         break;
       }
       --depth;
       const int mid = first + (last - first) / 2;
       if (lane == 0) sm_move_median_to_first(a, first, first + 1, mid, last - 1);
-      __syncthreads();
+      wsync();
       const int cut = wave_partition(a, first + 1, last, a[first].v, posL, posR, lane);
       if (sp < kSortStack) stack[sp++] = SortFrame{cut, last, depth};
       last = cut;
     }
   }
-  __syncthreads();
+  wsync();
 }
 
 // In-LDS bitonic sort of kpow (power of two) 64-bit keys, QP compare-exchange pairs per lane.
@@ -311,7 +322,7 @@ __device__ __forceinline__ void bitonic_sort_keys(uint64_t* keys, int kpow, int 
           }
         }
       }
-      __syncthreads();
+      wsync();
     }
   }
 }
@@ -333,9 +344,16 @@ __device__ __forceinline__ void bitonic_sort_keys(uint64_t* keys, int kpow, int 
 
 // WMAX: 64-bit words of segment-member masks (members <= 64*WMAX); QP: bitonic pairs per lane
 // (segment sort <= 128*QP keys).  <6,4> covers Horizon_SCAN <= 2048, <12,8> up to 4096.
-template <int WMAX, int QP>
-__global__ void __launch_bounds__(64)
+// NWV: waves per ring.  NWV = 1 for large launches (every SIMD holds many ring waves, so one wave
+// per ring hides its LDS latency behind the others).  With few rings per SIMD (single scans,
+// small batches) a ring's critical path is one wave's latency chain, so NWV > 1 spreads the
+// lane-parallel passes (flags and curvature, the conflict masks of each segment, the outputs)
+// over NWV waves, while wave 0 alone runs the walks (ballot masks, greedy rounds, the sorted
+// path) between workgroup barriers.
+template <int WMAX, int QP, int NWV>
+__global__ void __launch_bounds__(64 * NWV)
 k_features(FeatArgs a) {
+  constexpr int NT = 64 * NWV;
 #ifdef FBR_FEAT_STAMPS
   unsigned long long stamp_acc[12] = {0}, stamp_last = __builtin_amdgcn_s_memtime();
 #endif
@@ -344,7 +362,7 @@ k_features(FeatArgs a) {
   // Ring 0 of every job first: its segment 0 holds the stale cloudSmoothness[4] slot and runs the
   // serial walk, the longest wave of the launch; dispatching those waves first hides them behind
   // the other rings instead of leaving the last jobs' ones in the tail.
-  const int b = blockIdx.x, lane = threadIdx.x;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int job = b < a.B ? b : (b - a.B) / (H - 1);
   const int ring = b < a.B ? 0 : 1 + (b - a.B) % (H - 1);
   const int64_t HW = (int64_t)H * W;
@@ -353,7 +371,7 @@ k_features(FeatArgs a) {
   const int cb = s - 4, ca = e + 6;  // this ring's points [cb, ca)
   const int slot = job * H + ring;
   if (ca <= cb) {
-    if (lane == 0) a.corner_cnt[slot] = 0;
+    if (tid == 0) a.corner_cnt[slot] = 0;
     return;
   }
   FeatLds S;
@@ -363,7 +381,7 @@ k_features(FeatArgs a) {
   S.nw = (S.L + 63) >> 6;
   const int Lcap = a.lcap, segcap = a.segcap, nwcap = a.nwcap, kseg = a.kseg;
   if (S.L > Lcap) {
-    if (lane == 0) atomicOr(&a.err[job], 1);
+    if (tid == 0) atomicOr(&a.err[job], 1);
     return;
   }
   unsigned char* p = smem;
@@ -399,13 +417,14 @@ k_features(FeatArgs a) {
   const int32_t* C = a.col + job * HW;
   const float4* CL = a.cloud + job * HW;
   StreamState* st = a.stream + job;
-  for (int w = lane; w < 9 * nwcap; w += 64) words[w] = 0ull;
+  for (int w = tid; w < 9 * nwcap; w += NT) words[w] = 0ull;
   __syncthreads();
   FBR_STAMP(0);
   // ---- phase 2: occlusion marks, column gaps, curvature, threshold bits (chunk c = 64 indices) ----
-  // range / col are staged per group of 4 chunks: window [256g - 8, 256g + 264) in region B
-  // (the next group's window is loaded into registers while this group is processed)
-  float* rw = (float*)S.rb;
+  // range / col are staged per group of 4 chunks: window [256g - 8, 256g + 264) in region B (a
+  // window per wave); with one wave the next group's window is loaded into registers while this
+  // group is processed, with several the waves take the groups in turn
+  float* rw = (float*)(S.rb + wv * kWinBytes);
   int16_t* cw = (int16_t*)(rw + kWin);
   constexpr int kWq = (kWin + 63) / 64;
   float rv[kWq];
@@ -420,21 +439,17 @@ k_features(FeatArgs a) {
       cv[q] = in ? C[S.wlo + idx] : 0;
     }
   };
-  load_window(0);
-  for (int c = 0; c < S.nw; ++c) {
-    if ((c & 3) == 0) {
-      __syncthreads();
+  auto store_window = [&]() __attribute__((always_inline)) {
 #pragma unroll
-      for (int q = 0; q < kWq; ++q) {
-        const int t = 64 * q + lane;
-        if (t < kWin) {
-          rw[t] = rv[q];
-          cw[t] = (int16_t)cv[q];
-        }
+    for (int q = 0; q < kWq; ++q) {
+      const int t = 64 * q + lane;
+      if (t < kWin) {
+        rw[t] = rv[q];
+        cw[t] = (int16_t)cv[q];
       }
-      __syncthreads();
-      if (c + 4 < S.nw) load_window(c + 4);
     }
+  };
+  auto chunk = [&](int c) __attribute__((always_inline)) {
     const int i = 64 * c + lane;
     const int j = S.wlo + i;
     const int wo = 64 * (c & ~3) - 8;  // window origin of this chunk's group
@@ -469,10 +484,35 @@ k_features(FeatArgs a) {
       S.edgec.w[c] = be;
       S.surfc.w[c] = bs;
     }
+  };
+  if constexpr (NWV == 1) {
+    load_window(0);
+    for (int c = 0; c < S.nw; ++c) {
+      if ((c & 3) == 0) {
+        wsync();
+        store_window();
+        wsync();
+        if (c + 4 < S.nw) load_window(c + 4);
+      }
+      chunk(c);
+    }
+  } else {
+    const int G = (S.nw + 3) >> 2;  // groups of 4 chunks, dealt round-robin; uniform trip count
+    for (int g0 = 0; g0 < G; g0 += NWV) {
+      const int g = g0 + wv;
+      if (g < G) {
+        load_window(4 * g);
+        store_window();
+      }
+      __syncthreads();
+      if (g < G)
+        for (int c = 4 * g; c < min(4 * g + 4, S.nw); ++c) chunk(c);
+      __syncthreads();
+    }
   }
   __syncthreads();
   // cloudNeighborPicked: reset over [5, n-5) (:124) then the marks; indices < 5 keep stream state
-  for (int c = lane; c < S.nw; c += 64) {
+  for (int c = tid; c < S.nw; c += NT) {
     const uint64_t A = S.occa.w[c], An = c + 1 < S.nw ? S.occa.w[c + 1] : 0ull;
     const uint64_t B = S.occb.w[c], Bp = c > 0 ? S.occb.w[c - 1] : 0ull;
     uint64_t mk = S.occc.w[c] | A;
@@ -520,14 +560,14 @@ k_features(FeatArgs a) {
     if (sp >= ep) continue;
     const int m = ep - sp;
     if (m + 1 > segcap || m > kseg) {
-      if (lane == 0) atomicOr(&a.err[job], 2);
+      if (tid == 0) atomicOr(&a.err[job], 2);
       return;
     }
     // stage this segment's curvature window [sp-6, ep+7) in LDS (members +-5 plus ep)
     S.sbase = max(sp - S.wlo - 6, 0);
     const int slen = min(ep - S.wlo + 7, S.L) - S.sbase;
     if (pf_seg != j)
-      for (int t = lane; t < slen; t += 64) S.scurv[t] = S.gcurv[S.sbase + t];
+      for (int t = tid; t < slen; t += NT) S.scurv[t] = S.gcurv[S.sbase + t];
     __syncthreads();
 #ifdef FBR_FEAT_SKIP_STALE
     const bool has_stale = false;  // diagnostic ablation only
@@ -552,7 +592,7 @@ k_features(FeatArgs a) {
         }
         S.keys[t] = key;
       }
-      __syncthreads();
+      wsync();
       bitonic_sort_keys<QP>(S.keys, kpow, lane);
       bool tflag = false, nflag = false;
       for (int t = lane; t < m; t += 64) {
@@ -569,28 +609,28 @@ k_features(FeatArgs a) {
           const int pos = sp + t;
           S.seg[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.scurv[pos - S.wlo - S.sbase], pos};
         }
-        __syncthreads();
+        wsync();
         if (nan) {
           if (lane == 0) std_sort_emul(S.seg, m, S.sstack);
-          __syncthreads();
+          wsync();
         } else {
           wave_introsort_partitions(S.seg, m, S.sstack, (int*)S.cm, (int*)S.sorder, lane);
           for (int t = lane; t < kpow; t += 64)
             S.keys[t] = t < m ? (((uint64_t)__float_as_uint(S.seg[t].v) << 16) | (uint64_t)t) : kPadKey;
-          __syncthreads();
+          wsync();
           bitonic_sort_keys<QP>(S.keys, kpow, lane);  // stable sort of the partitioned array
           SmoothEntry* tmp = (SmoothEntry*)S.cm;       // cm + sorder + rankc = 8 B per entry
           for (int k = lane; k < m; k += 64) tmp[k] = S.seg[S.keys[k] & 0xFFFFu];
-          __syncthreads();
+          wsync();
           for (int k = lane; k < m; k += 64) S.seg[k] = tmp[k];
-          __syncthreads();
+          wsync();
         }
       } else if (has_stale) {
         for (int k = lane; k < m; k += 64) {
           const int pos = sp + (int)(S.keys[k] & 0xFFFFu);
           S.seg[k] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.scurv[pos - S.wlo - S.sbase], pos};
         }
-        __syncthreads();
+        wsync();
       }
       if (has_stale) {
         if (lane == 0) {
@@ -598,7 +638,7 @@ k_features(FeatArgs a) {
           st->smooth4_value = S.seg[4 - sp].v;            // the entry left at position 4 is the next
           st->smooth4_ind = S.seg[4 - sp].ind;            // scan's stale slot
         }
-        __syncthreads();
+        wsync();
       }
       if (!has_stale) {
         // members u in [0, m] (index sp+u): sorted order, visit ranks, conflict masks
@@ -607,7 +647,7 @@ k_features(FeatArgs a) {
           S.sorder[k] = (uint16_t)u;
           S.rankc[u] = (uint16_t)(k == m ? 0 : m - k);  // corner visit order: ep, then descending
         }
-        __syncthreads();
+        wsync();
         for (int u = lane; u <= m; u += 64) {
           const int li = sp + u - S.wlo;
           const int f = reach_fwd(S, li), b = reach_bwd(S, li);
@@ -628,7 +668,7 @@ k_features(FeatArgs a) {
           }
           S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
         }
-        __syncthreads();
+        wsync();
       }
     };
     float* tlv = (float*)S.rb;                         // direct path: taken corners (value, member)
@@ -637,7 +677,7 @@ k_features(FeatArgs a) {
     bool direct = !has_stale;
 #ifdef FBR_FEAT_SKIP_CM
     if (direct) {
-      for (int u = lane; u <= m; u += 64) S.cm[u] = 0u;
+      for (int u = tid; u <= m; u += NT) S.cm[u] = 0u;
       __syncthreads();
     }
     if (false) {
@@ -645,7 +685,7 @@ k_features(FeatArgs a) {
     if (direct) {
 #endif
       bool tf = false;
-      for (int k0 = 0; k0 <= m; k0 += 64) {
+      for (int k0 = 64 * wv; k0 <= m; k0 += NT) {
         const int u = k0 + lane;
         const int li0 = sp - S.wlo + k0, W0 = li0 >> 6;  // li0 >= 0
         const uint64_t gm1 = W0 >= 1 ? S.gap.w[W0 - 1] : ~0ull;  // wave-uniform words
@@ -682,19 +722,25 @@ k_features(FeatArgs a) {
           S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
         }
       }
-      direct = !__any(tf);
-      __syncthreads();
+      if constexpr (NWV == 1) {
+        direct = !__any(tf);
+        wsync();
+      } else {
+        __syncthreads();
+        direct = !__syncthreads_or(tf);
+      }
       FBR_STAMP(10);
     }
+    if (wv == 0) {  // the walks: wave 0 alone (helper waves wait at the segment's closing barrier)
     if (!direct) sorted_order();
     FBR_STAMP(3);
     if (has_stale) {
       SmoothEntry* ent = (SmoothEntry*)S.rb;  // the walk's entries in LDS (region B is free here)
       for (int k = lane; k <= m; k += 64) ent[k] = S.seg[k];
-      __syncthreads();
+      wsync();
       if (lane == 0) serial_walks(S, slen, ent, a, job, m, CL, corner_out, corner_cnt);
       corner_cnt = __shfl(corner_cnt, 0);
-      __syncthreads();
+      wsync();
     } else {
       // -- corner walk --
       uint64_t und[WMAX], tak[WMAX];
@@ -728,7 +774,7 @@ k_features(FeatArgs a) {
           }
           T += __popcll(tak[w]);
         }
-        __syncthreads();
+        wsync();
         bool tf = false;
         for (int c = lane; c < T; c += 64) {
           const int u = tlu[c];
@@ -747,11 +793,11 @@ k_features(FeatArgs a) {
         }
         if (__any(tf)) {  // tied taken corners: their order is introsort's
           direct = false;
-          __syncthreads();
+          wsync();
           sorted_order();
           corner_walk();
         }
-        __syncthreads();
+        wsync();
         FBR_STAMP(11);
       }
       if (lane < WMAX) {
@@ -761,7 +807,7 @@ k_features(FeatArgs a) {
           if (w == lane) t = tak[w];
         S.tmask[lane] = t;
       }
-      __syncthreads();
+      wsync();
       // the first kCornerPerSeg taken corners in visit order are kept (the walk breaks there)
       const int R = direct ? T : m + 1;
       int taken = 0;
@@ -782,9 +828,9 @@ k_features(FeatArgs a) {
         taken += __popcll(mk);
       }
       corner_cnt += min(taken, kCornerPerSeg);
-      __syncthreads();
+      wsync();
       FBR_STAMP(5);
-      prefetch_curv(j + 1);  // scurv is not read again in this segment
+      if constexpr (NWV == 1) prefetch_curv(j + 1);  // scurv is not read again in this segment
       // -- surf walk: ascending, ep last -> higher priority = not higher corner priority --
 #pragma unroll
       for (int w = 0; w < WMAX; ++w) {
@@ -820,32 +866,35 @@ k_features(FeatArgs a) {
         for (int q = 0; q < kCq; ++q)
           if (64 * q + lane < pf_len) S.scurv[64 * q + lane] = cpf[q];
       }
-      __syncthreads();
+      wsync();
     }
     FBR_STAMP(7);
     // surf candidates (label <= 0 in [sp, ep], :279-284) are selected by the per-ring VoxelGrid
     // straight from the label mask (k_voxel.hip, k_voxel_ring)
     FBR_STAMP(8);
+    }  // wave 0
+    if constexpr (NWV > 1) __syncthreads();
   }
   // ---- outputs ----
+  if constexpr (NWV > 1) __syncthreads();
   int8_t* LB = a.label + job * HW;
-  for (int k = max(cb, 0) + lane; k < ca; k += 64) {
+  for (int k = max(cb, 0) + tid; k < ca; k += NT) {
     const int li = k - S.wlo;
     const int8_t lab = S.labpos.get(li) ? 1 : (S.labneg.get(li) ? -1 : 0);
     if (k >= 5 && k < n - 5) LB[k] = lab;      // cloudLabel reset range (:126)
     else if (k < 5 && lab != 0) LB[k] = lab;   // stale slots keep earlier values
   }
-  if (cb <= 0 && lane < 5 && lane < S.L) st->picked04[lane] = S.picked.get(lane) ? 1 : 0;
-  if (lane == 0) a.corner_cnt[slot] = corner_cnt;
+  if (cb <= 0 && tid < 5 && tid < S.L) st->picked04[tid] = S.picked.get(tid) ? 1 : 0;
+  if (tid == 0) a.corner_cnt[slot] = corner_cnt;
 #ifdef FBR_FEAT_STAMPS
   FBR_STAMP(9);
-  if (lane == 0 && a.stamps)
+  if (tid == 0 && a.stamps)
     for (int i = 0; i < 12; ++i) a.stamps[(int64_t)slot * 12 + i] = stamp_acc[i];
 #endif
 }
 
-size_t features_lds_bytes(const FeatArgs& a) {
-  const size_t region_b = std::max<size_t>((size_t)kWin * (sizeof(float) + sizeof(int16_t)), (size_t)8 * a.segcap);
+size_t features_lds_bytes(const FeatArgs& a, int nwv) {
+  const size_t region_b = std::max<size_t>((size_t)nwv * kWinBytes, (size_t)8 * a.segcap);
   return (size_t)((a.segcap + 19) & ~3) * sizeof(float) + (size_t)9 * a.nwcap * sizeof(uint64_t) + sizeof(uint64_t) * 16 +
          sizeof(SortFrame) * kSortStack + sizeof(uint32_t) * a.segcap + 16 + region_b;
 }
@@ -856,11 +905,34 @@ size_t features_gslot_bytes(const FeatArgs& a) {
   return (b + 255) & ~(size_t)255;
 }
 
+// Waves per ring: FBR_FEAT_WAVES (1, 2 or 4) or, by default, 4 while a launch has at most 2048
+// rings (<= 2 rings per SIMD: single scans, small sub-batches), 1 above.
+int feature_waves(int rings) {
+  static const int forced = [] {
+    const char* e = std::getenv("FBR_FEAT_WAVES");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 4 ? 4 : v >= 2 ? 2 : v == 1 ? 1 : 0;
+  }();
+  if (forced) return forced;
+  return rings <= 2048 ? 4 : 1;
+}
+
 void launch_features(hipStream_t s, const FeatArgs& a) {
-  if (a.segcap <= 6 * 64 && a.kseg <= 4 * 128)
-    fbr_launch((k_features<6, 4>), dim3(a.B * a.H), dim3(64), features_lds_bytes(a), s, a);
-  else
-    fbr_launch((k_features<12, 8>), dim3(a.B * a.H), dim3(64), features_lds_bytes(a), s, a);
+  const int nwv = feature_waves(a.B * a.H);
+  const dim3 grid(a.B * a.H);
+  if (a.segcap <= 6 * 64 && a.kseg <= 4 * 128) {
+    if (nwv == 4)
+      fbr_launch((k_features<6, 4, 4>), grid, dim3(256), features_lds_bytes(a, 4), s, a);
+    else if (nwv == 2)
+      fbr_launch((k_features<6, 4, 2>), grid, dim3(128), features_lds_bytes(a, 2), s, a);
+    else
+      fbr_launch((k_features<6, 4, 1>), grid, dim3(64), features_lds_bytes(a, 1), s, a);
+  } else {
+    if (nwv > 1)
+      fbr_launch((k_features<12, 8, 4>), grid, dim3(256), features_lds_bytes(a, 4), s, a);
+    else
+      fbr_launch((k_features<12, 8, 1>), grid, dim3(64), features_lds_bytes(a, 1), s, a);
+  }
 }
 
 }  // namespace fbr
