@@ -36,6 +36,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace fbr {
 
@@ -129,7 +130,7 @@ __device__ __forceinline__ float curv_at(const FeatLds& S, int li, int slen) {
 }
 
 // Sequential walks (the reference loops verbatim) over S.seg[0..m] (seg[m] = the unsorted ep entry).
-__device__ void serial_walks(const FeatLds& S, int slen, const SmoothEntry* ent, const FeatArgs& a, int job, int m,
+__device__ __forceinline__ void serial_walks(const FeatLds& S, int slen, const SmoothEntry* ent, const FeatArgs& a, int job, int m,
                              const float4* CL, float4* corner_out, int& corner_cnt) {
   int largestPickedNum = 0;
   for (int k = m; k >= 0; k--) {  // corners, k = ep .. sp (:208-242)
@@ -182,7 +183,7 @@ __device__ __forceinline__ uint32_t win10(uint64_t a, uint64_t b, uint64_t c, in
 // Greedy rounds.  cmbits(u) = 10-bit mask of the higher-priority conflicting members of u.
 // und: candidate members on entry; on exit tak = the members the sequential walk takes.
 template <int WMAX, typename CmF>
-__device__ void greedy_rounds(int m, int lane, uint64_t (&und)[WMAX], uint64_t (&tak)[WMAX], CmF cmbits,
+__device__ __forceinline__ void greedy_rounds(int m, int lane, uint64_t (&und)[WMAX], uint64_t (&tak)[WMAX], CmF cmbits,
                               const FeatArgs& a, int job) {
   const int nwm = (m >> 6) + 1;
   uint32_t cmr[WMAX];
@@ -293,38 +294,159 @@ __device__ void wave_introsort_partitions(SmoothEntry* a, int n, SortFrame* stac
   wsync();
 }
 
-// In-LDS bitonic sort of kpow (power of two) 64-bit keys, QP compare-exchange pairs per lane.
+// Bitonic sort of kpow (power of two, <= 128 * QP) 64-bit keys held in registers: element
+// e = 64 * r + lane sits in register r of its lane, so a compare-exchange at distance j2 < 64 is a
+// lane shuffle and one at j2 >= 64 is between two registers of the same lane.  keys[] is read
+// once and written once (it was a global-scratch network with a wave sync per stage).
 template <int QP>
 __device__ __forceinline__ void bitonic_sort_keys(uint64_t* keys, int kpow, int lane) {
+  constexpr int KPL = 2 * QP;
+  uint64_t k[KPL];
+#pragma unroll
+  for (int r = 0; r < KPL; ++r) k[r] = 64 * r + lane < kpow ? keys[64 * r + lane] : kPadKey;
   for (int k2 = 2; k2 <= kpow; k2 <<= 1) {
     for (int j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
-      const int npairs = kpow >> 1;
-      uint64_t xs[QP], ys[QP];
-      int ts[QP];
+      if (j2 >= 64) {  // register distance jr (a compile-time index per case)
+        auto step = [&](auto JR) __attribute__((always_inline)) {
+          constexpr int jr = decltype(JR)::value;
 #pragma unroll
-      for (int q4 = 0; q4 < QP; ++q4) {
-        const int q = lane + 64 * q4;
-        ts[q4] = ((q & ~(j2 - 1)) << 1) | (q & (j2 - 1));  // j2 is a power of two
-        if (q < npairs) {
-          xs[q4] = keys[ts[q4]];
-          ys[q4] = keys[ts[q4] + j2];
-        }
-      }
-#pragma unroll
-      for (int q4 = 0; q4 < QP; ++q4) {
-        const int q = lane + 64 * q4;
-        if (q < npairs) {
-          const int t = ts[q4];
-          const bool up = (t & k2) == 0;
-          if ((xs[q4] > ys[q4]) == up) {
-            keys[t] = ys[q4];
-            keys[t + j2] = xs[q4];
+          for (int r = 0; r < KPL; ++r) {
+            if constexpr (jr < KPL) {
+              if ((r & jr) == 0 && r + jr < KPL) {
+                const int e = 64 * r + lane;
+                const bool up = (e & k2) == 0;
+                const uint64_t x = k[r], y = k[(r + jr) % KPL];
+                const bool sw = (x > y) == up;
+                k[r] = sw ? y : x;
+                k[(r + jr) % KPL] = sw ? x : y;
+              }
+            }
           }
+        };
+        switch (j2 >> 6) {
+          case 1: step(std::integral_constant<int, 1>{}); break;
+          case 2: step(std::integral_constant<int, 2>{}); break;
+          case 4: step(std::integral_constant<int, 4>{}); break;
+          case 8: step(std::integral_constant<int, 8>{}); break;
+          default: break;
+        }
+      } else {
+        const bool lower = (lane & j2) == 0;
+#pragma unroll
+        for (int r = 0; r < KPL; ++r) {
+          const int e = 64 * r + lane;
+          const bool up = (e & k2) == 0;
+          const uint64_t x = k[r];
+          const uint32_t ylo = __shfl_xor((uint32_t)x, j2), yhi = __shfl_xor((uint32_t)(x >> 32), j2);
+          const uint64_t y = ((uint64_t)yhi << 32) | ylo;
+          const uint64_t mn = x < y ? x : y, mx = x < y ? y : x;
+          k[r] = (lower == up) ? mn : mx;
         }
       }
-      wsync();
     }
   }
+#pragma unroll
+  for (int r = 0; r < KPL; ++r)
+    if (64 * r + lane < kpow) keys[64 * r + lane] = k[r];
+  wsync();
+}
+
+// The stale-slot segment's walks (the reference loops of serial_walks) with the wave's lanes as
+// the picked-word window: lane i holds picked word w_lo + i, so a test is one readlane of a
+// wave-uniform word and a suppression range is one masked OR per lane.  Every entry's window
+// index, candidate tests and suppression reach are computed lane-parallel first (info[k]); the
+// walks then visit the entries in order on wave-uniform values, record the taken corners and
+// write the picked / label words back.  Returns false (nothing written) when an entry lies
+// outside the ring window or the window spans more than 64 words; the caller then runs
+// serial_walks (which reports the error, as the reference's out-of-range access has no answer).
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ bool stale_walks_fast(const FeatLds& S, int slen, const SmoothEntry* ent, const FeatArgs& a, int m,
+                                 const float4* CL, float4* corner_out, int& corner_cnt, uint32_t* info,
+                                 int32_t* tlist, int lane) {
+  int lo_li = INT_MAX, hi_li = INT_MIN;
+  bool bad = false;
+  for (int k0 = 0; k0 <= m; k0 += 64) {
+    const int k = k0 + lane;
+    if (k <= m) {
+      const int li = ent[k].ind - S.wlo;
+      uint32_t v = 0u;
+      if (li >= 0 && li + 5 < S.L) {
+        const float cv = curv_at(S, li, slen);
+        const int f = reach_fwd(S, li), b = reach_bwd(S, li);
+        v = (uint32_t)li | ((uint32_t)f << 16) | ((uint32_t)b << 19) | ((cv > a.edge_thr) ? 1u << 22 : 0u) |
+            ((cv < a.surf_thr) ? 1u << 23 : 0u);
+        lo_li = min(lo_li, li - b);
+        hi_li = max(hi_li, li + f);
+      } else {
+        bad = true;
+      }
+      info[k] = v;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo_li = min(lo_li, __shfl_xor(lo_li, o));
+    hi_li = max(hi_li, __shfl_xor(hi_li, o));
+  }
+  wsync();
+  if (__any(bad) || lo_li < 0) return false;
+  const int w_lo = lo_li >> 6;
+  if ((hi_li >> 6) - w_lo >= 64) return false;
+  const int myw = w_lo + lane;
+  uint64_t pv = myw < S.nw ? S.picked.w[myw] : 0ull;
+  auto is_picked = [&](int li) __attribute__((always_inline)) {
+    return (readlane64(pv, (li >> 6) - w_lo) >> (li & 63)) & 1ull;
+  };
+  auto mark = [&](int lo, int hi) __attribute__((always_inline)) {  // picked over [lo, hi]
+    const int w0 = (lo >> 6) - w_lo, w1 = (hi >> 6) - w_lo;
+    uint64_t mm = (lane >= w0 && lane <= w1) ? ~0ull : 0ull;
+    if (lane == w0) mm &= ~0ull << (lo & 63);
+    if (lane == w1) mm &= (hi & 63) == 63 ? ~0ull : ((1ull << ((hi & 63) + 1)) - 1ull);
+    pv |= mm;
+  };
+  // corners: k = ep .. sp (:208-242)
+  int taken = 0;
+  bool stop = false;
+  for (int c0 = (m >> 6) << 6; c0 >= 0 && !stop; c0 -= 64) {
+    const uint32_t vv = c0 + lane <= m ? info[c0 + lane] : 0u;
+    for (int l = min(63, m - c0); l >= 0; --l) {
+      const uint32_t v = __builtin_amdgcn_readlane(vv, l);
+      if (!((v >> 22) & 1u)) continue;
+      const int li = (int)(v & 0xFFFFu);
+      if (is_picked(li)) continue;
+      if (++taken > kCornerPerSeg) {
+        stop = true;
+        break;
+      }
+      if (lane == 0) {
+        tlist[taken - 1] = li + S.wlo;
+        atomicOr((unsigned long long*)&S.labpos.w[li >> 6], 1ull << (li & 63));
+      }
+      mark(li - (int)((v >> 19) & 7u), li + (int)((v >> 16) & 7u));
+    }
+  }
+  const int nc = min(taken, kCornerPerSeg);
+  // surf: k = sp .. ep (:245-276)
+  for (int c0 = 0; c0 <= m; c0 += 64) {
+    const uint32_t vv = c0 + lane <= m ? info[c0 + lane] : 0u;
+    for (int l = 0; l <= min(63, m - c0); ++l) {
+      const uint32_t v = __builtin_amdgcn_readlane(vv, l);
+      if (!((v >> 23) & 1u)) continue;
+      const int li = (int)(v & 0xFFFFu);
+      if (is_picked(li)) continue;
+      if (lane == 0) atomicOr((unsigned long long*)&S.labneg.w[li >> 6], 1ull << (li & 63));
+      mark(li - (int)((v >> 19) & 7u), li + (int)((v >> 16) & 7u));
+    }
+  }
+  if (myw < S.nw) S.picked.w[myw] = pv;
+  wsync();
+  for (int t = lane; t < nc; t += 64) corner_out[corner_cnt + t] = CL[tlist[t]];
+  corner_cnt += nc;
+  wsync();
+  return true;
 }
 
 // Diagnostic build only (-DFBR_FEAT_STAMPS, tools/feat_stamps.py): per-phase s_memtime cycle sums
@@ -351,7 +473,7 @@ __device__ __forceinline__ void bitonic_sort_keys(uint64_t* keys, int kpow, int 
 // over NWV waves, while wave 0 alone runs the walks (ballot masks, greedy rounds, the sorted
 // path) between workgroup barriers.
 template <int WMAX, int QP, int NWV>
-__global__ void __launch_bounds__(64 * NWV)
+__global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(4)))
 k_features(FeatArgs a) {
   constexpr int NT = 64 * NWV;
 #ifdef FBR_FEAT_STAMPS
@@ -738,9 +860,14 @@ k_features(FeatArgs a) {
       SmoothEntry* ent = (SmoothEntry*)S.rb;  // the walk's entries in LDS (region B is free here)
       for (int k = lane; k <= m; k += 64) ent[k] = S.seg[k];
       wsync();
-      if (lane == 0) serial_walks(S, slen, ent, a, job, m, CL, corner_out, corner_cnt);
-      corner_cnt = __shfl(corner_cnt, 0);
-      wsync();
+      // cm is unused on this path: it holds the entries' walk info; the taken-corner list goes
+      // after the entries in region B
+      if (!stale_walks_fast(S, slen, ent, a, m, CL, corner_out, corner_cnt, S.cm,
+                               (int32_t*)(ent + segcap), lane)) {
+        if (lane == 0) serial_walks(S, slen, ent, a, job, m, CL, corner_out, corner_cnt);
+        corner_cnt = __shfl(corner_cnt, 0);
+        wsync();
+      }
     } else {
       // -- corner walk --
       uint64_t und[WMAX], tak[WMAX];
@@ -894,7 +1021,7 @@ k_features(FeatArgs a) {
 }
 
 size_t features_lds_bytes(const FeatArgs& a, int nwv) {
-  const size_t region_b = std::max<size_t>((size_t)nwv * kWinBytes, (size_t)8 * a.segcap);
+  const size_t region_b = std::max<size_t>((size_t)nwv * kWinBytes, (size_t)8 * a.segcap + sizeof(int32_t) * kCornerPerSeg);
   return (size_t)((a.segcap + 19) & ~3) * sizeof(float) + (size_t)9 * a.nwcap * sizeof(uint64_t) + sizeof(uint64_t) * 16 +
          sizeof(SortFrame) * kSortStack + sizeof(uint32_t) * a.segcap + 16 + region_b;
 }

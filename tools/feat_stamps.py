@@ -35,5 +35,11 @@ tot = out.astype(np.float64).mean(0)
 print("mean cycles per ring (s_memtime ticks):", int(tot.sum()))
 for n, v in zip(names, tot):
     print(f"  {n:20s} {v:12.0f}  {100 * v / tot.sum():5.1f}%")
+per_ring = out.astype(np.float64).reshape(B, H, 12)
+tot_r = per_ring.sum(2)  # [B][H]
+print(f"per-ring totals: ring 0 mean {tot_r[:, 0].mean():.0f}, rings 1.. mean {tot_r[:, 1:].mean():.0f}, "
+      f"max {tot_r.max():.0f} (ring {int(tot_r.argmax() % H)}), median {np.median(tot_r):.0f}")
+r0 = per_ring[:, 0, :].mean(0)
+print("ring 0 breakdown:", ", ".join(f"{n} {v:.0f}" for n, v in zip(names, r0) if v > 0))
 ctx.set_profiling(True); ctx.batch_launch(); ctx.batch_wait()
 print("features kernel ms:", ctx.kernel_time("features"))
