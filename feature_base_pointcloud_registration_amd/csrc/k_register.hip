@@ -162,9 +162,13 @@ __device__ unsigned long long fbr_knn_stats[10];
 // sum over rows of each row's longest lane (lanes of a wave scan different rows: the per-row loop
 // kept ~30 % of the lanes busy).  Pruning with a larger cut only scans more cells, and the 5-NN
 // list is a function of the scanned set, so both forms give the same neighbours.
-template <int R, int RX, bool kFlat = false, bool kSparse = false>
+// LPQ > 1 (wide mode, small launches): LPQ lanes share a query and lane `sub` scans the points of
+// absolute map index = sub (mod LPQ) (knn5_merge combines the lists).  A lane prunes with its own
+// 5th distance, which is never below the merged one (its list holds the 5 nearest of a subset),
+// so every point of the merged 5 nearest is still scanned by its lane.
+template <int R, int RX, bool kFlat = false, bool kSparse = false, int LPQ = 1>
 __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
-                          float bound, Knn5& r, unsigned* ks, int2* rows = nullptr) {
+                          float bound, Knn5& r, unsigned* ks, int2* rows = nullptr, int sub = 0) {
   constexpr int K = 2 * R + 1;  // rows per side in y and z; RX = cells per side along x
 #pragma unroll
   for (int t = 0; t < 5; ++t) r.k[t] = kKnnEmpty;
@@ -237,7 +241,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         if (e > b) rows[nrow++ * kResThreads] = make_int2(b, inside ? (int)((unsigned)e | 0x80000000u) : e);
         continue;
       }
-      for (int i = b; i < e; ++i) {
+      for (int i = LPQ == 1 ? b : b + ((sub - b) & (LPQ - 1)); i < e; i += LPQ) {
         const float4 p = m.pts[i];
         // pcl::CropBox (inclusive) as one mask: a point outside gets d2 = +inf (never inserted)
         bool out = false;  // rows inside the box skip the test
@@ -280,6 +284,24 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
 #endif
       knn_insert(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
     }
+  }
+}
+
+// Wide mode: the LPQ lanes of a query (consecutive lanes) exchange their lists in a butterfly and
+// each keeps the 5 smallest keys of the union (the lanes scanned disjoint point sets, so keys are
+// distinct and the result is the 5 nearest of the whole scanned set).
+template <int LPQ>
+__device__ __forceinline__ void knn5_merge(Knn5& r) {
+#pragma unroll
+  for (int off = 1; off < LPQ; off <<= 1) {
+    unsigned long long o[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const unsigned lo = __shfl_xor((unsigned)r.k[t], off), hi = __shfl_xor((unsigned)(r.k[t] >> 32), off);
+      o[t] = ((unsigned long long)hi << 32) | lo;
+    }
+#pragma unroll
+    for (int t = 0; t < 5; ++t) knn_insert(r, o[t]);
   }
 }
 
@@ -559,14 +581,21 @@ k_gn_residual(GnArgs a) {
 // R = grid cells per side covering radius 1 (both map grids share one cell size).  kFused: the
 // same lane goes on to its residual row and the workgroup reduces the item's normal-equation
 // partial (k_gn_residual's work, without re-reading the query and its neighbour indices).
-template <int R, int RX, bool kFused, bool kFlat, bool kSparse>
+// LPQ > 1 (wide mode, launches with few queries: single scans, tiny batches; neither fused nor
+// flat): a workgroup covers 256 / LPQ queries of an item with LPQ lanes each, so a query's search
+// chain is LPQ times shorter; lane `sub` == 0 of each query writes the results.
+template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ = 1>
 __global__ void __launch_bounds__(kResThreads)
 k_gn_knn(GnArgs a, int use_prev) {
+  static_assert(LPQ == 1 || (!kFused && !kFlat), "wide mode is the plain kNN pass");
   __shared__ double red[kFused ? kResThreads / 64 : 1][28];
   __shared__ int2 rows[kFlat ? (2 * R + 1) * (2 * R + 1) : 1][kResThreads];
-  const int tid = threadIdx.x;
+  constexpr int QPB = kResThreads / LPQ;  // queries per workgroup
+  const int sub = (int)threadIdx.x % LPQ;
   const int nitems = a.nitems[0];
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+  for (int v = blockIdx.x; v < nitems * LPQ; v += gridDim.x) {
+    const int it = v / LPQ;
+    const int tid = (v % LPQ) * QPB + (int)threadIdx.x / LPQ;  // query slot within the item
     const int4 item = a.items[it];
     const int job = item.x;
     const GnState& g = a.gn[job];
@@ -603,7 +632,9 @@ k_gn_knn(GnArgs a, int use_prev) {
       }
       Knn5 nn;
       unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      knn5_grid<R, RX, kFlat, kSparse>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks, &rows[0][tid]);
+      knn5_grid<R, RX, kFlat, kSparse, LPQ>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks,
+                                            &rows[0][threadIdx.x], sub);
+      if constexpr (LPQ > 1) knn5_merge<LPQ>(nn);
       const bool ok = nn.k[4] < kKnnEmpty;
       (void)ks;
       int32_t ids[5];
@@ -612,10 +643,13 @@ k_gn_knn(GnArgs a, int use_prev) {
       for (int k = 0; k < 5; ++k) {
         ids[k] = knn_id(nn.k[k]);
         same = same && ids[k] == oid[k];
-        o[k * kResThreads] = ok ? ids[k] : -1;
       }
+      if (LPQ > 1) __builtin_amdgcn_wave_barrier();  // every lane of the query read o[] (warm start)
+      if (sub == 0)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? ids[k] : -1;
       const int64_t q = (int64_t)it * kResThreads + tid;
-      if (!kFused) a.nsame[q] = same ? 1 : 0;
+      if (!kFused && sub == 0) a.nsame[q] = same ? 1 : 0;
 #ifdef FBR_KNN_STATS
       ks[5] = ok;
       ks[6] = corner;
@@ -879,19 +913,31 @@ void launch_export_records(hipStream_t s, int B, const float* pose_out, const fb
 }
 
 void launch_gn_init(hipStream_t s, const GnArgs& a) { fbr_launch(k_gn_init, dim3(1), dim3(1024), 0, s, a); }
-template <int R, bool F, bool L, bool S>
+template <int R, bool F, bool L, bool S, int LPQ = 1>
 void launch_gn_knn_rls(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
   const float invx = a.mc.g.inv_x;  // == a.ms.g.inv_x
-  if (invx > 4.0f) fbr_launch((k_gn_knn<R, 8, F, L, S>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
-  else if (invx > 2.0f) fbr_launch((k_gn_knn<R, 4, F, L, S>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
-  else if (invx > 1.0f) fbr_launch((k_gn_knn<R, 2, F, L, S>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
-  else fbr_launch((k_gn_knn<R, 1, F, L, S>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
+  grid *= LPQ;
+  if (invx > 4.0f) fbr_launch((k_gn_knn<R, 8, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
+  else if (invx > 2.0f) fbr_launch((k_gn_knn<R, 4, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
+  else if (invx > 1.0f) fbr_launch((k_gn_knn<R, 2, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
+  else fbr_launch((k_gn_knn<R, 1, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
 }
 // Dense or hashed-chunk map grids (one flag for both maps: fbr_set_map builds them alike).
-template <int R, bool F, bool L>
+template <int R, bool F, bool L, int LPQ = 1>
 void launch_gn_knn_rl(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
-  if (a.mc.g.sparse || a.ms.g.sparse) launch_gn_knn_rls<R, F, L, true>(s, a, grid, use_prev);
-  else launch_gn_knn_rls<R, F, L, false>(s, a, grid, use_prev);
+  if (a.mc.g.sparse || a.ms.g.sparse) launch_gn_knn_rls<R, F, L, true, LPQ>(s, a, grid, use_prev);
+  else launch_gn_knn_rls<R, F, L, false, LPQ>(s, a, grid, use_prev);
+}
+
+// Lanes per query of the plain kNN pass (FBR_KNN_LPQ = 1 or 8; default 8 for sub-batches of at
+// most 2 jobs, where one lane per query leaves the chip idle and the launch is one query's chain).
+int knn_lpq(int jobs) {
+  static const int forced = [] {
+    const char* e = std::getenv("FBR_KNN_LPQ");
+    return e ? (std::atoi(e) >= 8 ? 8 : 1) : 0;
+  }();
+  if (forced) return forced;
+  return jobs <= 2 ? 8 : 1;
 }
 
 // Flat row queue (FBR_KNN_FLAT=0 disables): from iteration 1 on (warm-start bound), 1 m y/z cells
@@ -906,6 +952,9 @@ bool knn_flat() {
 
 template <int R, bool F>
 void launch_gn_knn_r(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
+  if constexpr (!F) {
+    if (knn_lpq(a.B) == 8) return launch_gn_knn_rl<R, F, false, 8>(s, a, grid, use_prev);
+  }
   if constexpr (R == 1 && !F) {
     if (use_prev && knn_flat()) return launch_gn_knn_rl<R, F, true>(s, a, grid, use_prev);
   }
