@@ -156,17 +156,22 @@ def latency_line(cfg, corner_map, surf_map, n, cpu_scans=0):
             pose, _ = c.process_scan(scans[k], 0.2 * k, pose)
         warm_pose = pose.copy()
         api.debug_counters(reset=True)
+        api.host_times(reset=True)
         for k in range(3, n + 3):
             t = time.perf_counter()
             pose, st = c.process_scan(scans[k], 0.2 * k, pose)
             ms.append(1e3 * (time.perf_counter() - t))
             poses.append(pose.copy())
         launches, syncs, polls = api.debug_counters()
+        ht = api.host_times()
     ms = np.array(ms)
     out = {"scans": n, "ms_per_scan_mean": round(float(ms.mean()), 4), "ms_per_scan_p50": round(float(np.median(ms)), 4),
            "ms_per_scan_p99": round(float(np.percentile(ms, 99)), 4),
            "launches_per_scan": round(launches / n, 2), "host_syncs_per_scan": round(syncs / n, 2),
            "gn_flag_polls_per_scan": round(polls / n, 2),
+           # host wall time inside fbr_process_scan per scan: scan upload (staging copy + enqueue),
+           # stage enqueue (launches, GN flag polls), result wait, whole call
+           "host_ms_per_scan": {k: round(1e3 * v / n, 4) for k, v in zip(("upload", "enqueue", "result_wait", "call"), ht)},
            "path": "fbr_process_scan (host scan -> HBM, projection, features, registration, pose back)"}
     if cpu_scans:
         sys.path.insert(0, os.path.join(REPO, "oracle"))

@@ -142,6 +142,16 @@ def debug_counters(reset=False):
     return tuple(x.value for x in v)
 
 
+def host_times(reset=False):
+    """Host wall time (s) of the single-scan calls since the last reset: (upload, stage enqueue,
+    result wait, whole call) -- diagnostic (fbr_diag_host_times)."""
+    f = lib().fbr_diag_host_times
+    f.restype, f.argtypes = ctypes.c_int, [_VP, ctypes.c_int]
+    v = (ctypes.c_longlong * 4)()
+    _check(f(v, int(reset)), "fbr_diag_host_times")
+    return tuple(x * 1e-9 for x in v)
+
+
 def selftest_math(a, b):
     """Device sqrt(|a|), a/b, atan2f(a,b), a*b+b*a-a, sinf(a), cosf(a) (see fbr_selftest_math)."""
     a = np.ascontiguousarray(a, np.float32)

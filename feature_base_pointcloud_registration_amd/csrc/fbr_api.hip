@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -38,6 +39,12 @@ using namespace fbr;
   } while (0)
 
 namespace {
+
+// Host wall time since t0 into DebugCounters::host_ns[k] (fbr_diag_host_times).
+void host_time(int k, std::chrono::steady_clock::time_point t0) {
+  const auto ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  debug_counters().host_ns[k].fetch_add((long long)ns, std::memory_order_relaxed);
+}
 
 // Blocking host synchronisations, counted (fbr_debug_counters).
 hipError_t fbr_sync(hipStream_t s) {
@@ -626,7 +633,9 @@ int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool
   launch_pack_results(c->stream, B, with_reg ? 1 : 0, c->d_pose_out, c->d_stats, c->d_nvalid, c->d_ncorner, c->d_nsurf,
                       c->d_cropcnt, c->d_err, c->d_result);
   CK(hipMemcpyAsync(c->h_result, c->d_result, sizeof(JobResult) * B, hipMemcpyDeviceToHost, c->stream));
+  const auto tw = std::chrono::steady_clock::now();
   CK(fbr_sync(c->stream));
+  host_time(2, tw);
   // A capacity error in any job (features truncated) fails the call before anything is written:
   // poses_inout keeps the caller's guesses, as the reference leaves the pose on a failed scan.
   for (int j = 0; j < B; ++j)
@@ -1191,11 +1200,15 @@ int fbr_register(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corner, con
 int fbr_process_scan(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, double stamp, float pose_inout[6],
                      fbr_reg_stats* stats) {
   if (!c || !pose_inout || (n_in && !points)) return FBR_ERR_INVALID_ARG;
+  const auto t0 = std::chrono::steady_clock::now();
   CK(hipSetDevice(c->dev));
   drop_staged_batch(c);
   int rc = upload_scan(c, 0, points, n_in);
   if (rc) return rc;
-  return process_uploaded(c, stamp, pose_inout, stats);
+  host_time(0, t0);
+  rc = process_uploaded(c, stamp, pose_inout, stats);
+  host_time(3, t0);
+  return rc;
 }
 
 int fbr_process_msg(fbr_ctx* c, const fbr_pointcloud2* msg, double stamp, float pose_inout[6], fbr_reg_stats* stats,
@@ -1213,6 +1226,7 @@ namespace {
 // no host round trip (the features' capacity error is checked with the results); one packed copy
 // and one synchronisation return pose and stats.
 int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stats* stats) {
+  const auto t0 = std::chrono::steady_clock::now();
   int rc = stage_project(c, single_sub(c));
   if (!rc) rc = stage_features(c, single_sub(c), true);
   if (rc) return rc;
@@ -1227,6 +1241,7 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
     rc = stage_register(c, single_sub(c), false);
     if (rc) return rc;
   }
+  host_time(1, t0);
   rc = copy_results(c, 1, &st, pose, run);
   if (rc) return rc;  // capacity error: the pose stays the guess, the time gate is not consumed
   if (run) {
@@ -1510,6 +1525,16 @@ int fbr_debug_counters(long long* launches, long long* host_syncs, long long* fl
     d.launches = 0;
     d.host_syncs = 0;
     d.flag_polls = 0;
+  }
+  return FBR_OK;
+}
+
+// Diagnostic: host wall time (ns) of the single-scan calls since the last reset (DebugCounters).
+extern "C" int fbr_diag_host_times(long long* out4, int reset) {
+  DebugCounters& d = debug_counters();
+  for (int k = 0; k < 4; ++k) {
+    if (out4) out4[k] = d.host_ns[k].load();
+    if (reset) d.host_ns[k] = 0;
   }
   return FBR_OK;
 }

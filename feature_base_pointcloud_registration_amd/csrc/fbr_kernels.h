@@ -30,6 +30,9 @@ inline LaunchTimer& launch_timer() {
 // (stream syncs and synchronous copies of the boundary code) and Gauss-Newton flag polls.
 struct DebugCounters {
   std::atomic<long long> launches{0}, host_syncs{0}, flag_polls{0};
+  // host wall time (ns) of the single-scan calls: [0] scan upload (staging copy + enqueue),
+  // [1] enqueue of the stages (launches, GN flag polls), [2] result wait, [3] whole call
+  std::atomic<long long> host_ns[4] = {0, 0, 0, 0};
 };
 inline DebugCounters& debug_counters() {
   static DebugCounters c;
