@@ -16,13 +16,16 @@ from feature_base_pointcloud_registration_amd import api, synth  # noqa: E402
 from feature_base_pointcloud_registration_amd.fbr_types import default_params  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
-P = default_params(64, 1800, max_batch=B)
-cm, sm = synth.config_map("C2")
-jobs = synth.make_jobs("C2", B)
+CFG = os.environ.get("CFG", "C2")  # BASELINE config of the jobs and map
+P = synth.config_params(CFG, max_batch=B)
+cm, sm = synth.config_map(CFG)
+jobs = synth.make_jobs(CFG, B)
 L = api.lib()
 L.fbr_diag_knn_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
-for cell in (sys.argv[2:] or ["0.5"]):
-    os.environ["FBR_KNN_CELL"] = cell
+for cell in (sys.argv[2:] or ["0.5"]):  # "YZ" or "YZ/X" cell sizes in m
+    os.environ["FBR_KNN_CELL"] = cell.split("/")[0]
+    if "/" in cell:
+        os.environ["FBR_KNN_CELL_X"] = cell.split("/")[1]
     ctx = api.Context(P)
     ctx.set_map(cm, sm)
     ctx.batch_stage([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
