@@ -166,9 +166,21 @@ __device__ unsigned long long fbr_knn_stats[10];
 // absolute map index = sub (mod LPQ) (knn5_merge combines the lists).  A lane prunes with its own
 // 5th distance, which is never below the merged one (its list holds the 5 nearest of a subset),
 // so every point of the merged 5 nearest is still scanned by its lane.
-template <int R, int RX, bool kFlat = false, bool kSparse = false, int LPQ = 1>
+// LDS map tile (k_gn_knn_tile): the points of the cells [X0, X0 + NX1 - 1] of the rows
+// (Y0.., Z0..) copied to LDS in map order, and per row the LDS offsets of those cells' starts.
+struct TileView {
+  const float4* pts;  // LDS points
+  const int* cs;      // [row][NX1] LDS offset of cell X0 + j (j = NX1 - 1: the row end)
+  int X0, Y0, Z0, NX1, NY;
+};
+
+// kTile: the search reads the cells' point ranges and points from the workgroup's LDS tile (`tv`)
+// instead of the map grid in HBM; same rows, same ranges, same points in the same order.
+template <int R, int RX, bool kFlat = false, bool kSparse = false, int LPQ = 1, bool kTile = false>
 __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
-                          float bound, Knn5& r, unsigned* ks, int2* rows = nullptr, int sub = 0) {
+                          float bound, Knn5& r, unsigned* ks, int2* rows = nullptr, int sub = 0,
+                          const TileView* tv = nullptr) {
+  static_assert(!kTile || (!kFlat && !kSparse && LPQ == 1), "tile mode: dense grid, per-row loop");
   constexpr int K = 2 * R + 1;  // rows per side in y and z; RX = cells per side along x
 #pragma unroll
   for (int t = 0; t < 5; ++t) r.k[t] = kKnnEmpty;
@@ -231,7 +243,13 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       const int x0 = max(cx + xa, 0), x1 = min(cx + xb, X - 1);
       if (x0 > x1) continue;
       int b, e;
-      if (!row_range<kSparse>(m, y, z, x0, x1, b, e)) continue;
+      if constexpr (kTile) {
+        const int* cs = tv->cs + ((z - tv->Z0) * tv->NY + (y - tv->Y0)) * tv->NX1 - tv->X0;
+        b = cs[x0];
+        e = cs[x1 + 1];
+      } else if (!row_range<kSparse>(m, y, z, x0, x1, b, e)) {
+        continue;
+      }
       FBR_KS(2, 1);
       FBR_KS(3, e - b);
       // the whole row inside the crop box (pcl::CropBox, inclusive) -> no per-point test
@@ -242,7 +260,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         continue;
       }
       for (int i = LPQ == 1 ? b : b + ((sub - b) & (LPQ - 1)); i < e; i += LPQ) {
-        const float4 p = m.pts[i];
+        const float4 p = kTile ? tv->pts[i] : m.pts[i];
         // pcl::CropBox (inclusive) as one mask: a point outside gets d2 = +inf (never inserted)
         bool out = false;  // rows inside the box skip the test
         if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
@@ -665,6 +683,168 @@ k_gn_knn(GnArgs a, int use_prev) {
   }
 }
 
+// LDS-staged map tiles (dense maps: C3 / C5 mapping leaves).  The work item's 256
+// Morton-ordered queries are spatially compact, so their candidate cells overlap: the workgroup
+// takes the union box of the cells each query may visit (per axis, the cells whose lower-bound
+// distance is within min(warm-start bound, 1), the same float bounds the search prunes with),
+// copies those cells' points into LDS once with coalesced loads, and every lane then runs the
+// unchanged search over the LDS copy (same rows, same ranges, same points in the same order, so
+// the same neighbours).  Items whose box exceeds the tile capacity (iteration 0 has no warm-start
+// bound) search HBM as k_gn_knn does.  On dense maps the per-query point loads of the HBM search
+// miss L2 and wait on memory; from LDS they do not.
+constexpr int kTilePts = 2048;  // float4 points per tile (32 KB of dynamic LDS)
+constexpr int kTileCs = 2048;   // row cell offsets per tile
+constexpr int kTileRows = 256;  // (y, z) rows per tile
+
+template <int R, int RX>
+__global__ void __launch_bounds__(kResThreads)
+k_gn_knn_tile(GnArgs a, int use_prev) {
+  extern __shared__ float4 tpts[];        // [kTilePts]
+  __shared__ int tcs[kTileCs];
+  __shared__ int rowoff[kTileRows + 1];   // per tile row: LDS offset of its points
+  __shared__ int rowgb[kTileRows];        // per tile row: map index of its first point
+  __shared__ int box[6];                  // X0, Y0, Z0, X1, Y1, Z1 (cells)
+  const int tid = threadIdx.x;
+  const int nitems = a.nitems[0];
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int4 item = a.items[it];
+    const int job = item.x;
+    const GnState& g = a.gn[job];
+    if (!g.active) continue;  // block-uniform
+    const bool corner = item.y == 0;
+    const MapGrid& mg = corner ? a.mc : a.ms;
+    const bool valid = tid < item.w;
+    float x0 = 0.0f, y0 = 0.0f, z0 = 0.0f, bound = __int_as_float(0x7f800000);
+    int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
+    int32_t oid[5] = {-1, -1, -1, -1, -1};
+    bool have_prev = false;
+    if (tid < 6) box[tid] = tid < 3 ? INT_MAX : INT_MIN;
+    __syncthreads();
+    if (valid) {
+      const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
+      const float* T = g.T;
+      x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];  // pointAssociateToMap (:397-403)
+      y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
+      z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
+      have_prev = use_prev && o[0] >= 0;
+      if (have_prev) {
+        float mx = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) oid[k] = o[k * kResThreads];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const float4 q = mg.by_id[oid[k]];
+          float dist = 0.0f, diff;
+          diff = x0 - q.x; dist += diff * diff;
+          diff = y0 - q.y; dist += diff * diff;
+          diff = z0 - q.z; dist += diff * diff;
+          mx = fmaxf(mx, dist);
+        }
+        bound = mx;
+      }
+      // the cells this query may visit (knn5_grid's cell arithmetic and lower bounds)
+      const float inv = mg.g.inv_cell, c = 1.0f / inv, invx = mg.g.inv_x, cxs = 1.0f / invx;
+      const float sx = x0 * invx, sy = y0 * inv, sz = z0 * inv;
+      const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+      if (fabsf(fx) < 1e7f && fabsf(fy) < 1e7f && fabsf(fz) < 1e7f) {
+        const int cx = (int)fx - (int)mg.g.origin[0], cy = (int)fy - (int)mg.g.origin[1], cz = (int)fz - (int)mg.g.origin[2];
+        if (!(cx < -RX || cy < -R || cz < -R || cx >= mg.g.dims[0] + RX || cy >= mg.g.dims[1] + R ||
+              cz >= mg.g.dims[2] + R)) {
+          const float Bp = fminf(bound, kBelowOne);
+          int ylo = 0, yhi = 0, zlo = 0, zhi = 0, xlo = 0, xhi = 0;
+#pragma unroll
+          for (int oo = 1; oo <= R; ++oo) {
+            float l;
+            l = axis_lb(y0, fy, -oo, c); if (l * l <= Bp) ylo = -oo;
+            l = axis_lb(y0, fy, oo, c); if (l * l <= Bp) yhi = oo;
+            l = axis_lb(z0, fz, -oo, c); if (l * l <= Bp) zlo = -oo;
+            l = axis_lb(z0, fz, oo, c); if (l * l <= Bp) zhi = oo;
+          }
+#pragma unroll
+          for (int oo = 1; oo <= RX; ++oo) {
+            float l;
+            l = axis_lb(x0, fx, -oo, cxs); if (l * l <= Bp) xlo = -oo;
+            l = axis_lb(x0, fx, oo, cxs); if (l * l <= Bp) xhi = oo;
+          }
+          atomicMin(&box[0], cx + xlo);
+          atomicMin(&box[1], cy + ylo);
+          atomicMin(&box[2], cz + zlo);
+          atomicMax(&box[3], cx + xhi);
+          atomicMax(&box[4], cy + yhi);
+          atomicMax(&box[5], cz + zhi);
+        }
+      }
+    }
+    __syncthreads();
+    // clamp to the grid (the search skips cells outside it) and size the tile
+    const int X0 = max(box[0], 0), Y0 = max(box[1], 0), Z0 = max(box[2], 0);
+    const int X1 = min(box[3], mg.g.dims[0] - 1), Y1 = min(box[4], mg.g.dims[1] - 1), Z1 = min(box[5], mg.g.dims[2] - 1);
+    const int NX1 = X1 - X0 + 2, NY = Y1 - Y0 + 1, NZ = Z1 - Z0 + 1;
+    bool tile = X1 >= X0 && Y1 >= Y0 && Z1 >= Z0 && NY * NZ <= kTileRows && NY * NZ * NX1 <= kTileCs;
+    if (tile) {
+      const int rows = NY * NZ;
+      for (int e = tid; e < rows * NX1; e += kResThreads) {  // global cell starts of the tile rows
+        const int t = e / NX1, j = e - t * NX1;
+        const int y = Y0 + t % NY, z = Z0 + t / NY;
+        tcs[e] = mg.cell_start[(z * mg.g.dims[1] + y) * mg.g.dims[0] + X0 + j];
+      }
+      __syncthreads();
+      if (tid < 64) {  // exclusive prefix of the row point counts (one wave)
+        int carry = 0;
+        for (int t0 = 0; t0 < rows; t0 += 64) {
+          const int t = t0 + tid;
+          const int cnt = t < rows ? tcs[t * NX1 + NX1 - 1] - tcs[t * NX1] : 0;
+          int inc = cnt;
+          for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(inc, d);
+            if (tid >= d) inc += v;
+          }
+          if (t < rows) rowoff[t] = carry + inc - cnt;
+          carry += __shfl(inc, 63);
+        }
+        if (tid == 0) rowoff[rows] = carry;
+      }
+      __syncthreads();
+      tile = rowoff[rows] <= kTilePts;
+      if (tile) {
+        // copy the rows' points (coalesced), then turn the cell starts into LDS offsets
+        for (int t = 0; t < rows; ++t) {
+          const int gb = tcs[t * NX1], n = tcs[t * NX1 + NX1 - 1] - gb, lo = rowoff[t];
+          for (int i = tid; i < n; i += kResThreads) tpts[lo + i] = mg.pts[gb + i];
+          if (tid == 0) rowgb[t] = gb;
+        }
+        __syncthreads();
+        for (int e = tid; e < rows * NX1; e += kResThreads) {
+          const int t = e / NX1;
+          tcs[e] = rowoff[t] + (tcs[e] - rowgb[t]);
+        }
+      }
+    }
+    __syncthreads();
+    if (valid) {
+      Knn5 nn;
+      unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      if (tile) {
+        const TileView tv{tpts, tcs, X0, Y0, Z0, NX1, NY};
+        knn5_grid<R, RX, false, false, 1, true>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks, nullptr, 0, &tv);
+      } else {
+        knn5_grid<R, RX, false, false>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
+      }
+      (void)ks;
+      const bool ok = nn.k[4] < kKnnEmpty;
+      bool same = have_prev && ok && a.fit_cache;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int id = knn_id(nn.k[k]);
+        same = same && id == oid[k];
+        o[k * kResThreads] = ok ? id : -1;
+      }
+      a.nsame[(int64_t)it * kResThreads + tid] = same ? 1 : 0;
+    }
+    __syncthreads();  // the next item reuses the tile
+  }
+}
+
 // The normal equations of one job in float, as LMOptimization forms them (matAtA / matAtB).
 __device__ __forceinline__ void gn_normal_eq(const double* acc, float* AtA, float* X) {
   int q = 0;
@@ -950,10 +1130,33 @@ bool knn_flat() {
   return v;
 }
 
+// LDS map tiles (FBR_KNN_TILE = 0 / 1; default on for dense maps, y/z cells below 1 m, i.e. the
+// C3 / C5 mapping leaves): the plain kNN pass on dense grids.
+bool knn_tile(const GnArgs& a) {
+  static const int forced = [] {
+    const char* e = std::getenv("FBR_KNN_TILE");
+    return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
+  }();
+  if (a.mc.g.sparse || a.ms.g.sparse) return false;
+  return forced >= 0 ? forced == 1 : a.mc.g.inv_cell > 1.0f;
+}
+
+template <int R, int RX>
+void launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
+  fbr_launch((k_gn_knn_tile<R, RX>), dim3(grid), dim3(kResThreads), (uint32_t)(sizeof(float4) * kTilePts), s, a, use_prev);
+}
+
 template <int R, bool F>
 void launch_gn_knn_r(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
   if constexpr (!F) {
     if (knn_lpq(a.B) == 8) return launch_gn_knn_rl<R, F, false, 8>(s, a, grid, use_prev);
+    if (knn_tile(a)) {
+      const float invx = a.mc.g.inv_x;
+      if (invx > 4.0f) return launch_gn_knn_tile<R, 8>(s, a, grid, use_prev);
+      if (invx > 2.0f) return launch_gn_knn_tile<R, 4>(s, a, grid, use_prev);
+      if (invx > 1.0f) return launch_gn_knn_tile<R, 2>(s, a, grid, use_prev);
+      return launch_gn_knn_tile<R, 1>(s, a, grid, use_prev);
+    }
   }
   if constexpr (R == 1 && !F) {
     if (use_prev && knn_flat()) return launch_gn_knn_rl<R, F, true>(s, a, grid, use_prev);
