@@ -439,6 +439,9 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   const int64_t j0 = sb.j0, HW = c->HW, ib = j0 * c->items_per_job;
   const int mi = std::max(1, c->P.max_iterations);
   GnArgs a{};
+#ifdef FBR_KNN_STATS
+  a.knn_stats = knn_stats_buffer();
+#endif
   a.B = sb.B;
   a.max_iter = c->P.max_iterations;
   a.cornerDS = c->d_cornerDS + j0 * HW;

@@ -1,0 +1,589 @@
+// fbr_gn.h — device side of the Gauss-Newton correspondence search (A13-A15), shared by
+// k_register.hip (init, residual, solve, finalize) and the k_knn_*.hip translation units, which
+// instantiate the kNN kernels per cell radius R and fused flag (the instantiations compile in
+// parallel; one file holding all of them took ~8 minutes).  See k_register.hip for the design
+// notes and reference citations (mapOptmization.h:1002-1243, :1403-1442).
+#pragma once
+#include <cstdlib>
+
+#include "fbr_common.h"
+#include "fbr_kernels.h"
+#include "fbr_solvers.h"
+
+namespace fbr {
+
+namespace {
+constexpr int kResThreads = 256;
+constexpr int kSolveThreads = 128;  // k_gn_solve: wave 0 sums + solves, wave 1 the iteration-0 degeneracy
+constexpr int kPartial = 32;  // doubles per item partial: 21 AtA upper + 6 AtB + count
+}
+// The 5 nearest as sorted 64-bit keys (float bits of d2) << 32 | map index: d2 >= +0, so the
+// unsigned key order is exactly FLANN's (d2, index) order.  A key is built from a scanned point
+// without any instruction (hi = the distance register, lo = the w bit pattern).  Empty slots hold
+// kKnnEmpty = (bits(1.0f), 0): a point is only inserted with d2 < 1.0 (:1027, :1154).
+constexpr unsigned long long kKnnEmpty = (unsigned long long)0x3f800000u << 32;
+constexpr float kBelowOne = 0.99999994f;  // nextafterf(1.0f, 0.0f)
+
+struct Knn5 {
+  unsigned long long k[5];
+};
+
+__device__ __forceinline__ float knn_d(unsigned long long k) { return __int_as_float((int)(k >> 32)); }
+__device__ __forceinline__ int knn_id(unsigned long long k) { return (int)(unsigned)k; }
+
+// Branch-free sorted insertion: the "less than slot t" flags are monotone over t, so every slot
+// takes its own key, its left neighbour's, or the new one (5 compares + 20 selects, no SALU mask
+// arithmetic and no serial compare-swap chain).
+__device__ __forceinline__ void knn_insert(Knn5& r, unsigned long long x) {
+  bool lt[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) lt[t] = x < r.k[t];
+#pragma unroll
+  for (int t = 4; t > 0; --t) r.k[t] = lt[t - 1] ? r.k[t - 1] : (lt[t] ? x : r.k[t]);  // lt[t-1] implies lt[t]
+  r.k[0] = lt[0] ? x : r.k[0];
+}
+
+// Lower bound of |q - p| along one axis for a point p in the cell at offset o from q's cell
+// (cells are [k*c, (k+1)*c) with c a power of two, so every edge is exact).  Rounding is
+// monotone, so fl(edge - q) <= |fl(q - p)| and the bound composed in the distance's own
+// operation order never exceeds the distance computed for any point of that cell.
+__device__ __forceinline__ float axis_lb(float q, float fcell, int o, float c) {
+  if (o == 0) return 0.0f;
+  if (o > 0) return (fcell + (float)o) * c - q;
+  return q - (fcell + (float)(o + 1)) * c;
+}
+
+__device__ __forceinline__ int rank_offset(int k, int s) { return k == 0 ? 0 : ((k & 1) ? s * ((k + 1) >> 1) : -s * (k >> 1)); }
+
+// Sparse grids (k_grid.hip): the chunk of (z, y, x / kChunkX), or -1.  The table is at most half
+// full, so a free slot ends every probe sequence.
+__device__ __forceinline__ int chunk_find(const MapGrid& m, int z, int y, int xc) {
+  const unsigned long long key = chunk_key(z, y, xc);
+  uint32_t h = chunk_hash(key) & m.g.hmask;
+  for (uint32_t probe = 0; probe <= m.g.hmask; ++probe) {
+    const unsigned long long k = m.hkeys[h];
+    if (k == key) return m.hvals[h];
+    if (k == kChunkEmpty) break;
+    h = (h + 1) & m.g.hmask;
+  }
+  return -1;
+}
+
+// Point range [b, e) of the cells x0..x1 (x1 - x0 < 2 * kChunkX) of row (y, z).  The two chunks
+// are adjacent in the (z, y, x) sort, so their points form one contiguous range.
+template <bool kSparse>
+__device__ __forceinline__ bool row_range(const MapGrid& m, int y, int z, int x0, int x1, int& b, int& e) {
+  if constexpr (!kSparse) {
+    const int rowbase = (z * m.g.dims[1] + y) * m.g.dims[0];
+    b = m.cell_start[rowbase + x0];
+    e = m.cell_start[rowbase + x1 + 1];
+    return true;
+  } else {
+    const int ca = x0 / kChunkX, cb = x1 / kChunkX;
+    const int ia = chunk_find(m, z, y, ca);
+    const int ib = cb == ca ? ia : chunk_find(m, z, y, cb);
+    if (ia < 0 && ib < 0) return false;
+    constexpr int S = kChunkX + 1;
+    b = ia >= 0 ? m.cell_start[ia * S + (x0 - ca * kChunkX)] : m.cell_start[ib * S];
+    e = ib >= 0 ? m.cell_start[ib * S + (x1 - cb * kChunkX) + 1] : m.cell_start[ia * S + kChunkX];
+    return true;
+  }
+}
+
+#ifdef FBR_KNN_STATS
+// Diagnostic builds only (tools/knn_stats.py): [queries, rows considered, rows scanned, points
+// scanned, points inserted, accepted queries, corner queries, wave iterations of the point loop,
+// warm-started queries, queries whose neighbours equal the previous iteration's], accumulated into
+// GnArgs::knn_stats (one device buffer for every kNN translation unit)
+#define FBR_KS(i, v) ks[i] += (v)
+#else
+#define FBR_KS(i, v) \
+  do {               \
+  } while (0)
+#endif
+
+// Exact kNN-5 among map points inside the crop box with d2 < 1.0, ordered by (d2, map index):
+// the neighbour set FLANN's exact search returns on the cropped cloud whenever the reference
+// keeps the correspondence (pointSearchSqDis[4] < 1.0, :1027/:1154).  R = cells per side covering
+// radius 1 (compile time: the row loop is fully unrolled).  Cell rows (y,z) are visited in
+// near-side-first rank order; a row, and the cells of a row, are skipped once their lower-bound
+// distance exceeds the current 5th distance or reaches 1.0.  Rows entirely inside the crop box
+// skip the per-point box test.
+// `bound` is an upper bound of the 5th-neighbour distance known before the search (the largest
+// distance to the previous iteration's 5 neighbours, 5 distinct candidates of the same crop box):
+// cells whose lower bound exceeds it cannot hold any of the 5 nearest, ties included, so they are
+// pruned from the start instead of only once 5 points have been inserted.
+// kFlat: the rows are pruned once up front with `bound` (the warm start, tight from iteration 1
+// on) and their point ranges queued in LDS (`rows`, stride kResThreads); one loop then walks a
+// lane's queued points across rows.  A wave then runs for its longest lane's total instead of the
+// sum over rows of each row's longest lane (lanes of a wave scan different rows: the per-row loop
+// kept ~30 % of the lanes busy).  Pruning with a larger cut only scans more cells, and the 5-NN
+// list is a function of the scanned set, so both forms give the same neighbours.
+// LPQ > 1 (wide mode, small launches): LPQ lanes share a query and lane `sub` scans the points of
+// absolute map index = sub (mod LPQ) (knn5_merge combines the lists).  A lane prunes with its own
+// 5th distance, which is never below the merged one (its list holds the 5 nearest of a subset),
+// so every point of the merged 5 nearest is still scanned by its lane.
+template <int R, int RX, bool kFlat = false, bool kSparse = false, int LPQ = 1>
+__device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
+                          float bound, Knn5& r, unsigned* ks, int2* rows = nullptr, int sub = 0) {
+  constexpr int K = 2 * R + 1;  // rows per side in y and z; RX = cells per side along x
+#pragma unroll
+  for (int t = 0; t < 5; ++t) r.k[t] = kKnnEmpty;
+  const float inv = m.g.inv_cell, c = 1.0f / inv, invx = m.g.inv_x, cxs = 1.0f / invx;
+  const float sx = qx * invx, sy = qy * inv, sz = qz * inv;
+  const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+  if (!(fabsf(fx) < 1e7f && fabsf(fy) < 1e7f && fabsf(fz) < 1e7f)) return;
+  const int cx = (int)fx - (int)m.g.origin[0], cy = (int)fy - (int)m.g.origin[1], cz = (int)fz - (int)m.g.origin[2];
+  const int X = m.g.dims[0], Y = m.g.dims[1], Z = m.g.dims[2];
+  if (cx < -RX || cy < -R || cz < -R || cx >= X + RX || cy >= Y + R || cz >= Z + R) return;
+  const int sgy = (sy - fy) >= 0.5f ? 1 : -1, sgz = (sz - fz) >= 0.5f ? 1 : -1;
+  // squared per-axis lower bounds: y/z by visit rank, x by offset (negative / positive side)
+  float ly2[K], lz2[K], lxm2[RX + 1], lxp2[RX + 1];
+  int oyk[K], ozk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    oyk[k] = rank_offset(k, sgy);
+    ozk[k] = rank_offset(k, sgz);
+    const float ly = axis_lb(qy, fy, oyk[k], c), lz = axis_lb(qz, fz, ozk[k], c);
+    ly2[k] = ly * ly;
+    lz2[k] = lz * lz;
+  }
+#pragma unroll
+  for (int o = 1; o <= RX; ++o) {
+    const float a = axis_lb(qx, fx, -o, cxs), b = axis_lb(qx, fx, o, cxs);
+    lxm2[o] = a * a;
+    lxp2[o] = b * b;
+  }
+  // the crop box in registers (per job: wave-uniform)
+  const float bx0 = bmin[0], by0 = bmin[1], bz0 = bmin[2], bx1 = bmax[0], by1 = bmax[1], bz1 = bmax[2];
+  const float xlo = (fx - (float)RX) * cxs, xhi = (fx + (float)(RX + 1)) * cxs;  // row x extent (max)
+  const bool xin = xlo >= bx0 && xhi <= bx1;
+  int nrow = 0;  // kFlat: rows queued
+#pragma unroll
+  for (int ksum = 0; ksum <= 2 * (K - 1); ++ksum) {
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const int kz = ksum - ky;
+      if (kz < 0 || kz >= K) continue;  // compile time
+      const int y = cy + oyk[ky], z = cz + ozk[kz];
+      FBR_KS(1, 1);
+      float lb = 0.0f;
+      lb += ly2[ky];
+      lb += lz2[kz];
+      // "lb <= cut and lb < 1.0" as one compare: the largest float below 1.0 caps the cut
+      const float cut = fminf(fminf(knn_d(r.k[4]), bound), kBelowOne);
+      if (y < 0 || y >= Y || z < 0 || z >= Z || lb > cut) continue;
+      int xa = 0, xb = 0;
+      bool go_a = true, go_b = true;
+#pragma unroll
+      for (int o = 1; o <= RX; ++o) {
+        float ta = 0.0f, tb = 0.0f;
+        ta += lxm2[o]; ta += ly2[ky]; ta += lz2[kz];
+        tb += lxp2[o]; tb += ly2[ky]; tb += lz2[kz];
+        go_a = go_a && !(ta > cut);
+        go_b = go_b && !(tb > cut);
+        if (go_a) xa = -o;
+        if (go_b) xb = o;
+      }
+      const int x0 = max(cx + xa, 0), x1 = min(cx + xb, X - 1);
+      if (x0 > x1) continue;
+      int b, e;
+      if (!row_range<kSparse>(m, y, z, x0, x1, b, e)) continue;
+      FBR_KS(2, 1);
+      FBR_KS(3, e - b);
+      // the whole row inside the crop box (pcl::CropBox, inclusive) -> no per-point test
+      const float ylo = (fy + (float)oyk[ky]) * c, zlo = (fz + (float)ozk[kz]) * c;
+      const bool inside = xin & (ylo >= by0) & (ylo + c <= by1) & (zlo >= bz0) & (zlo + c <= bz1);
+      if constexpr (kFlat) {
+        if (e > b) rows[nrow++ * kResThreads] = make_int2(b, inside ? (int)((unsigned)e | 0x80000000u) : e);
+        continue;
+      }
+      for (int i = LPQ == 1 ? b : b + ((sub - b) & (LPQ - 1)); i < e; i += LPQ) {
+        const float4 p = m.pts[i];
+        // pcl::CropBox (inclusive) as one mask: a point outside gets d2 = +inf (never inserted)
+        bool out = false;  // rows inside the box skip the test
+        if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
+        float dist = 0.0f, diff;
+        diff = qx - p.x; dist += diff * diff;                            // flann::L2_Simple
+        diff = qy - p.y; dist += diff * diff;
+        diff = qz - p.z; dist += diff * diff;
+        const unsigned hi = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
+        FBR_KS(4, __int_as_float((int)hi) < knn_d(r.k[4]) ? 1 : 0);
+#ifdef FBR_KNN_STATS
+        if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ks[7] += 1;  // one per wave iteration
+#endif
+        knn_insert(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
+      }
+    }
+  }
+  if constexpr (kFlat) {
+    int j = 0, i = 0, e = 0;
+    bool inside = true;
+    while (true) {
+      if (i >= e) {  // next queued row (every queued row is non-empty)
+        if (j >= nrow) break;
+        const int2 q = rows[j++ * kResThreads];
+        i = q.x;
+        e = q.y & 0x7fffffff;
+        inside = q.y < 0;
+      }
+      const float4 p = m.pts[i++];
+      bool out = false;
+      if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
+      float dist = 0.0f, diff;
+      diff = qx - p.x; dist += diff * diff;  // flann::L2_Simple
+      diff = qy - p.y; dist += diff * diff;
+      diff = qz - p.z; dist += diff * diff;
+      const unsigned hi = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
+      FBR_KS(4, __int_as_float((int)hi) < knn_d(r.k[4]) ? 1 : 0);
+#ifdef FBR_KNN_STATS
+      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ks[7] += 1;  // one per wave iteration
+#endif
+      knn_insert(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
+    }
+  }
+}
+
+// Wide mode: the LPQ lanes of a query (consecutive lanes) exchange their lists in a butterfly and
+// each keeps the 5 smallest keys of the union (the lanes scanned disjoint point sets, so keys are
+// distinct and the result is the 5 nearest of the whole scanned set).
+template <int LPQ>
+__device__ __forceinline__ void knn5_merge(Knn5& r) {
+#pragma unroll
+  for (int off = 1; off < LPQ; off <<= 1) {
+    unsigned long long o[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const unsigned lo = __shfl_xor((unsigned)r.k[t], off), hi = __shfl_xor((unsigned)(r.k[t] >> 32), off);
+      o[t] = ((unsigned long long)hi << 32) | lo;
+    }
+#pragma unroll
+    for (int t = 0; t < 5; ++t) knn_insert(r, o[t]);
+  }
+}
+
+// cornerOptimization body (:1016-1121): coefficient row for one corner query, false if rejected.
+struct Nbr5 {
+  float x[5], y[5], z[5];
+};
+
+// The part of a correspondence that depends only on its 5 map neighbours: the corner line (two
+// points 0.1 along the principal axis through the mean, after the eigenvalue-ratio gate) or the
+// plane (pa, pb, pc, pd after the 0.2 m check).  A query whose kNN returns the same 5 neighbours as
+// in the previous Gauss-Newton iteration reuses it (bit-identical: same inputs, same operations);
+// only the query-dependent residual below is recomputed.  f[0..5]; false = rejected.
+__device__ bool corner_fit(const Nbr5& nn, float* f) {
+  float cx = 0, cy = 0, cz = 0;
+  for (int j = 0; j < 5; j++) { cx += nn.x[j]; cy += nn.y[j]; cz += nn.z[j]; }
+  cx /= 5.0f; cy /= 5.0f; cz /= 5.0f;
+  float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+  for (int j = 0; j < 5; j++) {
+    const float ax = nn.x[j] - cx, ay = nn.y[j] - cy, az = nn.z[j] - cz;
+    a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
+    a22 += ay * ay; a23 += ay * az;
+    a33 += az * az;
+  }
+  a11 /= 5.0f; a12 /= 5.0f; a13 /= 5.0f; a22 /= 5.0f; a23 /= 5.0f; a33 /= 5.0f;
+  float A1[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33};
+  float D1[3], V1[9];
+  jacobi_eigen<3>(A1, D1, V1);
+  if (!(D1[0] > 3.0f * D1[1])) return false;
+  f[0] = (float)((double)cx + 0.1 * (double)V1[0]);
+  f[1] = (float)((double)cy + 0.1 * (double)V1[1]);
+  f[2] = (float)((double)cz + 0.1 * (double)V1[2]);
+  f[3] = (float)((double)cx - 0.1 * (double)V1[0]);
+  f[4] = (float)((double)cy - 0.1 * (double)V1[1]);
+  f[5] = (float)((double)cz - 0.1 * (double)V1[2]);
+  return true;
+}
+
+// cornerOptimization's residual (:1083-1112) of query (x0, y0, z0) against the fitted line.
+__device__ bool corner_apply(const float* f, float x0, float y0, float z0, float4& coeff) {
+  const float x1 = f[0], y1 = f[1], z1 = f[2], x2 = f[3], y2 = f[4], z2 = f[5];
+  const float a012 = sqrt_rn(((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) +
+                                ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) +
+                                ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1)) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1)));
+  const float l12 = sqrt_rn((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
+  const float la = ((y1 - y2) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) +
+                    (z1 - z2) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1))) / a012 / l12;
+  const float lb = -((x1 - x2) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) -
+                     (z1 - z2) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1))) / a012 / l12;
+  const float lc = -((x1 - x2) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) +
+                     (y1 - y2) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1))) / a012 / l12;
+  const float ld2 = a012 / l12;
+  const float s = (float)(1.0 - 0.9 * (double)fabsf(ld2));
+  coeff = make_float4(s * la, s * lb, s * lc, s * ld2);
+  return (double)s > 0.1;
+}
+
+// surfOptimization's plane (:1145-1186): f[0..3] = (pa, pb, pc, pd); false when a neighbour is
+// more than 0.2 from it.
+__device__ bool surf_fit(const Nbr5& nn, float* f) {
+  float A0[5][3], B0[5], X0[3];
+  for (int j = 0; j < 5; j++) { A0[j][0] = nn.x[j]; A0[j][1] = nn.y[j]; A0[j][2] = nn.z[j]; B0[j] = -1.0f; }
+  colpiv_solve53(A0, B0, X0);
+  float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1.0f;
+  const float ps = sqrt_rn(pa * pa + pb * pb + pc * pc);
+  pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+  for (int j = 0; j < 5; j++)
+    if ((double)fabsf(pa * nn.x[j] + pb * nn.y[j] + pc * nn.z[j] + pd) > 0.2) return false;
+  f[0] = pa; f[1] = pb; f[2] = pc; f[3] = pd;
+  return true;
+}
+
+// surfOptimization's residual (:1198-1211) of query (x0, y0, z0) against the plane.
+__device__ bool surf_apply(const float* f, float x0, float y0, float z0, float4& coeff) {
+  const float pa = f[0], pb = f[1], pc = f[2], pd = f[3];
+  const float pd2 = pa * x0 + pb * y0 + pc * z0 + pd;
+  const float s = (float)(1.0 - 0.9 * (double)fabsf(pd2) /
+                                    (double)sqrt_rn(sqrt_rn(x0 * x0 + y0 * y0 + z0 * z0)));
+  coeff = make_float4(s * pa, s * pb, s * pc, s * pd2);
+  return (double)s > 0.1;
+}
+
+// Normal-equation product k of one row: 0-20 the upper AtA triangle, 21-26 AtB, 27 the count,
+// 28-31 zero (compile-time k after unrolling).
+__device__ __forceinline__ double res_product(int k, const float* row, float b, bool ok) {
+  constexpr int kR[21] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 5};
+  constexpr int kC[21] = {0, 1, 2, 3, 4, 5, 1, 2, 3, 4, 5, 2, 3, 4, 5, 3, 4, 5, 4, 5, 5};
+  if (k < 21) return (double)row[kR[k]] * (double)row[kC[k]];
+  if (k < 27) return (double)row[k - 21] * (double)b;
+  if (k == 27) return ok ? 1.0 : 0.0;
+  return 0.0;
+}
+
+// One transposed-butterfly step: H values per lane -> H/2 (the lower lane of each OFF pair keeps
+// the first half, the upper lane the second).
+template <int H, int OFF>
+__device__ __forceinline__ void res_halve(double* v, int lane) {
+  const bool up = (lane & OFF) != 0;
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    const double lo = v[j], hi = v[j + H];
+    v[j] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, OFF);
+  }
+}
+
+// cornerOptimization / surfOptimization + the LMOptimization row (:1286-1332) of one query whose 5
+// neighbours are the map points nb[0..4] (map indices); false when the correspondence is rejected.
+// fc / fs: the query's fit cache (fit floats at stride kResThreads, state 0 none / 1 fitted /
+// 2 rejected); same: the neighbours equal the previous iteration's, whose fit the cache holds.
+__device__ __forceinline__ bool res_row(const GnState& g, const float4* by_id, const int32_t* nb, int stride,
+                                        bool corner, const float4& p, float x0, float y0, float z0, float* row,
+                                        float& b, float* fc, int8_t* fs, bool same) {
+  float fit[6];
+  bool fit_ok;
+  const int8_t st = same ? *fs : (int8_t)0;
+  if (st != 0) {
+    fit_ok = st == 1;
+    if (fit_ok) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) fit[k] = fc[k * kResThreads];
+    }
+  } else {
+    Nbr5 nn;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const float4 q = by_id[nb[k * stride]];
+      nn.x[k] = q.x; nn.y[k] = q.y; nn.z[k] = q.z;
+    }
+    fit_ok = corner ? corner_fit(nn, fit) : surf_fit(nn, fit);
+    *fs = fit_ok ? 1 : 2;
+    if (fit_ok) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        if (corner || k < 4) fc[k * kResThreads] = fit[k];
+    }
+  }
+  if (!fit_ok) return false;
+  float4 c;
+  const bool ok = corner ? corner_apply(fit, x0, y0, z0, c) : surf_apply(fit, x0, y0, z0, c);
+  if (ok) {
+    // camera-frame swap
+    const float srx = g.trig[0], crx = g.trig[1], sry = g.trig[2], cry = g.trig[3], srz = g.trig[4], crz = g.trig[5];
+    const float pox = p.y, poy = p.z, poz = p.x;
+    const float cox = c.y, coy = c.z, coz = c.x;
+    const float arx = (crx * sry * srz * pox + crx * crz * sry * poy - srx * sry * poz) * cox +
+                      (-srx * srz * pox - crz * srx * poy - crx * poz) * coy +
+                      (crx * cry * srz * pox + crx * cry * crz * poy - cry * srx * poz) * coz;
+    const float ary = ((cry * srx * srz - crz * sry) * pox + (sry * srz + cry * crz * srx) * poy + crx * cry * poz) * cox +
+                      ((-cry * crz - srx * sry * srz) * pox + (cry * srz - crz * srx * sry) * poy - crx * sry * poz) * coz;
+    const float arz = ((crz * srx * sry - cry * srz) * pox + (-cry * crz - srx * sry * srz) * poy) * cox +
+                      (crx * crz * pox - crx * srz * poy) * coy +
+                      ((sry * srz + cry * crz * srx) * pox + (crz * sry - cry * srx * srz) * poy) * coz;
+    row[0] = arz; row[1] = arx; row[2] = ary; row[3] = coz; row[4] = cox; row[5] = coy;
+    b = -c.w;
+  }
+  return ok;
+}
+
+// The item's fp64 normal-equation partial (21 upper AtA entries, 6 AtB, count; 4 zero pads):
+// every lane of the workgroup calls this with its row (zeros when it has none).  The wave sum is a
+// transposed butterfly: at each halving step a lane keeps half of its values and trades the other
+// half with its partner, so 32 values cost 32 shuffles instead of 6 per value.  Lane l (bit 0
+// clear) ends with the wave sum of value res_index(l); the 4 wave sums are added in LDS.
+__device__ __forceinline__ void res_reduce(double (*red)[28], int tid, const float* row, float b, bool ok,
+                                           double* out) {
+  const int lane = tid & 63, wave = tid >> 6;
+  double v[16];
+  const bool up5 = (lane & 32) != 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const double lo = res_product(j, row, b, ok), hi = res_product(j + 16, row, b, ok);
+    v[j] = (up5 ? hi : lo) + __shfl_xor(up5 ? lo : hi, 32);
+  }
+  res_halve<8, 16>(v, lane);
+  res_halve<4, 8>(v, lane);
+  res_halve<2, 4>(v, lane);
+  res_halve<1, 2>(v, lane);
+  v[0] += __shfl_xor(v[0], 1);
+  const int ridx = ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 +
+                   ((lane >> 1) & 1);
+  if (!(lane & 1) && ridx < 28) red[wave][ridx] = v[0];
+  __syncthreads();
+  if (tid < 28) {
+    double s = 0.0;
+    for (int w = 0; w < kResThreads / 64; ++w) s += red[w][tid];
+    out[tid] = s;
+  }
+  __syncthreads();
+}
+
+// kNN pass: one lane per query, writes the 5 neighbour map indices (slot 0 = -1: no correspondence).
+// R = grid cells per side covering radius 1 (both map grids share one cell size).  kFused: the
+// same lane goes on to its residual row and the workgroup reduces the item's normal-equation
+// partial (k_gn_residual's work, without re-reading the query and its neighbour indices).
+// LPQ > 1 (wide mode, launches with few queries: single scans, tiny batches; neither fused nor
+// flat): a workgroup covers 256 / LPQ queries of an item with LPQ lanes each, so a query's search
+// chain is LPQ times shorter; lane `sub` == 0 of each query writes the results.
+template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ = 1>
+__global__ void __launch_bounds__(kResThreads)
+k_gn_knn(GnArgs a, int use_prev) {
+  static_assert(LPQ == 1 || (!kFused && !kFlat), "wide mode is the plain kNN pass");
+  __shared__ double red[kFused ? kResThreads / 64 : 1][28];
+  __shared__ int2 rows[kFlat ? (2 * R + 1) * (2 * R + 1) : 1][kResThreads];
+  constexpr int QPB = kResThreads / LPQ;  // queries per workgroup
+  const int sub = (int)threadIdx.x % LPQ;
+  const int nitems = a.nitems[0];
+  for (int v = blockIdx.x; v < nitems * LPQ; v += gridDim.x) {
+    const int it = v / LPQ;
+    const int tid = (v % LPQ) * QPB + (int)threadIdx.x / LPQ;  // query slot within the item
+    const int4 item = a.items[it];
+    const int job = item.x;
+    const GnState& g = a.gn[job];
+    if (!g.active) continue;  // block-uniform
+    float row[6] = {0, 0, 0, 0, 0, 0}, b = 0.0f;
+    bool rok = false;
+    if (tid < item.w) {
+      const bool corner = item.y == 0;
+      const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
+      const float* T = g.T;
+      // pointAssociateToMap (:397-403)
+      const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
+      const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
+      const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
+      const MapGrid& mg = corner ? a.mc : a.ms;
+      int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
+      float bound = __int_as_float(0x7f800000);
+      int32_t oid[5] = {-1, -1, -1, -1, -1};
+      const bool have_prev = use_prev && o[0] >= 0;
+      if (have_prev) {  // warm start: the previous iteration's neighbours of this query
+        float mx = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) oid[k] = o[k * kResThreads];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const float4 q = mg.by_id[oid[k]];
+          float dist = 0.0f, diff;
+          diff = x0 - q.x; dist += diff * diff;
+          diff = y0 - q.y; dist += diff * diff;
+          diff = z0 - q.z; dist += diff * diff;
+          mx = fmaxf(mx, dist);
+        }
+        bound = mx;
+      }
+      Knn5 nn;
+      unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      knn5_grid<R, RX, kFlat, kSparse, LPQ>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks,
+                                            &rows[0][threadIdx.x], sub);
+      if constexpr (LPQ > 1) knn5_merge<LPQ>(nn);
+      const bool ok = nn.k[4] < kKnnEmpty;
+      (void)ks;
+      int32_t ids[5];
+      bool same = have_prev && ok && a.fit_cache;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        ids[k] = knn_id(nn.k[k]);
+        same = same && ids[k] == oid[k];
+      }
+      if (LPQ > 1) __builtin_amdgcn_wave_barrier();  // every lane of the query read o[] (warm start)
+      if (sub == 0)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? ids[k] : -1;
+      const int64_t q = (int64_t)it * kResThreads + tid;
+      if (!kFused && sub == 0) a.nsame[q] = same ? 1 : 0;
+#ifdef FBR_KNN_STATS
+      ks[5] = ok;
+      ks[6] = corner;
+      ks[8] = have_prev;
+      ks[9] = same;
+      for (int k = 0; k < 10; ++k) atomicAdd(&a.knn_stats[k], (unsigned long long)ks[k]);
+#endif
+      if (kFused && ok)
+        rok = res_row(g, mg.by_id, ids, 1, corner, p, x0, y0, z0, row, b, a.fitc + (int64_t)it * 6 * kResThreads + tid,
+                      a.fits + q, same);
+    }
+    if (kFused) res_reduce(red, tid, row, b, rok, a.partial + (int64_t)it * kPartial);
+  }
+}
+
+// Host launchers of the kNN pass.  launch_gn_knn_r<R, F> is instantiated in k_knn_*.hip.
+template <int R, bool F, bool L, bool S, int LPQ = 1>
+void launch_gn_knn_rls(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
+  const float invx = a.mc.g.inv_x;  // == a.ms.g.inv_x
+  grid *= LPQ;
+  if (invx > 4.0f) fbr_launch((k_gn_knn<R, 8, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
+  else if (invx > 2.0f) fbr_launch((k_gn_knn<R, 4, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
+  else if (invx > 1.0f) fbr_launch((k_gn_knn<R, 2, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
+  else fbr_launch((k_gn_knn<R, 1, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
+}
+// Dense or hashed-chunk map grids (one flag for both maps: fbr_set_map builds them alike).
+template <int R, bool F, bool L, int LPQ = 1>
+void launch_gn_knn_rl(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
+  if (a.mc.g.sparse || a.ms.g.sparse) launch_gn_knn_rls<R, F, L, true, LPQ>(s, a, grid, use_prev);
+  else launch_gn_knn_rls<R, F, L, false, LPQ>(s, a, grid, use_prev);
+}
+
+// Lanes per query of the plain kNN pass (FBR_KNN_LPQ = 1 or 8; default 8 for sub-batches of at
+// most 2 jobs, where one lane per query leaves the chip idle and the launch is one query's chain).
+inline int knn_lpq(int jobs) {
+  static const int forced = [] {
+    const char* e = std::getenv("FBR_KNN_LPQ");
+    return e ? (std::atoi(e) >= 8 ? 8 : 1) : 0;
+  }();
+  if (forced) return forced;
+  return jobs <= 2 ? 8 : 1;
+}
+
+// Flat row queue (FBR_KNN_FLAT=0 disables): from iteration 1 on (warm-start bound), 1 m y/z cells
+// (9 rows: the queue is 18 KB of LDS per workgroup), not in the fused tail launch.
+inline bool knn_flat() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_KNN_FLAT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+template <int R, bool F>
+void launch_gn_knn_r(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
+  if constexpr (!F) {
+    if (knn_lpq(a.B) == 8) return launch_gn_knn_rl<R, F, false, 8>(s, a, grid, use_prev);
+  }
+  if constexpr (R == 1 && !F) {
+    if (use_prev && knn_flat()) return launch_gn_knn_rl<R, F, true>(s, a, grid, use_prev);
+  }
+  launch_gn_knn_rl<R, F, false>(s, a, grid, use_prev);
+}
+
+}  // namespace fbr

@@ -246,7 +246,11 @@ struct GnArgs {
   int nocrop;                // 1: keyframe local map, no CropBox (scan2MapOptimization on it)
   int deg_carry;             // isDegenerate before the first LMOptimization (the member carried
                              // across registration() calls, mapOptmization.h:137); 0 for batch jobs
+  unsigned long long* knn_stats;  // diagnostic builds (FBR_KNN_STATS): the kNN counters, else null
 };
+#ifdef FBR_KNN_STATS
+unsigned long long* knn_stats_buffer();
+#endif
 void launch_gn_init(hipStream_t s, const GnArgs& a);
 // fused: kNN + residual row + item partial in one launch (launch_gn_residual is then skipped)
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fused);

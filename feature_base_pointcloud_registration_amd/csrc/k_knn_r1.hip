@@ -1,0 +1,7 @@
+// k_knn_r1.hip — kNN kernels for 1 m y/z grid cells (R = 1 cells per side), plain kNN pass (flat queue, wide mode, per-row loop).
+// One translation unit per (R, fused) so the instantiations compile in parallel (fbr_gn.h).
+#include "fbr_gn.h"
+
+namespace fbr {
+template void launch_gn_knn_r<1, false>(hipStream_t, const GnArgs&, int, int);
+}  // namespace fbr

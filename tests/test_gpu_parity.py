@@ -509,31 +509,55 @@ def test_voxel_grid_inplace_lds_sort_matches_global_scratch_kernel():
 
 
 # ------------------------------------------------------------------------------- map grids
+def _c2_batch_in_child(jobs, env, sparse):
+    """Poses + stats bytes of `jobs` (C2) registered in a child process with extra environment
+    knobs (they are read once per process)."""
+    import subprocess
+    import sys
+    H, W = synth.CONFIGS["C2"][:2]
+    n = len(jobs)
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_child_jobs.npz")
+    np.savez(path, *[j[0] for j in jobs], guesses=np.stack([j[1] for j in jobs]))
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api, synth; "
+            "from feature_base_pointcloud_registration_amd.fbr_types import default_params; "
+            "d = np.load(%r); scans = [d['arr_%%d' %% k] for k in range(%d)]; "
+            "c = api.Context(default_params(%d, %d, max_batch=%d)); c.set_map(*synth.config_map('C2')); "
+            "assert c.map_grid_info()['sparse'] == %r; p, s = c.process_batch(scans, d['guesses']); "
+            "sys.stdout.buffer.write(p.tobytes() + s.tobytes())" % (REPO, path, n, H, W, n, bool(sparse)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, **env), timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r.stdout
+
+
+def _c2_batch_here(c2_map, jobs):
+    H, W = synth.CONFIGS["C2"][:2]
+    with api.Context(default_params(H, W, max_batch=len(jobs))) as ctx:
+        ctx.set_map(*c2_map)
+        assert not ctx.map_grid_info()["sparse"]
+        poses, stats = ctx.process_batch([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
+    return poses.tobytes() + stats.tobytes()
+
+
 def test_sparse_grid_registration_is_bit_identical_to_dense(c2_map):
     """The hashed-chunk kNN grid (k_grid.hip, used when a map's occupied box exceeds 2^26 dense
     cells) forced on the C2 map (FBR_GRID_SPARSE=1, child process) returns the dense grid's poses
     and stats bit for bit: both give the kNN the same candidate sets."""
-    import subprocess
-    import sys
     jobs = synth.make_jobs("C2", 12, base_seed=600)
-    H, W = synth.CONFIGS["C2"][:2]
-    P = default_params(H, W, max_batch=12)
-    with api.Context(P) as ctx:
-        ctx.set_map(*c2_map)
-        assert not ctx.map_grid_info()["sparse"]
-        poses, stats = ctx.process_batch([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
-    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_sparse_jobs.npz")
-    np.savez(path, *[j[0] for j in jobs], guesses=np.stack([j[1] for j in jobs]))
-    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api, synth; "
-            "from feature_base_pointcloud_registration_amd.fbr_types import default_params; "
-            "d = np.load(%r); scans = [d['arr_%%d' %% k] for k in range(12)]; "
-            "c = api.Context(default_params(%d, %d, max_batch=12)); c.set_map(*synth.config_map('C2')); "
-            "assert c.map_grid_info()['sparse']; p, s = c.process_batch(scans, d['guesses']); "
-            "sys.stdout.buffer.write(p.tobytes() + s.tobytes())" % (REPO, path, H, W))
-    env = dict(os.environ, FBR_GRID_SPARSE="1")
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=env, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
-    assert r.stdout == poses.tobytes() + stats.tobytes()
+    assert _c2_batch_in_child(jobs, {"FBR_GRID_SPARSE": "1"}, True) == _c2_batch_here(c2_map, jobs)
+
+
+@pytest.mark.parametrize("env,sparse", [
+    ({"FBR_KNN_CELL": "0.5"}, False),                          # R = 2 rows, the C3 / C5 cells
+    ({"FBR_KNN_CELL": "0.5", "FBR_GRID_SPARSE": "1"}, True),   # the same over hashed chunks
+    ({"FBR_KNN_LPQ": "8"}, False),                             # wide mode for every launch
+    ({"FBR_GN_FUSED": "1"}, False),                            # fused kNN + residual
+    ({"FBR_KNN_FLAT": "0"}, False),                            # per-row loop from iteration 1
+], ids=["cells-0.5", "cells-0.5-sparse", "wide", "fused", "no-flat"])
+def test_knn_variants_are_bit_identical(c2_map, env, sparse):
+    """Every kNN variant (cell sizes, grid layouts, wide / fused / per-row launches) selects the
+    same neighbour sets: poses and stats of 12 C2 jobs equal the default path's bit for bit."""
+    jobs = synth.make_jobs("C2", 12, base_seed=610)
+    assert _c2_batch_in_child(jobs, env, sparse) == _c2_batch_here(c2_map, jobs)
 
 
 def test_kilometre_prior_map_uses_sparse_grid_and_matches_oracle(c2_map):
