@@ -46,7 +46,8 @@ def kernel_bytes(name, tot):
     S, F, Q, IQ = tot["S"], tot["F"], tot["Q"], tot["IQ"]
     return {
         "project": 24.0 * n_in + 4.0 * n,        # raw point (24 B AoS) read + first-wins owner claim
-        "extract": 4.0 * HW + 24.0 * n + 24.0 * n,  # owner image read, owning raw point gather, xyzi+col+range write
+        "extract": 4.0 * HW + 4.0 * n + 24.0 * n + 24.0 * n,  # owner image read + claimed cells reset, owning
+                                                             # raw point gather, xyzi+col+range write
         "features": 24.0 * n + 1.0 * n + 16.0 * C,  # range+col+xyzi read, label write, corner picks write
         "voxel_ring": 17.0 * n + 16.0 * S,       # label + candidate point read, per-ring DS write
         "concat": 32.0 * F,                      # per-ring corner / surf outputs read + job clouds written
@@ -58,7 +59,7 @@ def kernel_bytes(name, tot):
 
 BYTE_MODEL = {
     "project": "24 B per raw point + 4 B owner claim per valid point",
-    "extract": "4 B per range-image cell + 24 B raw-point gather + 24 B written per valid point",
+    "extract": "4 B per range-image cell + 4 B owner reset + 24 B raw-point gather + 24 B written per valid point",
     "features": "24 B read + 1 B label per valid point + 16 B per corner pick",
     "voxel_ring": "17 B per valid point + 16 B per per-ring DS point",
     "concat": "32 B per feature point",

@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = [
     "fbr_register", "fbr_register_trace", "fbr_process_scan", "fbr_reset_stream",
     "fbr_process_batch", "fbr_ingest_bytes", "fbr_debug_counters", "fbr_map_grid_info", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
     "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
-    "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math", "fbr_selftest_eigen6",
+    "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math", "fbr_selftest_eigen6", "fbr_selftest_eig_certified",
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
     "fbr_msg_to_points", "fbr_points_to_msg_data", "fbr_project_msg", "fbr_process_msg",
     "fbr_imu_convert", "fbr_imu_deskew_info", "fbr_set_deskew", "fbr_stream_copy_bandwidth",
@@ -93,6 +93,7 @@ def lib():
             "fbr_pose_from_affine": (None, [_VP, _VP]),
             "fbr_selftest_math": (ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP]),
             "fbr_selftest_eigen6": (ctypes.c_int, [ctypes.c_int, _VP, _VP]),
+            "fbr_selftest_eig_certified": (ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_float, _VP]),
             "fbr_load_map": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_char_p]),
             "fbr_pcd_read": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64, _VP]),
             "fbr_pcd_write_ascii": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64]),
@@ -169,6 +170,15 @@ def selftest_eigen6(mats):
     _check(lib().fbr_selftest_eigen6(len(a), ptr(a), ptr(out)), "fbr_selftest_eigen6")
     n = len(a)
     return ((out[:, :6], out[:, 6:42].reshape(n, 6, 6)), (out[:, 42:48], out[:, 48:].reshape(n, 6, 6)))
+
+
+def selftest_eig_certified(mats, thr=100.0):
+    """1 where the device certifies every eigenvalue of a symmetric 6x6 float matrix above thr
+    without the Jacobi (fbr_selftest_eig_certified: the iteration-0 degeneracy fast path)."""
+    a = np.ascontiguousarray(mats, np.float32).reshape(-1, 36)
+    out = np.zeros(len(a), np.int32)
+    _check(lib().fbr_selftest_eig_certified(len(a), ptr(a), ctypes.c_float(thr), ptr(out)), "fbr_selftest_eig_certified")
+    return out
 
 
 def stream_copy_bandwidth(device=0, nbytes=2 << 30, iters=20):

@@ -11,12 +11,16 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
+#include <mutex>
 #include <set>
 #include <string>
 #include <thread>
@@ -143,6 +147,8 @@ struct fbr_ctx {
   uint8_t* d_msg = nullptr;                 // raw PointCloud2 bytes of the last *_msg call (grown on demand)
   uint64_t msg_cap = 0;
   bool crop_cached = false;  // d_cropcnt holds the staged batch's CropBox statistics
+  bool crop_join = false;    // single scan: copy_results takes the CropBox counts from h_crop (side stream)
+  int32_t* h_crop = nullptr;  // pinned [2]: the single-scan CropBox counts
   int max_items = 0;
   float* d_pose_out = nullptr;
   fbr_reg_stats* d_stats = nullptr;
@@ -369,8 +375,7 @@ int stage_project(fbr_ctx* c, const Sub& sb) {
   DeskArgs desk{nullptr, nullptr, nullptr};
   if (c->desk_any && !c->no_time_call)  // deskewFlag == -1 without a "time" field (:296-297, :548)
     desk = DeskArgs{c->d_desk_mode + j0, c->d_desk + j0, c->d_rowmin + j0 * c->H};
-  int32_t* owner = c->d_owner + j0 * c->HW;
-  CK(hipMemsetAsync(owner, 0x7F, sizeof(int32_t) * sb.B * c->HW, sb.st));
+  int32_t* owner = c->d_owner + j0 * c->HW;  // all kEmptyOwner: set at fbr_create, reset by k_compact
   TIMED_ON(c, sb.st, "project", launch_project(sb.st, c->d_pts + j0 * c->NMAX, c->d_nin + j0, c->NMAX, sb.B, c->H,
                                                c->W, owner));
   TIMED_ON(c, sb.st, "extract",
@@ -526,8 +531,7 @@ int register_prepare(fbr_ctx* c, const Sub& sb, bool trace) {
   TIMED_ON(c, sb.st, "voxel_scan", launch_voxel_grid(sb.st, v));
   GnArgs a = gn_args(c, sb, trace);
   if (trace) CK(hipMemsetAsync(a.trace, 0, sizeof(float) * sb.B * c->P.max_iterations * 6, sb.st));
-  CK(hipMemsetAsync(a.iter_cnt, 0, sizeof(int32_t) * 2 * std::max(1, c->P.max_iterations), sb.st));
-  TIMED_ON(c, sb.st, "gn_init", launch_gn_init(sb.st, a));
+  TIMED_ON(c, sb.st, "gn_init", launch_gn_init(sb.st, a));  // also zeroes a.iter_cnt
   // map-in-box statistics depend only on the guesses: computed once per staged batch
   if (!c->crop_cached) {
     const int rc = crop_stats(c, sb);
@@ -638,6 +642,12 @@ int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool
   CK(hipMemcpyAsync(c->h_result, c->d_result, sizeof(JobResult) * B, hipMemcpyDeviceToHost, c->stream));
   const auto tw = std::chrono::steady_clock::now();
   CK(fbr_sync(c->stream));
+  if (c->crop_join) {  // the single-scan CropBox statistics: their own copy on the side stream (no
+    c->crop_join = false;  // cross-stream dependency on the device; that stream finished long ago)
+    CK(fbr_sync(c->xstream[1]));
+    c->h_result[0].st.n_corner_map = c->h_crop[0];
+    c->h_result[0].st.n_surf_map = c->h_crop[1];
+  }
   host_time(2, tw);
   // A capacity error in any job (features truncated) fails the call before anything is written:
   // poses_inout keeps the caller's guesses, as the reference leaves the pose on a failed scan.
@@ -666,23 +676,95 @@ int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool
 
 int copy_stats(fbr_ctx* c, int B, fbr_reg_stats* stats) { return copy_results(c, B, stats, nullptr, true); }
 
-// Host copy into pinned staging, split over threads for large scans (a 64x1800 scan is 2.6 MB).
-void pinned_copy(void* dst, const void* src, size_t bytes) {
-  constexpr size_t kPart = 1 << 20;
-  const int nt = (int)std::min<size_t>(4, (bytes + kPart - 1) / kPart);
-  if (nt <= 1) {
-    std::memcpy(dst, src, bytes);
-    return;
+// Host copy workers of the single-scan uploads, alive for the process (spawning threads per call
+// cost ~30 us each).  run(fn) calls fn(p) on participants p = 0..kCopyWorkers (the caller is 0)
+// and returns when all are done.  Idle workers spin briefly on the generation counter (back-to-back
+// scans find them awake), then sleep on the condition variable.
+class CopyPool {
+ public:
+  static constexpr int kWorkers = 3;
+  CopyPool() {
+    for (int t = 1; t <= kWorkers; ++t) th_.emplace_back([this, t] { loop(t); });
   }
-  const size_t part = (bytes + nt - 1) / nt;
-  auto one = [&](int t) {
-    const size_t b = (size_t)t * part, e = std::min(bytes, b + part);
-    if (e > b) std::memcpy((uint8_t*)dst + b, (const uint8_t*)src + b, e - b);
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_.store(true);
+      gen_.fetch_add(1);
+    }
+    cv_.notify_all();
+    for (auto& x : th_) x.join();
+  }
+  void run(const std::function<void(int)>& fn) {
+    std::lock_guard<std::mutex> serial(run_mu_);  // one upload at a time (contexts may share it)
+    fn_ = &fn;
+    pending_.store(kWorkers);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      gen_.fetch_add(1);
+    }
+    cv_.notify_all();
+    fn(0);
+    while (pending_.load() != 0) __builtin_ia32_pause();
+  }
+
+ private:
+  void loop(int id) {
+    uint64_t seen = 0;
+    while (true) {
+      uint64_t g = gen_.load();
+      for (int spin = 0; g == seen && spin < 100000; ++spin) {  // ~1 ms awake after an upload
+        __builtin_ia32_pause();
+        g = gen_.load();
+      }
+      if (g == seen) {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return gen_.load() != seen; });
+        g = gen_.load();
+      }
+      seen = g;
+      if (stop_.load()) return;
+      (*fn_)(id);
+      pending_.fetch_sub(1);
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_, run_mu_;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<int> pending_{0};
+  const std::function<void(int)>* fn_ = nullptr;
+  std::atomic<bool> stop_{false};
+};
+
+CopyPool& copy_pool() {
+  static CopyPool* pool = new CopyPool();  // never destroyed: workers may outlive static teardown
+  return *pool;
+}
+
+// Host bytes -> pinned staging -> device, pipelined: the participants copy 512 KB chunks
+// round-robin and each enqueues its chunk's DMA on `st` as soon as the chunk is staged, so the
+// copy engine runs while the rest is still being copied (a 64x1800 scan is 2.6 MB).  The chunks
+// are disjoint, so their order on the stream does not matter; the caller enqueues the consumer
+// after this returns.
+hipError_t pinned_upload_async(void* d_dst, void* h_stage, const void* src, size_t bytes, hipStream_t st) {
+  constexpr size_t kChunk = 512 << 10;
+  if (bytes <= kChunk) {
+    std::memcpy(h_stage, src, bytes);
+    return hipMemcpyAsync(d_dst, h_stage, bytes, hipMemcpyHostToDevice, st);
+  }
+  const size_t nchunk = (bytes + kChunk - 1) / kChunk;
+  std::atomic<int> err{(int)hipSuccess};
+  const std::function<void(int)> fn = [&](int p) {
+    for (size_t k = (size_t)p; k < nchunk; k += CopyPool::kWorkers + 1) {
+      const size_t b = k * kChunk, e = std::min(bytes, b + kChunk);
+      std::memcpy((uint8_t*)h_stage + b, (const uint8_t*)src + b, e - b);
+      const hipError_t r = hipMemcpyAsync((uint8_t*)d_dst + b, (uint8_t*)h_stage + b, e - b, hipMemcpyHostToDevice, st);
+      if (r != hipSuccess) err.store((int)r);
+    }
   };
-  std::vector<std::thread> th;
-  for (int t = 1; t < nt; ++t) th.emplace_back(one, t);
-  one(0);
-  for (auto& x : th) x.join();
+  copy_pool().run(fn);
+  return (hipError_t)err.load();
 }
 
 // Single-scan uploads stage through our own pinned buffer with a threaded host copy (default;
@@ -704,9 +786,7 @@ int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n) {
   c->no_time_call = false;
   if (n && pinned_upload()) {
     CK(fbr_sync(c->stream));  // staging free (a no-op after the previous call's result copy)
-    pinned_copy(c->h_scan, pts, sizeof(fbr_point_xyzirt) * n);
-    CK(hipMemcpyAsync(c->d_pts + job * c->NMAX, c->h_scan, sizeof(fbr_point_xyzirt) * n, hipMemcpyHostToDevice,
-                      c->stream));
+    CK(pinned_upload_async(c->d_pts + job * c->NMAX, c->h_scan, pts, sizeof(fbr_point_xyzirt) * n, c->stream));
   } else if (n) {
     CK(hipMemcpyAsync(c->d_pts + job * c->NMAX, pts, sizeof(fbr_point_xyzirt) * n, hipMemcpyHostToDevice, c->stream));
   }
@@ -738,8 +818,7 @@ int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags) {
     c->h_msg_cap = L.bytes;
   }
   if (L.bytes) {
-    pinned_copy(c->h_msg, msg->data, L.bytes);
-    CK(hipMemcpyAsync(c->d_msg, c->h_msg, L.bytes, hipMemcpyHostToDevice, c->stream));
+    CK(pinned_upload_async(c->d_msg, c->h_msg, msg->data, L.bytes, c->stream));
   }
   MsgDev D;
   D.n = L.n;
@@ -976,7 +1055,8 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               hipHostMalloc((void**)&c->h_result, sizeof(JobResult) * B, hipHostMallocDefault) != hipSuccess ||
               hipHostMalloc((void**)&c->h_scan, sizeof(fbr_point_xyzirt) * std::max<int64_t>(c->NMAX, 1),
                             hipHostMallocDefault) != hipSuccess ||
-              hipHostMalloc((void**)&c->h_nin, sizeof(int64_t), hipHostMallocDefault) != hipSuccess;
+              hipHostMalloc((void**)&c->h_nin, sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
+              hipHostMalloc((void**)&c->h_crop, sizeof(int32_t) * 2, hipHostMallocDefault) != hipSuccess;
   if (fail) {
     fbr_destroy(c);
     return FBR_ERR_HIP;
@@ -985,7 +1065,8 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   if (hipMemset(c->d_sstream, 0, sizeof(StreamState)) != hipSuccess ||
       hipMemset(c->d_label_stream, 0, HW) != hipSuccess || hipMemset(c->d_col, 0, sizeof(int32_t) * B * HW) != hipSuccess ||
       hipMemset(c->d_range, 0, sizeof(float) * B * HW) != hipSuccess ||
-      hipMemset(c->d_desk_mode, 0, sizeof(int32_t) * B) != hipSuccess) {
+      hipMemset(c->d_desk_mode, 0, sizeof(int32_t) * B) != hipSuccess ||
+      hipMemset(c->d_owner, 0x7F, sizeof(int32_t) * B * HW) != hipSuccess) {  // k_compact resets it after use
     fbr_destroy(c);
     return FBR_ERR_HIP;
   }
@@ -1013,7 +1094,7 @@ int fbr_destroy(fbr_ctx* c) {
   free_grid(c->grid_c);
   free_grid(c->grid_s);
   arena_free(c->arena);
-  for (void* h : {(void*)c->h_result, (void*)c->h_scan, (void*)c->h_nin, (void*)c->h_msg})
+  for (void* h : {(void*)c->h_result, (void*)c->h_scan, (void*)c->h_nin, (void*)c->h_msg, (void*)c->h_crop})
     if (h) (void)hipHostFree(h);
   if (c->d_result) (void)hipFree(c->d_result);
   if (c->ing.cstream) (void)fbr_sync(c->ing.cstream);
@@ -1230,6 +1311,7 @@ namespace {
 // and one synchronisation return pose and stats.
 int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stats* stats) {
   const auto t0 = std::chrono::steady_clock::now();
+  c->crop_join = false;
   int rc = stage_project(c, single_sub(c));
   if (!rc) rc = stage_features(c, single_sub(c), true);
   if (rc) return rc;
@@ -1241,7 +1323,17 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
   float pose[6];
   if (run) {
     CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->stream));
+    // the CropBox statistics depend only on the guess: a side stream computes them while the
+    // registration runs, and copy_results joins it
+    CK(hipEventRecord(c->xev[1], c->stream));
+    CK(hipStreamWaitEvent(c->xstream[1], c->xev[1], 0));
+    rc = crop_stats(c, Sub{0, 1, 0, c->xstream[1], true});
+    if (rc) return rc;
+    CK(hipMemcpyAsync(c->h_crop, c->d_cropcnt, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, c->xstream[1]));
+    c->crop_join = true;
+    c->crop_cached = true;
     rc = stage_register(c, single_sub(c), false);
+    c->crop_cached = false;
     if (rc) return rc;
   }
   host_time(1, t0);

@@ -70,7 +70,7 @@ struct DeskArgs {
   int32_t* rowmin;
 };
 // choff: [B][H][ceil(W / 32)] scratch (claimed cells of a row before each compaction tile)
-void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,
+void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, int32_t* owner, int B, int H,
                     int W, int32_t* rowcnt, int32_t* choff, float4* cloud, int32_t* col, float* range,
                     int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk);
 

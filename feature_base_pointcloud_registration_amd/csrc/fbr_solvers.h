@@ -309,6 +309,39 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// isDegenerate without the eigen-decomposition (mapOptmization.h:1353-1366 only needs to know
+// whether some eigenvalue of the float matAtA is below thr = 100; matP is used only when one is).
+// Every eigenvalue exceeds thr + m, m = 1e-3 ||A||_F, iff A - (thr + m) I is positive definite,
+// which an LDL^T factorisation in double decides (its own rounding, ~1e-16 ||A||, is negligible
+// next to m).  OpenCV's float Jacobi returns eigenvalues within a few hundred float roundings of
+// the exact ones (~1e-5 ||A|| at most, against the 1e-3 ||A|| margin), so when this returns true
+// none of them can fall below thr and the reference's isDegenerate is false.  false = not
+// certified: run the Jacobi.  NaN / Inf inputs are never certified.
+template <int N>
+__device__ __forceinline__ bool eig_above_certified(const float* A, float thr) {
+  double fro = 0.0;
+#pragma unroll
+  for (int k = 0; k < N * N; ++k) fro += (double)A[k] * (double)A[k];
+  const double tau = (double)thr + 1e-3 * sqrt(fro);
+  double L[N][N], D[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    double d = (double)A[j * N + j] - tau;
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k] * D[k];
+    if (!(d > 0.0) || !(d < 1e300)) return false;
+    D[j] = d;
+#pragma unroll
+    for (int i = j + 1; i < N; ++i) {
+      double v = (double)A[i * N + j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k] * D[k];
+      L[i][j] = v / d;
+    }
+  }
+  return true;
+}
+
 // The same algorithm by one whole wave on shared arrays (A, V: N*N; W, indR, indC: N).  Every lane
 // finds the pivot (uniform LDS reads); the element pairs of one rotation are disjoint, so lane i
 // rotates the A pair and lane N+i the V pair of index i with the per-element operations of

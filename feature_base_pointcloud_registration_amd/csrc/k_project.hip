@@ -188,7 +188,7 @@ __device__ __forceinline__ float4 deskew_point(const fbr_point_xyzirt& q, const 
 // from it at the write, same expression, same bits): 20 KB per 1024-cell tile.
 template <bool kDesk>
 __global__ void __launch_bounds__(256)
-k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, const int32_t* __restrict__ owner,
+k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, int32_t* __restrict__ owner,
           const int32_t* __restrict__ rowcnt, const int32_t* __restrict__ choff, int B, int H, int W, int HB, int CG,
           float4* __restrict__ cloud, int32_t* __restrict__ col, float* __restrict__ range,
           int32_t* __restrict__ start_ring, int32_t* __restrict__ end_ring, int32_t* __restrict__ nvalid,
@@ -240,11 +240,18 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, const int32_t*
       }
     }
   }
-  // owners, row by row (coalesced)
-  const int32_t* O = owner + job * HW;
+  // owners, row by row (coalesced); the owner image is reset behind the read for the next scan
+  // (this tile is its last reader), which replaces a separate memset launch per call
+  int32_t* O = owner + job * HW;
   for (int i = tid; i < HB * CG; i += 256) {
     const int r = i / CG, c = i % CG;
-    own[i] = (r < nr && c < ncl) ? O[(int64_t)(r0 + r) * W + c0 + c] : kEmptyOwner;
+    int32_t o = kEmptyOwner;
+    if (r < nr && c < ncl) {
+      int32_t* a = O + (int64_t)(r0 + r) * W + c0 + c;
+      o = *a;
+      if (o != kEmptyOwner) *a = kEmptyOwner;
+    }
+    own[i] = o;
   }
   __syncthreads();
   // deskew: transStartInverse from the scan's first deskewed point (the minimum owner)
@@ -382,7 +389,7 @@ int compact_cells() {
   return v;
 }
 
-void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, const int32_t* owner, int B, int H,
+void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, int32_t* owner, int B, int H,
                     int W, int32_t* rowcnt, int32_t* choff, float4* cloud, int32_t* col, float* range,
                     int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk) {
   const CompactTile T = compact_tile(H, compact_cells());

@@ -54,6 +54,7 @@ __device__ void pose_to_T(const float* tr, float* T, float* trig) {
 __global__ void k_gn_init(GnArgs a) {
   __shared__ int32_t scan[1024];
   const int tid = threadIdx.x;
+  for (int i = tid; i < 2 * max(1, a.max_iter); i += 1024) a.iter_cnt[i] = 0;  // k_gn_solve's counters
   int base = 0;
   for (int j0 = 0; j0 < a.B; j0 += 1024) {
     const int job = j0 + tid;
@@ -151,7 +152,10 @@ __device__ __forceinline__ void gn_normal_eq(const double* acc, float* AtA, floa
 // Iteration-0 degeneracy projection (:1280-1305): 6x6 Jacobi, eigenvalues < 100 zero rows of V2,
 // matP = V^-1 * V2 by LU.  It depends only on AtA, so the second wave of k_gn_solve computes it
 // (the Jacobi rotations spread over its lanes, jacobi_eigen_wave) while the first solves
-// AtA X = AtB.  All 64 lanes of the wave call it; matP / degenerate are written by lane 0.
+// AtA X = AtB.  All 64 lanes of the wave call it; matP / degenerate are written by lane 0.  A
+// matrix whose eigenvalues are certified above 100 (eig_above_certified: an LDL^T test with a
+// 1e-3 ||A|| margin, the common case) skips the Jacobi and the LU: degenerate = 0, and matP is
+// then never read (gn_solve_job applies it only when degenerate).
 struct EigenLds {
   float A[36], V[36], W[6];
   int R[6], C[6];
@@ -163,6 +167,10 @@ __device__ void gn_degeneracy(const double* acc, EigenLds& e, float* matP, int* 
     e.A[lane] = (float)acc[lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];  // upper-triangle order
   }
   wave_lds_sync();
+  if (eig_above_certified<6>(e.A, 100.0f)) {  // every eigenvalue >= 100: not degenerate, matP unused
+    if (lane == 0) *degenerate = 0;
+    return;
+  }
   jacobi_eigen_wave<6>(e.A, e.W, e.V, e.R, e.C);
   if (lane != 0) return;
   float E[6], V[36], V2[36], Vi[36];

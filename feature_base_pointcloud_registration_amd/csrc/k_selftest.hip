@@ -50,7 +50,31 @@ __global__ void __launch_bounds__(64) k_selftest_eigen6(const float* a, float* o
   if (lane < 36) o[48 + lane] = V[lane];
 }
 
+// out[i] = 1 when eig_above_certified<6> certifies every eigenvalue of matrix i above `thr`.
+__global__ void k_selftest_eig_cert(int n, const float* a, float thr, int32_t* out) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < n) out[m] = eig_above_certified<6>(a + (int64_t)m * 36, thr) ? 1 : 0;
+}
+
 }  // namespace fbr
+
+extern "C" int fbr_selftest_eig_certified(int n, const float* a, float thr, int32_t* out) {
+  if (n <= 0 || !a || !out) return FBR_ERR_INVALID_ARG;
+  float* da = nullptr;
+  int32_t* dout = nullptr;
+  int rc = FBR_OK;
+  if (hipMalloc(&da, sizeof(float) * 36 * n) != hipSuccess || hipMalloc(&dout, sizeof(int32_t) * n) != hipSuccess) {
+    rc = FBR_ERR_HIP;
+  } else if (hipMemcpy(da, a, sizeof(float) * 36 * n, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = FBR_ERR_HIP;
+  } else {
+    hipLaunchKernelGGL(fbr::k_selftest_eig_cert, dim3((n + 63) / 64), dim3(64), 0, 0, n, da, thr, dout);
+    if (hipMemcpy(out, dout, sizeof(int32_t) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = FBR_ERR_HIP;
+  }
+  (void)hipFree(da);
+  (void)hipFree(dout);
+  return rc;
+}
 
 extern "C" int fbr_selftest_math(int n, const float* a, const float* b, float* out) {
   if (n <= 0 || !a || !b || !out) return FBR_ERR_INVALID_ARG;

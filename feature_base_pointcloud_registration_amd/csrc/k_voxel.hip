@@ -160,7 +160,21 @@ __device__ int vg_radix_sort(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, 
     const auto vout = lds_if<KV_LDS>(vb[cur ^ 1]);
     for (int b = tid; b < tot; b += T) hist[(b % NW) * NB + b / NW] = 0u;
     __syncthreads();
-    for (int i = c0 + lane; i < c1; i += 64) atomicAdd(&hist[w * NB + ((kin[i] >> shift) & dmask)], 1u);
+    // per-wave digit counts: one add per distinct digit of a 64-step, by the lowest lane holding it
+    // (ballot peer masks; per-element LDS atomics serialise on the long equal-digit runs that
+    // spatially ordered keys have in their upper digits)
+    for (int i0 = c0; i0 < c1; i0 += 64) {
+      const int i = i0 + lane;
+      const bool valid = i < c1;
+      const uint32_t d = valid ? (kin[i] >> shift) & dmask : 0u;
+      uint64_t peers = __ballot(valid);
+      for (int b = 0; b < dbits; ++b) {
+        const uint64_t bal = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? bal : ~bal;
+      }
+      if (valid && (peers & ((1ull << lane) - 1ull)) == 0ull) hist[w * NB + d] += (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+    }
     __syncthreads();
     {
       uint32_t v[PER], loc = 0;
@@ -242,9 +256,20 @@ __device__ void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint
     }
     for (int b = tid; b < tot; b += T) hist[(b % NW) * NB + b / NW] = 0u;
     __syncthreads();  // every wave holds its chunk: the scatter below may overwrite any position
+    // per-wave digit counts, one add per distinct digit of a step (see vg_radix_sort)
 #pragma unroll
-    for (int k = 0; k < KPL; ++k)
-      if (c0 + 64 * k + lane < c1) atomicAdd(&hist[w * NB + ((kr[k] >> shift) & dmask)], 1u);
+    for (int k = 0; k < KPL; ++k) {
+      if (c0 + 64 * k >= c1) break;  // wave-uniform
+      const bool valid = c0 + 64 * k + lane < c1;
+      const uint32_t d = (kr[k] >> shift) & dmask;
+      uint64_t peers = __ballot(valid);
+      for (int b = 0; b < dbits; ++b) {
+        const uint64_t bal = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? bal : ~bal;
+      }
+      if (valid && (peers & ((1ull << lane) - 1ull)) == 0ull) hist[w * NB + d] += (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+    }
     __syncthreads();
     {
       uint32_t v[PER], loc = 0;
@@ -274,6 +299,7 @@ __device__ void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < KPL; ++k) {
+      if (c0 + 64 * k >= c1) break;  // wave-uniform: the rest of the chunk is empty
       const bool valid = c0 + 64 * k + lane < c1;
       const uint32_t d = (kr[k] >> shift) & dmask;
       uint64_t peers = __ballot(valid);
@@ -332,6 +358,8 @@ __device__ int vg_emit(KP ks, VP vs, int n, uint32_t* hist, uint32_t* wsum, cons
   bool carry_open = false;
   float4 carry = make_float4(0.f, 0.f, 0.f, 0.f);
   int carry_start = 0, carry_out = 0;
+  // the gathers run one step ahead (the loop is otherwise one dependent HBM/L2 round trip per step)
+  float4 pnext = c0 + lane < n && c0 < c1 ? in[vs[c0 + lane]] : make_float4(0.f, 0.f, 0.f, 0.f);
   for (int i0 = c0; i0 < c1 || carry_open; i0 += 64) {
     const int i = i0 + lane;
     const bool valid = i < n;
@@ -340,7 +368,8 @@ __device__ int vg_emit(KP ks, VP vs, int n, uint32_t* hist, uint32_t* wsum, cons
     const bool head = valid && i < c1 && brk_i;
     const bool cont = carry_open && lane == 0;  // continues the carried run (brk_i is false)
     const uint64_t brk = __ballot(brk_i), hb = __ballot(head);
-    const float4 p = valid ? in[vs[i]] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 p = valid ? pnext : make_float4(0.f, 0.f, 0.f, 0.f);
+    pnext = i + 64 < n ? in[vs[i + 64]] : make_float4(0.f, 0.f, 0.f, 0.f);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     stg[lane] = p;
@@ -468,6 +497,21 @@ __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
 // of up to T * KPL points sort in place in LDS (keys u32 + u16 indices, vg_radix_sort_inplace), so
 // the only global writes are the centroids; larger segments take the global-scratch ping-pong of
 // k_voxel_grid.  Same semantics and output as k_voxel_grid.
+#ifdef FBR_VG_STAMPS
+// Diagnostic builds only: s_memtime at the phase boundaries of k_voxel_grid_ip's workgroup 0
+// (start, grid set-up, keys, sort, emit), read by fbr_diag_vg_stamps.
+__device__ unsigned long long fbr_vg_stamps[8];
+#define FBR_VG_STAMP(k)                                                                       \
+  do {                                                                                        \
+    __syncthreads();                                                                          \
+    if (blockIdx.x == 0 && threadIdx.x == 0) fbr_vg_stamps[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define FBR_VG_STAMP(k) \
+  do {                  \
+  } while (0)
+#endif
+
 template <int T, int KPL>
 __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
   constexpr int NW = T / 64, LCAP = T * KPL;
@@ -481,6 +525,7 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
   uint32_t* wsum = hist + (NW + 1) * 512;
   float* mm = (float*)(wsum + NW);
   int* misc = (int*)(mm + NW * 6);
+  FBR_VG_STAMP(0);
   const int n = (int)min((int64_t)S.cnt_in[seg], S.cap);
   const float4* in = S.in + (int64_t)seg * S.stride_in;
   float4* out = S.out + (int64_t)seg * S.stride_out;
@@ -501,6 +546,7 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
   vg_block_minmax<T>(mn, mx, mm);
   VgGrid G;
   G.init(mn, mx, S.leaf, S.morton != 0);
+  FBR_VG_STAMP(1);
   if (G.overflow) {
     for (int i = tid; i < n; i += T) out[i] = in[i];
     if (tid == 0) S.cnt_out[seg] = n;
@@ -516,8 +562,11 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
       vals[i] = (uint16_t)i;
     }
     __syncthreads();
+    FBR_VG_STAMP(2);
     vg_radix_sort_inplace<T, KPL>(keys, vals, n, G.nbits, hist, wsum);
+    FBR_VG_STAMP(3);
     total = vg_emit<T>(keys, vals, n, hist, wsum, in, out);
+    FBR_VG_STAMP(4);
   } else {
     uint32_t* sc = S.scratch + (int64_t)seg * 4 * S.cap;
     uint32_t* kb[2] = {sc, sc + S.cap};
@@ -1018,3 +1067,9 @@ int voxel_grid_large(hipStream_t s, DevArena& ar, const float4* in, int64_t n, f
 }
 
 }  // namespace fbr
+
+#ifdef FBR_VG_STAMPS
+extern "C" int fbr_diag_vg_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(fbr::fbr_vg_stamps), sizeof(unsigned long long) * 8) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -387,6 +387,12 @@ int fbr_selftest_math(int n, const float* a, const float* b, float* out);
  * {6 eigenvalues, 36 eigenvector entries} of each (tests compare both with the host restatement). */
 int fbr_selftest_eigen6(int n, const float* a, float* out);
 
+/* Diagnostic: the degeneracy fast path of the iteration-0 solve.  out[i] = 1 when every eigenvalue
+ * of the symmetric 6x6 float matrix a[36i..36i+35] is certified above thr (LDL^T of A - (thr +
+ * 1e-3 ||A||_F) I in double), so isDegenerate (mapOptmization.h:1353-1366) is false without the
+ * Jacobi; 0 = not certified (the device then runs cv::eigen's Jacobi). */
+int fbr_selftest_eig_certified(int n, const float* a, float thr, int32_t* out);
+
 /* Measurement helper: achievable HBM bandwidth of a device-wide float4 copy of `bytes` (read +
  * write counted), averaged over `iters` launches (the STREAM-copy figure bench.py reports next to
  * the 8 TB/s spec peak). */

@@ -129,6 +129,17 @@ def test_degeneracy_eigen6_wave_matches_single_lane_and_oracle():
         V = np.zeros((6, 6), np.float32)
         O.lib().orc_jacobi(ptr(a), 6, ptr(W), ptr(V))
         assert np.array_equal(bits(W), bits(w2[i])) and np.array_equal(bits(V), bits(v2[i])), i
+    # the iteration-0 fast path: a certified matrix has every Jacobi eigenvalue >= 100 (so
+    # isDegenerate is false without the Jacobi); realistic normal equations are certified
+    cert = api.selftest_eig_certified(mats)
+    assert (w2[cert == 1] >= 100.0).all()
+    fro = np.sqrt((mats.astype(np.float64) ** 2).sum(axis=(1, 2)))
+    clear = w2.min(axis=1) > 100.0 + 2e-3 * fro  # well above the threshold + margin
+    assert clear.sum() > 100 and cert[clear].all()
+    assert not cert[(w2 < 100.0).any(axis=1)].any()
+    nan = mats[:4].copy()
+    nan[:, 0, 0] = np.nan
+    assert not api.selftest_eig_certified(nan).any()
 
 
 # ------------------------------------------------------------------------------- projection
