@@ -7,6 +7,7 @@
 #include <cstdlib>
 
 #include "fbr_common.h"
+#include "fbr_imu.h"
 #include "fbr_kernels.h"
 #include "fbr_solvers.h"
 
@@ -456,85 +457,270 @@ __device__ __forceinline__ void res_reduce(double (*red)[28], int tid, const flo
 // LPQ > 1 (wide mode, launches with few queries: single scans, tiny batches; neither fused nor
 // flat): a workgroup covers 256 / LPQ queries of an item with LPQ lanes each, so a query's search
 // chain is LPQ times shorter; lane `sub` == 0 of each query writes the results.
+// One virtual workgroup v (item v / LPQ, query group v % LPQ) of the kNN pass (k_gn_knn's body).
+template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ>
+__device__ __forceinline__ void gn_knn_block(const GnArgs& a, int v, int use_prev, double (*red)[28], int2* rows) {
+  constexpr int QPB = kResThreads / LPQ;  // queries per workgroup
+  const int sub = (int)threadIdx.x % LPQ;
+  const int it = v / LPQ;
+  const int tid = (v % LPQ) * QPB + (int)threadIdx.x / LPQ;  // query slot within the item
+  const int4 item = a.items[it];
+  const int job = item.x;
+  const GnState& g = a.gn[job];
+  if (!g.active) return;  // block-uniform
+  float row[6] = {0, 0, 0, 0, 0, 0}, b = 0.0f;
+  bool rok = false;
+  if (tid < item.w) {
+    const bool corner = item.y == 0;
+    const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
+    const float* T = g.T;
+    // pointAssociateToMap (:397-403)
+    const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
+    const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
+    const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
+    const MapGrid& mg = corner ? a.mc : a.ms;
+    int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
+    float bound = __int_as_float(0x7f800000);
+    int32_t oid[5] = {-1, -1, -1, -1, -1};
+    const bool have_prev = use_prev && o[0] >= 0;
+    if (have_prev) {  // warm start: the previous iteration's neighbours of this query
+      float mx = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) oid[k] = o[k * kResThreads];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const float4 q = mg.by_id[oid[k]];
+        float dist = 0.0f, diff;
+        diff = x0 - q.x; dist += diff * diff;
+        diff = y0 - q.y; dist += diff * diff;
+        diff = z0 - q.z; dist += diff * diff;
+        mx = fmaxf(mx, dist);
+      }
+      bound = mx;
+    }
+    Knn5 nn;
+    unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    knn5_grid<R, RX, kFlat, kSparse, LPQ>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks, rows, sub);
+    if constexpr (LPQ > 1) knn5_merge<LPQ>(nn);
+    const bool ok = nn.k[4] < kKnnEmpty;
+    (void)ks;
+    int32_t ids[5];
+    bool same = have_prev && ok && a.fit_cache;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      ids[k] = knn_id(nn.k[k]);
+      same = same && ids[k] == oid[k];
+    }
+    if (LPQ > 1) __builtin_amdgcn_wave_barrier();  // every lane of the query read o[] (warm start)
+    if (sub == 0)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? ids[k] : -1;
+    const int64_t q = (int64_t)it * kResThreads + tid;
+    if (!kFused && sub == 0) a.nsame[q] = same ? 1 : 0;
+#ifdef FBR_KNN_STATS
+    ks[5] = ok;
+    ks[6] = corner;
+    ks[8] = have_prev;
+    ks[9] = same;
+    for (int k = 0; k < 10; ++k) atomicAdd(&a.knn_stats[k], (unsigned long long)ks[k]);
+#endif
+    if (kFused && ok)
+      rok = res_row(g, mg.by_id, ids, 1, corner, p, x0, y0, z0, row, b, a.fitc + (int64_t)it * 6 * kResThreads + tid,
+                    a.fits + q, same);
+  }
+  if (kFused) res_reduce(red, tid, row, b, rok, a.partial + (int64_t)it * kPartial);
+}
+
 template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ = 1>
 __global__ void __launch_bounds__(kResThreads)
 k_gn_knn(GnArgs a, int use_prev) {
   static_assert(LPQ == 1 || (!kFused && !kFlat), "wide mode is the plain kNN pass");
   __shared__ double red[kFused ? kResThreads / 64 : 1][28];
   __shared__ int2 rows[kFlat ? (2 * R + 1) * (2 * R + 1) : 1][kResThreads];
-  constexpr int QPB = kResThreads / LPQ;  // queries per workgroup
-  const int sub = (int)threadIdx.x % LPQ;
   const int nitems = a.nitems[0];
-  for (int v = blockIdx.x; v < nitems * LPQ; v += gridDim.x) {
-    const int it = v / LPQ;
-    const int tid = (v % LPQ) * QPB + (int)threadIdx.x / LPQ;  // query slot within the item
-    const int4 item = a.items[it];
-    const int job = item.x;
-    const GnState& g = a.gn[job];
-    if (!g.active) continue;  // block-uniform
-    float row[6] = {0, 0, 0, 0, 0, 0}, b = 0.0f;
-    bool rok = false;
-    if (tid < item.w) {
-      const bool corner = item.y == 0;
-      const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
-      const float* T = g.T;
-      // pointAssociateToMap (:397-403)
-      const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
-      const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
-      const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
-      const MapGrid& mg = corner ? a.mc : a.ms;
-      int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
-      float bound = __int_as_float(0x7f800000);
-      int32_t oid[5] = {-1, -1, -1, -1, -1};
-      const bool have_prev = use_prev && o[0] >= 0;
-      if (have_prev) {  // warm start: the previous iteration's neighbours of this query
-        float mx = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) oid[k] = o[k * kResThreads];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const float4 q = mg.by_id[oid[k]];
-          float dist = 0.0f, diff;
-          diff = x0 - q.x; dist += diff * diff;
-          diff = y0 - q.y; dist += diff * diff;
-          diff = z0 - q.z; dist += diff * diff;
-          mx = fmaxf(mx, dist);
-        }
-        bound = mx;
-      }
-      Knn5 nn;
-      unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      knn5_grid<R, RX, kFlat, kSparse, LPQ>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks,
-                                            &rows[0][threadIdx.x], sub);
-      if constexpr (LPQ > 1) knn5_merge<LPQ>(nn);
-      const bool ok = nn.k[4] < kKnnEmpty;
-      (void)ks;
-      int32_t ids[5];
-      bool same = have_prev && ok && a.fit_cache;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        ids[k] = knn_id(nn.k[k]);
-        same = same && ids[k] == oid[k];
-      }
-      if (LPQ > 1) __builtin_amdgcn_wave_barrier();  // every lane of the query read o[] (warm start)
-      if (sub == 0)
-#pragma unroll
-        for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? ids[k] : -1;
-      const int64_t q = (int64_t)it * kResThreads + tid;
-      if (!kFused && sub == 0) a.nsame[q] = same ? 1 : 0;
-#ifdef FBR_KNN_STATS
-      ks[5] = ok;
-      ks[6] = corner;
-      ks[8] = have_prev;
-      ks[9] = same;
-      for (int k = 0; k < 10; ++k) atomicAdd(&a.knn_stats[k], (unsigned long long)ks[k]);
-#endif
-      if (kFused && ok)
-        rok = res_row(g, mg.by_id, ids, 1, corner, p, x0, y0, z0, row, b, a.fitc + (int64_t)it * 6 * kResThreads + tid,
-                      a.fits + q, same);
-    }
-    if (kFused) res_reduce(red, tid, row, b, rok, a.partial + (int64_t)it * kPartial);
+  for (int v = blockIdx.x; v < nitems * LPQ; v += gridDim.x)
+    gn_knn_block<R, RX, kFused, kFlat, kSparse, LPQ>(a, v, use_prev, red, &rows[0][threadIdx.x]);
+}
+
+// pcl::getTransformation (x,y,z,roll,pitch,yaw) in float with glibc's sinf / cosf
+// (fbr_sincosf.h: the FMA variant restated bit for bit).
+__device__ void pose_to_T(const float* tr, float* T, float* trig) {
+  const float roll = tr[0], pitch = tr[1], yaw = tr[2];
+  const float A = gl_cosf(yaw), B = gl_sinf(yaw), C = gl_cosf(pitch), D = gl_sinf(pitch), E = gl_cosf(roll),
+              F = gl_sinf(roll);
+  const float DE = D * E, DF = D * F;
+  T[0] = A * C; T[1] = A * DF - B * E; T[2] = B * F + A * DE; T[3] = tr[3];
+  T[4] = B * C; T[5] = A * E + B * DF; T[6] = B * DE - A * F; T[7] = tr[4];
+  T[8] = -D;    T[9] = C * F;          T[10] = C * E;         T[11] = tr[5];
+  // LMOptimization (:1259-1264): srx, crx (pitch), sry, cry (yaw), srz, crz (roll)
+  trig[0] = D; trig[1] = C; trig[2] = B; trig[3] = A; trig[4] = F; trig[5] = E;
+}
+
+// The residual rows of work item `it` and its normal-equation partial (k_gn_residual's body).
+__device__ __forceinline__ void gn_residual_item(const GnArgs& a, int it, double (*red)[28]) {
+  const int tid = threadIdx.x;
+  const int4 item = a.items[it];
+  const int job = item.x;
+  const GnState& g = a.gn[job];
+  if (!g.active) return;  // block-uniform
+  float row[6] = {0, 0, 0, 0, 0, 0}, b = 0.0f;
+  bool ok = false;
+  const int32_t* nb = a.nbr + (int64_t)it * 5 * kResThreads + tid;
+  if (tid < item.w && nb[0] >= 0) {
+    const bool corner = item.y == 0;
+    const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
+    const float* T = g.T;
+    const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
+    const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
+    const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
+    const int64_t q = (int64_t)it * kResThreads + tid;
+    ok = res_row(g, corner ? a.mc.by_id : a.ms.by_id, nb, kResThreads, corner, p, x0, y0, z0, row, b,
+                 a.fitc + (int64_t)it * 6 * kResThreads + tid, a.fits + q, a.nsame[q] != 0);
   }
+  res_reduce(red, tid, row, b, ok, a.partial + (int64_t)it * kPartial);
+}
+
+// The normal equations of one job in float, as LMOptimization forms them (matAtA / matAtB).
+__device__ __forceinline__ void gn_normal_eq(const double* acc, float* AtA, float* X) {
+  int q = 0;
+  for (int r = 0; r < 6; ++r)
+    for (int c = r; c < 6; ++c) {
+      AtA[r * 6 + c] = (float)acc[q];
+      AtA[c * 6 + r] = (float)acc[q];
+      ++q;
+    }
+  for (int r = 0; r < 6; ++r) X[r] = (float)acc[21 + r];
+}
+
+// Iteration-0 degeneracy projection (:1280-1305): 6x6 Jacobi, eigenvalues < 100 zero rows of V2,
+// matP = V^-1 * V2 by LU.  It depends only on AtA, so the second wave of k_gn_solve computes it
+// (the Jacobi rotations spread over its lanes, jacobi_eigen_wave) while the first solves
+// AtA X = AtB.  All 64 lanes of the wave call it; matP / degenerate are written by lane 0.  A
+// matrix whose eigenvalues are certified above 100 (eig_above_certified: an LDL^T test with a
+// 1e-3 ||A|| margin, the common case) skips the Jacobi and the LU: degenerate = 0, and matP is
+// then never read (gn_solve_job applies it only when degenerate).
+struct EigenLds {
+  float A[36], V[36], W[6];
+  int R[6], C[6];
+};
+__device__ void gn_degeneracy(const double* acc, EigenLds& e, float* matP, int* degenerate) {
+  const int lane = threadIdx.x & 63;
+  if (lane < 36) {
+    const int r = lane / 6, c = lane % 6, lo = r < c ? r : c, hi = r < c ? c : r;
+    e.A[lane] = (float)acc[lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];  // upper-triangle order
+  }
+  wave_lds_sync();
+  if (eig_above_certified<6>(e.A, 100.0f)) {  // every eigenvalue >= 100: not degenerate, matP unused
+    if (lane == 0) *degenerate = 0;
+    return;
+  }
+  jacobi_eigen_wave<6>(e.A, e.W, e.V, e.R, e.C);
+  if (lane != 0) return;
+  float E[6], V[36], V2[36], Vi[36];
+  for (int k = 0; k < 6; ++k) E[k] = e.W[k];
+  for (int k = 0; k < 36; ++k) V[k] = e.V[k];
+  for (int k = 0; k < 36; ++k) V2[k] = V[k];
+  int deg = 0;
+  for (int i = 5; i >= 0; i--) {
+    if (E[i] < 100.0f) {
+      for (int j = 0; j < 6; j++) V2[i * 6 + j] = 0.0f;
+      deg = 1;
+    } else {
+      break;
+    }
+  }
+  *degenerate = deg;
+  if (!lu_inv6(V, Vi))
+    for (int k = 0; k < 36; ++k) Vi[k] = 0.0f;
+  float P[36];
+  for (int k = 0; k < 36; ++k) P[k] = 0.0f;
+  gemm_f32_acc64<6, 6, 6>(Vi, V2, P);
+  for (int k = 0; k < 36; ++k) matP[k] = P[k];
+}
+
+// matAtA X = matAtB by OpenCV's float Householder QR (:1276); X = 0 if singular.
+__device__ void gn_qr_step(const double* acc, float* X) {
+  float AtA[36];
+  gn_normal_eq(acc, AtA, X);
+  if (!qr_solve6(AtA, X))
+    for (int k = 0; k < 6; ++k) X[k] = 0.0f;
+}
+
+// One job's LMOptimization step on one lane (acc = the job's summed normal-equation products,
+// X = gn_qr_step's solution, matP0 / deg0 = gn_degeneracy's result at iteration 0).
+__device__ void gn_solve_job(const GnArgs& a, int job, const double* acc, float* X, const float* matP0, int deg0) {
+  GnState& g = a.gn[job];
+  const int iterCount = g.iter;
+  g.iter = iterCount + 1;
+  const int sel = (int)acc[27];
+  g.n_sel = sel;
+  if (a.trace) {
+    // filled below after the update; pre-fill with the current pose for the early-return case
+    for (int k = 0; k < 6; ++k) a.trace[((int64_t)job * a.max_iter + iterCount) * 6 + k] = g.pose[k];
+  }
+  if (sel < 50) {  // :1268 return false
+    if (g.iter >= a.max_iter) g.active = 0;
+    return;
+  }
+  // the local cv::Mat matP (:1278) is zero after iteration 0
+  if (iterCount == 0) g.degenerate = deg0;
+  if (g.degenerate) {
+    float X2[6];
+    for (int k = 0; k < 6; ++k) X2[k] = X[k];
+    if (iterCount == 0) {
+      float P[36];
+      for (int k = 0; k < 36; ++k) P[k] = matP0[k];
+      gemm_f32_acc64<6, 6, 1>(P, X2, X);
+    } else {
+      float P[36];
+      for (int k = 0; k < 36; ++k) P[k] = 0.0f;
+      gemm_f32_acc64<6, 6, 1>(P, X2, X);
+    }
+  }
+  for (int k = 0; k < 6; ++k) g.pose[k] += X[k];
+  if (a.trace)
+    for (int k = 0; k < 6; ++k) a.trace[((int64_t)job * a.max_iter + iterCount) * 6 + k] = g.pose[k];
+  const double r0 = (double)(X[0] * 57.29578f), r1 = (double)(X[1] * 57.29578f), r2 = (double)(X[2] * 57.29578f);
+  const float deltaR = (float)sqrt(r0 * r0 + r1 * r1 + r2 * r2);
+  const double t0 = (double)(X[3] * 100.0f), t1 = (double)(X[4] * 100.0f), t2 = (double)(X[5] * 100.0f);
+  const float deltaT = (float)sqrt(t0 * t0 + t1 * t1 + t2 * t2);
+  if ((double)deltaR < 0.05 && (double)deltaT < 0.05) {
+    g.converged = 1;
+    g.active = 0;
+  } else if (g.iter >= a.max_iter) {
+    g.active = 0;
+  }
+  pose_to_T(g.pose, g.T, g.trig);
+}
+
+// One job's LMOptimization step by the first two waves of a workgroup (k_gn_solve's body; extra
+// waves only pass the barriers).
+struct SolveLds {
+  double acc[28];
+  float matP0[36];
+  int deg0;
+  EigenLds eig;
+};
+__device__ __forceinline__ void gn_solve_block(const GnArgs& a, int job, SolveLds& s) {
+  const int tid = threadIdx.x;
+  GnState& g = a.gn[job];
+  if (!g.active) return;  // block-uniform
+  const int iter0 = g.iter == 0;  // read before lane 0 updates it (ordered by the barriers)
+  if (tid < 28) {
+    double sum = 0.0;
+    const int i0 = a.item_range[2 * job], i1 = a.item_range[2 * job + 1];
+#pragma unroll 8
+    for (int it = i0; it < i1; ++it) sum += a.partial[(int64_t)it * kPartial + tid];
+    s.acc[tid] = sum;
+  }
+  __syncthreads();
+  float X[6];
+  const bool solve = (int)s.acc[27] >= 50;
+  if (tid >= 64 && tid < 128 && iter0 && solve) gn_degeneracy(s.acc, s.eig, s.matP0, &s.deg0);
+  if (tid == 0 && solve) gn_qr_step(s.acc, X);
+  __syncthreads();
+  if (tid == 0) gn_solve_job(a, job, s.acc, X, s.matP0, s.deg0);
+  __syncthreads();
 }
 
 // Host launchers of the kNN pass.  launch_gn_knn_r<R, F> is instantiated in k_knn_*.hip.

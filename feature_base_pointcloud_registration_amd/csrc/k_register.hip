@@ -37,19 +37,6 @@
 namespace fbr {
 
 
-// pcl::getTransformation (x,y,z,roll,pitch,yaw) in float with glibc's sinf / cosf
-// (fbr_sincosf.h: the FMA variant restated bit for bit).
-__device__ void pose_to_T(const float* tr, float* T, float* trig) {
-  const float roll = tr[0], pitch = tr[1], yaw = tr[2];
-  const float A = gl_cosf(yaw), B = gl_sinf(yaw), C = gl_cosf(pitch), D = gl_sinf(pitch), E = gl_cosf(roll),
-              F = gl_sinf(roll);
-  const float DE = D * E, DF = D * F;
-  T[0] = A * C; T[1] = A * DF - B * E; T[2] = B * F + A * DE; T[3] = tr[3];
-  T[4] = B * C; T[5] = A * E + B * DF; T[6] = B * DE - A * F; T[7] = tr[4];
-  T[8] = -D;    T[9] = C * F;          T[10] = C * E;         T[11] = tr[5];
-  // LMOptimization (:1259-1264): srx, crx (pitch), sry, cry (yaw), srz, crz (roll)
-  trig[0] = D; trig[1] = C; trig[2] = B; trig[3] = A; trig[4] = F; trig[5] = E;
-}
 
 __global__ void k_gn_init(GnArgs a) {
   __shared__ int32_t scan[1024];
@@ -112,143 +99,10 @@ __global__ void k_gn_init(GnArgs a) {
 __global__ void __launch_bounds__(kResThreads)
 k_gn_residual(GnArgs a) {
   __shared__ double red[kResThreads / 64][28];
-  const int tid = threadIdx.x;
   const int nitems = a.nitems[0];
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
-    const int4 item = a.items[it];
-    const int job = item.x;
-    const GnState& g = a.gn[job];
-    if (!g.active) continue;  // block-uniform
-    float row[6] = {0, 0, 0, 0, 0, 0}, b = 0.0f;
-    bool ok = false;
-    const int32_t* nb = a.nbr + (int64_t)it * 5 * kResThreads + tid;
-    if (tid < item.w && nb[0] >= 0) {
-      const bool corner = item.y == 0;
-      const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
-      const float* T = g.T;
-      const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
-      const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
-      const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
-      const int64_t q = (int64_t)it * kResThreads + tid;
-      ok = res_row(g, corner ? a.mc.by_id : a.ms.by_id, nb, kResThreads, corner, p, x0, y0, z0, row, b,
-                   a.fitc + (int64_t)it * 6 * kResThreads + tid, a.fits + q, a.nsame[q] != 0);
-    }
-    res_reduce(red, tid, row, b, ok, a.partial + (int64_t)it * kPartial);
-  }
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) gn_residual_item(a, it, red);
 }
 
-// The normal equations of one job in float, as LMOptimization forms them (matAtA / matAtB).
-__device__ __forceinline__ void gn_normal_eq(const double* acc, float* AtA, float* X) {
-  int q = 0;
-  for (int r = 0; r < 6; ++r)
-    for (int c = r; c < 6; ++c) {
-      AtA[r * 6 + c] = (float)acc[q];
-      AtA[c * 6 + r] = (float)acc[q];
-      ++q;
-    }
-  for (int r = 0; r < 6; ++r) X[r] = (float)acc[21 + r];
-}
-
-// Iteration-0 degeneracy projection (:1280-1305): 6x6 Jacobi, eigenvalues < 100 zero rows of V2,
-// matP = V^-1 * V2 by LU.  It depends only on AtA, so the second wave of k_gn_solve computes it
-// (the Jacobi rotations spread over its lanes, jacobi_eigen_wave) while the first solves
-// AtA X = AtB.  All 64 lanes of the wave call it; matP / degenerate are written by lane 0.  A
-// matrix whose eigenvalues are certified above 100 (eig_above_certified: an LDL^T test with a
-// 1e-3 ||A|| margin, the common case) skips the Jacobi and the LU: degenerate = 0, and matP is
-// then never read (gn_solve_job applies it only when degenerate).
-struct EigenLds {
-  float A[36], V[36], W[6];
-  int R[6], C[6];
-};
-__device__ void gn_degeneracy(const double* acc, EigenLds& e, float* matP, int* degenerate) {
-  const int lane = threadIdx.x & 63;
-  if (lane < 36) {
-    const int r = lane / 6, c = lane % 6, lo = r < c ? r : c, hi = r < c ? c : r;
-    e.A[lane] = (float)acc[lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];  // upper-triangle order
-  }
-  wave_lds_sync();
-  if (eig_above_certified<6>(e.A, 100.0f)) {  // every eigenvalue >= 100: not degenerate, matP unused
-    if (lane == 0) *degenerate = 0;
-    return;
-  }
-  jacobi_eigen_wave<6>(e.A, e.W, e.V, e.R, e.C);
-  if (lane != 0) return;
-  float E[6], V[36], V2[36], Vi[36];
-  for (int k = 0; k < 6; ++k) E[k] = e.W[k];
-  for (int k = 0; k < 36; ++k) V[k] = e.V[k];
-  for (int k = 0; k < 36; ++k) V2[k] = V[k];
-  int deg = 0;
-  for (int i = 5; i >= 0; i--) {
-    if (E[i] < 100.0f) {
-      for (int j = 0; j < 6; j++) V2[i * 6 + j] = 0.0f;
-      deg = 1;
-    } else {
-      break;
-    }
-  }
-  *degenerate = deg;
-  if (!lu_inv6(V, Vi))
-    for (int k = 0; k < 36; ++k) Vi[k] = 0.0f;
-  float P[36];
-  for (int k = 0; k < 36; ++k) P[k] = 0.0f;
-  gemm_f32_acc64<6, 6, 6>(Vi, V2, P);
-  for (int k = 0; k < 36; ++k) matP[k] = P[k];
-}
-
-// matAtA X = matAtB by OpenCV's float Householder QR (:1276); X = 0 if singular.
-__device__ void gn_qr_step(const double* acc, float* X) {
-  float AtA[36];
-  gn_normal_eq(acc, AtA, X);
-  if (!qr_solve6(AtA, X))
-    for (int k = 0; k < 6; ++k) X[k] = 0.0f;
-}
-
-// One job's LMOptimization step on one lane (acc = the job's summed normal-equation products,
-// X = gn_qr_step's solution, matP0 / deg0 = gn_degeneracy's result at iteration 0).
-__device__ void gn_solve_job(const GnArgs& a, int job, const double* acc, float* X, const float* matP0, int deg0) {
-  GnState& g = a.gn[job];
-  const int iterCount = g.iter;
-  g.iter = iterCount + 1;
-  const int sel = (int)acc[27];
-  g.n_sel = sel;
-  if (a.trace) {
-    // filled below after the update; pre-fill with the current pose for the early-return case
-    for (int k = 0; k < 6; ++k) a.trace[((int64_t)job * a.max_iter + iterCount) * 6 + k] = g.pose[k];
-  }
-  if (sel < 50) {  // :1268 return false
-    if (g.iter >= a.max_iter) g.active = 0;
-    return;
-  }
-  // the local cv::Mat matP (:1278) is zero after iteration 0
-  if (iterCount == 0) g.degenerate = deg0;
-  if (g.degenerate) {
-    float X2[6];
-    for (int k = 0; k < 6; ++k) X2[k] = X[k];
-    if (iterCount == 0) {
-      float P[36];
-      for (int k = 0; k < 36; ++k) P[k] = matP0[k];
-      gemm_f32_acc64<6, 6, 1>(P, X2, X);
-    } else {
-      float P[36];
-      for (int k = 0; k < 36; ++k) P[k] = 0.0f;
-      gemm_f32_acc64<6, 6, 1>(P, X2, X);
-    }
-  }
-  for (int k = 0; k < 6; ++k) g.pose[k] += X[k];
-  if (a.trace)
-    for (int k = 0; k < 6; ++k) a.trace[((int64_t)job * a.max_iter + iterCount) * 6 + k] = g.pose[k];
-  const double r0 = (double)(X[0] * 57.29578f), r1 = (double)(X[1] * 57.29578f), r2 = (double)(X[2] * 57.29578f);
-  const float deltaR = (float)sqrt(r0 * r0 + r1 * r1 + r2 * r2);
-  const double t0 = (double)(X[3] * 100.0f), t1 = (double)(X[4] * 100.0f), t2 = (double)(X[5] * 100.0f);
-  const float deltaT = (float)sqrt(t0 * t0 + t1 * t1 + t2 * t2);
-  if ((double)deltaR < 0.05 && (double)deltaT < 0.05) {
-    g.converged = 1;
-    g.active = 0;
-  } else if (g.iter >= a.max_iter) {
-    g.active = 0;
-  }
-  pose_to_T(g.pose, g.T, g.trig);
-}
 
 // Two waves per job: wave 0's lanes 0..27 sum the job's item partials (each entry in item order,
 // as before); then wave 0's lane 0 solves the normal equations while, at iteration 0, wave 1's
@@ -258,29 +112,10 @@ __device__ void gn_solve_job(const GnArgs& a, int job, const double* acc, float*
 // host-mapped memory as (generation << 32 | count) so the host stops enqueueing iterations once
 // the batch converged.
 __global__ void __launch_bounds__(kSolveThreads) k_gn_solve(GnArgs a, int iter_idx, unsigned long long gen) {
-  __shared__ double acc[28];
-  __shared__ float matP0[36];
-  __shared__ int deg0;
-  __shared__ EigenLds eig;
+  __shared__ SolveLds sl;
   const int job = blockIdx.x, tid = threadIdx.x;
-  GnState& g = a.gn[job];
-  if (g.active) {  // block-uniform
-    const int iter0 = g.iter == 0;  // read before lane 0 updates it (ordered by the barriers)
-    if (tid < 28) {
-      double sum = 0.0;
-      const int i0 = a.item_range[2 * job], i1 = a.item_range[2 * job + 1];
-#pragma unroll 8
-      for (int it = i0; it < i1; ++it) sum += a.partial[(int64_t)it * kPartial + tid];
-      acc[tid] = sum;
-    }
-    __syncthreads();
-    float X[6];
-    const bool solve = (int)acc[27] >= 50;
-    if (tid >= 64 && iter0 && solve) gn_degeneracy(acc, eig, matP0, &deg0);
-    if (tid == 0 && solve) gn_qr_step(acc, X);
-    __syncthreads();
-    if (tid == 0) gn_solve_job(a, job, acc, X, matP0, deg0);
-  }
+  gn_solve_block(a, job, sl);
+  const GnState& g = a.gn[job];
   if (tid == 0) {
     atomicAdd(&a.iter_cnt[2 * iter_idx], g.active);
     __threadfence();

@@ -322,7 +322,10 @@ static void voxel_grid(const P4* in, int64_t n, float leaf, std::vector<P4>& out
     int idx = ijk0 * divb_mul[0] + ijk1 * divb_mul[1] + ijk2 * divb_mul[2];
     iv.push_back(cloud_point_index_idx{(unsigned)idx, (unsigned)i});
   }
-  std::sort(iv.begin(), iv.end(), std::less<cloud_point_index_idx>());  // unstable, libstdc++
+  // unstable, libstdc++ (ORC_VG_STABLE=1, diagnostics only: std::stable_sort, the index order)
+  static const bool stable_diag = std::getenv("ORC_VG_STABLE") && std::atoi(std::getenv("ORC_VG_STABLE")) != 0;
+  if (stable_diag) std::stable_sort(iv.begin(), iv.end(), std::less<cloud_point_index_idx>());
+  else std::sort(iv.begin(), iv.end(), std::less<cloud_point_index_idx>());
   size_t index = 0;
   while (index < iv.size()) {
     size_t i = index + 1;
