@@ -1,0 +1,316 @@
+// fbr_introsort.h — the point order inside a voxel of pcl::VoxelGrid, on the device.
+//
+// PCL's applyFilter (voxel_grid.cpp) sorts the index vector {idx, cloud_point_index} with
+// std::sort, comparing idx only, and sums each voxel's points in the resulting order
+// (featureExtraction.h:288-292, mapOptmization.h:251-257, 981-993).  std::sort is unstable, so
+// that order -- and with it the last bits of every centroid -- is libstdc++'s introsort's.
+//
+// libstdc++ (stl_algo.h; unchanged since GCC 4.8, the reference's toolchains included):
+//   __introsort_loop(first, last, depth = 2 * floor(log2 n)):
+//     while (last - first > 16) {
+//       if (depth == 0) { partial_sort(first, last, last); return; }        // heap sort
+//       --depth;
+//       __move_median_to_first(first, first + 1, mid, last - 1);
+//       cut = __unguarded_partition(first + 1, last, first);
+//       __introsort_loop(cut, last, depth); last = cut;
+//     }
+//   __final_insertion_sort(first, last): an insertion sort, i.e. STABLE on its input.
+// So std::sort's result is the stable sort (by key) of the array the partition phase leaves, and
+// that phase is what this header reproduces:
+//   * frames (sub-ranges) of one recursion level are disjoint, so they are processed level by
+//     level, in parallel (the order of disjoint frames does not change the array);
+//   * __unguarded_partition(lo, hi, pivot p) in closed form: the k-th element from the left that
+//     is not < p (a "left stopper" g_k) is swapped with the k-th element from the right that is
+//     not > p (r_k) for as long as g_k < r_k; with K such swaps the cut is min(g_K, r_{K-1}) (the
+//     swapped elements stop the scans).  g_k / r_k are ballot-ranked (one wave per small frame) or
+//     block-scan-ranked (the whole workgroup on frames larger than kIsBig);
+//   * median-of-3 and the depth-exhausted heap sort run on one lane, as serial code.
+// A stable radix sort of the result by key (the kernels' existing sorts) then gives std::sort's
+// order exactly; tests/test_voxel_order.py checks it against the host std::sort (oracle), and the
+// VoxelGrid tests compare the centroids bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+namespace fbr {
+
+#define FBR_IS_LDS __attribute__((address_space(3)))
+
+struct IsFrame {
+  int first, last, depth;
+};
+
+__host__ __device__ inline int is_lg(int n) {
+  int r = -1;
+  while (n) {
+    n >>= 1;
+    ++r;
+  }
+  return r;
+}
+
+// Visibility of this wave's LDS / global writes to its other lanes (and to later workgroup
+// barriers): workgroup-scope release / acquire around a wave barrier.
+__device__ __forceinline__ void is_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <typename KP, typename VP>
+__device__ __forceinline__ void is_swap(KP k, VP v, int a, int b) {
+  const auto ka = k[a];
+  k[a] = k[b];
+  k[b] = ka;
+  const auto va = v[a];
+  v[a] = v[b];
+  v[b] = va;
+}
+
+// __move_median_to_first(result, a, b, c) (one lane)
+template <typename KP, typename VP>
+__device__ void is_median_to_first(KP k, VP v, int result, int a, int b, int c) {
+  if (k[a] < k[b]) {
+    if (k[b] < k[c]) is_swap(k, v, result, b);
+    else if (k[a] < k[c]) is_swap(k, v, result, c);
+    else is_swap(k, v, result, a);
+  } else if (k[a] < k[c]) {
+    is_swap(k, v, result, a);
+  } else if (k[b] < k[c]) {
+    is_swap(k, v, result, c);
+  } else {
+    is_swap(k, v, result, b);
+  }
+}
+
+// std::partial_sort(first, last, last) = __make_heap + __sort_heap (stl_heap.h), one lane.
+template <typename KP, typename VP>
+__device__ void is_adjust_heap(KP k, VP v, int first, int hole, int len, uint32_t vk, uint32_t vv) {
+  const int top = hole;
+  int second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (k[first + second] < k[first + second - 1]) second--;
+    k[first + hole] = k[first + second];
+    v[first + hole] = v[first + second];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    k[first + hole] = k[first + second - 1];
+    v[first + hole] = v[first + second - 1];
+    hole = second - 1;
+  }
+  int parent = (hole - 1) / 2;  // __push_heap
+  while (hole > top && k[first + parent] < vk) {
+    k[first + hole] = k[first + parent];
+    v[first + hole] = v[first + parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  k[first + hole] = vk;
+  v[first + hole] = vv;
+}
+
+template <typename KP, typename VP>
+__device__ void is_heap_sort(KP k, VP v, int first, int last) {
+  const int len = last - first;
+  if (len >= 2) {
+    int parent = (len - 2) / 2;
+    while (true) {
+      is_adjust_heap(k, v, first, parent, len, (uint32_t)k[first + parent], (uint32_t)v[first + parent]);
+      if (parent == 0) break;
+      parent--;
+    }
+  }
+  while (last - first > 1) {
+    --last;
+    const uint32_t vk = k[last], vv = v[last];  // __pop_heap(first, last, last)
+    k[last] = k[first];
+    v[last] = v[first];
+    is_adjust_heap(k, v, first, 0, last - first, vk, vv);
+  }
+}
+
+// __unguarded_partition(lo, hi, pivot value p) by one wave; posL / posR: scratch indexed [lo, hi).
+// Returns the cut.  Ends with a wave sync.
+template <typename KP, typename VP, typename PP>
+__device__ int is_wave_partition(KP k, VP v, PP posL, PP posR, int lo, int hi, uint32_t p, int lane) {
+  const uint64_t below = (1ull << lane) - 1ull;
+  int cL = 0;
+  for (int b = lo; b < hi; b += 64) {
+    const int i = b + lane;
+    const bool isL = i < hi && !(k[i] < p);
+    const uint64_t bl = __ballot(isL);
+    if (isL) posL[lo + cL + __popcll(bl & below)] = i;
+    cL += __popcll(bl);
+  }
+  int cR = 0;
+  for (int t = hi - 1; t >= lo; t -= 64) {
+    const int i = t - lane;
+    const bool isR = i >= lo && !(p < k[i]);
+    const uint64_t br = __ballot(isR);
+    if (isR) posR[lo + cR + __popcll(br & below)] = i;
+    cR += __popcll(br);
+  }
+  is_wave_sync();
+  const int mn = min(cL, cR);
+  int K = 0;  // swaps: the k with g_k < r_k form a prefix (g increases, r decreases)
+  for (int k0 = 0; k0 < mn; k0 += 64) {
+    const int kk = k0 + lane;
+    const uint64_t bo = __ballot(kk < mn && (int)posL[lo + kk] < (int)posR[lo + kk]);
+    K += __popcll(bo);
+    if (bo != ~0ull) break;
+  }
+  for (int kk = lane; kk < K; kk += 64) is_swap(k, v, (int)posL[lo + kk], (int)posR[lo + kk]);
+  int cut = K < cL ? (int)posL[lo + K] : INT_MAX;
+  if (K > 0) cut = min(cut, (int)posR[lo + K - 1]);
+  is_wave_sync();
+  return min(cut, hi);
+}
+
+// The same by the whole workgroup (T threads) on a large frame; sh: LDS ints, >= 2 * T / 64 + 4.
+// Returns the cut to every thread.  Starts and ends with a barrier.
+template <int T, typename KP, typename VP, typename PP>
+__device__ int is_block_partition(KP k, VP v, PP posL, PP posR, int lo, int hi, uint32_t p, int* sh) {
+  constexpr int NW = T / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int m = hi - lo, per = (m + T - 1) / T;
+  const int b0 = lo + min(m, tid * per), b1 = lo + min(m, (tid + 1) * per);
+  int nl = 0, nr = 0;
+  for (int i = b0; i < b1; ++i) {
+    const uint32_t x = k[i];
+    nl += !(x < p);
+    nr += !(p < x);
+  }
+  // exclusive prefix of (nl, nr) over the threads in order
+  int il = nl, ir = nr;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int a = __shfl_up(il, o), b = __shfl_up(ir, o);
+    if (lane >= o) {
+      il += a;
+      ir += b;
+    }
+  }
+  __syncthreads();
+  if (lane == 63) {
+    sh[w] = il;
+    sh[NW + w] = ir;
+  }
+  __syncthreads();
+  int bl = 0, br = 0, cL = 0, cR = 0;
+  for (int ww = 0; ww < NW; ++ww) {
+    bl += ww < w ? sh[ww] : 0;
+    br += ww < w ? sh[NW + ww] : 0;
+    cL += sh[ww];
+    cR += sh[NW + ww];
+  }
+  int ol = bl + il - nl, orr = br + ir - nr;  // this thread's first left / right stopper ranks
+  for (int i = b0; i < b1; ++i) {
+    const uint32_t x = k[i];
+    if (!(x < p)) posL[lo + ol++] = i;
+    if (!(p < x)) posR[lo + (cR - 1 - orr++)] = i;  // rank from the right
+  }
+  __syncthreads();
+  if (tid == 0) {  // K: first k < min(cL, cR) with g_k >= r_k (binary search over the prefix)
+    int a = 0, b = min(cL, cR);
+    while (a < b) {
+      const int c = (a + b) >> 1;
+      if ((int)posL[lo + c] < (int)posR[lo + c]) a = c + 1;
+      else b = c;
+    }
+    const int K = a;
+    int cut = K < cL ? (int)posL[lo + K] : INT_MAX;
+    if (K > 0) cut = min(cut, (int)posR[lo + K - 1]);
+    sh[2 * NW] = K;
+    sh[2 * NW + 1] = min(cut, hi);
+  }
+  __syncthreads();
+  const int K = sh[2 * NW], cut = sh[2 * NW + 1];
+  for (int kk = tid; kk < K; kk += T) is_swap(k, v, (int)posL[lo + kk], (int)posR[lo + kk]);
+  __syncthreads();
+  return cut;
+}
+
+template <typename FP>
+__device__ __forceinline__ void is_push(FP f, int i, int first, int last, int depth) {
+  f[3 * i] = first;
+  f[3 * i + 1] = last;
+  f[3 * i + 2] = depth;
+}
+
+constexpr int kIsBig = 2048;  // frames larger than this are partitioned by the whole workgroup
+
+// The partition phase of std::sort on (k, v)[0, n) by one workgroup of T threads.  posL / posR:
+// n-entry scratch; fa / fb: int frame lists {first, last, depth} of >= n / 17 + 2 entries each
+// (3 ints per frame); sh: LDS ints (>= 2 * T / 64 + 8).  Starts and ends with a barrier.  A stable sort by key of the result is std::sort's.
+template <int T, typename KP, typename VP, typename PP, typename FP>
+__device__ void is_partition_phase(KP k, VP v, PP posL, PP posR, int n, FP fa, FP fb, int* sh) {
+  constexpr int NW = T / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int* ncur = sh + 2 * NW + 2;
+  int* nnext = sh + 2 * NW + 3;
+  __syncthreads();
+  if (tid == 0) {
+    *ncur = 0;
+    if (n > 16) {
+      fa[0] = 0;
+      fa[1] = n;
+      fa[2] = 2 * is_lg(n);
+      *ncur = 1;
+    }
+  }
+  __syncthreads();
+  while (true) {
+    const int nc = *ncur;
+    if (nc == 0) break;
+    __syncthreads();
+    if (tid == 0) *nnext = 0;
+    __syncthreads();
+    // large frames: one at a time, every thread (their count is small)
+    for (int f = 0; f < nc; ++f) {
+      const IsFrame F{fa[3 * f], fa[3 * f + 1], fa[3 * f + 2]};
+      if (F.last - F.first <= kIsBig || F.depth == 0) continue;  // uniform
+      if (tid == 0) is_median_to_first(k, v, F.first, F.first + 1, F.first + (F.last - F.first) / 2, F.last - 1);
+      __syncthreads();
+      const uint32_t p = k[F.first];
+      const int cut = is_block_partition<T>(k, v, posL, posR, F.first + 1, F.last, p, sh);
+      if (tid == 0) {
+        if (cut - F.first > 16) is_push(fb, atomicAdd(nnext, 1), F.first, cut, F.depth - 1);
+        if (F.last - cut > 16) is_push(fb, atomicAdd(nnext, 1), cut, F.last, F.depth - 1);
+      }
+    }
+    // small frames (and depth-exhausted ones): one wave each, wave w takes frames w, w + NW, ...
+    // (every wave runs the same number of rounds: no wave leaves the loop early)
+    for (int base = 0; base < nc; base += NW) {
+      const int f = base + w;
+      if (f >= nc) continue;  // wave-uniform
+      const IsFrame F{fa[3 * f], fa[3 * f + 1], fa[3 * f + 2]};
+      if (F.last - F.first > kIsBig && F.depth > 0) continue;  // done above
+      if (F.depth == 0) {
+        if (lane == 0) is_heap_sort(k, v, F.first, F.last);
+        is_wave_sync();
+        continue;
+      }
+      if (lane == 0) is_median_to_first(k, v, F.first, F.first + 1, F.first + (F.last - F.first) / 2, F.last - 1);
+      is_wave_sync();
+      const uint32_t p = k[F.first];
+      const int cut = is_wave_partition(k, v, posL, posR, F.first + 1, F.last, p, lane);
+      if (lane == 0) {
+        if (cut - F.first > 16) is_push(fb, atomicAdd(nnext, 1), F.first, cut, F.depth - 1);
+        if (F.last - cut > 16) is_push(fb, atomicAdd(nnext, 1), cut, F.last, F.depth - 1);
+      }
+    }
+    __syncthreads();
+    if (tid == 0) *ncur = *nnext;
+    FP t = fa;
+    fa = fb;
+    fb = t;
+    __syncthreads();
+  }
+  (void)w;
+}
+
+}  // namespace fbr

@@ -10,6 +10,7 @@
 #include "fbr_common.h"
 #include "fbr_fdlibm.h"
 #include "fbr_sincosf.h"
+#include "fbr_introsort.h"
 #include "fbr_solvers.h"
 
 namespace fbr {
@@ -56,7 +57,59 @@ __global__ void k_selftest_eig_cert(int n, const float* a, float thr, int32_t* o
   if (m < n) out[m] = eig_above_certified<6>(a + (int64_t)m * 36, thr) ? 1 : 0;
 }
 
+// std::sort's partition phase (fbr_introsort.h) on one array: lds = 0 keeps everything in global
+// memory (the device-wide VoxelGrid's variant), lds = 1 the keys / values / positions in LDS
+// (n <= kIsortLdsCap, the per-segment kernels' variant).  v[] ends as the permuted indices.
+constexpr int kIsortLdsCap = 8192;
+__global__ void __launch_bounds__(1024) k_selftest_isort(uint32_t* k, uint32_t* v, int32_t* posL, int32_t* posR,
+                                                         int* fa, int* fb, int n, int lds) {
+  __shared__ int sh[64];
+  if (!lds) {
+    is_partition_phase<1024>(k, v, posL, posR, n, fa, fb, sh);
+    return;
+  }
+  __shared__ uint32_t lk[kIsortLdsCap];
+  __shared__ uint16_t lv[kIsortLdsCap], lpl[kIsortLdsCap], lpr[kIsortLdsCap];
+  __shared__ int lfa[3 * (kIsortLdsCap / 17 + 2)], lfb[3 * (kIsortLdsCap / 17 + 2)];
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    lk[i] = k[i];
+    lv[i] = (uint16_t)i;
+  }
+  is_partition_phase<1024>((FBR_IS_LDS uint32_t*)lk, (FBR_IS_LDS uint16_t*)lv, (FBR_IS_LDS uint16_t*)lpl,
+                           (FBR_IS_LDS uint16_t*)lpr, n, (FBR_IS_LDS int*)lfa, (FBR_IS_LDS int*)lfb, sh);
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    k[i] = lk[i];
+    v[i] = lv[i];
+  }
+}
+
 }  // namespace fbr
+
+extern "C" int fbr_selftest_voxel_order(int64_t n, const uint32_t* keys, int lds, uint32_t* perm) {
+  if (n < 0 || n > (int64_t)INT32_MAX / 4 || (n && (!keys || !perm)) || (lds && n > fbr::kIsortLdsCap))
+    return FBR_ERR_INVALID_ARG;
+  if (n == 0) return FBR_OK;
+  std::vector<uint32_t> iv(n);
+  for (int64_t i = 0; i < n; ++i) iv[i] = (uint32_t)i;
+  uint32_t *dk = nullptr, *dv = nullptr;
+  int32_t *pl = nullptr, *pr = nullptr;
+  int *fa = nullptr, *fb = nullptr;
+  const int64_t nf = n / 17 + 2;
+  int rc = FBR_OK;
+  if (hipMalloc(&dk, 4 * n) != hipSuccess || hipMalloc(&dv, 4 * n) != hipSuccess || hipMalloc(&pl, 4 * n) != hipSuccess ||
+      hipMalloc(&pr, 4 * n) != hipSuccess || hipMalloc(&fa, 3 * sizeof(int) * nf) != hipSuccess ||
+      hipMalloc(&fb, 3 * sizeof(int) * nf) != hipSuccess) {
+    rc = FBR_ERR_HIP;
+  } else if (hipMemcpy(dk, keys, 4 * n, hipMemcpyHostToDevice) != hipSuccess ||
+             hipMemcpy(dv, iv.data(), 4 * n, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = FBR_ERR_HIP;
+  } else {
+    hipLaunchKernelGGL(fbr::k_selftest_isort, dim3(1), dim3(1024), 0, 0, dk, dv, pl, pr, fa, fb, (int)n, lds);
+    if (hipMemcpy(perm, dv, 4 * n, hipMemcpyDeviceToHost) != hipSuccess) rc = FBR_ERR_HIP;
+  }
+  for (void* q : {(void*)dk, (void*)dv, (void*)pl, (void*)pr, (void*)fa, (void*)fb}) (void)hipFree(q);
+  return rc;
+}
 
 extern "C" int fbr_selftest_eig_certified(int n, const float* a, float thr, int32_t* out) {
   if (n <= 0 || !a || !out) return FBR_ERR_INVALID_ARG;

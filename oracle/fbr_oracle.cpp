@@ -1576,6 +1576,14 @@ void orc_sort_smoothness(const float* values, int64_t n, int64_t* ind_out) {
   std::sort(v.begin(), v.end(), by_value());
   for (int64_t i = 0; i < n; ++i) ind_out[i] = (int64_t)v[i].ind;
 }
+// Sort probe: libstdc++ std::sort of PCL's cloud_point_index_idx {idx, i} by idx (VoxelGrid,
+// voxel_grid.cpp); writes the resulting cloud_point_index order.
+void orc_sort_voxel_pairs(const uint32_t* keys, int64_t n, int64_t* ind_out) {
+  std::vector<cloud_point_index_idx> v(n);
+  for (int64_t i = 0; i < n; ++i) v[i] = cloud_point_index_idx{keys[i], (unsigned)i};
+  std::sort(v.begin(), v.end(), std::less<cloud_point_index_idx>());
+  for (int64_t i = 0; i < n; ++i) ind_out[i] = (int64_t)v[i].cloud_point_index;
+}
 int orc_num_threads_max(void) { return omp_get_max_threads(); }
 
 // Accumulated per-stage wall time (ms) of process_scan / register calls since the last reset:

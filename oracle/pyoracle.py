@@ -67,6 +67,7 @@ def lib():
         L.orc_colpiv_solve.argtypes = [_VP, _VP, _VP]
         L.orc_knn5.argtypes = [_VP, _I64, _VP, _I64, _VP, _VP]
         L.orc_sort_smoothness.argtypes = [_VP, _I64, _VP]
+        L.orc_sort_voxel_pairs.argtypes = [_VP, _I64, _VP]
         L.orc_stage_ms.argtypes = [_VP, ctypes.c_int]
         _LIB = L
     return _LIB
@@ -212,6 +213,14 @@ def sort_smoothness(values):
     v = np.ascontiguousarray(values, np.float32)
     out = np.zeros(len(v), np.int64)
     lib().orc_sort_smoothness(ptr(v), len(v), ptr(out))
+    return out
+
+
+def sort_voxel_pairs(keys):
+    """The point order std::sort leaves PCL's VoxelGrid index vector in (keys = voxel indices)."""
+    k = np.ascontiguousarray(keys, np.uint32)
+    out = np.zeros(len(k), np.int64)
+    lib().orc_sort_voxel_pairs(ptr(k), len(k), ptr(out))
     return out
 
 
