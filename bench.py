@@ -99,6 +99,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="worker threads of the all-cores CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exact-line", type=int, default=1,
+                    help="rank 0 at N=1: a child run with FBR_VG_EXACT=1 (PCL's point order inside voxels, "
+                         "bit-identical poses) reports its throughput and parity block; 0 disables")
     ap.add_argument("--deskew", action="store_true",
                     help="enable the IMU deskew path (SURVEY 8f row 3): one imuDeskewInfo table per job")
     ap.add_argument("--dist", action="store_true",
@@ -191,6 +194,24 @@ def latency_line(cfg, corner_map, surf_map, n, cpu_scans=0):
         out["cpu_oracle_threads"] = int(P.number_of_cores)
         out["chain_max_abs_pose_diff_vs_oracle"] = dmax
     return out
+
+
+def exact_line(args):
+    """The same workload with FBR_VG_EXACT=1 in a child process (the knob is read once per process):
+    every VoxelGrid sums a voxel's points in std::sort's order (csrc/fbr_introsort.h), so the poses
+    equal the oracle's bit for bit.  B = 256 jobs, its parity block over the oracle sample."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--batch", "256", "--steps", "5",
+           "--warmup", "2", "--latency", "0", "--ingest", "0", "--profile", "off", "--exact-line", "0",
+           "--cpu-sample", str(args.cpu_sample), "--pmc-json", "none"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=dict(os.environ, FBR_VG_EXACT="1"))
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"], "jobs_per_step": 256,
+            "path": "FBR_VG_EXACT=1: std::sort's partition phase emulated in every VoxelGrid (per-ring, mapping DS, "
+                    "start-up map), then the stable radix sort",
+            "parity_vs_ref": d.get("parity_vs_ref"), "pose_rmse_vs_ref": d.get("pose_rmse_vs_ref")}
 
 
 def main():
@@ -490,6 +511,8 @@ def main():
         result["cpu_baseline_all_cores"] = {
             "value": round(S / cpu_all_s, 3), "unit": "scans/s", "cores": nth, "kind": "port",
             "sample": f"the same {S} jobs, {nth} independent single-threaded jobs at a time"}
+    if world == 1 and args.exact_line and not args.no_cpu_baseline and os.environ.get("FBR_VG_EXACT", "0") == "0":
+        result["exact_voxel_order"] = exact_line(args)
     print(json.dumps(result), flush=True)
     ctx.close()
     if dist is not None:

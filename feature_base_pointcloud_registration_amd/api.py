@@ -187,7 +187,7 @@ def selftest_voxel_order(keys, lds=False):
     std::sort leaves (keys[i], i) in, i.e. the stable key sort of the partitioned sequence."""
     k = np.ascontiguousarray(keys, np.uint32)
     perm = np.zeros(len(k), np.uint32)
-    _check(lib().fbr_selftest_voxel_order(len(k), ptr(k), 1 if lds else 0, ptr(perm)), "fbr_selftest_voxel_order")
+    _check(lib().fbr_selftest_voxel_order(len(k), ptr(k), int(lds), ptr(perm)), "fbr_selftest_voxel_order")
     return perm[np.argsort(k[perm], kind="stable")].astype(np.int64)
 
 

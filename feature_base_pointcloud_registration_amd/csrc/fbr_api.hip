@@ -305,7 +305,7 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
   uint32_t* d_sc = nullptr;
   int rc = FBR_OK;
   const bool large = n >= vg_large_min();
-  if (dalloc(&d_in, n) || dalloc(&d_out, n) || dalloc(&d_cnt, 2) || (!large && dalloc(&d_sc, 4 * n))) {
+  if (dalloc(&d_in, n) || dalloc(&d_out, n) || dalloc(&d_cnt, 2) || (!large && dalloc(&d_sc, kVgScratch * n))) {
     rc = FBR_ERR_HIP;
   } else {
     int32_t nn = (int32_t)n;
@@ -335,6 +335,7 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
       a.s[0].scratch = d_sc;
       a.s[0].leaf = leaf;
       a.s[0].nseg = 1;
+      a.s[0].exact = vg_exact() ? 1 : 0;
       launch_voxel_grid(c->stream, a);
       int32_t nout = 0;
       if (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
@@ -431,6 +432,7 @@ int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode) {
   v.stride_out = c->W;
   v.cnt_out = c->d_surf_ring_cnt + j0 * H;
   v.dbg = std::getenv("FBR_VR_DBG") ? std::atoi(std::getenv("FBR_VR_DBG")) : 0;
+  v.exact = vg_exact() ? 1 : 0;
   v.stamps = a.stamps;
   TIMED_ON(c, sb.st, "voxel_ring", launch_voxel_ring(sb.st, v));
   TIMED_ON(c, sb.st, "concat",
@@ -525,9 +527,10 @@ int register_prepare(fbr_ctx* c, const Sub& sb, bool trace) {
   VgArgs v{};
   const int64_t ccap = std::min<int64_t>(HW, (int64_t)kCornerPerRing * c->H);
   v.s[0] = VgSet{c->d_surf_all + j0 * HW, HW, c->d_nsurf + j0, HW, c->d_surfDS + j0 * HW, HW, c->d_nsds + j0,
-                 c->d_vg_scratch + j0 * 4 * HW, c->P.mapping_surf_leaf_size, sb.B, 1};
+                 c->d_vg_scratch + j0 * kVgScratch * HW, c->P.mapping_surf_leaf_size, sb.B, 1, vg_exact() ? 1 : 0};
   v.s[1] = VgSet{c->d_corner_all + j0 * HW, HW, c->d_ncorner + j0, ccap, c->d_cornerDS + j0 * HW, HW, c->d_ncds + j0,
-                 c->d_vg_scratch + (int64_t)c->Bcap * 4 * HW + j0 * 4 * ccap, c->P.mapping_corner_leaf_size, sb.B, 1};
+                 c->d_vg_scratch + (int64_t)c->Bcap * kVgScratch * HW + j0 * kVgScratch * ccap, c->P.mapping_corner_leaf_size,
+                 sb.B, 1, vg_exact() ? 1 : 0};
   TIMED_ON(c, sb.st, "voxel_scan", launch_voxel_grid(sb.st, v));
   GnArgs a = gn_args(c, sb, trace);
   if (trace) CK(hipMemsetAsync(a.trace, 0, sizeof(float) * sb.B * c->P.max_iterations * 6, sb.st));
@@ -894,7 +897,7 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
     (void)hipFree(d_cnt);
     return rc;
   }
-  if (dalloc(&d_cnt, 2) || dalloc(&d_sc, 4 * n)) {
+  if (dalloc(&d_cnt, 2) || dalloc(&d_sc, kVgScratch * n)) {
     rc = FBR_ERR_HIP;
   } else {
     int32_t nn = (int32_t)n, nout = 0;
@@ -909,6 +912,7 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
     a.s[0].scratch = d_sc;
     a.s[0].leaf = leaf;
     a.s[0].nseg = 1;
+    a.s[0].exact = vg_exact() ? 1 : 0;
     if (hipMemcpyAsync(d_cnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
       rc = FBR_ERR_HIP;
     } else {
@@ -1026,7 +1030,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   if (const char* e = std::getenv("FBR_NSUB")) c->nsub_pref = std::max(1, std::min(kMaxSub, std::atoi(e)));
   c->items_per_job = (int)(2 * ((HW + 255) / 256 + 1));
   c->max_items = (int)(B * c->items_per_job);
-  c->vg_scratch_elems = 4 * B * (HW + std::min<int64_t>(HW, (int64_t)kCornerPerRing * H));
+  c->vg_scratch_elems = kVgScratch * B * (HW + std::min<int64_t>(HW, (int64_t)kCornerPerRing * H));
   bool fail = dalloc(&c->d_pts, B * c->NMAX) || dalloc(&c->d_nin, B) || dalloc(&c->d_guess, B * 6) ||
               dalloc(&c->d_owner, B * HW) || dalloc(&c->d_rowcnt, B * H) || dalloc(&c->d_col, B * HW) ||
               dalloc(&c->d_start, B * H) || dalloc(&c->d_end, B * H) || dalloc(&c->d_nvalid, B) ||

@@ -234,6 +234,92 @@ __device__ int is_block_partition(KP k, VP v, PP posL, PP posR, int lo, int hi, 
   return cut;
 }
 
+// A frame of at most 64 elements and its whole subtree of the introsort recursion, by one wave
+// with the elements in registers (lane j holds element first + j): median-of-3 and the partition's
+// swaps are lane exchanges, the stoppers' ranks ballots; the k-th left / right stopper positions
+// go through the frame's own slots of posL / posR (rank -> lane).  The sub-frames are kept on a
+// wave-uniform stack (children of one frame are disjoint, so their order is immaterial).  A
+// depth-exhausted sub-frame is written back and heap-sorted by lane 0 (rare).  Ends with a wave
+// sync after the write-back.
+template <typename KP, typename VP, typename PP>
+__device__ void is_wave_small(KP k, VP v, PP posL, PP posR, int first, int last, int depth, int lane) {
+  const int m = last - first;
+  uint32_t key = lane < m ? (uint32_t)k[first + lane] : 0xFFFFFFFFu;
+  uint32_t val = lane < m ? (uint32_t)v[first + lane] : 0u;
+  // the stack of pending sub-frames lives in the lanes' registers (slot j in lane j), so the
+  // dynamically indexed entries are lane exchanges instead of scratch memory
+  int st_a = 0, st_b = m, st_d = depth;
+  int sp = 1;
+  const uint64_t below = (1ull << lane) - 1ull, above = lane == 63 ? 0ull : ~0ull << (lane + 1);
+  while (sp > 0) {
+    --sp;
+    const int a = __shfl(st_a, sp), b = __shfl(st_b, sp);
+    int d = __shfl(st_d, sp);
+    if (b - a <= 16) continue;
+    if (d == 0) {  // partial_sort(a, b, b): through memory, one lane
+      if (lane < m) {
+        k[first + lane] = key;
+        v[first + lane] = val;
+      }
+      is_wave_sync();
+      if (lane == 0) is_heap_sort(k, v, first + a, first + b);
+      is_wave_sync();
+      key = lane < m ? (uint32_t)k[first + lane] : 0xFFFFFFFFu;
+      val = lane < m ? (uint32_t)v[first + lane] : 0u;
+      continue;
+    }
+    --d;
+    // __move_median_to_first(a, a + 1, mid, b - 1): exchange lane a with the median's lane
+    const int mid = a + (b - a) / 2;
+    const uint32_t x = __shfl(key, a + 1), y = __shfl(key, mid), z = __shfl(key, b - 1);
+    int c;
+    if (x < y) c = (y < z) ? mid : ((x < z) ? b - 1 : a + 1);
+    else c = (x < z) ? a + 1 : ((y < z) ? b - 1 : mid);
+    {
+      const int src = lane == a ? c : (lane == c ? a : lane);
+      key = __shfl(key, src);
+      val = __shfl(val, src);
+    }
+    const uint32_t p = __shfl(key, a);
+    // __unguarded_partition(a + 1, b, pivot p) in closed form
+    const bool in = lane > a && lane < b;
+    const bool isL = in && !(key < p), isR = in && !(p < key);
+    const uint64_t bl = __ballot(isL), br = __ballot(isR);
+    const int cL = __popcll(bl), cR = __popcll(br);
+    const int rL = __popcll(bl & below), rR = __popcll(br & above);  // rank from the left / right
+    if (isL) posL[first + rL] = lane;  // g_k
+    if (isR) posR[first + rR] = lane;  // r_k
+    is_wave_sync();
+    const int mn = min(cL, cR);
+    const int rk = isL && rL < mn ? (int)posR[first + rL] : -1;  // r_k of this left stopper
+    const int K = __popcll(__ballot(isL && rL < mn && lane < rk));
+    int partner = lane;
+    if (isL && rL < K) partner = rk;
+    if (isR && rR < K) partner = (int)posL[first + rR];
+    int cut = K < cL ? (int)posL[first + K] : 64;
+    if (K > 0) cut = min(cut, (int)posR[first + K - 1]);
+    cut = min(cut, b);
+    is_wave_sync();  // the rank slots are rewritten by the next frame
+    key = __shfl(key, partner);
+    val = __shfl(val, partner);
+    if (lane == sp) {
+      st_a = a;
+      st_b = cut;
+      st_d = d;
+    } else if (lane == sp + 1) {
+      st_a = cut;
+      st_b = b;
+      st_d = d;
+    }
+    sp += 2;
+  }
+  if (lane < m) {
+    k[first + lane] = key;
+    v[first + lane] = val;
+  }
+  is_wave_sync();
+}
+
 template <typename FP>
 __device__ __forceinline__ void is_push(FP f, int i, int first, int last, int depth) {
   f[3 * i] = first;
@@ -241,12 +327,12 @@ __device__ __forceinline__ void is_push(FP f, int i, int first, int last, int de
   f[3 * i + 2] = depth;
 }
 
-constexpr int kIsBig = 2048;  // frames larger than this are partitioned by the whole workgroup
+constexpr int kIsBig = 2048;  // default: frames larger than this are partitioned by the whole workgroup
 
 // The partition phase of std::sort on (k, v)[0, n) by one workgroup of T threads.  posL / posR:
 // n-entry scratch; fa / fb: int frame lists {first, last, depth} of >= n / 17 + 2 entries each
 // (3 ints per frame); sh: LDS ints (>= 2 * T / 64 + 8).  Starts and ends with a barrier.  A stable sort by key of the result is std::sort's.
-template <int T, typename KP, typename VP, typename PP, typename FP>
+template <int T, typename KP, typename VP, typename PP, typename FP, int BIG = kIsBig>
 __device__ void is_partition_phase(KP k, VP v, PP posL, PP posR, int n, FP fa, FP fb, int* sh) {
   constexpr int NW = T / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -272,7 +358,7 @@ __device__ void is_partition_phase(KP k, VP v, PP posL, PP posR, int n, FP fa, F
     // large frames: one at a time, every thread (their count is small)
     for (int f = 0; f < nc; ++f) {
       const IsFrame F{fa[3 * f], fa[3 * f + 1], fa[3 * f + 2]};
-      if (F.last - F.first <= kIsBig || F.depth == 0) continue;  // uniform
+      if (F.last - F.first <= BIG || F.depth == 0) continue;  // uniform
       if (tid == 0) is_median_to_first(k, v, F.first, F.first + 1, F.first + (F.last - F.first) / 2, F.last - 1);
       __syncthreads();
       const uint32_t p = k[F.first];
@@ -288,10 +374,14 @@ __device__ void is_partition_phase(KP k, VP v, PP posL, PP posR, int n, FP fa, F
       const int f = base + w;
       if (f >= nc) continue;  // wave-uniform
       const IsFrame F{fa[3 * f], fa[3 * f + 1], fa[3 * f + 2]};
-      if (F.last - F.first > kIsBig && F.depth > 0) continue;  // done above
+      if (F.last - F.first > BIG && F.depth > 0) continue;  // done above
       if (F.depth == 0) {
         if (lane == 0) is_heap_sort(k, v, F.first, F.last);
         is_wave_sync();
+        continue;
+      }
+      if (F.last - F.first <= 64) {  // the frame's whole subtree in registers
+        is_wave_small(k, v, posL, posR, F.first, F.last, F.depth, lane);
         continue;
       }
       if (lane == 0) is_median_to_first(k, v, F.first, F.first + 1, F.first + (F.last - F.first) / 2, F.last - 1);

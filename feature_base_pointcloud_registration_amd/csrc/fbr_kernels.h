@@ -109,11 +109,18 @@ struct VgSet {               // nseg segments of one cloud family, one leaf size
   float4* out;
   int64_t stride_out;
   int32_t* cnt_out;
-  uint32_t* scratch;         // global mode: [nseg][4][cap]
+  uint32_t* scratch;         // global mode: [nseg][kVgScratch][cap]
   float leaf;
   int nseg;
   int morton;                // 1: emit voxels in Morton order of (i,j,k) instead of PCL key order
+  int exact;                 // 1: PCL's point order inside voxels (std::sort's, fbr_introsort.h)
 };
+// Per-point u32 slots of a VoxelGrid segment's global scratch: keys / indices ping-pong (4) and
+// the std::sort emulation's frame lists (1).
+constexpr int64_t kVgScratch = 5;
+// FBR_VG_EXACT=1: sum a voxel's points in std::sort's order (PCL's), bit-identical centroids;
+// default 0: index order (centroids to float rounding)
+bool vg_exact();
 struct VgArgs {
   VgSet s[2];                // segments of set 0, then of set 1 (set 1 may be empty)
 };
@@ -175,6 +182,7 @@ struct VgRing {
   int64_t stride_out;
   int32_t* cnt_out;          // [B*H]
   int dbg;                   // diagnostic phase cut (FBR_VR_DBG; 0 = full kernel)
+  int exact;                 // 1: PCL's point order inside voxels (std::sort's, fbr_introsort.h)
   unsigned long long* stamps;  // diagnostic builds (FBR_VR_STAMPS) only: [B*H][12]
 };
 void launch_voxel_ring(hipStream_t s, const VgRing& a);

@@ -59,7 +59,8 @@ __global__ void k_selftest_eig_cert(int n, const float* a, float thr, int32_t* o
 
 // std::sort's partition phase (fbr_introsort.h) on one array: lds = 0 keeps everything in global
 // memory (the device-wide VoxelGrid's variant), lds = 1 the keys / values / positions in LDS
-// (n <= kIsortLdsCap, the per-segment kernels' variant).  v[] ends as the permuted indices.
+// (n <= kIsortLdsCap, the per-segment kernels' variant), lds = 2 keys / values in LDS and the
+// positions in global memory (the mapping-DS kernel's variant).  v[] ends as the permuted indices.
 constexpr int kIsortLdsCap = 8192;
 __global__ void __launch_bounds__(1024) k_selftest_isort(uint32_t* k, uint32_t* v, int32_t* posL, int32_t* posR,
                                                          int* fa, int* fb, int n, int lds) {
@@ -83,10 +84,32 @@ __global__ void __launch_bounds__(1024) k_selftest_isort(uint32_t* k, uint32_t* 
   }
 }
 
+// lds = 2: keys / values in LDS up to the mapping-DS kernel's 1024 * 18 points, positions in
+// global memory (k_voxel_grid_ip's variant).
+constexpr int kIsortLdsCap2 = 1024 * 18;
+__global__ void __launch_bounds__(1024) k_selftest_isort2(uint32_t* k, uint32_t* v, int32_t* posL, int32_t* posR,
+                                                          int n) {
+  __shared__ int sh[64];
+  __shared__ uint32_t lk[kIsortLdsCap2];
+  __shared__ uint16_t lv[kIsortLdsCap2];
+  __shared__ int lfa[3 * (kIsortLdsCap2 / 17 + 2)], lfb[3 * (kIsortLdsCap2 / 17 + 2)];
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    lk[i] = k[i];
+    lv[i] = (uint16_t)i;
+  }
+  is_partition_phase<1024>((FBR_IS_LDS uint32_t*)lk, (FBR_IS_LDS uint16_t*)lv, posL, posR, n, (FBR_IS_LDS int*)lfa,
+                           (FBR_IS_LDS int*)lfb, sh);
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    k[i] = lk[i];
+    v[i] = lv[i];
+  }
+}
+
 }  // namespace fbr
 
 extern "C" int fbr_selftest_voxel_order(int64_t n, const uint32_t* keys, int lds, uint32_t* perm) {
-  if (n < 0 || n > (int64_t)INT32_MAX / 4 || (n && (!keys || !perm)) || (lds && n > fbr::kIsortLdsCap))
+  if (n < 0 || n > (int64_t)INT32_MAX / 4 || (n && (!keys || !perm)) || (lds == 1 && n > fbr::kIsortLdsCap) ||
+      (lds == 2 && n > fbr::kIsortLdsCap2))
     return FBR_ERR_INVALID_ARG;
   if (n == 0) return FBR_OK;
   std::vector<uint32_t> iv(n);
@@ -104,7 +127,8 @@ extern "C" int fbr_selftest_voxel_order(int64_t n, const uint32_t* keys, int lds
              hipMemcpy(dv, iv.data(), 4 * n, hipMemcpyHostToDevice) != hipSuccess) {
     rc = FBR_ERR_HIP;
   } else {
-    hipLaunchKernelGGL(fbr::k_selftest_isort, dim3(1), dim3(1024), 0, 0, dk, dv, pl, pr, fa, fb, (int)n, lds);
+    if (lds == 2) hipLaunchKernelGGL(fbr::k_selftest_isort2, dim3(1), dim3(1024), 0, 0, dk, dv, pl, pr, (int)n);
+    else hipLaunchKernelGGL(fbr::k_selftest_isort, dim3(1), dim3(1024), 0, 0, dk, dv, pl, pr, fa, fb, (int)n, lds);
     if (hipMemcpy(perm, dv, 4 * n, hipMemcpyDeviceToHost) != hipSuccess) rc = FBR_ERR_HIP;
   }
   for (void* q : {(void*)dk, (void*)dv, (void*)pl, (void*)pr, (void*)fa, (void*)fb}) (void)hipFree(q);

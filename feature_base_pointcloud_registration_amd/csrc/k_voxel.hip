@@ -7,9 +7,11 @@
 // key = ijk0 + ijk1*div_x + ijk2*div_x*div_y with ijk = int(floor(p*inv_leaf) - float(min_b)),
 // voxels emitted in ascending key order, centroid = float sum of x,y,z,intensity / count.
 // PCL sorts (key, index) with the unstable std::sort, so the order of points inside one voxel —
-// and hence the last bits of the centroid sum — is introsort-specific; this kernel sorts stably
-// (ascending input index inside a voxel).  Voxel membership and output order are exact; centroids
-// agree with the reference to float rounding (tests state the tolerance).
+// and hence the last bits of the centroid sum — is introsort-specific.  The kernels reproduce it
+// (fbr_introsort.h) when FBR_VG_EXACT=1: std::sort's partition phase on (PCL key, index), then
+// their stable radix sort of that sequence, which is std::sort's result; centroids are bit-exact.
+// By default the partition phase is skipped (points summed in index order, centroids to float
+// rounding, at about twice the exact mode's throughput).
 //
 // Morton mode (downsampleCurrentScan only): the same voxels and centroids, emitted in Morton order
 // of (i,j,k) so that consecutive output points are spatially compact.  The order of the mapping
@@ -24,10 +26,12 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include "fbr_common.h"
+#include "fbr_introsort.h"
 #include "fbr_kernels.h"
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace fbr {
 
@@ -114,6 +118,19 @@ struct VgGrid {
         nbits = maxk == 0 ? 1 : 32 - __clz(maxk);
       }
     }
+  }
+  // PCL's key (the one std::sort compares), whatever the output order
+  __device__ __forceinline__ uint32_t pcl_key(const float4& p) const {
+    const int ijk0 = (int)(floorf(p.x * inv) - (float)min_b[0]);
+    const int ijk1 = (int)(floorf(p.y * inv) - (float)min_b[1]);
+    const int ijk2 = (int)(floorf(p.z * inv) - (float)min_b[2]);
+    return (uint32_t)ijk0 + (uint32_t)ijk1 * mul1 + (uint32_t)ijk2 * mul2;
+  }
+  // the output-order key of a PCL key (its Morton code in Morton mode; ijk < div_b decodes uniquely)
+  __device__ __forceinline__ uint32_t out_key(uint32_t k) const {
+    if (!morton) return k;
+    const uint32_t k2 = k / mul2, r = k - k2 * mul2, k1 = r / mul1, k0 = r - k1 * mul1;
+    return spread3_10(k0) | (spread3_10(k1) << 1) | (spread3_10(k2) << 2);
   }
   __device__ __forceinline__ uint32_t key(const float4& p) const {
     const int ijk0 = (int)(floorf(p.x * inv) - (float)min_b[0]);
@@ -256,20 +273,9 @@ __device__ void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint
     }
     for (int b = tid; b < tot; b += T) hist[(b % NW) * NB + b / NW] = 0u;
     __syncthreads();  // every wave holds its chunk: the scatter below may overwrite any position
-    // per-wave digit counts, one add per distinct digit of a step (see vg_radix_sort)
 #pragma unroll
-    for (int k = 0; k < KPL; ++k) {
-      if (c0 + 64 * k >= c1) break;  // wave-uniform
-      const bool valid = c0 + 64 * k + lane < c1;
-      const uint32_t d = (kr[k] >> shift) & dmask;
-      uint64_t peers = __ballot(valid);
-      for (int b = 0; b < dbits; ++b) {
-        const uint64_t bal = __ballot((d >> b) & 1u);
-        peers &= ((d >> b) & 1u) ? bal : ~bal;
-      }
-      if (valid && (peers & ((1ull << lane) - 1ull)) == 0ull) hist[w * NB + d] += (uint32_t)__popcll(peers);
-      __builtin_amdgcn_wave_barrier();
-    }
+    for (int k = 0; k < KPL; ++k)
+      if (c0 + 64 * k + lane < c1) atomicAdd(&hist[w * NB + ((kr[k] >> shift) & dmask)], 1u);
     __syncthreads();
     {
       uint32_t v[PER], loc = 0;
@@ -299,7 +305,6 @@ __device__ void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < KPL; ++k) {
-      if (c0 + 64 * k >= c1) break;  // wave-uniform: the rest of the chunk is empty
       const bool valid = c0 + 64 * k + lane < c1;
       const uint32_t d = (kr[k] >> shift) & dmask;
       uint64_t peers = __ballot(valid);
@@ -430,7 +435,7 @@ __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, u
 }
 
 // Generic front end: segments of a VgArgs (per-job mapping DS, start-up map filter, fbr_voxel_grid).
-template <int T, typename V, bool LDS>
+template <int T, typename V, bool LDS, bool kExact>
 __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
   constexpr int NW = T / 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -478,17 +483,32 @@ __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
     vb[0] = (V*)(kb[1] + cap);
     vb[1] = vb[0] + cap;
   } else {
-    uint32_t* sc = S.scratch + (int64_t)seg * 4 * S.cap;
+    uint32_t* sc = S.scratch + (int64_t)seg * kVgScratch * S.cap;
     kb[0] = sc;
     kb[1] = sc + S.cap;
     vb[0] = (V*)(sc + 2 * S.cap);
     vb[1] = (V*)(sc + 3 * S.cap);
   }
   for (int i = tid; i < n; i += T) {
-    kb[0][i] = G.key(in[i]);
+    kb[0][i] = kExact ? G.pcl_key(in[i]) : G.key(in[i]);
     vb[0][i] = (V)i;
   }
   __syncthreads();
+  if constexpr (kExact) {  // PCL's order inside a voxel: std::sort's partition phase, then the stable sort
+    const int cap = (int)S.cap, nf = 3 * (cap / 17 + 2);
+    if constexpr (LDS) {
+      FBR_LDS_AS uint16_t* pl = (FBR_LDS_AS uint16_t*)kb[1];  // the free ping-pong half
+      FBR_LDS_AS int* fr = (FBR_LDS_AS int*)hist;
+      is_partition_phase<T>((FBR_LDS_AS uint32_t*)kb[0], (FBR_LDS_AS V*)vb[0], pl, pl + cap, n, fr, fr + nf, (int*)wsum);
+    } else {
+      int* fr = (int*)(S.scratch + (int64_t)seg * kVgScratch * S.cap + 4 * S.cap);
+      is_partition_phase<T>(kb[0], vb[0], (int32_t*)kb[1], (int32_t*)vb[1], n, fr, fr + nf, (int*)wsum);
+    }
+    if (G.morton) {
+      for (int i = tid; i < n; i += T) kb[0][i] = G.out_key(kb[0][i]);
+      __syncthreads();
+    }
+  }
   const int total = vg_sort_emit<T, V, 9, LDS>(kb, vb, n, G.nbits, hist, wsum, in, out);
   if (tid == 0) S.cnt_out[seg] = total;
 }
@@ -512,7 +532,7 @@ __device__ unsigned long long fbr_vg_stamps[8];
   } while (0)
 #endif
 
-template <int T, int KPL>
+template <int T, int KPL, bool kExact>
 __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
   constexpr int NW = T / 64, LCAP = T * KPL;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -558,24 +578,42 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
     FBR_LDS_AS uint32_t* keys = (FBR_LDS_AS uint32_t*)q;
     FBR_LDS_AS uint16_t* vals = (FBR_LDS_AS uint16_t*)((FBR_LDS_AS uint32_t*)q + LCAP);
     for (int i = tid; i < n; i += T) {
-      keys[i] = G.key(in[i]);
+      keys[i] = kExact ? G.pcl_key(in[i]) : G.key(in[i]);
       vals[i] = (uint16_t)i;
     }
     __syncthreads();
+    if constexpr (kExact) {  // PCL's order inside a voxel: std::sort's partition phase, then the stable sort
+      int32_t* sc = (int32_t*)(S.scratch + (int64_t)seg * kVgScratch * S.cap);  // positions (global)
+      FBR_LDS_AS int* fr = (FBR_LDS_AS int*)hist;
+      is_partition_phase<T>(keys, vals, sc, sc + S.cap, n, fr, fr + 3 * (LCAP / 17 + 2), (int*)wsum);
+      if (G.morton) {
+        for (int i = tid; i < n; i += T) keys[i] = G.out_key(keys[i]);
+        __syncthreads();
+      }
+    }
     FBR_VG_STAMP(2);
     vg_radix_sort_inplace<T, KPL>(keys, vals, n, G.nbits, hist, wsum);
     FBR_VG_STAMP(3);
     total = vg_emit<T>(keys, vals, n, hist, wsum, in, out);
     FBR_VG_STAMP(4);
   } else {
-    uint32_t* sc = S.scratch + (int64_t)seg * 4 * S.cap;
+    uint32_t* sc = S.scratch + (int64_t)seg * kVgScratch * S.cap;
     uint32_t* kb[2] = {sc, sc + S.cap};
     uint32_t* vb[2] = {sc + 2 * S.cap, sc + 3 * S.cap};
     for (int i = tid; i < n; i += T) {
-      kb[0][i] = G.key(in[i]);
+      kb[0][i] = kExact ? G.pcl_key(in[i]) : G.key(in[i]);
       vb[0][i] = (uint32_t)i;
     }
     __syncthreads();
+    if constexpr (kExact) {
+      int* fr = (int*)(sc + 4 * S.cap);
+      is_partition_phase<T>(kb[0], vb[0], (int32_t*)kb[1], (int32_t*)vb[1], n, fr, fr + 3 * ((int)S.cap / 17 + 2),
+                            (int*)wsum);
+      if (G.morton) {
+        for (int i = tid; i < n; i += T) kb[0][i] = G.out_key(kb[0][i]);
+        __syncthreads();
+      }
+    }
     total = vg_sort_emit<T, uint32_t, 9, false>(kb, vb, n, G.nbits, hist, wsum, in, out);
   }
   if (tid == 0) S.cnt_out[seg] = total;
@@ -586,7 +624,7 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
 // in index order, read straight from the projected cloud and the label mask (the label of
 // index 4 may be stale across scans exactly as the reference's cloudLabel[4]).  One register
 // pass feeds min/max, the keys and the compaction; the sort runs in LDS (u16 ring offsets).
-template <int T, int KPT>
+template <int T, int KPT, bool kExact>
 __global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(KPT <= 4 ? 8 : 1)))
 k_voxel_ring(VgRing A) {
   constexpr int NW = T / 64, MAXD = 8;  // 8-bit digits: 3 passes cover the <= 24-bit ring keys
@@ -700,6 +738,17 @@ k_voxel_ring(VgRing A) {
       off[pos[r]] = (uint16_t)(r * T + tid);   // offset from the ring start s
     }
   __syncthreads();
+  if constexpr (kExact) {
+    // PCL's order inside a voxel: std::sort's partition phase on (key, offset) (fbr_introsort.h);
+    // everything below treats the permuted sequence as the input order, and its stable run sort
+    // completes std::sort.  Scratch: the free ping-pong half kb[1] (positions, u16), the digit
+    // histogram (frame lists) and wsum.. (the workgroup's scan slots).
+    FBR_LDS_AS uint16_t* pl = (FBR_LDS_AS uint16_t*)kb[1];
+    FBR_LDS_AS int* fr = (FBR_LDS_AS int*)hist;
+    // frames above 512 points are partitioned by the whole workgroup (the top levels of a ring)
+    is_partition_phase<T, FBR_LDS_AS uint32_t*, FBR_LDS_AS uint16_t*, FBR_LDS_AS uint16_t*, FBR_LDS_AS int*, 512>(
+        (FBR_LDS_AS uint32_t*)kb[0], (FBR_LDS_AS uint16_t*)off, pl, pl + cap, n, fr, fr + 3 * (cap / 17 + 2), (int*)wsum);
+  }
   VR_TS(2);
   // Runs of equal keys in index order (points adjacent along the ring share voxels: ~6.6
   // candidates per run on C2, and nearly one run per voxel).  Only the runs are sorted; the
@@ -833,12 +882,27 @@ void launch_voxel_ring(hipStream_t s, const VgRing& a) {
   if (nseg <= 0) return;
   // 512 threads, KPT = ceil(W / 512) points per thread (instances up to W = 4096)
   const int kpt = (int)((a.cap + 511) / 512);
-  if (kpt <= 2)
-    fbr_launch((k_voxel_ring<512, 2>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 2), s, a);
-  else if (kpt <= 4)
-    fbr_launch((k_voxel_ring<512, 4>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 4), s, a);
-  else
-    fbr_launch((k_voxel_ring<512, 8>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 8), s, a);
+  auto go = [&](auto ex) {
+    constexpr bool E = decltype(ex)::value;
+    if (kpt <= 2)
+      fbr_launch((k_voxel_ring<512, 2, E>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 2), s, a);
+    else if (kpt <= 4)
+      fbr_launch((k_voxel_ring<512, 4, E>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 4), s, a);
+    else
+      fbr_launch((k_voxel_ring<512, 8, E>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 8), s, a);
+  };
+  if (a.exact) go(std::true_type{});
+  else go(std::false_type{});
+}
+
+// PCL's point order inside voxels (FBR_VG_EXACT=1): bit-identical centroids, hence poses, at
+// about half the batch throughput; off by default.
+bool vg_exact() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_VG_EXACT");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
 }
 
 // In-place LDS sort of the mapping-DS segments (FBR_VG_INPLACE=0: the global-scratch kernel).
@@ -871,15 +935,22 @@ void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
   int64_t cap = 0;
   for (int k = 0; k < 2; ++k)
     if (a.s[k].nseg > 0) cap = std::max<int64_t>(cap, a.s[k].cap);
-  if (cap <= kVgLdsCap) {
-    fbr_launch((k_voxel_grid<256, uint16_t, true>), dim3(nseg), dim3(256), voxel_lds_bytes(a, 256, true), s, a);
-  } else if (vg_inplace()) {
-    const size_t lds = voxel_lds_bytes(a, 1024, false) + (size_t)1024 * kVgIpKpl * (sizeof(uint32_t) + sizeof(uint16_t));
-    fbr_launch((k_voxel_grid_ip<1024, kVgIpKpl>), dim3(nseg), dim3(1024), lds, s, a);
-  } else {
-    fbr_launch((k_voxel_grid<1024, uint32_t, false>), dim3(nseg), dim3(1024), voxel_lds_bytes(a, 1024, false), s,
-                       a);
-  }
+  const bool exact = a.s[0].exact || a.s[1].exact;  // both sets share vg_exact()
+  auto go = [&](auto ex) {
+    constexpr bool E = decltype(ex)::value;
+    if (cap <= kVgLdsCap) {
+      fbr_launch((k_voxel_grid<256, uint16_t, true, E>), dim3(nseg), dim3(256), voxel_lds_bytes(a, 256, true), s, a);
+    } else if (vg_inplace()) {
+      const size_t lds =
+          voxel_lds_bytes(a, 1024, false) + (size_t)1024 * kVgIpKpl * (sizeof(uint32_t) + sizeof(uint16_t));
+      fbr_launch((k_voxel_grid_ip<1024, kVgIpKpl, E>), dim3(nseg), dim3(1024), lds, s, a);
+    } else {
+      fbr_launch((k_voxel_grid<1024, uint32_t, false, E>), dim3(nseg), dim3(1024), voxel_lds_bytes(a, 1024, false),
+                 s, a);
+    }
+  };
+  if (exact) go(std::true_type{});
+  else go(std::false_type{});
 }
 
 // Ring-ordered concatenation of the per-ring corner picks and per-ring surf DS outputs
@@ -979,12 +1050,29 @@ __global__ void k_vgl_grid(const uint32_t* mm, float leaf, int morton, VglState*
 }
 
 __global__ void __launch_bounds__(256)
-k_vgl_keys(const float4* __restrict__ in, int64_t n, const VglState* __restrict__ st, uint32_t* keys, uint32_t* vals) {
+k_vgl_keys(const float4* __restrict__ in, int64_t n, const VglState* __restrict__ st, int exact, uint32_t* keys,
+           uint32_t* vals) {
   const VgGrid G = st->G;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    keys[i] = G.overflow ? 0u : G.key(in[i]);
+    keys[i] = G.overflow ? 0u : (exact ? G.pcl_key(in[i]) : G.key(in[i]));
     vals[i] = (uint32_t)i;
   }
+}
+
+// std::sort's partition phase over the whole cloud (fbr_introsort.h) by one workgroup: PCL's
+// order inside the voxels for the stable device-wide radix sort that follows.  n / 17 + 2 frames
+// per list in fa / fb.
+__global__ void __launch_bounds__(1024)
+k_vgl_isort(uint32_t* keys, uint32_t* vals, int32_t* posL, int32_t* posR, int* fa, int* fb, int n) {
+  __shared__ int sh[64];
+  is_partition_phase<1024>(keys, vals, posL, posR, n, fa, fb, sh);
+}
+
+__global__ void __launch_bounds__(256) k_vgl_outkeys(uint32_t* keys, int64_t n, const VglState* __restrict__ st) {
+  const VgGrid G = st->G;
+  if (!G.morton || G.overflow) return;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    keys[i] = G.out_key(keys[i]);
 }
 
 __global__ void __launch_bounds__(256) k_vgl_heads(const uint32_t* __restrict__ keys, int64_t n, uint32_t* head) {
@@ -1055,7 +1143,13 @@ int voxel_grid_large(hipStream_t s, DevArena& ar, const float4* in, int64_t n, f
   if (ok(hipMemsetD32Async((hipDeviceptr_t)mm, 0xFFFFFFFFu, 3, s)) && ok(hipMemsetD32Async((hipDeviceptr_t)(mm + 3), 0u, 3, s))) {
     fbr_launch(k_vgl_minmax, dim3(grid), dim3(256), 0, s, in, n, mm);
     fbr_launch(k_vgl_grid, dim3(1), dim3(1), 0, s, mm, leaf, morton, st);
-    fbr_launch(k_vgl_keys, dim3(grid), dim3(256), 0, s, in, n, st, k0, v0);
+    const int exact = vg_exact() ? 1 : 0;
+    fbr_launch(k_vgl_keys, dim3(grid), dim3(256), 0, s, in, n, st, exact, k0, v0);
+    if (exact) {  // scratch: head / vox (positions) and k1 / v1 (frame lists), all free until the sort
+      fbr_launch(k_vgl_isort, dim3(1), dim3(1024), 0, s, k0, v0, (int32_t*)head, (int32_t*)vox, (int*)k1, (int*)v1,
+                 (int)n);
+      fbr_launch(k_vgl_outkeys, dim3(grid), dim3(256), 0, s, k0, n, st);
+    }
     if (ok(rocprim::radix_sort_pairs(tmp, tb_sort, k0, k1, v0, v1, N, 0, 32, s))) {
       fbr_launch(k_vgl_heads, dim3(grid), dim3(256), 0, s, k1, n, head);
       // head flags -> voxel index (out of place)

@@ -396,7 +396,8 @@ int fbr_selftest_eig_certified(int n, const float* a, float thr, int32_t* out);
 /* Diagnostic: PCL VoxelGrid's point order inside voxels.  perm[0..n) = the index order the device's
  * emulation of std::sort's partition phase (libstdc++ introsort, fbr_introsort.h) leaves the
  * (keys[i], i) pairs in; a stable sort of that sequence by key is std::sort's result.  lds = 1
- * runs the LDS variant of the per-segment kernels (n <= 8192), 0 the global-memory one. */
+ * runs the LDS variant of the per-segment kernels (n <= 8192), 2 LDS keys with global-memory
+ * positions (the mapping-DS kernel's, n <= 18432), 0 the global-memory one. */
 int fbr_selftest_voxel_order(int64_t n, const uint32_t* keys, int lds, uint32_t* perm);
 
 /* Measurement helper: achievable HBM bandwidth of a device-wide float4 copy of `bytes` (read +

@@ -557,6 +557,48 @@ def test_sparse_grid_registration_is_bit_identical_to_dense(c2_map):
     assert _c2_batch_in_child(jobs, {"FBR_GRID_SPARSE": "1"}, True) == _c2_batch_here(c2_map, jobs)
 
 
+def test_exact_voxel_order_gives_bit_identical_poses(c2_map):
+    """FBR_VG_EXACT=1 (child process): every VoxelGrid sums a voxel's points in std::sort's order
+    (csrc/fbr_introsort.h), so the per-ring, mapping-DS and start-up map centroids are PCL's bit for
+    bit, and the registered poses equal the oracle's (the reference algorithm with the host's
+    libstdc++ std::sort) exactly, not just within POSE_TOL."""
+    jobs = synth.make_jobs("C2", 8, base_seed=620)
+    out = _c2_batch_in_child(jobs, {"FBR_VG_EXACT": "1"}, False)
+    poses = np.frombuffer(out[:8 * 6 * 4], np.float32).reshape(8, 6)
+    H, W = synth.CONFIGS["C2"][:2]
+    P = default_params(H, W)
+    m = O.Map(P, *c2_map)
+    for k, (pts, guess, _) in enumerate(jobs):
+        po, so = O.Stream(P).process_scan(m, pts, 0.0, guess, n_threads=8)
+        assert np.array_equal(poses[k].view(np.uint32), np.asarray(po, np.float32).view(np.uint32)), (k, poses[k], po)
+
+
+def test_exact_voxel_grid_is_bit_identical_to_oracle():
+    """fbr_voxel_grid with FBR_VG_EXACT=1 (child process) returns PCL's centroids bit for bit on
+    every kernel path: in-LDS, global scratch and device-wide clouds."""
+    import subprocess
+    import sys
+    rng = np.random.default_rng(23)
+    clouds = {}
+    for n in (3000, 18432, 18433, 40000):
+        pts = np.zeros(n, POINT_XYZI)
+        pts["x"], pts["y"] = rng.uniform(-30, 30, n), rng.uniform(-30, 30, n)
+        pts["z"] = rng.normal(0, 0.4, n) + (rng.random(n) < 0.3) * rng.uniform(0, 6, n)
+        pts["intensity"] = rng.uniform(0, 255, n)
+        clouds[n] = pts
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_vg_exact_in.npz")
+    np.savez(path, **{str(n): p for n, p in clouds.items()})
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api; "
+            "from feature_base_pointcloud_registration_amd.fbr_types import default_params; "
+            "c = api.Context(default_params(16, 900)); d = np.load(%r); "
+            "sys.stdout.buffer.write(b''.join(c.voxel_grid(d[k], 0.4).tobytes() for k in %r))"
+            % (REPO, path, [str(n) for n in clouds]))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, FBR_VG_EXACT="1"),
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout == b"".join(O.voxel_grid(p, 0.4).tobytes() for p in clouds.values())
+
+
 @pytest.mark.parametrize("env,sparse", [
     ({"FBR_KNN_CELL": "0.5"}, False),                          # R = 2 rows, the C3 / C5 cells
     ({"FBR_KNN_CELL": "0.5", "FBR_GRID_SPARSE": "1"}, True),   # the same over hashed chunks

@@ -121,8 +121,11 @@ def test_partition_phase_then_stable_sort_is_std_sort():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lds", [False, True])
+@pytest.mark.parametrize("lds", [0, 1, 2])
 def test_device_voxel_order_is_std_sort(lds):
     rng = np.random.default_rng(2 + lds)
-    for keys in key_cases(rng, 120, 8000 if lds else 60000):
+    for keys in key_cases(rng, 120, {0: 60000, 1: 8000, 2: 18432}[lds]):
         assert np.array_equal(api.selftest_voxel_order(keys, lds=lds), O.sort_voxel_pairs(keys)), len(keys)
+    for n in {0: (17, 2049, 18432, 18433), 1: (17, 2049, 8192), 2: (17, 2049, 8192, 18431, 18432)}[lds]:
+        keys = rng.integers(0, max(1, n // 6), n).astype(np.uint32)
+        assert np.array_equal(api.selftest_voxel_order(keys, lds=lds), O.sort_voxel_pairs(keys)), n
