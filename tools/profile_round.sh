@@ -14,4 +14,5 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o bench --output-for
 python3 tools/hbm_traffic.py $(find $OUT/fetch -name "*counter_collection.csv") $(find $OUT/write -name "*counter_collection.csv") C2 ${BATCH:-1024} $OUT/hbm_traffic.json || exit 14
 cp $OUT/hbm_traffic.json profiles/hbm_traffic.json
 timeout -k 10 600 python3 bench.py > $OUT/bench_final.log 2>&1 || exit 15
+python3 tools/roofline_check.py $(find $OUT/trace -name "*kernel_stats.csv" | head -1) $OUT/bench_trace.log > $OUT/roofline_check.txt 2>&1 || exit 16
 find $OUT -name "*stats.csv" -o -name "*.json" | head
