@@ -102,7 +102,9 @@ struct fbr_ctx {
   hipStream_t stream = nullptr;   // primary stream (single-scan calls, batch sub-batch 0, export)
   hipStream_t xstream[kMaxSub] = {};  // extra streams of batch sub-batches 1.. (index 0 unused)
   hipEvent_t xev[kMaxSub] = {};       // fork / join events
-  int nsub_pref = 3;                  // sub-batches per batch launch (FBR_NSUB overrides; 1-4 measured: 38.0k, 44.4k, 45.6k, 45.7k scans/s)
+  int nsub_pref = 3;                  // sub-batches per batch launch (FBR_NSUB overrides; at B = 128: 2 -> 76.1k,
+                                      // 3 -> 78.5k, 4 -> 46.7k scans/s: 4 sub-batch streams plus the
+                                      // primary exceed the 4 hardware queues HIP gives a process)
   int H = 0, W = 0, Bcap = 0;
   int items_per_job = 0;
   int64_t HW = 0, NMAX = 0;
