@@ -404,6 +404,33 @@ def test_full_size_batch_properties(c2_map):
 
 
 # ------------------------------------------------------------------------------- C3 / C5 configs
+def _cfg_batch_in_child(cfg, scans, guesses, env):
+    """Poses (B, 6) and REG_STATS records of a batch of `cfg` scans registered in a child process
+    with extra environment knobs (read once per process), against the config's map."""
+    import subprocess
+    import sys
+    from feature_base_pointcloud_registration_amd.fbr_types import REG_STATS
+    n = len(scans)
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_child_%s_jobs.npz" % cfg)
+    np.savez(path, *scans, guesses=np.asarray(guesses, np.float32))
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api, synth; "
+            "d = np.load(%r); scans = [d['arr_%%d' %% k] for k in range(%d)]; "
+            "c = api.Context(synth.config_params(%r, max_batch=%d)); c.set_map(*synth.config_map(%r)); "
+            "p, s = c.process_batch(scans, d['guesses']); sys.stdout.buffer.write(p.tobytes() + s.tobytes())"
+            % (REPO, path, n, cfg, n, cfg))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, **env), timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    poses = np.frombuffer(r.stdout[:n * 24], np.float32).reshape(n, 6)
+    return poses, np.frombuffer(r.stdout[n * 24:], REG_STATS)
+
+
+def assert_exact_order_bitwise(pose, stats, po, so):
+    """FBR_VG_EXACT=1 run against the oracle: the same correspondence count in the final
+    iteration, the same iterations and the pose's bits."""
+    assert (int(stats["iterations"]), int(stats["n_sel"]), int(stats["status"])) == (so["iterations"], so["n_sel"], so["status"])
+    assert np.array_equal(np.asarray(pose, np.float32).view(np.uint32), np.asarray(po, np.float32).view(np.uint32)), (pose, po)
+
+
 def test_c3_ouster_registration_matches_oracle():
     """BASELINE configs[2]: 128x2048 Ouster-style scans against a ~500k-point local map."""
     P = synth.config_params("C3", max_batch=2)
@@ -413,6 +440,8 @@ def test_c3_ouster_registration_matches_oracle():
     with api.Context(P) as ctx:
         ctx.set_map(cmap, smap)
         poses, stats = ctx.process_batch([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
+    # the same jobs with PCL's in-voxel point order (FBR_VG_EXACT=1): bit-identical to the oracle
+    pe, se = _cfg_batch_in_child("C3", [j[0] for j in jobs], np.stack([j[1] for j in jobs]), {"FBR_VG_EXACT": "1"})
     for k, (pts, guess, gt) in enumerate(jobs):
         po, so = O.Stream(P).process_scan(m, pts, 0.0, guess, n_threads=8)
         assert stats["status"][k] == so["status"] == 0 and stats["iterations"][k] == so["iterations"]
@@ -421,6 +450,7 @@ def test_c3_ouster_registration_matches_oracle():
         assert stats["n_corner_map"][k] + stats["n_surf_map"][k] > 450000  # ~500k-point local map
         assert_pose_close(poses[k], po)
         assert np.abs(poses[k][3:] - gt[3:]).max() < 0.05
+        assert_exact_order_bitwise(pe[k], se[k], po, so)
 
 
 def test_c5_dense_scan_matches_oracle():
@@ -446,6 +476,10 @@ def test_c5_dense_scan_matches_oracle():
     assert sg["n_corner_map"] + sg["n_surf_map"] > 5000000
     assert_pose_close(pg, po)
     assert np.abs(pg[3:] - gt[3:]).max() < 0.05
+    # PCL's in-voxel point order (FBR_VG_EXACT=1, child process): the dense scan's feature clouds
+    # take the global-scratch VoxelGrid, and the pose and correspondence count equal the oracle's
+    pe, se = _cfg_batch_in_child("C5", [pts], np.asarray(guess, np.float32)[None], {"FBR_VG_EXACT": "1"})
+    assert_exact_order_bitwise(pe[0], se[0], po, so)
 
 
 def test_voxel_grid_large_cloud_kernel():
