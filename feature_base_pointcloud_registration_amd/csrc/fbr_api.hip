@@ -126,6 +126,8 @@ struct fbr_ctx {
   int32_t* d_corner_cnt = nullptr;
   float4* d_surf_ring = nullptr;
   int32_t* d_surf_ring_cnt = nullptr;
+  float* d_ring_box = nullptr;  // [B][H][kRingBox]: k_concat's per-ring cloud bounds
+  bool ring_box_valid = false;  // d_corner_all / d_surf_all came from k_concat (not upload_cloud)
   int32_t* d_err = nullptr;
   float4 *d_corner_all = nullptr, *d_surf_all = nullptr, *d_cornerDS = nullptr, *d_surfDS = nullptr;
   int32_t *d_ncorner = nullptr, *d_nsurf = nullptr, *d_ncds = nullptr, *d_nsds = nullptr;
@@ -440,7 +442,8 @@ int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode) {
   TIMED_ON(c, sb.st, "concat",
            launch_concat(sb.st, sb.B, c->H, c->W, a.corner_slot, a.corner_cnt, v.out, v.cnt_out,
                          c->d_corner_all + j0 * HW, HW, c->d_ncorner + j0, c->d_surf_all + j0 * HW, HW,
-                         c->d_nsurf + j0));
+                         c->d_nsurf + j0, c->d_ring_box + j0 * H * kRingBox));
+  c->ring_box_valid = true;
   return FBR_OK;
 }
 
@@ -533,6 +536,14 @@ int register_prepare(fbr_ctx* c, const Sub& sb, bool trace) {
   v.s[1] = VgSet{c->d_corner_all + j0 * HW, HW, c->d_ncorner + j0, ccap, c->d_cornerDS + j0 * HW, HW, c->d_ncds + j0,
                  c->d_vg_scratch + (int64_t)c->Bcap * kVgScratch * HW + j0 * kVgScratch * ccap, c->P.mapping_corner_leaf_size,
                  sb.B, 1, vg_exact() ? 1 : 0};
+  if (c->ring_box_valid) {  // the clouds' bounds from k_concat: the filter reads each cloud twice, not 3 times
+    const float* rb = c->d_ring_box + j0 * c->H * kRingBox;
+    for (int k = 0; k < 2; ++k) {
+      v.s[k].box = rb + (k == 0 ? 6 : 0);  // set 0 = surf (box floats 6-11), set 1 = corner (0-5)
+      v.s[k].box_n = c->H;
+      v.s[k].box_stride = (int64_t)c->H * kRingBox;
+    }
+  }
   TIMED_ON(c, sb.st, "voxel_scan", launch_voxel_grid(sb.st, v));
   GnArgs a = gn_args(c, sb, trace);
   if (trace) CK(hipMemsetAsync(a.trace, 0, sizeof(float) * sb.B * c->P.max_iterations * 6, sb.st));
@@ -851,6 +862,7 @@ int check_err(fbr_ctx* c, int B) {
 int upload_cloud(fbr_ctx* c, float4* dst, int32_t* dcnt, const fbr_point_xyzi* src, int64_t n) {
   if (n < 0 || n > c->HW) return FBR_ERR_CAPACITY;
   if (n && !src) return FBR_ERR_INVALID_ARG;
+  c->ring_box_valid = false;  // clouds from the host: the mapping DS takes their bounds from the points
   if (n) CK(hipMemcpyAsync(dst, src, sizeof(float4) * n, hipMemcpyHostToDevice, c->stream));
   int32_t nn = (int32_t)n;
   CK(hipMemcpyAsync(dcnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
@@ -1040,7 +1052,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_sstream, 1) || dalloc(&c->d_label, B * HW) || dalloc(&c->d_label_stream, HW) ||
               dalloc(&c->d_corner_slot, B * H * kCornerPerRing) || dalloc(&c->d_corner_cnt, B * H) ||
               dalloc(&c->d_surf_ring, B * HW) ||
-              dalloc(&c->d_surf_ring_cnt, B * H) || dalloc(&c->d_err, B) || dalloc(&c->d_corner_all, B * HW) ||
+              dalloc(&c->d_surf_ring_cnt, B * H) || dalloc(&c->d_ring_box, B * H * kRingBox) || dalloc(&c->d_err, B) || dalloc(&c->d_corner_all, B * HW) ||
               dalloc(&c->d_surf_all, B * HW) || dalloc(&c->d_cornerDS, B * HW) || dalloc(&c->d_surfDS, B * HW) ||
               dalloc(&c->d_ncorner, B) || dalloc(&c->d_nsurf, B) || dalloc(&c->d_ncds, B) || dalloc(&c->d_nsds, B) ||
               dalloc(&c->d_vg_scratch, c->vg_scratch_elems) ||
@@ -1088,7 +1100,7 @@ int fbr_destroy(fbr_ctx* c) {
     if (c->xstream[k]) (void)fbr_sync(c->xstream[k]);
   void* ptrs[] = {c->d_pts, c->d_nin, c->d_guess, c->d_owner, c->d_rowcnt, c->d_col, c->d_start, c->d_end,
                   c->d_nvalid, c->d_cloud, c->d_range, c->d_sstate, c->d_sstream, c->d_label, c->d_label_stream,
-                  c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring, c->d_surf_ring_cnt,
+                  c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring, c->d_surf_ring_cnt, c->d_ring_box,
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_fitc, c->d_fits, c->d_nsame, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,

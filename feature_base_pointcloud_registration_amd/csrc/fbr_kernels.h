@@ -114,6 +114,11 @@ struct VgSet {               // nseg segments of one cloud family, one leaf size
   int nseg;
   int morton;                // 1: emit voxels in Morton order of (i,j,k) instead of PCL key order
   int exact;                 // 1: PCL's point order inside voxels (std::sort's, fbr_introsort.h)
+  // Optional precomputed bounds (k_concat's ring boxes): segment seg's box k at
+  // box + seg * box_stride + k * kRingBox, k < box_n, each {min xyz, max xyz}; null: from the points
+  const float* box;
+  int box_n;
+  int64_t box_stride;
 };
 // Per-point u32 slots of a VoxelGrid segment's global scratch: keys / indices ping-pong (4) and
 // the std::sort emulation's frame lists (1).
@@ -188,10 +193,13 @@ struct VgRing {
 void launch_voxel_ring(hipStream_t s, const VgRing& a);
 
 // Concatenate per-ring corner slots / per-ring surf DS outputs into per-job clouds (the
-// cornerCloud / surfaceCloud push_back order of featureExtraction.h:219,292).
+// cornerCloud / surfaceCloud push_back order of featureExtraction.h:219,292).  ring_box (may be
+// null): per (job, ring) the corner then the surf points' {min xyz, max xyz} (kRingBox floats;
+// empty rings +FLT_MAX / -FLT_MAX), so the mapping DS need not read its clouds for the bounds.
+constexpr int kRingBox = 12;
 void launch_concat(hipStream_t s, int B, int H, int W, const float4* corner_slot, const int32_t* corner_cnt,
                    const float4* surf_ring, const int32_t* surf_ring_cnt, float4* corner_all, int64_t capc,
-                   int32_t* n_corner, float4* surf_all, int64_t caps, int32_t* n_surf);
+                   int32_t* n_corner, float4* surf_all, int64_t caps, int32_t* n_surf, float* ring_box);
 
 // ---- A10-A18 (k_register.hip) ----
 struct MapGrid {

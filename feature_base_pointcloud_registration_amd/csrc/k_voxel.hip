@@ -83,6 +83,41 @@ __device__ void vg_block_minmax(float (&mn)[3], float (&mx)[3], float* mm) {
   }
 }
 
+// getMinMax3D of segment seg (its first n points): from the producer's ring boxes when the set
+// has them (k_concat; bounds are exact under any merge order), else from the points.  All threads
+// get the result.
+template <int T>
+__device__ void vg_seg_bounds(const VgSet& S, int seg, int n, const float4* in, float (&mn)[3], float (&mx)[3],
+                              float* mm) {
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    mn[d] = FLT_MAX;
+    mx[d] = -FLT_MAX;
+  }
+  if (S.box && (int64_t)S.cnt_in[seg] <= S.cap) {  // boxes cover exactly the segment's points
+    const float* bx = S.box + (int64_t)seg * S.box_stride;
+    for (int k = threadIdx.x; k < S.box_n; k += T) {
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const float a = bx[(int64_t)k * kRingBox + d], b = bx[(int64_t)k * kRingBox + 3 + d];
+        mn[d] = (a < mn[d]) ? a : mn[d];
+        mx[d] = (mx[d] < b) ? b : mx[d];
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < n; i += T) {
+      const float4 p = in[i];
+      const float v[3] = {p.x, p.y, p.z};
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
+        mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
+      }
+    }
+  }
+  vg_block_minmax<T>(mn, mx, mm);
+}
+
 // PCL applyFilter's grid (leaf inverse, min_b, div_b) and the key function.
 struct VgGrid {
   float inv;
@@ -455,17 +490,8 @@ __global__ void __launch_bounds__(T) k_voxel_grid(VgArgs A) {
     if (tid == 0) S.cnt_out[seg] = 0;
     return;
   }
-  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-  for (int i = tid; i < n; i += T) {
-    const float4 p = in[i];
-    const float v[3] = {p.x, p.y, p.z};
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
-      mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
-    }
-  }
-  vg_block_minmax<T>(mn, mx, mm);
+  float mn[3], mx[3];
+  vg_seg_bounds<T>(S, seg, n, in, mn, mx, mm);
   VgGrid G;
   G.init(mn, mx, S.leaf, S.morton != 0);
   if (G.overflow) {
@@ -553,17 +579,8 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
     if (tid == 0) S.cnt_out[seg] = 0;
     return;
   }
-  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-  for (int i = tid; i < n; i += T) {
-    const float4 p = in[i];
-    const float v[3] = {p.x, p.y, p.z};
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
-      mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
-    }
-  }
-  vg_block_minmax<T>(mn, mx, mm);
+  float mn[3], mx[3];
+  vg_seg_bounds<T>(S, seg, n, in, mn, mx, mm);
   VgGrid G;
   G.init(mn, mx, S.leaf, S.morton != 0);
   FBR_VG_STAMP(1);
@@ -961,7 +978,7 @@ void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
 __global__ void __launch_bounds__(256)
 k_concat(int H, int W, const float4* corner_slot, const int32_t* corner_cnt, const float4* surf_ring,
          const int32_t* surf_ring_cnt, float4* corner_all, int64_t capc, int32_t* n_corner, float4* surf_all,
-         int64_t caps, int32_t* n_surf) {
+         int64_t caps, int32_t* n_surf, float* ring_box) {
   const int lane = threadIdx.x & 63, rpj = (H + 3) / 4;
   const int job = blockIdx.x / rpj, r = (blockIdx.x % rpj) * 4 + (threadIdx.x >> 6);
   if (r >= H) return;
@@ -983,16 +1000,57 @@ k_concat(int H, int W, const float4* corner_slot, const int32_t* corner_cnt, con
   }
   const float4* cs = corner_slot + ((int64_t)job * H + r) * kCornerPerRing;
   const float4* ss = surf_ring + ((int64_t)job * H + r) * W;
-  for (int i = lane; i < nc; i += 64) corner_all[job * capc + oc + i] = cs[i];
-  for (int i = lane; i < ns; i += 64) surf_all[job * caps + os + i] = ss[i];
+  float bx[2][6];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      bx[c][d] = FLT_MAX;
+      bx[c][3 + d] = -FLT_MAX;
+    }
+  auto grow = [&](float (&b)[6], const float4& p) {
+    const float v[3] = {p.x, p.y, p.z};
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      b[d] = (v[d] < b[d]) ? v[d] : b[d];
+      b[3 + d] = (b[3 + d] < v[d]) ? v[d] : b[3 + d];
+    }
+  };
+  for (int i = lane; i < nc; i += 64) {
+    const float4 p = cs[i];
+    corner_all[job * capc + oc + i] = p;
+    grow(bx[0], p);
+  }
+  for (int i = lane; i < ns; i += 64) {
+    const float4 p = ss[i];
+    surf_all[job * caps + os + i] = p;
+    grow(bx[1], p);
+  }
+  if (!ring_box) return;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+      for (int o = 32; o > 0; o >>= 1) {
+        const float a = __shfl_xor(bx[c][d], o), b = __shfl_xor(bx[c][3 + d], o);
+        bx[c][d] = (a < bx[c][d]) ? a : bx[c][d];
+        bx[c][3 + d] = (bx[c][3 + d] < b) ? b : bx[c][3 + d];
+      }
+  if (lane < kRingBox) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < kRingBox; ++k)
+      if (lane == k) v = bx[k / 6][k % 6];
+    ring_box[((int64_t)job * H + r) * kRingBox + lane] = v;
+  }
 }
 
 void launch_concat(hipStream_t s, int B, int H, int W, const float4* corner_slot, const int32_t* corner_cnt,
                    const float4* surf_ring, const int32_t* surf_ring_cnt, float4* corner_all, int64_t capc,
-                   int32_t* n_corner, float4* surf_all, int64_t caps, int32_t* n_surf) {
+                   int32_t* n_corner, float4* surf_all, int64_t caps, int32_t* n_surf, float* ring_box) {
   if (B <= 0 || H <= 0) return;
   fbr_launch(k_concat, dim3(B * ((H + 3) / 4)), dim3(256), 0, s, H, W, corner_slot, corner_cnt, surf_ring,
-                     surf_ring_cnt, corner_all, capc, n_corner, surf_all, caps, n_surf);
+                     surf_ring_cnt, corner_all, capc, n_corner, surf_all, caps, n_surf, ring_box);
 }
 
 
