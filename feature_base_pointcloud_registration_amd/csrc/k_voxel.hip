@@ -285,9 +285,11 @@ __device__ int vg_radix_sort(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, 
 // its chunk (KPL 64-element steps) in registers, so a pass reads the whole chunk before the barrier
 // and scatters straight into the same LDS arrays after it -- no ping-pong buffer, no global scratch.
 // The ranking is vg_radix_sort's (wave chunks in order, ballot peer masks), so the sort is stable.
-// 8-bit digits (hist holds (NW + 1) * 256 counters).  Ends with a barrier.
+// 8-bit digits (hist holds (NW + 1) * 256 counters).  Ends with a barrier.  Always inlined: with
+// two callers (the exact and default kernels) the compiler outlined it, and the call frame put
+// 80 B per lane in scratch (spilled on every call: ~50 MB of writes per B = 1024 launch).
 template <int T, int KPL>
-__device__ void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint16_t* vals, int n, int nbits,
+__device__ __attribute__((always_inline)) void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint16_t* vals, int n, int nbits,
                                       uint32_t* hist, uint32_t* wsum) {
   constexpr int NW = T / 64, NB = 256, PER = NB * NW / T;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -369,8 +371,12 @@ __device__ int vg_sort_emit(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, u
                             const float4* in, float4* out, int dbg = 0, unsigned long long* t_sorted = nullptr);
 
 // One centroid per run of equal keys of the sorted pairs ks / vs (n), in ascending key order.
-// hist must hold NW KB (the per-wave point stage).  Returns the voxel count (all threads).
-template <int T, typename KP, typename VP>
+// hist must hold NW KB (the per-wave point stage), and with kStage NW * 2176 B: the centroids then
+// collect in a per-wave LDS ring of kEmitRing and leave as whole 128-B lines (a step completes a
+// few scattered centroids, and partial-line stores cost the L2 a write each time the line is
+// evicted half written).  Returns the voxel count (all threads).
+constexpr int kEmitRing = 72;  // >= 7 unflushed + 65 written in one step (see the flush below)
+template <int T, bool kStage = false, typename KP, typename VP>
 __device__ int vg_emit(KP ks, VP vs, int n, uint32_t* hist, uint32_t* wsum, const float4* in, float4* out) {
   constexpr int NW = T / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -398,6 +404,25 @@ __device__ int vg_emit(KP ks, VP vs, int n, uint32_t* hist, uint32_t* wsum, cons
   bool carry_open = false;
   float4 carry = make_float4(0.f, 0.f, 0.f, 0.f);
   int carry_start = 0, carry_out = 0;
+  // kStage: this wave's voxels are [pos0, pos0 + nh); those below fl have been stored.  Every
+  // index below the frontier (the open carry's, else pos) is written after a step, and a step
+  // writes indices <= frontier + 64, so the live ring entries span < 8 + 65 <= kEmitRing.
+  float4* ost = reinterpret_cast<float4*>(hist) + NW * 64 + w * kEmitRing;
+  const int pos0 = pos;
+  int fl = pos0 & ~7;
+  auto flush = [&](int fe) {  // store ring entries [fl, fe) (wave-uniform fe)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int b = fl; b < fe; b += 64) {
+      const int idx = b + lane;
+      if (idx < fe && idx >= pos0) out[idx] = ost[idx % kEmitRing];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    fl = fe;
+  };
   // the gathers run one step ahead (the loop is otherwise one dependent HBM/L2 round trip per step)
   float4 pnext = c0 + lane < n && c0 < c1 ? in[vs[c0 + lane]] : make_float4(0.f, 0.f, 0.f, 0.f);
   for (int i0 = c0; i0 < c1 || carry_open; i0 += 64) {
@@ -445,7 +470,9 @@ __device__ int vg_emit(KP ks, VP vs, int n, uint32_t* hist, uint32_t* wsum, cons
     const int oidx = cont ? carry_out : pos + __popcll(hb & ((1ull << lane) - 1ull));
     if (starter && !spills) {
       const float cnt = (float)(i0 + nb - start);
-      out[oidx] = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
+      const float4 r = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
+      if constexpr (kStage) ost[oidx % kEmitRing] = r;
+      else out[oidx] = r;
     }
     const uint64_t sp = __ballot(spills);
     carry_open = sp != 0ull;
@@ -456,7 +483,12 @@ __device__ int vg_emit(KP ks, VP vs, int n, uint32_t* hist, uint32_t* wsum, cons
       carry_out = __shfl(oidx, src);
     }
     pos += __popcll(hb);
+    if constexpr (kStage) {
+      const int fe = (carry_open ? carry_out : pos) & ~7;
+      if (fe > fl) flush(fe);
+    }
   }
+  if constexpr (kStage) flush(pos);
   return total;
 }
 
@@ -561,6 +593,7 @@ __device__ unsigned long long fbr_vg_stamps[8];
 template <int T, int KPL, bool kExact>
 __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
   constexpr int NW = T / 64, LCAP = T * KPL;
+  static_assert(NW * (64 + kEmitRing) * 16 <= (NW + 1) * 512 * 4, "vg_emit's point stage + centroid ring exceed hist");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   int seg = blockIdx.x;
@@ -611,7 +644,7 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
     FBR_VG_STAMP(2);
     vg_radix_sort_inplace<T, KPL>(keys, vals, n, G.nbits, hist, wsum);
     FBR_VG_STAMP(3);
-    total = vg_emit<T>(keys, vals, n, hist, wsum, in, out);
+    total = vg_emit<T, true>(keys, vals, n, hist, wsum, in, out);  // hist: (NW + 1) * 2 KB
     FBR_VG_STAMP(4);
   } else {
     uint32_t* sc = S.scratch + (int64_t)seg * kVgScratch * S.cap;
