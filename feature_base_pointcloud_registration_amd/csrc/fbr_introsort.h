@@ -333,7 +333,7 @@ constexpr int kIsBig = 2048;  // default: frames larger than this are partitione
 // n-entry scratch; fa / fb: int frame lists {first, last, depth} of >= n / 17 + 2 entries each
 // (3 ints per frame); sh: LDS ints (>= 2 * T / 64 + 8).  Starts and ends with a barrier.  A stable sort by key of the result is std::sort's.
 template <int T, typename KP, typename VP, typename PP, typename FP, int BIG = kIsBig>
-__device__ void is_partition_phase(KP k, VP v, PP posL, PP posR, int n, FP fa, FP fb, int* sh) {
+__device__ __attribute__((always_inline)) void is_partition_phase(KP k, VP v, PP posL, PP posR, int n, FP fa, FP fb, int* sh) {
   constexpr int NW = T / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int* ncur = sh + 2 * NW + 2;

@@ -675,7 +675,7 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
 // index 4 may be stale across scans exactly as the reference's cloudLabel[4]).  One register
 // pass feeds min/max, the keys and the compaction; the sort runs in LDS (u16 ring offsets).
 template <int T, int KPT, bool kExact>
-__global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(KPT <= 4 ? 8 : 1)))
+__global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(KPT <= 4 && !kExact ? 8 : 1)))
 k_voxel_ring(VgRing A) {
   constexpr int NW = T / 64, MAXD = 8;  // 8-bit digits: 3 passes cover the <= 24-bit ring keys
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
