@@ -473,7 +473,7 @@ __device__ __forceinline__ bool stale_walks_fast(const FeatLds& S, int slen, con
 // over NWV waves, while wave 0 alone runs the walks (ballot masks, greedy rounds, the sorted
 // path) between workgroup barriers.
 template <int WMAX, int QP, int NWV>
-__global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV > 1 ? 2 : 4)))
 k_features(FeatArgs a) {
   constexpr int NT = 64 * NWV;
 #ifdef FBR_FEAT_STAMPS
