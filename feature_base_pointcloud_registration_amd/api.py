@@ -154,6 +154,16 @@ def host_times(reset=False):
     return tuple(x * 1e-9 for x in v)
 
 
+def batch_times(reset=False):
+    """Host wall time (s) of fbr_batch_launch calls since the last reset, and the part of it spent
+    waiting for the Gauss-Newton iteration flags -- diagnostic (fbr_diag_batch_times)."""
+    f = lib().fbr_diag_batch_times
+    f.restype, f.argtypes = ctypes.c_int, [_VP, ctypes.c_int]
+    v = (ctypes.c_longlong * 2)()
+    _check(f(v, int(reset)), "fbr_diag_batch_times")
+    return tuple(x * 1e-9 for x in v)
+
+
 def selftest_math(a, b):
     """Device sqrt(|a|), a/b, atan2f(a,b), a*b+b*a-a, sinf(a), cosf(a) (see fbr_selftest_math)."""
     a = np.ascontiguousarray(a, np.float32)

@@ -77,7 +77,8 @@ int dalloc(T** p, size_t count) {
 
 }  // namespace
 
-constexpr int kMaxSub = 4;
+constexpr int kMaxSub = 8;  // sub-batch streams per launch (FBR_NSUB); more than 3 pays only with
+                             // GPU_MAX_HW_QUEUES above HIP's default of 4 (one hardware queue per stream)
 
 // Host ingest of fbr_process_batch: the caller's (pageable) scans are packed into a ring of pinned
 // staging chunks by host threads and copied to HBM on a copy stream, into the input slot the
@@ -609,6 +610,7 @@ int register_iterate(fbr_ctx* c, const Sub* subs, int nsub, bool trace) {
       if (watch[k] && it >= kLag) {
         volatile unsigned long long* f = c->h_iter_flags + (int64_t)sb.k * mi + (it - kLag);
         unsigned long long v = *f;
+        const auto tspin = std::chrono::steady_clock::now();
         for (long spins = 0; (v >> 32) != (gen & 0xFFFFFFFFull); ++spins) {
           if ((spins & 1023) == 1023) {
             const hipError_t q = hipStreamQuery(sb.st);
@@ -621,6 +623,9 @@ int register_iterate(fbr_ctx* c, const Sub* subs, int nsub, bool trace) {
           v = *f;
         }
         debug_counters().flag_polls.fetch_add(1, std::memory_order_relaxed);
+        debug_counters().batch_ns[1].fetch_add(
+            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tspin).count(),
+            std::memory_order_relaxed);
         if (watch[k]) active[k] = (int)(v & 0xFFFFFFFFull);
         if (watch[k] && active[k] == 0) {
           live[k] = false;
@@ -1032,8 +1037,12 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   c->Bcap = p->max_batch;
   c->NMAX = p->max_points_per_scan;
   const int64_t B = c->Bcap, HW = c->HW, H = c->H;
+  if (const char* e = std::getenv("FBR_NSUB")) c->nsub_pref = std::max(1, std::min(kMaxSub, std::atoi(e)));
+  // streams of the sub-batches this context can use (each stream takes a hardware queue: unused
+  // ones are not created, so they cannot share a queue with a busy one)
+  const int nstreams = std::max(2, c->nsub_pref);
   bool sfail = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess;
-  for (int k = 0; k < kMaxSub && !sfail; ++k) {
+  for (int k = 0; k < nstreams && !sfail; ++k) {
     if (k > 0) sfail = hipStreamCreateWithFlags(&c->xstream[k], hipStreamNonBlocking) != hipSuccess;
     if (!sfail) sfail = hipEventCreateWithFlags(&c->xev[k], hipEventDisableTiming) != hipSuccess;
   }
@@ -1041,7 +1050,6 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
     fbr_destroy(c);
     return FBR_ERR_HIP;
   }
-  if (const char* e = std::getenv("FBR_NSUB")) c->nsub_pref = std::max(1, std::min(kMaxSub, std::atoi(e)));
   c->items_per_job = (int)(2 * ((HW + 255) / 256 + 1));
   c->max_items = (int)(B * c->items_per_job);
   c->vg_scratch_elems = kVgScratch * B * (HW + std::min<int64_t>(HW, (int64_t)kCornerPerRing * H));
@@ -1440,6 +1448,7 @@ int fbr_batch_launch(fbr_ctx* c) {
   if (c->staged_B <= 0) return FBR_ERR_STATE;
   if (!c->has_map) return FBR_ERR_NO_MAP;
   CK(hipSetDevice(c->dev));
+  const auto t0 = std::chrono::steady_clock::now();
   // Sub-batches on separate streams: one sub-batch's low-occupancy phases (the features' ring-0
   // waves, the last Gauss-Newton iterations) overlap the others' work.
   const int B = c->staged_B;
@@ -1464,6 +1473,9 @@ int fbr_batch_launch(fbr_ctx* c) {
     CK(hipEventRecord(c->xev[k], c->xstream[k]));
     CK(hipStreamWaitEvent(c->stream, c->xev[k], 0));
   }
+  debug_counters().batch_ns[0].fetch_add(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
+      std::memory_order_relaxed);
   return rc;
 }
 
@@ -1648,6 +1660,17 @@ extern "C" int fbr_diag_host_times(long long* out4, int reset) {
   for (int k = 0; k < 4; ++k) {
     if (out4) out4[k] = d.host_ns[k].load();
     if (reset) d.host_ns[k] = 0;
+  }
+  return FBR_OK;
+}
+
+// Diagnostic: host wall time (ns) of fbr_batch_launch calls and the part of it spent waiting for
+// the Gauss-Newton iteration flags, since the last reset.
+extern "C" int fbr_diag_batch_times(long long* out2, int reset) {
+  DebugCounters& d = debug_counters();
+  for (int k = 0; k < 2; ++k) {
+    if (out2) out2[k] = d.batch_ns[k].load();
+    if (reset) d.batch_ns[k] = 0;
   }
   return FBR_OK;
 }

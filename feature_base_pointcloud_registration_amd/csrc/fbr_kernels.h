@@ -33,6 +33,8 @@ struct DebugCounters {
   // host wall time (ns) of the single-scan calls: [0] scan upload (staging copy + enqueue),
   // [1] enqueue of the stages (launches, GN flag polls), [2] result wait, [3] whole call
   std::atomic<long long> host_ns[4] = {0, 0, 0, 0};
+  // batch calls: [0] fbr_batch_launch wall time, [1] of it spent waiting for GN iteration flags
+  std::atomic<long long> batch_ns[2] = {0, 0};
 };
 inline DebugCounters& debug_counters() {
   static DebugCounters c;

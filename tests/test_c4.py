@@ -1,0 +1,79 @@
+"""C4 (BASELINE.json configs[3]) at its own size: 1,024 independent 64x1800 scan-to-map jobs.
+
+* One 1,024-job C2 batch on one GPU: properties on every job, and 16 jobs spread over the batch
+  against the CPU oracle (iterations, n_sel, pose within 1e-4).
+* The strong split of the same 1,024 jobs over 8 ranks (128 per rank, C4's per-GPU share), all on
+  the box's one GPU with a gloo group: the gathered pose records equal a world-1 run bit for bit.
+  The jobs are independent (imageProjection.cpp:206-218 is the only cross-scan dependency and C4
+  removes it), so any difference would be a sharding or buffer-reuse bug.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+from feature_base_pointcloud_registration_amd import api, shard, synth
+from feature_base_pointcloud_registration_amd.fbr_types import default_params
+from test_distributed import _run_bench
+
+pytestmark = pytest.mark.gpu
+POSE_TOL = 1e-4
+C4_JOBS = 1024
+
+
+def _close(p, q):
+    p, q = np.asarray(p, np.float64), np.asarray(q, np.float64)
+    return max(np.abs(p[3:] - q[3:]).max(), np.abs(np.angle(np.exp(1j * (p[:3] - q[:3])))).max())
+
+
+@pytest.mark.timeout(900)
+def test_c4_full_batch_1024_jobs():
+    H, W = synth.CONFIGS["C2"][:2]
+    P = default_params(H, W, max_batch=C4_JOBS)
+    cmap, smap = synth.config_map("C2")
+    jobs = synth.make_jobs("C2", C4_JOBS, base_seed=1000)  # job j uses seed 1000 + j
+    scans = [j[0] for j in jobs]
+    guesses = np.stack([j[1] for j in jobs]).astype(np.float32)
+    gts = np.stack([j[2] for j in jobs])
+    with api.Context(P) as ctx:
+        ctx.set_map(cmap, smap)
+        ctx.batch_stage(scans, guesses)
+        ctx.batch_launch()
+        ctx.batch_wait()
+        poses, stats = ctx.batch_results()
+    # every job: registered, converged, near ground truth, against the ~100k-point local map
+    assert (stats["status"] == 0).all()
+    assert (stats["converged"] == 1).all()
+    assert np.abs(poses[:, 3:] - gts[:, 3:]).max() < 0.05
+    m_local = stats["n_corner_map"] + stats["n_surf_map"]
+    assert m_local.min() > 60000 and m_local.mean() > 80000
+    assert (stats["n_points"] <= np.array([len(s) for s in scans])).all()
+    # 16 jobs spread over the whole batch (every sub-batch, first and last job) against the oracle
+    pick = sorted(set(np.linspace(0, C4_JOBS - 1, 16).round().astype(int).tolist()))
+    omap = O.Map(P, cmap, smap)
+    for j in pick:
+        po, so = O.Stream(P).process_scan(omap, scans[j], 0.0, guesses[j], n_threads=8)
+        assert so["status"] == 0
+        assert (int(stats["iterations"][j]), int(stats["n_sel"][j])) == (so["iterations"], so["n_sel"]), j
+        for f in ("n_points", "n_corner", "n_corner_map", "n_surf_map"):
+            assert stats[f][j] == so[f], (j, f)
+        assert _close(poses[j], po) <= POSE_TOL, (j, poses[j], po)
+
+
+@pytest.mark.timeout(900)
+def test_c4_strong_split_world8_matches_world1(tmp_path):
+    """bench.py under torch.distributed.run: 1,024 jobs split into 8 contiguous blocks of 128 (each
+    rank a 128-job context on device 0, gloo group) against one rank running all 1,024."""
+    common = ["--total-jobs", str(C4_JOBS), "--backend", "gloo", "--latency", "0", "--ingest", "0",
+              "--exact-line", "0", "--profile", "off"]
+    r8, rec8 = _run_bench(8, common + ["--same-device"], tmp_path, "w8")
+    r1, rec1 = _run_bench(1, common, tmp_path, "w1")
+    assert r8["n_gpus"] == 8 and r8["scaling"] == "strong"
+    assert r8["config"]["jobs_per_step"] == C4_JOBS and r8["config"]["jobs_per_gpu_per_step"] == C4_JOBS // 8
+    assert r8["records_check"] == {"jobs": C4_JOBS, "mismatched_words": 0}
+    assert r1["records_check"] == {"jobs": C4_JOBS, "mismatched_words": 0}
+    assert rec1.shape == rec8.shape == (C4_JOBS * shard.RECORD_FLOATS,)
+    assert np.array_equal(rec1.view(np.int32), rec8.view(np.int32))
+    _, iters, status = shard.decode_records(rec1)
+    assert (status == 0).all() and (iters > 0).all()
