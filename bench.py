@@ -36,11 +36,14 @@ WORKLOAD = {"C1": "VLP-16-style scans, local corner+surf map",
             "C3": "Ouster-style scans, ~500k-pt local corner+surf map (mapping leaves 0.1/0.2)",
             "C5": "dense scans, ~5.8M-pt map inside the crop box (mapping leaves 0.05)"}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# VALU issue peak: a wave64 VALU instruction holds a SIMD's issue for 2 cycles at best, so 1024 SIMDs
+# at 2.4 GHz issue at most 1228.8 G wave-instructions/s (= the 157 TF f32 vector peak / 128 flop)
+VALU_PEAK_GINST = 1024 * 2.4 / 2.0
 
 # Algorithmic bytes per unit for each kernel family: the minimal HBM traffic the kernel's job needs
-# (DESIGN.md §4 holds the same table).  Units per step: n_in raw points, HW range-image cells, n
-# valid points, C corner picks, S per-ring surf DS points, F = C + S feature points, Q DS queries,
-# IQ query-iterations.
+# (DESIGN.md §4 holds the same table; every model is <= the FETCH/WRITE counter bytes).  Units per
+# step: n_in raw points, HW range-image cells, n valid points, C corner picks, S per-ring surf DS
+# points, F = C + S feature points, Q DS queries, IQ query-iterations, MG the map grid's points.
 def kernel_bytes(name, tot):
     n_in, HW, n, C = tot["n_in"], tot["HW"], tot["n"], tot["C"]
     S, F, Q, IQ = tot["S"], tot["F"], tot["Q"], tot["IQ"]
@@ -48,24 +51,25 @@ def kernel_bytes(name, tot):
         "project": 24.0 * n_in + 4.0 * n,        # raw point (24 B AoS) read + first-wins owner claim
         "extract": 4.0 * HW + 4.0 * n + 24.0 * n + 24.0 * n,  # owner image read + claimed cells reset, owning
                                                              # raw point gather, xyzi+col+range write
-        "features": 24.0 * n + 1.0 * n + 16.0 * C,  # range+col+xyzi read, label write, corner picks write
+        "features": 9.0 * n + 32.0 * C,          # range + col read, label written; corner points read + written
         "voxel_ring": 17.0 * n + 16.0 * S,       # label + candidate point read, per-ring DS write
         "concat": 32.0 * F,                      # per-ring corner / surf outputs read + job clouds written
         "voxel_scan": 16.0 * F + 16.0 * Q,       # corner + surf clouds read, DS queries written
-        "gn_knn": 96.0 * IQ,                     # query 16 B + the 5 neighbours found 80 B
-        "gn_residual": 116.0 * IQ,               # query 16 B + 5 map indices 20 B + 5 neighbour gathers 80 B
+        "gn_knn": 36.0 * IQ,                     # query 16 B read + 5 map indices 20 B written (the map's
+                                                 # neighbour rows are cache hits: C2's map is 1.5 MB)
+        "gn_residual": 36.0 * IQ,                # query 16 B + 5 map indices 20 B read (neighbour gathers: cache)
     }.get(name, 0.0)
 
 
 BYTE_MODEL = {
     "project": "24 B per raw point + 4 B owner claim per valid point",
     "extract": "4 B per range-image cell + 4 B owner reset + 24 B raw-point gather + 24 B written per valid point",
-    "features": "24 B read + 1 B label per valid point + 16 B per corner pick",
+    "features": "9 B per valid point (range + col read, label written) + 32 B per corner pick",
     "voxel_ring": "17 B per valid point + 16 B per per-ring DS point",
     "concat": "32 B per feature point",
     "voxel_scan": "16 B per feature point + 16 B per DS query",
-    "gn_knn": "96 B per query-iteration (SURVEY 8d: query 16 B + 5 neighbours 80 B)",
-    "gn_residual": "116 B per query-iteration (query 16 B + 5 indices 20 B + 5 neighbour gathers 80 B)",
+    "gn_knn": "36 B per query-iteration (query 16 B + 5 indices 20 B; neighbour rows of the map are L2/MALL hits)",
+    "gn_residual": "36 B per query-iteration (query 16 B + 5 indices 20 B; neighbour gathers are L2/MALL hits)",
 }
 
 # rocprofv3 kernel symbols behind each launcher name (tools/roofline_check.py maps a profile's rows)
@@ -111,6 +115,8 @@ def parse():
                          "events): every kernel (default), only the roofline kernel, or none")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "hbm_traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from rocprofv3 PMC passes")
+    ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "valu_pmc.json"),
+                    help="per-launch VALU instructions of every kernel from a rocprofv3 SQ pass (tools/valu_pmc.py)")
     return ap.parse_args()
 
 
@@ -256,25 +262,33 @@ def main():
         ctx.set_deskew(tabs)
     ctx.batch_stage(scans, guesses)
 
-    gather_buf = lib_stream = None
+    gather_buf = None
+    ext_streams = {}  # library stream handle -> torch.cuda.ExternalStream
     if dist is not None:
         import torch
         if args.backend == "nccl":
             gather_buf = torch.zeros(Bpad * shard.RECORD_FLOATS, dtype=torch.float32, device=f"cuda:{dev}")
-            lib_stream = torch.cuda.ExternalStream(ctx.stream_handle, device=f"cuda:{dev}")
     gathered = [None]
+
+    def gather_ready():
+        """All-gather the records of the latest launch the library has fully enqueued (launches are
+        pipelined: after launch n that is launch n-1).  The export waits for the previous gather
+        (torch's stream still reading gather_buf); the gather waits for the export."""
+        cur = torch.cuda.current_stream()
+        lid, sh = ctx.batch_export_ready(gather_buf.data_ptr(), cur.cuda_stream)
+        if lid < 0:
+            return
+        if sh not in ext_streams:
+            ext_streams[sh] = torch.cuda.ExternalStream(sh, device=f"cuda:{dev}")
+        cur.wait_stream(ext_streams[sh])
+        gathered[0] = shard.gather_records(dist, gather_buf, world)
 
     def step():
         ctx.batch_launch()
         if dist is None:
             return
         if args.backend == "nccl":
-            # the export (library stream) must not overwrite gather_buf while the previous step's
-            # all_gather (torch's stream) still reads it, and the gather must see this export
-            lib_stream.wait_stream(torch.cuda.current_stream())
-            ctx.batch_export(gather_buf.data_ptr())
-            torch.cuda.current_stream().wait_stream(lib_stream)
-            gathered[0] = shard.gather_records(dist, gather_buf, world)
+            gather_ready()
         else:  # gloo: host records
             poses_h, stats_h = ctx.batch_results()
             rec = np.zeros(Bpad * shard.RECORD_FLOATS, np.float32)
@@ -283,12 +297,18 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if dist is not None and args.backend == "nccl":
+        ctx.batch_flush()
+        gather_ready()
     ctx.batch_wait()
     kernels = ["gn_knn", "gn_residual", "gn_solve", "project", "extract", "features", "voxel_ring", "concat",
                "voxel_scan", "gn_init", "crop", "gn_finalize"]
     # one untimed profiled step: per-kernel device times (HIP events) and the dominant kernel
     ctx.set_profiling(True)
     step()
+    if dist is not None and args.backend == "nccl":
+        ctx.batch_flush()
+        gather_ready()
     ctx.batch_wait()
     ctx.set_profiling(False)
     prof = {k: ctx.kernel_time(k) for k in kernels}
@@ -307,6 +327,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if dist is not None and args.backend == "nccl":  # the last launch's records
+        ctx.batch_flush()
+        gather_ready()
     ctx.batch_wait()
     if dist is not None:
         torch.cuda.synchronize()
@@ -355,6 +378,17 @@ def main():
                IQ=float(((stats["n_corner_ds"] + stats["n_surf_ds"]) * stats["iterations"]).sum()),
                M=float((stats["n_corner_map"] + stats["n_surf_map"]).sum()))
 
+    # per-launch VALU instructions (rocprofv3 SQ pass of the same config and batch, tools/valu_pmc.py)
+    valu = {}
+    if os.path.exists(args.valu_json):
+        try:
+            with open(args.valu_json) as f:
+                vj = json.load(f)
+            if vj.get("config") == cfg and vj.get("batch") == B:
+                valu = vj.get("kernels", {})
+        except Exception:
+            valu = {}
+
     def kernel_roofline(k):
         if timed[k][1] > 0:  # live: the timed region's dispatches
             ms, launches, steps_measured, live = timed[k][0], timed[k][1], args.steps, True
@@ -364,13 +398,22 @@ def main():
         bpl = kernel_bytes(k, tot) / max(lps, 1e-9)
         avg_s = ms / 1000.0 / max(launches, 1)
         ach = bpl / avg_s / 1e9 if avg_s > 0 else 0.0
-        return dict(bytes_per_launch=bpl, avg_launch_us=round(avg_s * 1e6, 3), launches_per_step=lps,
-                    achieved_GBps=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
-                    ms_per_step=round(ms / max(steps_measured, 1), 4), live=live)
+        r = dict(bytes_per_launch=bpl, avg_launch_us=round(avg_s * 1e6, 3), launches_per_step=lps,
+                 achieved_GBps=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
+                 ms_per_step=round(ms / max(steps_measured, 1), 4), live=live)
+        if k in valu and avg_s > 0:  # the live VALU-issue fraction of the launch
+            ipl = valu[k]["insts_valu_per_launch"]
+            r["valu_insts_per_launch"] = ipl
+            r["valu_achieved_ginst_s"] = round(ipl / avg_s / 1e9, 2)
+            r["valu_frac"] = round(ipl / avg_s / 1e9 / VALU_PEAK_GINST, 5)
+            r["valu_busy_alone"] = round(valu[k]["valu_busy_alone"], 4)
+        return r
 
     kroof = {k: kernel_roofline(k) for k in modelled}
     bytes_per_launch, launches_per_step = kroof[dom]["bytes_per_launch"], kroof[dom]["launches_per_step"]
     avg_launch_s, achieved, live = kroof[dom]["avg_launch_us"] * 1e-6, kroof[dom]["achieved_GBps"], kroof[dom]["live"]
+    # the roof the dominant kernel is closer to: VALU issue when its VALU fraction exceeds its HBM one
+    valu_bound = "valu_frac" in kroof[dom] and kroof[dom]["valu_frac"] > kroof[dom]["frac"]
     traffic = None
     if os.path.exists(args.pmc_json):
         try:
@@ -411,14 +454,19 @@ def main():
             "imu_deskew": bool(args.deskew),
         },
         "roofline": {
-            "bound": "hbm",
+            "bound": "valu" if valu_bound else "hbm",
             "kernel": dom,
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "achieved": kroof[dom]["valu_achieved_ginst_s"] if valu_bound else round(achieved, 2),
+            "peak": VALU_PEAK_GINST if valu_bound else HBM_PEAK_GBS,
+            "unit": "G wave-VALU-inst/s" if valu_bound else "GB/s",
+            "frac": kroof[dom]["valu_frac"] if valu_bound else round(achieved / HBM_PEAK_GBS, 5),
+            "valu_frac": kroof[dom].get("valu_frac"),
+            "valu_busy_alone": kroof[dom].get("valu_busy_alone"),
+            "hbm_achieved_GBps": round(achieved, 2),
+            "hbm_frac": round(achieved / HBM_PEAK_GBS, 5),
+            "valu_source": os.path.relpath(args.valu_json, REPO) if valu else None,
             "stream_copy_GBps": round(stream_gbps, 1),
-            "frac_vs_stream_copy": round(achieved / stream_gbps, 5),
+            "hbm_frac_vs_stream_copy": round(achieved / stream_gbps, 5),
             "traffic": traffic,
             "bytes_per_launch": bytes_per_launch,
             "avg_launch_us": round(avg_launch_s * 1e6, 3),

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = [
     "fbr_destroy", "fbr_set_map", "fbr_get_map", "fbr_project", "fbr_extract_features",
     "fbr_register", "fbr_register_trace", "fbr_process_scan", "fbr_reset_stream",
     "fbr_process_batch", "fbr_ingest_bytes", "fbr_debug_counters", "fbr_map_grid_info", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
-    "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
+    "fbr_batch_flush", "fbr_batch_export_ready", "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
     "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math", "fbr_selftest_eigen6", "fbr_selftest_eig_certified", "fbr_selftest_voxel_order",
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
     "fbr_msg_to_points", "fbr_points_to_msg_data", "fbr_project_msg", "fbr_process_msg",
@@ -83,6 +83,8 @@ def lib():
             "fbr_batch_wait": (ctypes.c_int, [_VP]),
             "fbr_batch_results": (ctypes.c_int, [_VP, _VP, _VP]),
             "fbr_batch_export": (ctypes.c_int, [_VP, _VP]),
+            "fbr_batch_flush": (ctypes.c_int, [_VP]),
+            "fbr_batch_export_ready": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
             "fbr_batch_bytes": (ctypes.c_int, [_VP, _VP, _VP]),
             "fbr_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
             "fbr_set_profiling_kernels": (ctypes.c_int, [_VP, ctypes.c_char_p]),
@@ -509,6 +511,19 @@ class Context:
     def batch_export(self, device_ptr):
         """Enqueue the 32 B/job pose records into device memory at `device_ptr` (int address)."""
         _check(lib().fbr_batch_export(self._h, ctypes.c_void_p(device_ptr)), "fbr_batch_export")
+
+    def batch_flush(self):
+        """Enqueue the rest of every launch in flight (no device synchronisation)."""
+        _check(lib().fbr_batch_flush(self._h), "fbr_batch_flush")
+
+    def batch_export_ready(self, device_ptr, wait_stream=0):
+        """Pipelined export: the records of the latest fully enqueued, not yet exported launch into
+        `device_ptr`, after the work queued on `wait_stream` (a HIP stream handle, 0 = none).
+        Returns (launch_id, export stream handle); launch_id -1 = nothing exported."""
+        st, lid = _VP(), _I64()
+        _check(lib().fbr_batch_export_ready(self._h, ctypes.c_void_p(device_ptr), ctypes.c_void_p(wait_stream or None),
+                                            ctypes.byref(st), ctypes.byref(lid)), "fbr_batch_export_ready")
+        return lid.value, st.value or 0
 
     def batch_bytes(self):
         t, g = ctypes.c_double(), ctypes.c_double()

@@ -97,6 +97,35 @@ struct Ingest {
   double h2d_bytes = 0.0;            // bytes copied host -> device by the last fbr_process_batch
 };
 
+// A contiguous sub-batch of jobs driven on one stream.  j0 is the first job of the sub-batch's
+// work buffers (every per-job intermediate array, and the Gauss-Newton work-item arrays at
+// j0 * items_per_job); in0 the first job of its inputs (raw scans, counts, guesses, deskew tables,
+// CropBox statistics).  A batch launch in work slot s has j0 = s * max_batch + in0, so two launches
+// in flight never share intermediates.  k indexes the sub-batch's GN flags / counters.
+struct Sub {
+  int j0, B, k;  // first work job, job count, GN flag index (< kMaxSub)
+  hipStream_t st;
+  bool stream_mode = false;  // single-scan call (carries stream state) vs independent batch jobs
+  int in0 = 0;               // first input job
+};
+
+// The Gauss-Newton iterations of one launch that the host has still to enqueue.  The host stays
+// kLag iterations ahead of each sub-batch and stops once its k_gn_solve reports that no job is
+// active (flags in host-mapped memory), so a launch's tail cannot be enqueued before the device
+// has run most of it; two launches in flight are advanced together (fbr_batch_launch).
+struct GnRun {
+  bool pending = false;
+  bool trace = false;
+  int nsub = 0;
+  unsigned long long gen = 0;
+  Sub subs[kMaxSub];
+  GnArgs a[kMaxSub];
+  bool live[kMaxSub] = {}, watch[kMaxSub] = {}, done[kMaxSub] = {};
+  int active[kMaxSub] = {};  // jobs still iterating kLag iterations ago (an upper bound now)
+  int it[kMaxSub] = {};      // next iteration to enqueue
+  long polls[kMaxSub] = {};  // unanswered flag reads of the current wait
+};
+
 struct fbr_ctx {
   fbr_params P;
   int dev = 0;
@@ -107,6 +136,20 @@ struct fbr_ctx {
                                       // 3 -> 78.5k, 4 -> 46.7k scans/s: 4 sub-batch streams plus the
                                       // primary exceed the 4 hardware queues HIP gives a process)
   int H = 0, W = 0, Bcap = 0;
+  // Batch launches alternate between nslot work slots (2 unless FBR_PIPE=0 or max_batch = 1): the
+  // next launch's projection / features overlap the previous one's Gauss-Newton tail.  Work arrays
+  // hold Bwork = nslot * Bcap jobs; inputs hold Bcap.
+  int nslot = 1;
+  int64_t Bwork = 0;
+  GnRun run[2];
+  int64_t launch_seq = 0;     // batch launches so far
+  int last_slot = -1;         // slot of the latest launch (-1: none since the last stage)
+  int last_nsub[2] = {0, 0};  // sub-batches of each slot's latest launch
+  int64_t slot_launch[2] = {-1, -1};  // launch number of each slot's latest launch
+  int64_t exported = -1;      // latest launch whose records fbr_batch_export_ready exported
+  hipEvent_t ev_staged = nullptr;  // the staged inputs are on the device (recorded on stream)
+  hipEvent_t ev_fork = nullptr;    // single-scan side-stream fork
+  hipEvent_t ev_ext = nullptr;     // a caller's stream, waited on before an export (fbr_batch_export_ready)
   int items_per_job = 0;
   int64_t HW = 0, NMAX = 0;
   // inputs
@@ -363,29 +406,23 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
 // ---------------------------------------------------------------------------------------------
 // pipeline stages
 // ---------------------------------------------------------------------------------------------
-// A contiguous sub-batch of jobs [j0, j0 + B) driven on one stream.  The stages below offset every
-// per-job device array by j0, and the Gauss-Newton work-item arrays by j0 * items_per_job, so
-// sub-batches share the context's buffers without overlapping.
-struct Sub {
-  int j0, B, k;  // first job, job count, sub-batch index (< kMaxSub)
-  hipStream_t st;
-  bool stream_mode = false;  // single-scan call (carries stream state) vs independent batch jobs
-};
+// Sub-batches (struct Sub above) share the context's buffers without overlapping: the stages offset
+// every per-job work array by j0 and every input array by in0.
 
 // The single-scan sub-batch: job slot 0 on the primary stream, stream mode (the state the
 // reference's stage objects keep between scans is carried between calls).
 Sub single_sub(fbr_ctx* c) { return Sub{0, 1, 0, c->stream, true}; }
 
 int stage_project(fbr_ctx* c, const Sub& sb) {
-  const int64_t j0 = sb.j0;
+  const int64_t j0 = sb.j0, i0 = sb.in0;
   DeskArgs desk{nullptr, nullptr, nullptr};
   if (c->desk_any && !c->no_time_call)  // deskewFlag == -1 without a "time" field (:296-297, :548)
-    desk = DeskArgs{c->d_desk_mode + j0, c->d_desk + j0, c->d_rowmin + j0 * c->H};
+    desk = DeskArgs{c->d_desk_mode + i0, c->d_desk + i0, c->d_rowmin + j0 * c->H};
   int32_t* owner = c->d_owner + j0 * c->HW;  // all kEmptyOwner: set at fbr_create, reset by k_compact
-  TIMED_ON(c, sb.st, "project", launch_project(sb.st, c->d_pts + j0 * c->NMAX, c->d_nin + j0, c->NMAX, sb.B, c->H,
+  TIMED_ON(c, sb.st, "project", launch_project(sb.st, c->d_pts + i0 * c->NMAX, c->d_nin + i0, c->NMAX, sb.B, c->H,
                                                c->W, owner));
   TIMED_ON(c, sb.st, "extract",
-           launch_extract(sb.st, c->d_pts + j0 * c->NMAX, c->NMAX, owner, sb.B, c->H, c->W, c->d_rowcnt + j0 * c->H,
+           launch_extract(sb.st, c->d_pts + i0 * c->NMAX, c->NMAX, owner, sb.B, c->H, c->W, c->d_rowcnt + j0 * c->H,
                           c->d_choff + j0 * c->H * (c->W / 32 + 1),
                           c->d_cloud + j0 * c->HW, c->d_col + j0 * c->HW, c->d_range + j0 * c->HW,
                           c->d_start + j0 * c->H, c->d_end + j0 * c->H, c->d_nvalid + j0, desk));
@@ -466,7 +503,7 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   a.mc = c->grid_c.view();
   a.ms = c->grid_s.view();
   a.gn = c->d_gn + j0;
-  a.guess = c->d_guess + j0 * 6;
+  a.guess = c->d_guess + (int64_t)sb.in0 * 6;
   a.items = c->d_items + ib;
   a.nitems = c->d_nitems + sb.k;
   a.item_range = c->d_item_range + j0 * 2;
@@ -491,8 +528,8 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   a.fit_cache = fit_cache;
   a.iter_flags = c->d_iter_flags + (int64_t)sb.k * mi;
   a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 2 * mi;
-  a.desk_mode = c->desk_any ? c->d_desk_mode + j0 : nullptr;
-  a.desk = c->desk_any ? c->d_desk + j0 : nullptr;
+  a.desk_mode = c->desk_any ? c->d_desk_mode + sb.in0 : nullptr;
+  a.desk = c->desk_any ? c->d_desk + sb.in0 : nullptr;
   a.nocrop = c->map_nocrop ? 1 : 0;
   a.deg_carry = sb.stream_mode ? c->stream_degenerate : 0;
   return a;
@@ -501,14 +538,19 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
 // Registration of the clouds in d_corner_all / d_surf_all (counts d_ncorner / d_nsurf) from d_guess.
 // Single-scan entry points reuse job slot 0 of the device buffers: a staged batch is dropped
 // (fbr_batch_launch then reports FBR_ERR_STATE until the next fbr_batch_stage).
-void drop_staged_batch(fbr_ctx* c) {
+int batch_quiesce(fbr_ctx* c);
+int drop_staged_batch(fbr_ctx* c) {
+  const int rc = batch_quiesce(c);
   c->staged_B = 0;
   c->crop_cached = false;
+  c->last_slot = -1;
+  c->exported = -1;
+  return rc;
 }
 
 int crop_stats(fbr_ctx* c, const Sub& sb) {
   GnArgs a = gn_args(c, sb, false);
-  int32_t* cnt = c->d_cropcnt + (int64_t)sb.j0 * 2;
+  int32_t* cnt = c->d_cropcnt + (int64_t)sb.in0 * 2;
   if (c->map_nocrop) {  // keyframe local map: laserCloud*FromMapDSNum = the whole DS map
     std::vector<int32_t> v(2 * sb.B);
     for (int j = 0; j < sb.B; ++j) {
@@ -535,7 +577,7 @@ int register_prepare(fbr_ctx* c, const Sub& sb, bool trace) {
   v.s[0] = VgSet{c->d_surf_all + j0 * HW, HW, c->d_nsurf + j0, HW, c->d_surfDS + j0 * HW, HW, c->d_nsds + j0,
                  c->d_vg_scratch + j0 * kVgScratch * HW, c->P.mapping_surf_leaf_size, sb.B, 1, vg_exact() ? 1 : 0};
   v.s[1] = VgSet{c->d_corner_all + j0 * HW, HW, c->d_ncorner + j0, ccap, c->d_cornerDS + j0 * HW, HW, c->d_ncds + j0,
-                 c->d_vg_scratch + (int64_t)c->Bcap * kVgScratch * HW + j0 * kVgScratch * ccap, c->P.mapping_corner_leaf_size,
+                 c->d_vg_scratch + c->Bwork * kVgScratch * HW + j0 * kVgScratch * ccap, c->P.mapping_corner_leaf_size,
                  sb.B, 1, vg_exact() ? 1 : 0};
   if (c->ring_box_valid) {  // the clouds' bounds from k_concat: the filter reads each cloud twice, not 3 times
     const float* rb = c->d_ring_box + j0 * c->H * kRingBox;
@@ -587,64 +629,140 @@ int gn_tail_div() {
   return v;
 }
 
-// The Gauss-Newton iterations of one or two sub-batches.  Iterations run on the device without
-// host round trips; for each sub-batch the host stays kLag iterations ahead and stops enqueueing
-// once its k_gn_solve reports that no job is active (flags in host-mapped memory).
-int register_iterate(fbr_ctx* c, const Sub* subs, int nsub, bool trace) {
-  constexpr int kLag = 2;
-  const unsigned long long gen = ++c->gn_gen;
-  const int mi = std::max(1, c->P.max_iterations);
-  GnArgs a[kMaxSub];
-  bool live[kMaxSub] = {}, watch[kMaxSub] = {};
-  int active[kMaxSub] = {};  // jobs still iterating kLag iterations ago (an upper bound now)
+constexpr int kLag = 2;  // iterations the host enqueues ahead of a sub-batch's latest flag
+
+void gn_run_start(fbr_ctx* c, GnRun& r, const Sub* subs, int nsub, bool trace) {
+  r = GnRun{};
+  r.pending = true;
+  r.trace = trace;
+  r.nsub = nsub;
+  r.gen = ++c->gn_gen;
   for (int k = 0; k < nsub; ++k) {
-    a[k] = gn_args(c, subs[k], trace);
-    live[k] = true;
-    active[k] = subs[k].B;
-    watch[k] = c->h_iter_flags != nullptr;
+    r.subs[k] = subs[k];
+    r.a[k] = gn_args(c, subs[k], trace);
+    r.live[k] = true;
+    r.active[k] = subs[k].B;
+    r.watch[k] = c->h_iter_flags != nullptr;
   }
-  for (int it = 0; it < c->P.max_iterations; ++it) {
-    for (int k = 0; k < nsub; ++k) {
-      if (!live[k]) continue;
-      const Sub& sb = subs[k];
-      if (watch[k] && it >= kLag) {
-        volatile unsigned long long* f = c->h_iter_flags + (int64_t)sb.k * mi + (it - kLag);
-        unsigned long long v = *f;
-        const auto tspin = std::chrono::steady_clock::now();
-        for (long spins = 0; (v >> 32) != (gen & 0xFFFFFFFFull); ++spins) {
-          if ((spins & 1023) == 1023) {
-            const hipError_t q = hipStreamQuery(sb.st);
-            if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
-            if (q == hipSuccess && ((v = *f) >> 32) != (gen & 0xFFFFFFFFull)) {
-              watch[k] = false;  // flag not visible although the stream drained: enqueue the rest
-              break;
-            }
+}
+
+// One pass over the run's sub-batches: each enqueues its next iteration if the flag it needs is
+// visible (block: wait for it).  A sub-batch whose jobs all stopped, or that reached
+// max_iterations, gets its transformUpdate.  *progress: something was enqueued.
+int gn_run_pass(fbr_ctx* c, GnRun& r, bool block, bool* progress) {
+  const int mi = std::max(1, c->P.max_iterations);
+  const unsigned long long g32 = r.gen & 0xFFFFFFFFull;
+  bool all_done = true;
+  for (int k = 0; k < r.nsub; ++k) {
+    if (r.done[k]) continue;
+    const Sub& sb = r.subs[k];
+    const int it = r.it[k];
+    if (r.live[k] && it < c->P.max_iterations && r.watch[k] && it >= kLag) {
+      volatile unsigned long long* f = c->h_iter_flags + (int64_t)sb.k * mi + (it - kLag);
+      unsigned long long v = *f;
+      const auto tspin = std::chrono::steady_clock::now();
+      while ((v >> 32) != g32) {
+        if ((++r.polls[k] & 1023) == 1023) {
+          const hipError_t q = hipStreamQuery(sb.st);
+          if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
+          if (q == hipSuccess && ((v = *f) >> 32) != g32) {
+            r.watch[k] = false;  // flag not visible although the stream drained: enqueue the rest
+            break;
           }
-          v = *f;
         }
-        debug_counters().flag_polls.fetch_add(1, std::memory_order_relaxed);
+        if (!block) break;
+        v = *f;
+      }
+      if (block || (v >> 32) == g32 || !r.watch[k])
         debug_counters().batch_ns[1].fetch_add(
             std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tspin).count(),
             std::memory_order_relaxed);
-        if (watch[k]) active[k] = (int)(v & 0xFFFFFFFFull);
-        if (watch[k] && active[k] == 0) {
-          live[k] = false;
-          continue;
-        }
+      if (r.watch[k] && (v >> 32) != g32) {  // not yet (non-blocking pass)
+        all_done = false;
+        continue;
       }
-      const bool tail = gn_tail_div() > 0 && (int64_t)active[k] * gn_tail_div() <= sb.B;
-      const int grid = std::max(1, std::min(a[k].max_items, tail ? std::min(gn_grid_cap(), 1024) : gn_grid_cap()));
-      if (gn_fused() || tail) {
-        TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a[k], grid, it, true));
-      } else {
-        TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a[k], grid, it, false));
-        TIMED_ON(c, sb.st, "gn_residual", launch_gn_residual(sb.st, a[k], grid));
-      }
-      TIMED_ON(c, sb.st, "gn_solve", launch_gn_solve(sb.st, a[k], it, gen));
+      r.polls[k] = 0;
+      debug_counters().flag_polls.fetch_add(1, std::memory_order_relaxed);
+      if (r.watch[k]) r.active[k] = (int)(v & 0xFFFFFFFFull);
+      if (r.watch[k] && r.active[k] == 0) r.live[k] = false;
     }
+    if (!r.live[k] || it >= c->P.max_iterations) {
+      TIMED_ON(c, sb.st, "gn_finalize", launch_gn_finalize(sb.st, r.a[k]));
+      CK(hipEventRecord(c->xev[sb.k], sb.st));  // the sub-batch's last work (batch_quiesce joins it)
+      r.done[k] = true;
+      *progress = true;
+      continue;
+    }
+    all_done = false;
+    const bool tail = gn_tail_div() > 0 && (int64_t)r.active[k] * gn_tail_div() <= sb.B;
+    const int grid = std::max(1, std::min(r.a[k].max_items, tail ? std::min(gn_grid_cap(), 1024) : gn_grid_cap()));
+    if (gn_fused() || tail) {
+      TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, r.a[k], grid, it, true));
+    } else {
+      TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, r.a[k], grid, it, false));
+      TIMED_ON(c, sb.st, "gn_residual", launch_gn_residual(sb.st, r.a[k], grid));
+    }
+    TIMED_ON(c, sb.st, "gn_solve", launch_gn_solve(sb.st, r.a[k], it, r.gen));
+    r.it[k] = it + 1;
+    *progress = true;
   }
-  for (int k = 0; k < nsub; ++k) TIMED_ON(c, subs[k].st, "gn_finalize", launch_gn_finalize(subs[k].st, a[k]));
+  if (all_done) r.pending = false;
   return FBR_OK;
+}
+
+// Enqueue the rest of a run, waiting for its flags.
+int gn_run_finish(fbr_ctx* c, GnRun& r) {
+  while (r.pending) {
+    bool p = false;
+    const int rc = gn_run_pass(c, r, true, &p);
+    if (rc) return rc;
+  }
+  return FBR_OK;
+}
+
+// Advance the batch launches in flight together (non-blocking passes; spin while neither can
+// progress) until run[target] is fully enqueued (target -1: every run).
+int advance_runs(fbr_ctx* c, int target) {
+  auto busy = [&] { return target < 0 ? (c->run[0].pending || c->run[1].pending) : c->run[target].pending; };
+  auto tw = std::chrono::steady_clock::now();
+  bool waiting = false;
+  while (busy()) {
+    bool p = false;
+    for (int s = 0; s < 2; ++s)
+      if (c->run[s].pending) {
+        const int rc = gn_run_pass(c, c->run[s], false, &p);
+        if (rc) return rc;
+      }
+    if (p && waiting) {
+      debug_counters().batch_ns[1].fetch_add(
+          std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tw).count(),
+          std::memory_order_relaxed);
+      waiting = false;
+    } else if (!p && !waiting) {
+      waiting = true;
+      tw = std::chrono::steady_clock::now();
+    }
+    if (!p) __builtin_ia32_pause();
+  }
+  return FBR_OK;
+}
+
+// Every batch launch fully enqueued, and the primary stream ordered after all of them (on the
+// device): the caller may then overwrite the inputs or use job slot 0 on the primary stream.
+int batch_quiesce(fbr_ctx* c) {
+  const int rc = advance_runs(c, -1);
+  if (rc) return rc;
+  for (int s = 0; s < 2; ++s)
+    for (int k = 0; k < c->run[s].nsub; ++k)
+      if (c->run[s].subs[k].st != c->stream) CK(hipStreamWaitEvent(c->stream, c->xev[c->run[s].subs[k].k], 0));
+  return FBR_OK;
+}
+
+// The Gauss-Newton iterations of sub-batches enqueued to the end (single-scan calls).
+int register_iterate(fbr_ctx* c, const Sub* subs, int nsub, bool trace) {
+  GnRun r;
+  gn_run_start(c, r, subs, nsub, trace);
+  return gn_run_finish(c, r);
 }
 
 int stage_register(fbr_ctx* c, const Sub& sb, bool trace) {
@@ -657,9 +775,9 @@ int stage_register(fbr_ctx* c, const Sub& sb, bool trace) {
 // Per-job results of the last B jobs, packed on the device and returned by one copy (then one
 // host synchronisation): poses (when poses_out), stats, and the features' capacity errors
 // (FBR_ERR_UNSUPPORTED if any job has one).  with_reg = false: the registration was gated off.
-int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool with_reg = true) {
-  launch_pack_results(c->stream, B, with_reg ? 1 : 0, c->d_pose_out, c->d_stats, c->d_nvalid, c->d_ncorner, c->d_nsurf,
-                      c->d_cropcnt, c->d_err, c->d_result);
+int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool with_reg = true, int64_t w0 = 0) {
+  launch_pack_results(c->stream, B, with_reg ? 1 : 0, c->d_pose_out + w0 * 6, c->d_stats + w0, c->d_nvalid + w0,
+                      c->d_ncorner + w0, c->d_nsurf + w0, c->d_cropcnt, c->d_err + w0, c->d_result);
   CK(hipMemcpyAsync(c->h_result, c->d_result, sizeof(JobResult) * B, hipMemcpyDeviceToHost, c->stream));
   const auto tw = std::chrono::steady_clock::now();
   CK(fbr_sync(c->stream));
@@ -1036,48 +1154,60 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   c->HW = (int64_t)c->H * c->W;
   c->Bcap = p->max_batch;
   c->NMAX = p->max_points_per_scan;
-  const int64_t B = c->Bcap, HW = c->HW, H = c->H;
   if (const char* e = std::getenv("FBR_NSUB")) c->nsub_pref = std::max(1, std::min(kMaxSub, std::atoi(e)));
-  // streams of the sub-batches this context can use (each stream takes a hardware queue: unused
-  // ones are not created, so they cannot share a queue with a busy one)
-  const int nstreams = std::max(2, c->nsub_pref);
+  static const bool pipe = [] {
+    const char* e = std::getenv("FBR_PIPE");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  c->nslot = (pipe && p->max_batch > 1) ? 2 : 1;
+  if (c->nslot == 2) c->nsub_pref = std::min(c->nsub_pref, kMaxSub / 2);
+  c->Bwork = (int64_t)c->nslot * c->Bcap;
+  const int64_t B = c->Bcap, Bw = c->Bwork, HW = c->HW, H = c->H;
+  // streams of the sub-batches this context can use, per slot (each stream takes a hardware queue:
+  // unused ones are not created, so they cannot share a queue with a busy one)
+  const int nstreams = std::max(2, c->nslot * c->nsub_pref);
   bool sfail = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess;
   for (int k = 0; k < nstreams && !sfail; ++k) {
     if (k > 0) sfail = hipStreamCreateWithFlags(&c->xstream[k], hipStreamNonBlocking) != hipSuccess;
     if (!sfail) sfail = hipEventCreateWithFlags(&c->xev[k], hipEventDisableTiming) != hipSuccess;
   }
+  if (!sfail) sfail = hipEventCreateWithFlags(&c->ev_staged, hipEventDisableTiming) != hipSuccess ||
+                     hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+                     hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming) != hipSuccess;
   if (sfail) {
     fbr_destroy(c);
     return FBR_ERR_HIP;
   }
   c->items_per_job = (int)(2 * ((HW + 255) / 256 + 1));
-  c->max_items = (int)(B * c->items_per_job);
-  c->vg_scratch_elems = kVgScratch * B * (HW + std::min<int64_t>(HW, (int64_t)kCornerPerRing * H));
+  c->max_items = (int)(Bw * c->items_per_job);
+  c->vg_scratch_elems = kVgScratch * Bw * (HW + std::min<int64_t>(HW, (int64_t)kCornerPerRing * H));
+  // inputs: B jobs; work arrays: Bw jobs (nslot launch slots)
   bool fail = dalloc(&c->d_pts, B * c->NMAX) || dalloc(&c->d_nin, B) || dalloc(&c->d_guess, B * 6) ||
-              dalloc(&c->d_owner, B * HW) || dalloc(&c->d_rowcnt, B * H) || dalloc(&c->d_col, B * HW) ||
-              dalloc(&c->d_start, B * H) || dalloc(&c->d_end, B * H) || dalloc(&c->d_nvalid, B) ||
-              dalloc(&c->d_cloud, B * HW) || dalloc(&c->d_range, B * HW) || dalloc(&c->d_sstate, B) ||
-              dalloc(&c->d_sstream, 1) || dalloc(&c->d_label, B * HW) || dalloc(&c->d_label_stream, HW) ||
-              dalloc(&c->d_corner_slot, B * H * kCornerPerRing) || dalloc(&c->d_corner_cnt, B * H) ||
-              dalloc(&c->d_surf_ring, B * HW) ||
-              dalloc(&c->d_surf_ring_cnt, B * H) || dalloc(&c->d_ring_box, B * H * kRingBox) || dalloc(&c->d_err, B) || dalloc(&c->d_corner_all, B * HW) ||
-              dalloc(&c->d_surf_all, B * HW) || dalloc(&c->d_cornerDS, B * HW) || dalloc(&c->d_surfDS, B * HW) ||
-              dalloc(&c->d_ncorner, B) || dalloc(&c->d_nsurf, B) || dalloc(&c->d_ncds, B) || dalloc(&c->d_nsds, B) ||
+              dalloc(&c->d_owner, Bw * HW) || dalloc(&c->d_rowcnt, Bw * H) || dalloc(&c->d_col, Bw * HW) ||
+              dalloc(&c->d_start, Bw * H) || dalloc(&c->d_end, Bw * H) || dalloc(&c->d_nvalid, Bw) ||
+              dalloc(&c->d_cloud, Bw * HW) || dalloc(&c->d_range, Bw * HW) || dalloc(&c->d_sstate, Bw) ||
+              dalloc(&c->d_sstream, 1) || dalloc(&c->d_label, Bw * HW) || dalloc(&c->d_label_stream, HW) ||
+              dalloc(&c->d_corner_slot, Bw * H * kCornerPerRing) || dalloc(&c->d_corner_cnt, Bw * H) ||
+              dalloc(&c->d_surf_ring, Bw * HW) ||
+              dalloc(&c->d_surf_ring_cnt, Bw * H) || dalloc(&c->d_ring_box, Bw * H * kRingBox) || dalloc(&c->d_err, Bw) ||
+              dalloc(&c->d_corner_all, Bw * HW) ||
+              dalloc(&c->d_surf_all, Bw * HW) || dalloc(&c->d_cornerDS, Bw * HW) || dalloc(&c->d_surfDS, Bw * HW) ||
+              dalloc(&c->d_ncorner, Bw) || dalloc(&c->d_nsurf, Bw) || dalloc(&c->d_ncds, Bw) || dalloc(&c->d_nsds, Bw) ||
               dalloc(&c->d_vg_scratch, c->vg_scratch_elems) ||
-              dalloc(&c->d_gn, B) || dalloc(&c->d_items, c->max_items) || dalloc(&c->d_nitems, kMaxSub) ||
-              dalloc(&c->d_item_range, 2 * B) || dalloc(&c->d_cropcnt, 2 * B) ||
+              dalloc(&c->d_gn, Bw) || dalloc(&c->d_items, c->max_items) || dalloc(&c->d_nitems, kMaxSub) ||
+              dalloc(&c->d_item_range, 2 * Bw) || dalloc(&c->d_cropcnt, 2 * B) ||
               dalloc(&c->d_partial, (int64_t)c->max_items * 32) ||
               dalloc(&c->d_nbr, (int64_t)c->max_items * 5 * 256) ||
               dalloc(&c->d_fitc, (int64_t)c->max_items * 6 * 256) || dalloc(&c->d_fits, (int64_t)c->max_items * 256) ||
               dalloc(&c->d_nsame, (int64_t)c->max_items * 256) ||
               dalloc(&c->d_iter_cnt, kMaxSub * 2 * std::max(1, p->max_iterations)) ||
-              dalloc(&c->d_feat_scratch, (int64_t)B * H * feat_slot_bytes(c->W)) ||
+              dalloc(&c->d_feat_scratch, Bw * H * feat_slot_bytes(c->W)) ||
               hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * kMaxSub * std::max(1, p->max_iterations),
                             hipHostMallocMapped) != hipSuccess ||
-              hipHostGetDevicePointer((void**)&c->d_iter_flags, c->h_iter_flags, 0) != hipSuccess || dalloc(&c->d_pose_out, B * 6) ||
-              dalloc(&c->d_stats, B) || dalloc(&c->d_trace, B * p->max_iterations * 6) ||
-              dalloc(&c->d_desk_mode, B) || dalloc(&c->d_rowmin, B * H) || dalloc(&c->d_result, B) ||
-              dalloc(&c->d_choff, B * H * (c->W / 32 + 1)) ||
+              hipHostGetDevicePointer((void**)&c->d_iter_flags, c->h_iter_flags, 0) != hipSuccess || dalloc(&c->d_pose_out, Bw * 6) ||
+              dalloc(&c->d_stats, Bw) || dalloc(&c->d_trace, Bw * p->max_iterations * 6) ||
+              dalloc(&c->d_desk_mode, B) || dalloc(&c->d_rowmin, Bw * H) || dalloc(&c->d_result, B) ||
+              dalloc(&c->d_choff, Bw * H * (c->W / 32 + 1)) ||
               hipHostMalloc((void**)&c->h_result, sizeof(JobResult) * B, hipHostMallocDefault) != hipSuccess ||
               hipHostMalloc((void**)&c->h_scan, sizeof(fbr_point_xyzirt) * std::max<int64_t>(c->NMAX, 1),
                             hipHostMallocDefault) != hipSuccess ||
@@ -1089,10 +1219,10 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   }
   std::memset(c->h_iter_flags, 0, sizeof(unsigned long long) * kMaxSub * std::max(1, p->max_iterations));
   if (hipMemset(c->d_sstream, 0, sizeof(StreamState)) != hipSuccess ||
-      hipMemset(c->d_label_stream, 0, HW) != hipSuccess || hipMemset(c->d_col, 0, sizeof(int32_t) * B * HW) != hipSuccess ||
-      hipMemset(c->d_range, 0, sizeof(float) * B * HW) != hipSuccess ||
+      hipMemset(c->d_label_stream, 0, HW) != hipSuccess || hipMemset(c->d_col, 0, sizeof(int32_t) * Bw * HW) != hipSuccess ||
+      hipMemset(c->d_range, 0, sizeof(float) * Bw * HW) != hipSuccess ||
       hipMemset(c->d_desk_mode, 0, sizeof(int32_t) * B) != hipSuccess ||
-      hipMemset(c->d_owner, 0x7F, sizeof(int32_t) * B * HW) != hipSuccess) {  // k_compact resets it after use
+      hipMemset(c->d_owner, 0x7F, sizeof(int32_t) * Bw * HW) != hipSuccess) {  // k_compact resets it after use
     fbr_destroy(c);
     return FBR_ERR_HIP;
   }
@@ -1146,6 +1276,9 @@ int fbr_destroy(fbr_ctx* c) {
     if (c->xstream[k]) (void)hipStreamDestroy(c->xstream[k]);
     if (c->xev[k]) (void)hipEventDestroy(c->xev[k]);
   }
+  if (c->ev_staged) (void)hipEventDestroy(c->ev_staged);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_ext) (void)hipEventDestroy(c->ev_ext);
   delete c;
   return FBR_OK;
 }
@@ -1218,8 +1351,9 @@ int fbr_project(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, int32_
                 int32_t* col_ind, float* range, fbr_point_xyzi* cloud, int64_t* n_out) {
   if (!c || (n_in && !points)) return FBR_ERR_INVALID_ARG;
   CK(hipSetDevice(c->dev));
-  drop_staged_batch(c);
-  int rc = upload_scan(c, 0, points, n_in);
+  int rc = drop_staged_batch(c);
+  if (rc) return rc;
+  rc = upload_scan(c, 0, points, n_in);
   if (rc) return rc;
   return project_uploaded(c, start_ring, end_ring, col_ind, range, cloud, n_out);
 }
@@ -1228,8 +1362,9 @@ int fbr_project_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* start_ring,
                     float* range, fbr_point_xyzi* cloud, int64_t* n_out, int32_t* msg_flags) {
   if (!c || !msg) return FBR_ERR_INVALID_ARG;
   CK(hipSetDevice(c->dev));
-  drop_staged_batch(c);
-  int rc = upload_msg(c, msg, msg_flags);
+  int rc = drop_staged_batch(c);
+  if (rc) return rc;
+  rc = upload_msg(c, msg, msg_flags);
   if (rc) return rc;
   return project_uploaded(c, start_ring, end_ring, col_ind, range, cloud, n_out);
 }
@@ -1279,8 +1414,8 @@ int fbr_register_trace(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corne
   if (!c || !pose_inout) return FBR_ERR_INVALID_ARG;
   if (!c->has_map) return FBR_ERR_NO_MAP;
   CK(hipSetDevice(c->dev));
-  drop_staged_batch(c);
-  int rc = upload_cloud(c, c->d_corner_all, c->d_ncorner, corner, n_corner);
+  int rc = drop_staged_batch(c);
+  if (!rc) rc = upload_cloud(c, c->d_corner_all, c->d_ncorner, corner, n_corner);
   if (!rc) rc = upload_cloud(c, c->d_surf_all, c->d_nsurf, surf, n_surf);
   if (rc) return rc;
   CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->stream));
@@ -1312,8 +1447,9 @@ int fbr_process_scan(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, d
   if (!c || !pose_inout || (n_in && !points)) return FBR_ERR_INVALID_ARG;
   const auto t0 = std::chrono::steady_clock::now();
   CK(hipSetDevice(c->dev));
-  drop_staged_batch(c);
-  int rc = upload_scan(c, 0, points, n_in);
+  int rc = drop_staged_batch(c);
+  if (rc) return rc;
+  rc = upload_scan(c, 0, points, n_in);
   if (rc) return rc;
   host_time(0, t0);
   rc = process_uploaded(c, stamp, pose_inout, stats);
@@ -1325,8 +1461,9 @@ int fbr_process_msg(fbr_ctx* c, const fbr_pointcloud2* msg, double stamp, float 
                     int32_t* msg_flags) {
   if (!c || !msg || !pose_inout) return FBR_ERR_INVALID_ARG;
   CK(hipSetDevice(c->dev));
-  drop_staged_batch(c);
-  int rc = upload_msg(c, msg, msg_flags);
+  int rc = drop_staged_batch(c);
+  if (rc) return rc;
+  rc = upload_msg(c, msg, msg_flags);
   if (rc) return rc;
   return process_uploaded(c, stamp, pose_inout, stats);
 }
@@ -1351,8 +1488,8 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
     CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->stream));
     // the CropBox statistics depend only on the guess: a side stream computes them while the
     // registration runs, and copy_results joins it
-    CK(hipEventRecord(c->xev[1], c->stream));
-    CK(hipStreamWaitEvent(c->xstream[1], c->xev[1], 0));
+    CK(hipEventRecord(c->ev_fork, c->stream));
+    CK(hipStreamWaitEvent(c->xstream[1], c->ev_fork, 0));
     rc = crop_stats(c, Sub{0, 1, 0, c->xstream[1], true});
     if (rc) return rc;
     CK(hipMemcpyAsync(c->h_crop, c->d_cropcnt, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, c->xstream[1]));
@@ -1400,9 +1537,9 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
     if (n_in[j] && !scans[j]) return FBR_ERR_INVALID_ARG;
   }
   CK(hipSetDevice(c->dev));
-  drop_staged_batch(c);
+  int rc = drop_staged_batch(c);  // launches in flight read the inputs: they are enqueued first
+  if (rc) return rc;
   c->no_time_call = false;
-  int rc = FBR_OK;
   auto q = [&](hipError_t e) {
     if (e != hipSuccess && !rc) rc = FBR_ERR_HIP;
   };
@@ -1413,6 +1550,7 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
   if (!rc) q(hipMemcpyAsync(c->d_nin, n_in, sizeof(int64_t) * n_jobs, hipMemcpyHostToDevice, c->stream));
   if (!rc) q(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * n_jobs, hipMemcpyHostToDevice, c->stream));
   if (!rc && c->has_map) rc = crop_stats(c, Sub{0, n_jobs, 0, c->stream});
+  if (!rc) q(hipEventRecord(c->ev_staged, c->stream));  // every launch's streams start after it
   // the caller's host buffers may be reused once this returns: drain the queued copies on every path
   q(fbr_sync(c->stream));
   if (rc) return rc;
@@ -1450,55 +1588,101 @@ int fbr_batch_launch(fbr_ctx* c) {
   CK(hipSetDevice(c->dev));
   const auto t0 = std::chrono::steady_clock::now();
   // Sub-batches on separate streams: one sub-batch's low-occupancy phases (the features' ring-0
-  // waves, the last Gauss-Newton iterations) overlap the others' work.
+  // waves, the last Gauss-Newton iterations) overlap the others' work.  Consecutive launches take
+  // alternate work slots with their own streams, and this call returns once the previous launch is
+  // fully enqueued: this launch's projection and features run beside the previous one's GN tail.
   const int B = c->staged_B;
-  const int nsub = std::max(1, std::min({c->nsub_pref, kMaxSub, B / 8}));
+  const int slot = c->nslot == 2 ? (int)(c->launch_seq & 1) : 0;
+  int rc = advance_runs(c, slot);  // (already enqueued by the previous call: launches n-2 < n-1)
+  if (rc) return rc;
+  const int nsub = std::max(1, std::min({c->nsub_pref, kMaxSub / c->nslot, B / 8}));
   Sub subs[kMaxSub];
   for (int k = 0; k < nsub; ++k) {
     const int j0 = (int)((int64_t)B * k / nsub), j1 = (int)((int64_t)B * (k + 1) / nsub);
-    subs[k] = Sub{j0, j1 - j0, k, k == 0 ? c->stream : c->xstream[k]};
+    const int idx = slot * nsub + k;
+    subs[k] = Sub{(int)((int64_t)slot * c->Bcap + j0), j1 - j0, idx, idx == 0 ? c->stream : c->xstream[idx], false, j0};
+    CK(hipStreamWaitEvent(subs[k].st, c->ev_staged, 0));  // the staged inputs
   }
-  if (nsub > 1) {  // fork: the extra streams start after the staged inputs (copied on stream)
-    CK(hipEventRecord(c->xev[0], c->stream));
-    for (int k = 1; k < nsub; ++k) CK(hipStreamWaitEvent(c->xstream[k], c->xev[0], 0));
-  }
-  int rc = FBR_OK;
   for (int k = 0; k < nsub && !rc; ++k) {
     rc = stage_project(c, subs[k]);
     if (!rc) rc = stage_features(c, subs[k], false);
     if (!rc) rc = register_prepare(c, subs[k], false);
   }
-  if (!rc) rc = register_iterate(c, subs, nsub, false);
-  for (int k = 1; k < nsub && !rc; ++k) {  // join: later work on stream (results, export) sees all
-    CK(hipEventRecord(c->xev[k], c->xstream[k]));
-    CK(hipStreamWaitEvent(c->stream, c->xev[k], 0));
-  }
+  if (rc) return rc;
+  gn_run_start(c, c->run[slot], subs, nsub, false);
+  c->last_slot = slot;
+  c->slot_launch[slot] = c->launch_seq++;
+  bool p = false;
+  rc = gn_run_pass(c, c->run[slot], false, &p);  // the iterations that need no flag yet
+  if (!rc) rc = advance_runs(c, c->nslot == 2 ? slot ^ 1 : slot);
   debug_counters().batch_ns[0].fetch_add(
       std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
       std::memory_order_relaxed);
   return rc;
 }
 
+int fbr_batch_flush(fbr_ctx* c) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  CK(hipSetDevice(c->dev));
+  return advance_runs(c, -1);
+}
+
 int fbr_batch_wait(fbr_ctx* c) {
   if (!c) return FBR_ERR_INVALID_ARG;
   CK(hipSetDevice(c->dev));
+  const int rc = batch_quiesce(c);
+  if (rc) return rc;
   CK(fbr_sync(c->stream));
   return FBR_OK;
 }
 
 int fbr_batch_results(fbr_ctx* c, float* poses_out, fbr_reg_stats* stats) {
   if (!c) return FBR_ERR_INVALID_ARG;
-  if (c->staged_B <= 0) return FBR_ERR_STATE;
+  if (c->staged_B <= 0 || c->last_slot < 0) return FBR_ERR_STATE;
   CK(hipSetDevice(c->dev));
-  return copy_results(c, c->staged_B, stats, poses_out, true);
+  const int rc = batch_quiesce(c);
+  if (rc) return rc;
+  return copy_results(c, c->staged_B, stats, poses_out, true, (int64_t)c->last_slot * c->Bcap);
 }
 
 int fbr_batch_export(fbr_ctx* c, void* device_dst) {
   if (!c || !device_dst) return FBR_ERR_INVALID_ARG;
+  if (c->staged_B <= 0 || c->last_slot < 0) return FBR_ERR_STATE;
+  CK(hipSetDevice(c->dev));
+  const int rc = batch_quiesce(c);
+  if (rc) return rc;
+  const int64_t w0 = (int64_t)c->last_slot * c->Bcap;
+  launch_export_records(c->stream, c->staged_B, c->d_pose_out + w0 * 6, c->d_stats + w0, (float*)device_dst);
+  CK(hipGetLastError());
+  c->exported = c->slot_launch[c->last_slot];
+  return FBR_OK;
+}
+
+int fbr_batch_export_ready(fbr_ctx* c, void* device_dst, void* wait_stream, void** export_stream, int64_t* launch_id) {
+  if (!c || !device_dst || !export_stream || !launch_id) return FBR_ERR_INVALID_ARG;
+  *export_stream = nullptr;
+  *launch_id = -1;
   if (c->staged_B <= 0) return FBR_ERR_STATE;
   CK(hipSetDevice(c->dev));
-  launch_export_records(c->stream, c->staged_B, c->d_pose_out, c->d_stats, (float*)device_dst);
+  int s = -1;  // the latest launch that is fully enqueued and not yet exported
+  for (int q = 0; q < c->nslot; ++q)
+    if (c->slot_launch[q] > c->exported && !c->run[q].pending && c->run[q].nsub > 0 &&
+        (s < 0 || c->slot_launch[q] > c->slot_launch[s]))
+      s = q;
+  if (s < 0) return FBR_OK;
+  const GnRun& r = c->run[s];
+  hipStream_t st = r.subs[0].st;
+  for (int k = 1; k < r.nsub; ++k) CK(hipStreamWaitEvent(st, c->xev[r.subs[k].k], 0));
+  if (wait_stream) {  // the caller's previous reader of device_dst
+    CK(hipEventRecord(c->ev_ext, (hipStream_t)wait_stream));
+    CK(hipStreamWaitEvent(st, c->ev_ext, 0));
+  }
+  const int64_t w0 = (int64_t)s * c->Bcap;
+  launch_export_records(st, c->staged_B, c->d_pose_out + w0 * 6, c->d_stats + w0, (float*)device_dst);
   CK(hipGetLastError());
+  c->exported = c->slot_launch[s];
+  *export_stream = (void*)st;
+  *launch_id = c->slot_launch[s];
   return FBR_OK;
 }
 
@@ -1584,7 +1768,8 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
 // Stage device batch `slot` whose scans ingest_upload queued: job metadata on the primary stream,
 // which then waits for the slot's upload.
 int ingest_stage(fbr_ctx* c, int slot, const int64_t* n_in, int B, const float* poses_in) {
-  drop_staged_batch(c);
+  const int rc0 = drop_staged_batch(c);
+  if (rc0) return rc0;
   c->no_time_call = false;
   c->d_pts = c->ing.d_pts_slot[slot];
   CK(hipMemcpyAsync(c->d_nin, n_in, sizeof(int64_t) * B, hipMemcpyHostToDevice, c->stream));
@@ -1594,6 +1779,7 @@ int ingest_stage(fbr_ctx* c, int slot, const int64_t* n_in, int B, const float* 
     const int rc = crop_stats(c, Sub{0, B, 0, c->stream});
     if (rc) return rc;
   }
+  CK(hipEventRecord(c->ev_staged, c->stream));
   CK(fbr_sync(c->stream));  // n_in / poses_in are the caller's
   c->crop_cached = c->has_map;
   c->staged_B = B;
@@ -1637,7 +1823,7 @@ int fbr_process_batch(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const in
   }
   (void)fbr_sync(c->ing.cstream);
   c->d_pts = c->ing.d_pts_slot[0];
-  if (rc) drop_staged_batch(c);
+  if (rc) (void)drop_staged_batch(c);
   return rc;
 }
 

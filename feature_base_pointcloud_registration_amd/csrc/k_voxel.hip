@@ -919,6 +919,318 @@ k_voxel_ring(VgRing A) {
 #undef VR_TS_PTR
 }
 
+// ---- the per-ring surf filter, one wave per ring (default order) ----
+// The same filter as k_voxel_ring for the index-order sums, without workgroup barriers: one wave
+// owns a (job, ring).  A ring holds ~1.5k candidates in ~230 runs of equal keys (C2), so the
+// 512-thread kernel above spent most of its cycles in barriers and 3-pass radix sorts of a few
+// hundred keys.  Here: pass A (labels + points: min / max and the candidate count), pass B (keys,
+// compacted in index order into LDS), pass C (run heads: run keys in place, run starts), then a
+// register bitonic sort of the (key << 16 | run id) values (run ids are in index order, so equal
+// keys keep it: the stable order), voxel heads by one lane exchange, and one lane per voxel sums
+// the voxel's points in index order.  Rings with more than 512 runs (none on the synthetic C2 / C3 /
+// C5 scans: at most ~460) rank their runs by counting into the ring's output slot (global scratch)
+// instead.  Output bytes are identical to
+// k_voxel_ring's default mode.
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
+  const uint32_t lo = __shfl_xor((uint32_t)x, m), hi = __shfl_xor((uint32_t)(x >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Ascending bitonic sort of 64 * E distinct u64 values held lane-major (element g = lane * E + e):
+// compare-exchanges inside a lane for distances below E, xor lane exchanges above.
+template <int E>
+__device__ __forceinline__ void wave_bitonic_u64(uint64_t (&v)[E], int lane) {
+  constexpr int N = 64 * E;
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= E) {
+        const int m = j / E;
+        const bool lower = (lane & m) == 0;
+        const bool asc = ((lane * E) & k) == 0;  // k > j >= E: the same for all e of the lane
+        const bool take_min = lower == asc;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const uint64_t o = shfl_xor_u64(v[e], m);
+          v[e] = (take_min ? (o < v[e]) : (v[e] < o)) ? o : v[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          if (e & j) continue;
+          const bool asc = ((lane * E + e) & k) == 0;
+          const uint64_t a = v[e], b = v[e | j];
+          const bool sw = asc ? (b < a) : (a < b);
+          v[e] = sw ? b : a;
+          v[e | j] = sw ? a : b;
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Sorted run ids sid[0, R) and voxel starts vst[0, V] (vst[V] = R) from the register-sorted values.
+template <int E>
+__device__ int vr_sort_runs(const uint32_t* kb, int R, uint16_t* sid, uint16_t* vst, int lane) {
+  uint64_t v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int g = lane * E + e;
+    v[e] = g < R ? (((uint64_t)kb[g] << 16) | (uint64_t)g) : ~0ull;
+  }
+  wave_bitonic_u64<E>(v, lane);
+  const uint32_t lo = __shfl_up((uint32_t)v[E - 1], 1), hi = __shfl_up((uint32_t)(v[E - 1] >> 32), 1);
+  const uint64_t prev_last = ((uint64_t)hi << 32) | lo;
+  bool hd[E];
+  int nh = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int g = lane * E + e;
+    const uint64_t pk = e ? (v[e - 1] >> 16) : (prev_last >> 16);
+    hd[e] = g < R && (g == 0 || (v[e] >> 16) != pk);
+    nh += hd[e] ? 1 : 0;
+  }
+  int inc = nh;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  const int V = __shfl(inc, 63);
+  int vi = inc - nh;
+  wave_lds_sync();  // every lane read its kb values (sid overwrites them)
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int g = lane * E + e;
+    if (g < R) sid[g] = (uint16_t)(v[e] & 0xFFFFull);
+    if (hd[e]) vst[vi++] = (uint16_t)g;
+  }
+  if (lane == 0) vst[V] = (uint16_t)R;
+  wave_lds_sync();
+  return V;
+}
+
+// More than 512 runs: rank by counting (stable by run id), the sorted values staged in the ring's
+// output slot (global; it is written by the emit only after this).
+__device__ int vr_sort_runs_count(const uint32_t* kb, int R, uint16_t* sid, uint16_t* vst, uint64_t* scr, int lane) {
+  for (int r = lane; r < R; r += 64) {
+    const uint32_t key = kb[r];
+    int rank = 0;
+    for (int j = 0; j < R; ++j) {
+      const uint32_t kj = kb[j];
+      rank += (kj < key || (kj == key && j < r)) ? 1 : 0;
+    }
+    scr[rank] = ((uint64_t)key << 16) | (uint64_t)r;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  int V = 0;
+  for (int g0 = 0; g0 < R; g0 += 64) {
+    const int g = g0 + lane;
+    const uint64_t x = g < R ? scr[g] : ~0ull;
+    const uint64_t px = (g > 0 && g < R) ? scr[g - 1] : ~0ull;
+    const bool hd = g < R && (g == 0 || (x >> 16) != (px >> 16));
+    const uint64_t b = __ballot(hd);
+    wave_lds_sync();  // (sid may alias kb entries read above: all reads of kb are done)
+    if (g < R) sid[g] = (uint16_t)(x & 0xFFFFull);
+    if (hd) vst[V + __popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)g;
+    V += __popcll(b);
+  }
+  if (lane == 0) vst[V] = (uint16_t)R;
+  wave_lds_sync();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // scratch reads done before the emit's stores
+  return V;
+}
+
+__global__ void __launch_bounds__(64) k_voxel_ring_wave(VgRing A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int slot = blockIdx.x, job = slot / A.H;
+  const int s = A.start_ring[slot], e = A.end_ring[slot];
+  float4* out = A.out + (int64_t)slot * A.stride_out;
+  if (e <= s) {
+    if (lane == 0) A.cnt_out[slot] = 0;
+    return;
+  }
+  int sp6[6], ep6[6];
+  bool all6 = true;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    sp6[j] = (s * (6 - j) + e * j) / 6;
+    ep6[j] = (s * (5 - j) + e * (j + 1)) / 6 - 1;
+    all6 = all6 && sp6[j] < ep6[j];
+  }
+  // candidates: the ring's non-empty segments [sp, ep] (:195-200) with cloudLabel <= 0, which lie
+  // in [s, e - 1] (segment j ends at sp_{j+1} - 1, segment 5 at e - 1)
+  auto in_seg = [&](int k) {
+    if (all6) return k <= ep6[5];
+    bool in = false;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) in |= sp6[j] < ep6[j] && k >= sp6[j] && k <= ep6[j];
+    return in;
+  };
+  const float4* CL = A.cloud + (int64_t)job * A.HW + s;
+  const int8_t* LB = A.label + (int64_t)job * A.HW + s;
+  const int len = min(e - s, (int)A.cap);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  // ---- pass A: min / max of the candidates and their count.  Steps go in groups of kG with
+  // every label and point load of the group issued before the first use (one memory round trip
+  // per group, not per step: a lone wave has no other waves of its ring to hide latency behind) ----
+  constexpr int kG = 8;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  int n = 0;
+  for (int i0 = 0; i0 < len; i0 += 64 * kG) {
+    int8_t lab[kG];
+    float4 pt[kG];
+#pragma unroll
+    for (int u = 0; u < kG; ++u) {
+      const int i = i0 + 64 * u + lane;
+      const bool ok = i < len;
+      lab[u] = ok ? LB[i] : (int8_t)1;
+      pt[u] = ok ? CL[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kG; ++u) {
+      const int i = i0 + 64 * u + lane;
+      const bool cd = i < len && lab[u] <= 0 && in_seg(s + i);
+      if (cd) {
+        const float v[3] = {pt[u].x, pt[u].y, pt[u].z};
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
+          mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
+        }
+      }
+      n += __popcll(__ballot(cd));
+    }
+  }
+  if (n == 0) {
+    if (lane == 0) A.cnt_out[slot] = 0;
+    return;
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+    for (int o = 32; o > 0; o >>= 1) {
+      const float a = __shfl_xor(mn[d], o), b = __shfl_xor(mx[d], o);
+      mn[d] = (a < mn[d]) ? a : mn[d];
+      mx[d] = (mx[d] < b) ? b : mx[d];
+    }
+  VgGrid G;
+  G.init(mn, mx, A.leaf, false);
+  const int cap = (int)A.cap;
+  uint32_t* kb = (uint32_t*)smem;           // [cap + 1] candidate keys, then run keys; then sid / vst (u16)
+  uint16_t* off = (uint16_t*)(kb + cap + 1);  // [cap] ring offset of the t-th candidate
+  uint16_t* rst = off + cap;                // [cap + 1] first candidate of each run
+  // ---- pass B: keys in index order (or, on PCL's overflow, the candidates themselves) ----
+  int base = 0;
+  for (int i0 = 0; i0 < len; i0 += 64 * kG) {
+    int8_t lab[kG];
+    float4 pt[kG];
+#pragma unroll
+    for (int u = 0; u < kG; ++u) {
+      const int i = i0 + 64 * u + lane;
+      const bool ok = i < len;
+      lab[u] = ok ? LB[i] : (int8_t)1;
+      pt[u] = ok ? CL[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kG; ++u) {
+      const int i = i0 + 64 * u + lane;
+      const bool cd = i < len && lab[u] <= 0 && in_seg(s + i);
+      const uint64_t b = __ballot(cd);
+      const int pos = base + __popcll(b & lt);
+      if (cd) {
+        if (G.overflow) {
+          out[pos] = pt[u];  // PCL: "Leaf size is too small" -> output = input, in index order
+        } else {
+          kb[pos] = G.key(pt[u]);
+          off[pos] = (uint16_t)i;
+        }
+      }
+      base += __popcll(b);
+    }
+  }
+  if (G.overflow) {
+    if (lane == 0) A.cnt_out[slot] = n;
+    return;
+  }
+  wave_lds_sync();
+  // ---- pass C: runs of equal keys in index order (run r's key goes to kb[r] <= its head t: a
+  // later step never reads an overwritten key, and r == t rewrites the same value) ----
+  int R = 0;
+  for (int t0 = 0; t0 < n; t0 += 64) {
+    const int t = t0 + lane;
+    const bool valid = t < n;
+    const uint32_t key = valid ? kb[t] : 0u;
+    const uint32_t prev = (valid && t > 0) ? kb[t - 1] : 0u;
+    const bool head = valid && (t == 0 || key != prev);
+    const uint64_t hb = __ballot(head);
+    wave_lds_sync();
+    if (head) {
+      const int r = R + __popcll(hb & lt);
+      kb[r] = key;
+      rst[r] = (uint16_t)t;
+    }
+    R += __popcll(hb);
+    wave_lds_sync();
+  }
+  if (lane == 0) rst[R] = (uint16_t)n;
+  wave_lds_sync();
+  // ---- sort the runs (stable by run id), voxel starts ----
+  uint16_t* sid = (uint16_t*)kb;  // [R]
+  uint16_t* vst = sid + cap + 1;  // [V + 1]
+  int V;
+  if (R <= 256) V = vr_sort_runs<4>(kb, R, sid, vst, lane);
+  else if (R <= 512) V = vr_sort_runs<8>(kb, R, sid, vst, lane);
+  else V = vr_sort_runs_count(kb, R, sid, vst, reinterpret_cast<uint64_t*>(out), lane);
+  // ---- one lane per voxel: the float sum of its points in index order (runs in id order) ----
+  for (int vv = lane; vv < V; vv += 64) {
+    const int g0 = vst[vv], g1 = vst[vv + 1];
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    int cnt = 0;
+    for (int g = g0; g < g1; ++g) {
+      const int rid = sid[g];
+      const int t0 = rst[rid], t1 = rst[rid + 1];
+      for (int t = t0; t < t1; t += 8) {  // a run's points, 8 gathers in flight
+        float4 pp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pp[u] = CL[off[min(t + u, t1 - 1)]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (t + u < t1) {
+            if (cnt == 0) {
+              c = pp[u];
+            } else {
+              c.x += pp[u].x;
+              c.y += pp[u].y;
+              c.z += pp[u].z;
+              c.w += pp[u].w;
+            }
+            ++cnt;
+          }
+      }
+    }
+    const float fc = (float)cnt;
+    out[vv] = make_float4(c.x / fc, c.y / fc, c.z / fc, c.w / fc);
+  }
+  if (lane == 0) A.cnt_out[slot] = V;
+}
+
+// The wave-per-ring filter for the default order (FBR_VR_WAVE=0: the 512-thread kernel).
+bool vr_wave() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_VR_WAVE");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 size_t voxel_ring_lds_bytes(const VgRing& a, int threads, int kpt) {
   const int nw = threads / 64;
   size_t b = sizeof(uint32_t) * ((size_t)(nw + 1) * 256 + nw) + sizeof(float) * nw * 6 + sizeof(int) * kpt * nw;
@@ -941,8 +1253,14 @@ void launch_voxel_ring(hipStream_t s, const VgRing& a) {
     else
       fbr_launch((k_voxel_ring<512, 8, E>), dim3(nseg), dim3(512), voxel_ring_lds_bytes(a, 512, 8), s, a);
   };
-  if (a.exact) go(std::true_type{});
-  else go(std::false_type{});
+  if (a.exact) {
+    go(std::true_type{});
+  } else if (vr_wave() && a.dbg == 0 && a.cap <= 4096) {
+    const size_t lds = (((size_t)a.cap + 1) * 4 + (size_t)a.cap * 2 + ((size_t)a.cap + 1) * 2 + 15) & ~(size_t)15;
+    fbr_launch(k_voxel_ring_wave, dim3(nseg), dim3(64), lds, s, a);
+  } else {
+    go(std::false_type{});
+  }
 }
 
 // PCL's point order inside voxels (FBR_VG_EXACT=1): bit-identical centroids, hence poses, at

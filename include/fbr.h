@@ -348,20 +348,35 @@ int fbr_debug_counters(long long* launches, long long* host_syncs, long long* fl
 
 /* Device-resident batch (throughput measurement): stage copies the scans and guesses to HBM (and
  * computes the per-job CropBox map statistics, which depend only on the guesses); launch enqueues
- * the whole path for the staged batch on the ctx stream (asynchronous, inputs are not modified so
- * it may be re-launched); wait blocks; results copies poses/stats out.  The single-scan entry
- * points (fbr_project, fbr_register*, fbr_process_scan) share the device buffers and drop a staged
- * batch: fbr_batch_launch then returns FBR_ERR_STATE until the next fbr_batch_stage. */
+ * the whole path for the staged batch (asynchronous, inputs are not modified so it may be
+ * re-launched); wait blocks; results copies the latest launch's poses/stats out.
+ * Launches are pipelined two deep (unless FBR_PIPE=0 or max_batch = 1): consecutive launches use
+ * alternate work buffers and streams, and fbr_batch_launch returns once the *previous* launch is
+ * fully enqueued, leaving the tail of its own Gauss-Newton loop (whose length the device decides)
+ * to the next launch / flush / wait call.  So launch n's projection and features run beside launch
+ * n-1's last iterations.  The single-scan entry points (fbr_project, fbr_register*,
+ * fbr_process_scan) share the device buffers and drop a staged batch (after enqueueing every
+ * launch in flight): fbr_batch_launch then returns FBR_ERR_STATE until the next fbr_batch_stage. */
 int fbr_batch_stage(fbr_ctx* ctx, const fbr_point_xyzirt* const* scans, const int64_t* n_in,
                     int n_jobs, const float* poses_in /* [n_jobs][6] */);
 int fbr_batch_launch(fbr_ctx* ctx);
+/* Enqueue the rest of every launch in flight (host side only; no device synchronisation). */
+int fbr_batch_flush(fbr_ctx* ctx);
 int fbr_batch_wait(fbr_ctx* ctx);
 int fbr_batch_results(fbr_ctx* ctx, float* poses_out /* [n_jobs][6] */,
                       fbr_reg_stats* stats /* [n_jobs] or NULL */);
-/* Enqueue (on the ctx stream, after the launched batch) a copy of the per-job pose records
- * {pose[6] f32, iterations i32, status i32} = 32 B/job into `device_dst` (device memory of the
- * ctx's device, [n_jobs][8] x 4 B) — the payload of the cross-GPU pose all-gather. */
+/* Enqueue (on the ctx stream, after every launch in flight) a copy of the latest launch's per-job
+ * pose records {pose[6] f32, iterations i32, status i32} = 32 B/job into `device_dst` (device
+ * memory of the ctx's device, [n_jobs][8] x 4 B) — the payload of the cross-GPU pose all-gather. */
 int fbr_batch_export(fbr_ctx* ctx, void* device_dst);
+/* Pipelined form: export the records of the latest launch that is fully enqueued and not yet
+ * exported (after fbr_batch_launch n: launch n-1; after fbr_batch_flush: the latest), without
+ * waiting for the launch in flight.  The copy runs on that launch's stream after it, and after the
+ * work queued so far on `wait_stream` (a HIP stream of the caller still reading device_dst, or
+ * NULL); *export_stream receives the stream to wait on before reading device_dst, *launch_id the
+ * launch number (0, 1, ... since the context was created), or -1 (nothing to export: no copy). */
+int fbr_batch_export_ready(fbr_ctx* ctx, void* device_dst, void* wait_stream, void** export_stream,
+                           int64_t* launch_id);
 /* Sum of the per-scan algorithmic byte counts of the last completed batch (roofline input). */
 int fbr_batch_bytes(fbr_ctx* ctx, double* bytes_total, double* bytes_gn);
 

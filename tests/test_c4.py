@@ -77,3 +77,58 @@ def test_c4_strong_split_world8_matches_world1(tmp_path):
     assert np.array_equal(rec1.view(np.int32), rec8.view(np.int32))
     _, iters, status = shard.decode_records(rec1)
     assert (status == 0).all() and (iters > 0).all()
+
+
+_PIPE_CHILD = r"""
+import sys, json
+import numpy as np
+import torch  # torch's HIP runtime first: the library shares it (bench.py does the same)
+torch.cuda.init()
+sys.path.insert(0, %(repo)r)
+from feature_base_pointcloud_registration_amd import api, shard, synth
+from feature_base_pointcloud_registration_amd.fbr_types import default_params
+H, W = synth.CONFIGS["C2"][:2]
+B = 24
+P = default_params(H, W, max_batch=B)
+jobs = synth.make_jobs("C2", B, base_seed=6000)
+buf = torch.zeros((4, B * shard.RECORD_FLOATS), dtype=torch.float32, device="cuda:0")
+with api.Context(P) as ctx:
+    ctx.set_map(*synth.config_map("C2"))
+    ctx.batch_stage([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
+    ctx.batch_launch()
+    ctx.batch_wait()
+    p0, s0 = ctx.batch_results()
+    ids = []
+    for k in range(3):
+        ctx.batch_launch()
+        ids.append(ctx.batch_export_ready(buf[k].data_ptr())[0])
+    ctx.batch_flush()
+    ids.append(ctx.batch_export_ready(buf[3].data_ptr())[0])
+    again = ctx.batch_export_ready(buf[3].data_ptr())[0]
+    ctx.batch_wait()
+    p1, s1 = ctx.batch_results()
+torch.cuda.synchronize()
+rec0 = shard.encode_records(p0, s0["iterations"], s0["status"])
+print(json.dumps({"ids": ids, "again": again,
+                  "same_results": bool(np.array_equal(p0.view(np.int32), p1.view(np.int32)) and np.array_equal(s0, s1)),
+                  "exports_equal": [bool(np.array_equal(buf[k].cpu().numpy().view(np.int32), rec0.view(np.int32))) for k in range(4)],
+                  "status_ok": int((s0["status"] == 0).sum())}))
+"""
+
+
+def test_pipelined_launches_are_bit_identical_and_export_in_order():
+    """Consecutive fbr_batch_launch calls run two deep (alternate work slots and streams; a launch
+    returns once the previous one is fully enqueued).  Every launch of the same staged batch gives
+    the same bytes, and fbr_batch_export_ready hands out the launches' records in launch order.
+    (Child process: torch, which allocates the export buffers, must initialise HIP first.)"""
+    import json
+    import subprocess
+    import sys
+    from conftest import REPO
+    r = subprocess.run([sys.executable, "-c", _PIPE_CHILD % {"repo": REPO}], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    # after launch n returns, launch n-1 is the latest fully enqueued one (launch 0 was waited for)
+    assert d["ids"] == [0, 1, 2, 3] and d["again"] == -1, d
+    assert d["same_results"] and d["exports_equal"] == [True] * 4 and d["status_ok"] == 24, d

@@ -633,6 +633,74 @@ def test_exact_voxel_grid_is_bit_identical_to_oracle():
     assert r.stdout == b"".join(O.voxel_grid(p, 0.4).tobytes() for p in clouds.values())
 
 
+def _adversarial_ring_scan(H, W, seed):
+    """A scan whose rings span the per-ring filter's sort paths: smooth walls (few long runs), rings
+    of random ranges (every candidate its own voxel: > 512 runs), half-random rings and near-empty
+    rings."""
+    rng = np.random.default_rng(seed)
+    pts = []
+    for r in range(H):
+        el = np.deg2rad(-15.0 + 30.0 * r / max(H - 1, 1))
+        az = np.deg2rad(np.arange(W) * 360.0 / W + rng.uniform(-0.01, 0.01, W))
+        kind = r % 4
+        if kind == 0:
+            rr = 12.0 + 0.5 * np.sin(az * 3)
+        elif kind == 1:
+            rr = rng.uniform(3.0, 60.0, W)
+        elif kind == 2:
+            rr = np.where(np.arange(W) % 2 == 0, rng.uniform(3.0, 60.0, W), 20.0)
+        else:
+            rr = np.where(rng.random(W) < 0.01, 15.0, 0.5)  # mostly below the 1 m range gate
+        p = np.zeros(W, POINT_XYZIRT)
+        p["x"] = rr * np.cos(el) * np.cos(az)
+        p["y"] = rr * np.cos(el) * np.sin(az)
+        p["z"] = rr * np.sin(el)
+        p["intensity"] = rng.uniform(0, 255, W)
+        p["ring"] = r
+        p["time"] = np.arange(W) / W * 0.1
+        pts.append(p)
+    return np.concatenate(pts)
+
+
+def test_wave_ring_filter_is_bit_identical_to_workgroup_kernel():
+    """The one-wave-per-ring surf VoxelGrid (k_voxel_ring_wave, register bitonic / counting-rank run
+    sorts) against the 512-thread kernel (FBR_VR_WAVE=0, child process): identical surf clouds,
+    labels and corners on C1 / C2 / C3 scans and on adversarial rings (every candidate its own
+    voxel), and within SURF_ULPS of the oracle."""
+    import subprocess
+    import sys
+    cases = [("C1", synth.scan(synth.job(1)[0], 16, 1800, seed=1)),
+             ("C2", synth.make_jobs("C2", 1, base_seed=77)[0][0]),
+             ("C3", synth.make_jobs("C3", 1, base_seed=78)[0][0]),
+             ("C1", _adversarial_ring_scan(16, 1800, 5))]
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_vr_wave_in.npz")
+    np.savez(path, *[c[1] for c in cases])
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api, synth; "
+            "d = np.load(%r); out = []\n"
+            "for k, cfg in enumerate(%r):\n"
+            "    c = api.Context(synth.config_params(cfg)); f = c.features(d['arr_%%d' %% k]); c.close()\n"
+            "    out += [f['label'].tobytes(), f['corner'].tobytes(), f['surf'].tobytes()]\n"
+            "sys.stdout.buffer.write(b''.join(len(x).to_bytes(8, 'little') + x for x in out))"
+            % (REPO, path, [c[0] for c in cases]))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, FBR_VR_WAVE="0"),
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    blob, ref = r.stdout, []
+    while blob:
+        n = int.from_bytes(blob[:8], "little")
+        ref.append(blob[8:8 + n])
+        blob = blob[8 + n:]
+    for k, (cfg, pts) in enumerate(cases):
+        P = synth.config_params(cfg)
+        with api.Context(P) as ctx:
+            fg = ctx.features(pts)
+        assert fg["label"].tobytes() == ref[3 * k], (k, cfg)
+        assert fg["corner"].tobytes() == ref[3 * k + 1], (k, cfg)
+        assert fg["surf"].tobytes() == ref[3 * k + 2], (k, cfg, len(fg["surf"]), len(ref[3 * k + 2]) // 16)
+        fo = O.Stream(P).features(pts)
+        assert_features_equal(fo, fg)
+
+
 @pytest.mark.parametrize("env,sparse", [
     ({"FBR_KNN_CELL": "0.5"}, False),                          # R = 2 rows, the C3 / C5 cells
     ({"FBR_KNN_CELL": "0.5", "FBR_GRID_SPARSE": "1"}, True),   # the same over hashed chunks
