@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = [
     "fbr_register", "fbr_register_trace", "fbr_process_scan", "fbr_reset_stream",
     "fbr_process_batch", "fbr_ingest_bytes", "fbr_debug_counters", "fbr_map_grid_info", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
     "fbr_batch_flush", "fbr_batch_export_ready", "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
-    "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math", "fbr_selftest_eigen6", "fbr_selftest_eig_certified", "fbr_selftest_voxel_order",
+    "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math", "fbr_selftest_eigen6", "fbr_selftest_eig_certified", "fbr_selftest_voxel_order", "fbr_selftest_radix_sort",
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
     "fbr_msg_to_points", "fbr_points_to_msg_data", "fbr_project_msg", "fbr_process_msg",
     "fbr_imu_convert", "fbr_imu_deskew_info", "fbr_set_deskew", "fbr_stream_copy_bandwidth",
@@ -97,6 +97,7 @@ def lib():
             "fbr_selftest_eigen6": (ctypes.c_int, [ctypes.c_int, _VP, _VP]),
             "fbr_selftest_eig_certified": (ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_float, _VP]),
             "fbr_selftest_voxel_order": (ctypes.c_int, [_I64, _VP, ctypes.c_int, _VP]),
+            "fbr_selftest_radix_sort": (ctypes.c_int, [_I64, ctypes.c_int, ctypes.c_int, _VP, _VP]),
             "fbr_load_map": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_char_p]),
             "fbr_pcd_read": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64, _VP]),
             "fbr_pcd_write_ascii": (ctypes.c_int, [ctypes.c_char_p, _VP, _I64]),
@@ -201,6 +202,15 @@ def selftest_voxel_order(keys, lds=False):
     perm = np.zeros(len(k), np.uint32)
     _check(lib().fbr_selftest_voxel_order(len(k), ptr(k), int(lds), ptr(perm)), "fbr_selftest_voxel_order")
     return perm[np.argsort(k[perm], kind="stable")].astype(np.int64)
+
+
+def selftest_radix_sort(keys, nbits, variant):
+    """One of the VoxelGrid kernels' radix sorts on the device (fbr_selftest_radix_sort): (sorted
+    keys, source index of every sorted position)."""
+    k = np.ascontiguousarray(keys, np.uint32).copy()
+    perm = np.zeros(len(k), np.uint32)
+    _check(lib().fbr_selftest_radix_sort(len(k), int(nbits), int(variant), ptr(k), ptr(perm)), "fbr_selftest_radix_sort")
+    return k, perm.astype(np.int64)
 
 
 def stream_copy_bandwidth(device=0, nbytes=2 << 30, iters=20):

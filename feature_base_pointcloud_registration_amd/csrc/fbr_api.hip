@@ -132,9 +132,8 @@ struct fbr_ctx {
   hipStream_t stream = nullptr;   // primary stream (single-scan calls, batch sub-batch 0, export)
   hipStream_t xstream[kMaxSub] = {};  // extra streams of batch sub-batches 1.. (index 0 unused)
   hipEvent_t xev[kMaxSub] = {};       // fork / join events
-  int nsub_pref = 3;                  // sub-batches per batch launch (FBR_NSUB overrides; at B = 128: 2 -> 76.1k,
-                                      // 3 -> 78.5k, 4 -> 46.7k scans/s: 4 sub-batch streams plus the
-                                      // primary exceed the 4 hardware queues HIP gives a process)
+  int nsub_pref = 3;                  // sub-batches per batch launch (FBR_NSUB overrides): 3 unpipelined (at
+                                      // B = 128: 2 -> 76.1k, 3 -> 78.5k, 4 -> 46.7k scans/s), 1 pipelined
   int H = 0, W = 0, Bcap = 0;
   // Batch launches alternate between nslot work slots (2 unless FBR_PIPE=0 or max_batch = 1): the
   // next launch's projection / features overlap the previous one's Gauss-Newton tail.  Work arrays
@@ -1160,7 +1159,10 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
     return e ? std::atoi(e) != 0 : true;
   }();
   c->nslot = (pipe && p->max_batch > 1) ? 2 : 1;
-  if (c->nslot == 2) c->nsub_pref = std::min(c->nsub_pref, kMaxSub / 2);
+  // Pipelined, one sub-batch per launch is best at every batch size (the two launches in flight
+  // overlap as the sub-batches did): B = 128 / 256 / 1024 give 91.8k / 96.7k / 97.4k scans/s
+  // against 83.2k / 93.1k / 96.7k with 3 sub-batches (profiles/r04f_pipe_nsub_sweep.txt).
+  if (c->nslot == 2) c->nsub_pref = std::getenv("FBR_NSUB") ? std::min(c->nsub_pref, kMaxSub / 2) : 1;
   c->Bwork = (int64_t)c->nslot * c->Bcap;
   const int64_t B = c->Bcap, Bw = c->Bwork, HW = c->HW, H = c->H;
   // streams of the sub-batches this context can use, per slot (each stream takes a hardware queue:

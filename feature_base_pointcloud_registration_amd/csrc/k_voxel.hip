@@ -288,7 +288,9 @@ __device__ int vg_radix_sort(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, 
 // 8-bit digits (hist holds (NW + 1) * 256 counters).  Ends with a barrier.  Always inlined: with
 // two callers (the exact and default kernels) the compiler outlined it, and the call frame put
 // 80 B per lane in scratch (spilled on every call: ~50 MB of writes per B = 1024 launch).
-template <int T, int KPL>
+// kLeader (diagnostic, fbr_selftest_radix_sort only): per-wave digit counts by the lowest lane of
+// each digit's ballot peer group instead of LDS atomics (round 3's variant).
+template <int T, int KPL, bool kLeader = false>
 __device__ __attribute__((always_inline)) void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint16_t* vals, int n, int nbits,
                                       uint32_t* hist, uint32_t* wsum) {
   constexpr int NW = T / 64, NB = 256, PER = NB * NW / T;
@@ -310,9 +312,24 @@ __device__ __attribute__((always_inline)) void vg_radix_sort_inplace(FBR_LDS_AS 
     }
     for (int b = tid; b < tot; b += T) hist[(b % NW) * NB + b / NW] = 0u;
     __syncthreads();  // every wave holds its chunk: the scatter below may overwrite any position
+    if constexpr (kLeader) {
 #pragma unroll
-    for (int k = 0; k < KPL; ++k)
-      if (c0 + 64 * k + lane < c1) atomicAdd(&hist[w * NB + ((kr[k] >> shift) & dmask)], 1u);
+      for (int k = 0; k < KPL; ++k) {
+        const bool valid = c0 + 64 * k + lane < c1;
+        const uint32_t d = (kr[k] >> shift) & dmask;
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < dbits; ++b) {
+          const uint64_t bal = __ballot((d >> b) & 1u);
+          peers &= ((d >> b) & 1u) ? bal : ~bal;
+        }
+        if (valid && (peers & ((1ull << lane) - 1ull)) == 0ull) hist[w * NB + d] += (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < KPL; ++k)
+        if (c0 + 64 * k + lane < c1) atomicAdd(&hist[w * NB + ((kr[k] >> shift) & dmask)], 1u);
+    }
     __syncthreads();
     {
       uint32_t v[PER], loc = 0;
@@ -1222,11 +1239,13 @@ __global__ void __launch_bounds__(64) k_voxel_ring_wave(VgRing A) {
   if (lane == 0) A.cnt_out[slot] = V;
 }
 
-// The wave-per-ring filter for the default order (FBR_VR_WAVE=0: the 512-thread kernel).
+// The wave-per-ring filter for the default order (FBR_VR_WAVE=1; default: the 512-thread kernel,
+// which measured faster: 407 vs 481 us per sequential 256-job launch, 97.4k vs 95.2k scans/s at
+// B = 1024, profiles/r04e_voxel_ring_wave_ab.txt, r04f_pipe_nsub_sweep.txt).
 bool vr_wave() {
   static const bool v = [] {
     const char* e = std::getenv("FBR_VR_WAVE");
-    return e ? std::atoi(e) != 0 : true;
+    return e ? std::atoi(e) != 0 : false;
   }();
   return v;
 }
@@ -1404,6 +1423,114 @@ void launch_concat(hipStream_t s, int B, int H, int W, const float4* corner_slot
                      surf_ring_cnt, corner_all, capc, n_corner, surf_all, caps, n_surf, ring_box);
 }
 
+
+// ---- radix sort selftests (fbr_selftest_radix_sort): one workgroup sorts one array with the
+// product's configurations of the wave-chunk sorts ----
+// variant 0: vg_radix_sort<512, u16, 8, LDS> (per-ring filter), 1: vg_radix_sort<256, u16, 9, LDS>
+// (per-segment LDS kernel), 2: vg_radix_sort<1024, u32, 9, global> (global-scratch kernel),
+// 3: vg_radix_sort_inplace<1024, 18> (mapping DS), 4: the same with ballot-leader digit counts.
+template <int T, typename V, int MAXD, bool KV_LDS>
+__global__ void __launch_bounds__(T) k_selftest_radix(uint32_t* keys, uint32_t* vals, uint32_t* scratch, int n, int nbits) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NW = T / 64;
+  uint32_t* hist = (uint32_t*)smem;
+  uint32_t* wsum = hist + (NW + 1) * 512;
+  unsigned char* q = (unsigned char*)(wsum + NW);
+  q = smem + (((q - smem) + 15) & ~15);
+  uint32_t* kb[2];
+  V* vb[2];
+  if constexpr (KV_LDS) {
+    kb[0] = (uint32_t*)q;
+    kb[1] = kb[0] + n;
+    vb[0] = (V*)(kb[1] + n);
+    vb[1] = vb[0] + n;
+  } else {
+    kb[0] = scratch;
+    kb[1] = scratch + n;
+    vb[0] = (V*)(scratch + 2 * n);
+    vb[1] = (V*)(scratch + 3 * n);
+  }
+  for (int i = threadIdx.x; i < n; i += T) {
+    kb[0][i] = keys[i];
+    vb[0][i] = (V)i;
+  }
+  __syncthreads();
+  const int cur = vg_radix_sort<T, V, MAXD, KV_LDS>(kb, vb, n, nbits, hist, wsum);
+  for (int i = threadIdx.x; i < n; i += T) {
+    keys[i] = kb[cur][i];
+    vals[i] = (uint32_t)vb[cur][i];
+  }
+}
+
+template <bool kLeader>
+__global__ void __launch_bounds__(1024) k_selftest_radix_ip(uint32_t* keys, uint32_t* vals, int n, int nbits) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NW = 16, LCAP = 1024 * kVgIpKpl;
+  uint32_t* hist = (uint32_t*)smem;
+  uint32_t* wsum = hist + (NW + 1) * 512;
+  unsigned char* q = (unsigned char*)(wsum + NW);
+  q = smem + (((q - smem) + 15) & ~15);
+  FBR_LDS_AS uint32_t* k = (FBR_LDS_AS uint32_t*)q;
+  FBR_LDS_AS uint16_t* v = (FBR_LDS_AS uint16_t*)((FBR_LDS_AS uint32_t*)q + LCAP);
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    k[i] = keys[i];
+    v[i] = (uint16_t)i;
+  }
+  __syncthreads();
+  vg_radix_sort_inplace<1024, kVgIpKpl, kLeader>(k, v, n, nbits, hist, wsum);
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    keys[i] = k[i];
+    vals[i] = v[i];
+  }
+}
+
+}  // namespace fbr
+
+// Diagnostic entry point (tests/test_gpu_parity.py): sort n keys (low nbits significant) with one of
+// the product's radix sort configurations; keys_inout gets the sorted keys, perm the source index of
+// each sorted position.
+extern "C" int fbr_selftest_radix_sort(int64_t n, int nbits, int variant, uint32_t* keys_inout, uint32_t* perm) {
+  using namespace fbr;
+  const int64_t lcap[5] = {4096, 4096, 1 << 20, 1024 * kVgIpKpl, 1024 * kVgIpKpl};
+  if (n < 0 || variant < 0 || variant > 4 || n > lcap[variant] || nbits < 1 || nbits > 32 || (n && (!keys_inout || !perm)))
+    return FBR_ERR_INVALID_ARG;
+  if (n == 0) return FBR_OK;
+  uint32_t *dk = nullptr, *dv = nullptr, *ds = nullptr;
+  int rc = FBR_OK;
+  if (hipMalloc(&dk, 4 * n) != hipSuccess || hipMalloc(&dv, 4 * n) != hipSuccess || hipMalloc(&ds, 16 * n) != hipSuccess ||
+      hipMemcpy(dk, keys_inout, 4 * n, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = FBR_ERR_HIP;
+  } else {
+    const int nn = (int)n;
+    auto hdr = [](int T) { return (((size_t)(T / 64 + 1) * 512 + T / 64) * 4 + 15) & ~(size_t)15; };
+    switch (variant) {
+      case 0:
+        hipLaunchKernelGGL((k_selftest_radix<512, uint16_t, 8, true>), dim3(1), dim3(512), hdr(512) + (size_t)n * 12, 0,
+                           dk, dv, ds, nn, nbits);
+        break;
+      case 1:
+        hipLaunchKernelGGL((k_selftest_radix<256, uint16_t, 9, true>), dim3(1), dim3(256), hdr(256) + (size_t)n * 12, 0,
+                           dk, dv, ds, nn, nbits);
+        break;
+      case 2:
+        hipLaunchKernelGGL((k_selftest_radix<1024, uint32_t, 9, false>), dim3(1), dim3(1024), hdr(1024), 0, dk, dv, ds,
+                           nn, nbits);
+        break;
+      default: {
+        const size_t lds = hdr(1024) + (size_t)1024 * kVgIpKpl * 6;
+        if (variant == 3) hipLaunchKernelGGL(k_selftest_radix_ip<false>, dim3(1), dim3(1024), lds, 0, dk, dv, nn, nbits);
+        else hipLaunchKernelGGL(k_selftest_radix_ip<true>, dim3(1), dim3(1024), lds, 0, dk, dv, nn, nbits);
+      }
+    }
+    if (hipGetLastError() != hipSuccess || hipMemcpy(keys_inout, dk, 4 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(perm, dv, 4 * n, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = FBR_ERR_HIP;
+  }
+  for (void* q : {(void*)dk, (void*)dv, (void*)ds}) (void)hipFree(q);
+  return rc;
+}
+
+namespace fbr {
 
 // ---------------------------------------------------------------------------------------------
 // Device-wide VoxelGrid of one large cloud (the start-up map filter, the keyframe local map,

@@ -414,6 +414,13 @@ int fbr_selftest_eig_certified(int n, const float* a, float thr, int32_t* out);
  * runs the LDS variant of the per-segment kernels (n <= 8192), 2 LDS keys with global-memory
  * positions (the mapping-DS kernel's, n <= 18432), 0 the global-memory one. */
 int fbr_selftest_voxel_order(int64_t n, const uint32_t* keys, int lds, uint32_t* perm);
+/* Diagnostic: the VoxelGrid kernels' stable LSD radix sorts on one array of n keys (the low
+ * `nbits` significant), one workgroup: variant 0 = the per-ring filter's LDS sort (512 threads,
+ * 8-bit digits, n <= 4096), 1 = the per-segment LDS sort (256 threads, 9-bit digits, n <= 4096),
+ * 2 = the global-scratch sort (1024 threads), 3 = the mapping DS's in-place LDS sort (1024 x 18),
+ * 4 = variant 3 with ballot-leader digit counts (round 3's rejected form).  keys_inout receives
+ * the sorted keys, perm the source index of every sorted position. */
+int fbr_selftest_radix_sort(int64_t n, int nbits, int variant, uint32_t* keys_inout, uint32_t* perm);
 
 /* Measurement helper: achievable HBM bandwidth of a device-wide float4 copy of `bytes` (read +
  * write counted), averaged over `iters` launches (the STREAM-copy figure bench.py reports next to

@@ -129,3 +129,44 @@ def test_device_voxel_order_is_std_sort(lds):
     for n in {0: (17, 2049, 18432, 18433), 1: (17, 2049, 8192), 2: (17, 2049, 8192, 18431, 18432)}[lds]:
         keys = rng.integers(0, max(1, n // 6), n).astype(np.uint32)
         assert np.array_equal(api.selftest_voxel_order(keys, lds=lds), O.sort_voxel_pairs(keys)), n
+
+
+def _radix_cases(cap, nw):
+    """Key arrays for a wave-chunk radix sort with nw waves and capacity cap: every chunk fill up to
+    full chunks (steps of 64 per wave), ragged sizes, and key patterns with long equal-digit runs
+    (sorted / spatially ordered / constant / few distinct) next to random ones."""
+    rng = np.random.default_rng(11)
+    sizes = sorted({1, 2, 63, 64, 65, 127, 640, cap // 2 + 3, cap - 65, cap - 1, cap}
+                   | {min(cap, nw * 64 * k) for k in (1, 2, 5, 9, 13, 17, 18) if nw * 64 * k <= cap})
+    for n in sizes:
+        yield n, 24, rng.integers(0, 1 << 24, n)
+        yield n, 24, np.sort(rng.integers(0, 1 << 24, n))                     # long runs in the upper digits
+        yield n, 18, np.repeat(rng.integers(0, 1 << 18, (n + 99) // 100), 100)[:n]  # runs of 100 equal keys
+        yield n, 9, np.full(n, 300)                                           # one key
+        yield n, 30, (np.arange(n) * 2654435761) % (1 << 30)                  # distinct, scattered
+        x, y, z = rng.integers(0, 1024, (3, n))
+        o = np.lexsort((x, y, z))                                             # spatially ordered Morton keys
+        yield n, 30, np.array([_morton(a, b, c) for a, b, c in zip(x[o], y[o], z[o])], np.int64)
+
+
+def _morton(x, y, z):
+    k = 0
+    for b in range(10):
+        k |= ((int(x) >> b) & 1) << (3 * b) | ((int(y) >> b) & 1) << (3 * b + 1) | ((int(z) >> b) & 1) << (3 * b + 2)
+    return k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant,cap,nw", [(0, 4096, 8), (1, 4096, 4), (2, 40000, 16), (3, 18432, 16), (4, 18432, 16)],
+                         ids=["ring-lds-512", "segment-lds-256", "global-1024", "inplace-atomic", "inplace-leader"])
+def test_voxel_radix_sorts_are_stable_sorts(variant, cap, nw):
+    """Every wave-chunk radix sort configuration of k_voxel.hip (fbr_selftest_radix_sort) against a
+    host stable sort, on every chunk fill including full ones and on long equal-digit runs.  Variant
+    4 is round 3's ballot-leader digit count in the in-place sort."""
+    from feature_base_pointcloud_registration_amd import api
+    for n, nbits, keys in _radix_cases(cap, nw):
+        keys = np.asarray(keys, np.uint64).astype(np.uint32) & np.uint32((1 << nbits) - 1 if nbits < 32 else 0xFFFFFFFF)
+        sk, perm = api.selftest_radix_sort(keys, nbits, variant)
+        ref = np.argsort(keys, kind="stable")
+        assert np.array_equal(perm, ref), (variant, n, nbits, int(np.nonzero(perm != ref)[0][0]))
+        assert np.array_equal(sk, keys[ref]), (variant, n, nbits)
