@@ -95,6 +95,10 @@ struct Ingest {
   fbr_point_xyzirt* d_pts_slot[2] = {};  // slot 0 = the context's scan buffer, slot 1 allocated here
   int nthreads = 8;                  // packing threads per chunk
   double h2d_bytes = 0.0;            // bytes copied host -> device by the last fbr_process_batch
+  // Compact records (no deskew tables set: `time` is never read): per scan the rings (u16) and
+  // xyzi (f32 x 4), 18 B per point instead of 24, expanded on the device by k_expand_scans.
+  uint8_t* d_stage = nullptr;        // [Bcap][ingest_region_bytes(NMAX)]
+  bool compact_used = false;         // the last fbr_process_batch used compact records
 };
 
 // A contiguous sub-batch of jobs driven on one stream.  j0 is the first job of the sub-batch's
@@ -1258,6 +1262,7 @@ int fbr_destroy(fbr_ctx* c) {
   if (c->ing.cstream) (void)fbr_sync(c->ing.cstream);
   if (c->ing.h_stage) (void)hipHostFree(c->ing.h_stage);
   if (c->ing.d_pts_slot[1]) (void)hipFree(c->ing.d_pts_slot[1]);
+  if (c->ing.d_stage) (void)hipFree(c->ing.d_stage);
   for (auto& e : c->ing.up_ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ing.chunk_ev)
@@ -1666,12 +1671,13 @@ int fbr_batch_export_ready(fbr_ctx* c, void* device_dst, void* wait_stream, void
   *launch_id = -1;
   if (c->staged_B <= 0) return FBR_ERR_STATE;
   CK(hipSetDevice(c->dev));
-  int s = -1;  // the latest launch that is fully enqueued and not yet exported
+  // the oldest launch not yet exported, if it is fully enqueued: launches are exported in order
+  // (one call per fbr_batch_launch never falls behind: launch n returns with n-1 enqueued)
+  int s = -1;
   for (int q = 0; q < c->nslot; ++q)
-    if (c->slot_launch[q] > c->exported && !c->run[q].pending && c->run[q].nsub > 0 &&
-        (s < 0 || c->slot_launch[q] > c->slot_launch[s]))
+    if (c->slot_launch[q] > c->exported && c->run[q].nsub > 0 && (s < 0 || c->slot_launch[q] < c->slot_launch[s]))
       s = q;
-  if (s < 0) return FBR_OK;
+  if (s < 0 || c->run[s].pending) return FBR_OK;
   const GnRun& r = c->run[s];
   hipStream_t st = r.subs[0].st;
   for (int k = 1; k < r.nsub; ++k) CK(hipStreamWaitEvent(st, c->xev[r.subs[k].k], 0));
@@ -1720,7 +1726,17 @@ int ingest_init(fbr_ctx* c) {
   CK(hipHostMalloc((void**)&g.h_stage, (size_t)g.chunk_bytes * Ingest::kChunks, hipHostMallocDefault));
   g.d_pts_slot[0] = c->d_pts;
   if (dalloc(&g.d_pts_slot[1], (int64_t)c->Bcap * c->NMAX)) return FBR_ERR_HIP;
+  if (dalloc(&g.d_stage, (int64_t)c->Bcap * ingest_region_bytes(c->NMAX))) return FBR_ERR_HIP;
   return FBR_OK;
+}
+
+// FBR_INGEST_COMPACT=0: always ship the 24-B records.
+bool ingest_compact_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_INGEST_COMPACT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
 }
 
 // Upload B scans into input slot `slot`: pack them into free pinned chunks (host threads), queue
@@ -1730,6 +1746,11 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
   CK(hipSetDevice(c->dev));
   Ingest& g = c->ing;
   fbr_point_xyzirt* dst = g.d_pts_slot[slot];
+  // compact records unless a deskew table may read the per-point time (deskewPoint, :545-580)
+  const bool compact = ingest_compact_enabled() && !c->desk_any;
+  g.compact_used = compact;
+  const int64_t ring_bytes = (2 * c->NMAX + 15) & ~(int64_t)15, region = ingest_region_bytes(c->NMAX);
+  auto host_bytes = [&](int64_t n) { return compact ? ring_bytes + 16 * n : n * (int64_t)sizeof(fbr_point_xyzirt); };
   std::vector<int64_t> off;
   for (int j = 0; j < B;) {
     const int k = g.next_chunk;
@@ -1739,30 +1760,52 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
     int j1 = j;
     int64_t used = 0;
     off.clear();
-    while (j1 < B && used + n_in[j1] * (int64_t)sizeof(fbr_point_xyzirt) <= g.chunk_bytes) {
+    while (j1 < B && used + host_bytes(n_in[j1]) <= g.chunk_bytes) {
       off.push_back(used);
-      used += n_in[j1] * (int64_t)sizeof(fbr_point_xyzirt);
+      used += (host_bytes(n_in[j1]) + 15) & ~(int64_t)15;
       ++j1;
     }
     if (j1 == j) return FBR_ERR_CAPACITY;  // (chunk_bytes >= NMAX * 24: not reached)
     const int nt = std::max(1, std::min(g.nthreads, j1 - j));
     auto pack = [&](int t) {
-      for (int jj = j + t; jj < j1; jj += nt)
-        if (n_in[jj]) std::memcpy(base + off[jj - j], scans[jj], n_in[jj] * sizeof(fbr_point_xyzirt));
+      for (int jj = j + t; jj < j1; jj += nt) {
+        const int64_t n = n_in[jj];
+        if (!n) continue;
+        if (!compact) {
+          std::memcpy(base + off[jj - j], scans[jj], n * sizeof(fbr_point_xyzirt));
+          continue;
+        }
+        const fbr_point_xyzirt* src = scans[jj];
+        uint16_t* rr = reinterpret_cast<uint16_t*>(base + off[jj - j]);
+        float* xyzi = reinterpret_cast<float*>(base + off[jj - j] + ring_bytes);
+        for (int64_t i = 0; i < n; ++i) {
+          rr[i] = src[i].ring;
+          xyzi[4 * i] = src[i].x;
+          xyzi[4 * i + 1] = src[i].y;
+          xyzi[4 * i + 2] = src[i].z;
+          xyzi[4 * i + 3] = src[i].intensity;
+        }
+      }
     };
     std::vector<std::thread> th;
     for (int t = 1; t < nt; ++t) th.emplace_back(pack, t);
     pack(0);
     for (auto& x : th) x.join();
     for (int jj = j; jj < j1; ++jj)
-      if (n_in[jj])
-        CK(hipMemcpyAsync(dst + (int64_t)jj * c->NMAX, base + off[jj - j], n_in[jj] * sizeof(fbr_point_xyzirt),
-                          hipMemcpyHostToDevice, g.cstream));
+      if (n_in[jj]) {
+        if (compact)
+          CK(hipMemcpyAsync(g.d_stage + (int64_t)jj * region, base + off[jj - j], host_bytes(n_in[jj]),
+                            hipMemcpyHostToDevice, g.cstream));
+        else
+          CK(hipMemcpyAsync(dst + (int64_t)jj * c->NMAX, base + off[jj - j], n_in[jj] * sizeof(fbr_point_xyzirt),
+                            hipMemcpyHostToDevice, g.cstream));
+      }
     CK(hipEventRecord(g.chunk_ev[k], g.cstream));
     g.chunk_used[k] = true;
-    g.h2d_bytes += (double)used;
+    for (int jj = j; jj < j1; ++jj) g.h2d_bytes += (double)(n_in[jj] ? host_bytes(n_in[jj]) : 0);
     j = j1;
   }
+  if (compact) launch_expand_scans(g.cstream, g.d_stage, c->NMAX, B, dst);  // stream order: after the copies
   CK(hipEventRecord(g.up_ev[slot], g.cstream));
   return FBR_OK;
 }

@@ -119,7 +119,7 @@ print(json.dumps({"ids": ids, "again": again,
 def test_pipelined_launches_are_bit_identical_and_export_in_order():
     """Consecutive fbr_batch_launch calls run two deep (alternate work slots and streams; a launch
     returns once the previous one is fully enqueued).  Every launch of the same staged batch gives
-    the same bytes, and fbr_batch_export_ready hands out the launches' records in launch order.
+    the same bytes, and fbr_batch_export_ready hands out every launch's records, in launch order.
     (Child process: torch, which allocates the export buffers, must initialise HIP first.)"""
     import json
     import subprocess
