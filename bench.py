@@ -36,9 +36,10 @@ WORKLOAD = {"C1": "VLP-16-style scans, local corner+surf map",
             "C3": "Ouster-style scans, ~500k-pt local corner+surf map (mapping leaves 0.1/0.2)",
             "C5": "dense scans, ~5.8M-pt map inside the crop box (mapping leaves 0.05)"}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue peak: a wave64 VALU instruction holds a SIMD's issue for 2 cycles at best, so 1024 SIMDs
-# at 2.4 GHz issue at most 1228.8 G wave-instructions/s (= the 157 TF f32 vector peak / 128 flop)
-VALU_PEAK_GINST = 1024 * 2.4 / 2.0
+# VALU roof: 1024 SIMDs at 2.4 GHz (peak engine clock) = 2457.6 G SIMD-cycles/s; the VALU-busy cycles
+# of a launch come from SQ_ACTIVE_INST_VALU (quad-cycles, tools/valu_pmc.py).  On gfx950 every
+# wave64 VALU instruction of these kernels counts 4 cycles (none is packed f32)
+VALU_PEAK_GCYC = 1024 * 2.4
 
 # Algorithmic bytes per unit for each kernel family: the minimal HBM traffic the kernel's job needs
 # (DESIGN.md §4 holds the same table; every model is <= the FETCH/WRITE counter bytes).  Units per
@@ -401,11 +402,13 @@ def main():
         r = dict(bytes_per_launch=bpl, avg_launch_us=round(avg_s * 1e6, 3), launches_per_step=lps,
                  achieved_GBps=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
                  ms_per_step=round(ms / max(steps_measured, 1), 4), live=live)
-        if k in valu and avg_s > 0:  # the live VALU-issue fraction of the launch
-            ipl = valu[k]["insts_valu_per_launch"]
+        if k in valu and avg_s > 0:  # the launch's VALU cycles / instructions over its live duration
+            cpl, ipl = valu[k].get("valu_cycles_per_launch"), valu[k]["insts_valu_per_launch"]
             r["valu_insts_per_launch"] = ipl
-            r["valu_achieved_ginst_s"] = round(ipl / avg_s / 1e9, 2)
-            r["valu_frac"] = round(ipl / avg_s / 1e9 / VALU_PEAK_GINST, 5)
+            if cpl:
+                r["valu_cycles_per_launch"] = cpl
+                r["valu_achieved_gcyc_s"] = round(cpl / avg_s / 1e9, 2)
+                r["valu_frac"] = round(cpl / avg_s / 1e9 / VALU_PEAK_GCYC, 5)
             r["valu_busy_alone"] = round(valu[k]["valu_busy_alone"], 4)
         return r
 
@@ -456,9 +459,9 @@ def main():
         "roofline": {
             "bound": "valu" if valu_bound else "hbm",
             "kernel": dom,
-            "achieved": kroof[dom]["valu_achieved_ginst_s"] if valu_bound else round(achieved, 2),
-            "peak": VALU_PEAK_GINST if valu_bound else HBM_PEAK_GBS,
-            "unit": "G wave-VALU-inst/s" if valu_bound else "GB/s",
+            "achieved": kroof[dom]["valu_achieved_gcyc_s"] if valu_bound else round(achieved, 2),
+            "peak": VALU_PEAK_GCYC if valu_bound else HBM_PEAK_GBS,
+            "unit": "G VALU-busy SIMD-cycles/s" if valu_bound else "GB/s",
             "frac": kroof[dom]["valu_frac"] if valu_bound else round(achieved / HBM_PEAK_GBS, 5),
             "valu_frac": kroof[dom].get("valu_frac"),
             "valu_busy_alone": kroof[dom].get("valu_busy_alone"),

@@ -778,9 +778,11 @@ int stage_register(fbr_ctx* c, const Sub& sb, bool trace) {
 // Per-job results of the last B jobs, packed on the device and returned by one copy (then one
 // host synchronisation): poses (when poses_out), stats, and the features' capacity errors
 // (FBR_ERR_UNSUPPORTED if any job has one).  with_reg = false: the registration was gated off.
-int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool with_reg = true, int64_t w0 = 0) {
+int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool with_reg = true, int64_t w0 = 0,
+                 bool per_job = false) {
   launch_pack_results(c->stream, B, with_reg ? 1 : 0, c->d_pose_out + w0 * 6, c->d_stats + w0, c->d_nvalid + w0,
-                      c->d_ncorner + w0, c->d_nsurf + w0, c->d_cropcnt, c->d_err + w0, c->d_result);
+                      c->d_ncorner + w0, c->d_nsurf + w0, c->d_cropcnt, c->d_err + w0, per_job ? c->d_guess : nullptr,
+                      c->d_result);
   CK(hipMemcpyAsync(c->h_result, c->d_result, sizeof(JobResult) * B, hipMemcpyDeviceToHost, c->stream));
   const auto tw = std::chrono::steady_clock::now();
   CK(fbr_sync(c->stream));
@@ -791,10 +793,13 @@ int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool
     c->h_result[0].st.n_surf_map = c->h_crop[1];
   }
   host_time(2, tw);
-  // A capacity error in any job (features truncated) fails the call before anything is written:
-  // poses_inout keeps the caller's guesses, as the reference leaves the pose on a failed scan.
-  for (int j = 0; j < B; ++j)
-    if (c->h_result[j].err) return FBR_ERR_UNSUPPORTED;
+  // Single scans: a capacity error (features truncated) fails the call before anything is written
+  // (pose_inout keeps the guess, as the reference leaves the pose on a failed scan).  Batches: the
+  // failed jobs carry FBR_REG_FEATURE_CAPACITY and their guesses (k_pack_results), the rest their
+  // results.
+  if (!per_job)
+    for (int j = 0; j < B; ++j)
+      if (c->h_result[j].err) return FBR_ERR_UNSUPPORTED;
   if (with_reg) {
     c->last_iters.resize(B);
     c->last_q.resize(B);
@@ -1649,7 +1654,7 @@ int fbr_batch_results(fbr_ctx* c, float* poses_out, fbr_reg_stats* stats) {
   CK(hipSetDevice(c->dev));
   const int rc = batch_quiesce(c);
   if (rc) return rc;
-  return copy_results(c, c->staged_B, stats, poses_out, true, (int64_t)c->last_slot * c->Bcap);
+  return copy_results(c, c->staged_B, stats, poses_out, true, (int64_t)c->last_slot * c->Bcap, true);
 }
 
 int fbr_batch_export(fbr_ctx* c, void* device_dst) {

@@ -286,10 +286,12 @@ struct JobResult {
   int32_t err;  // k_features capacity error of the job
   int32_t pad;
 };
-// with_reg = 0: the registration did not run (interval gate): stats hold only the cloud counts
+// with_reg = 0: the registration did not run (interval gate): stats hold only the cloud counts.
+// guess (batch calls): a job with a features capacity error gets it as pose, status
+// FBR_REG_FEATURE_CAPACITY; null: the caller fails the call on any error instead
 void launch_pack_results(hipStream_t s, int B, int with_reg, const float* pose_out, const fbr_reg_stats* stats,
                          const int32_t* nvalid, const int32_t* ncorner, const int32_t* nsurf, const int32_t* cropcnt,
-                         const int32_t* err, JobResult* out);
+                         const int32_t* err, const float* guess, JobResult* out);
 // laserCloud{Corner,Surf}FromMapDSNum: CropBox counts of the global map per job.
 void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, float* dst);
 void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* map_pts, int64_t n, int which,

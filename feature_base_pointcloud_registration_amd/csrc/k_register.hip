@@ -193,11 +193,17 @@ __global__ void k_export_records(int B, const float* pose_out, const fbr_reg_sta
 
 __global__ void k_pack_results(int B, int with_reg, const float* pose_out, const fbr_reg_stats* stats,
                                const int32_t* nvalid, const int32_t* ncorner, const int32_t* nsurf,
-                               const int32_t* cropcnt, const int32_t* err, JobResult* out) {
+                               const int32_t* cropcnt, const int32_t* err, const float* guess, JobResult* out) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= B) return;
   JobResult r;
-  if (with_reg) {
+  if (with_reg && guess && err[j]) {  // batch job over the feature capacity: the guess, flagged
+    for (int k = 0; k < 6; ++k) r.pose[k] = guess[6 * j + k];
+    r.st = fbr_reg_stats{};
+    r.st.status = FBR_REG_FEATURE_CAPACITY;
+    r.st.n_corner_map = cropcnt[2 * j];
+    r.st.n_surf_map = cropcnt[2 * j + 1];
+  } else if (with_reg) {
     for (int k = 0; k < 6; ++k) r.pose[k] = pose_out[6 * j + k];
     r.st = stats[j];
     r.st.n_corner_map = cropcnt[2 * j];
@@ -217,9 +223,9 @@ __global__ void k_pack_results(int B, int with_reg, const float* pose_out, const
 
 void launch_pack_results(hipStream_t s, int B, int with_reg, const float* pose_out, const fbr_reg_stats* stats,
                          const int32_t* nvalid, const int32_t* ncorner, const int32_t* nsurf, const int32_t* cropcnt,
-                         const int32_t* err, JobResult* out) {
+                         const int32_t* err, const float* guess, JobResult* out) {
   fbr_launch(k_pack_results, dim3((B + 63) / 64), dim3(64), 0, s, B, with_reg, pose_out, stats, nvalid, ncorner, nsurf,
-             cropcnt, err, out);
+             cropcnt, err, guess, out);
 }
 
 void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, float* dst) {

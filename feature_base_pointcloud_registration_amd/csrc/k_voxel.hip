@@ -659,7 +659,11 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
       }
     }
     FBR_VG_STAMP(2);
+#ifdef FBR_VG_IP_LEADER  // diagnostic build (tools/gpu_leader.sh): round 3's ballot-leader digit counts
+    vg_radix_sort_inplace<T, KPL, true>(keys, vals, n, G.nbits, hist, wsum);
+#else
     vg_radix_sort_inplace<T, KPL>(keys, vals, n, G.nbits, hist, wsum);
+#endif
     FBR_VG_STAMP(3);
     total = vg_emit<T, true>(keys, vals, n, hist, wsum, in, out);  // hist: (NW + 1) * 2 KB
     FBR_VG_STAMP(4);

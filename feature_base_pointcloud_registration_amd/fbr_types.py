@@ -58,6 +58,7 @@ FBR_OK = 0
 FBR_REG_OK = 0
 FBR_REG_NOT_ENOUGH_FEATURES = 1
 FBR_REG_SKIPPED_INTERVAL = 2
+FBR_REG_FEATURE_CAPACITY = 3  # batch job over the device feature capacity: pose = guess
 
 
 class FbrParams(ctypes.Structure):

@@ -46,6 +46,9 @@ extern "C" {
 #define FBR_REG_OK 0                    /* scan2MapOptimization ran                           */
 #define FBR_REG_NOT_ENOUGH_FEATURES 1   /* mapOptmization.h:1410/1440 gate: pose left at guess */
 #define FBR_REG_SKIPPED_INTERVAL 2      /* mapOptmization.h:279 mappingProcessInterval gate    */
+#define FBR_REG_FEATURE_CAPACITY 3      /* batch job: features exceeded the device capacity;   */
+                                        /* its pose is left at the guess (single-scan calls    */
+                                        /* return FBR_ERR_UNSUPPORTED instead)                 */
 
 /* Raw lidar point: the PointXYZIRT payload of imageProjection.cpp:8-21 (x,y,z,intensity f32,
  * ring u16, time f32), laid out with natural alignment (24 bytes). */
@@ -363,6 +366,9 @@ int fbr_batch_launch(fbr_ctx* ctx);
 /* Enqueue the rest of every launch in flight (host side only; no device synchronisation). */
 int fbr_batch_flush(fbr_ctx* ctx);
 int fbr_batch_wait(fbr_ctx* ctx);
+/* A job whose features exceeded the device capacity (k_features' window / segment limits) does not
+ * fail the batch: it gets status FBR_REG_FEATURE_CAPACITY and its guess as pose, and the others
+ * their results (fbr_batch_results, fbr_process_batch). */
 int fbr_batch_results(fbr_ctx* ctx, float* poses_out /* [n_jobs][6] */,
                       fbr_reg_stats* stats /* [n_jobs] or NULL */);
 /* Enqueue (on the ctx stream, after every launch in flight) a copy of the latest launch's per-job

@@ -46,7 +46,7 @@ def main():
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import KERNEL_SYMBOLS as symbols
-    from bench import VALU_PEAK_GINST
+    from bench import VALU_PEAK_GCYC
     print(f"{'kernel':12s} {'bytes/launch':>14s} {'bench us':>10s} {'rocprof us':>11s} {'calls':>6s} "
           f"{'bench frac':>10s} {'rocprof frac':>12s} {'bench valu':>10s} {'rocprof valu':>12s}")
     nan = float("nan")
@@ -55,7 +55,7 @@ def main():
         bpl = r["bytes_per_launch"]
         rf = bpl / (avg * 1e-6) / 1e9 / a.peak if avg else nan
         vb = r.get("valu_frac", nan)
-        vr = r["valu_insts_per_launch"] / (avg * 1e-6) / 1e9 / VALU_PEAK_GINST if avg and "valu_insts_per_launch" in r else nan
+        vr = r["valu_cycles_per_launch"] / (avg * 1e-6) / 1e9 / VALU_PEAK_GCYC if avg and "valu_cycles_per_launch" in r else nan
         mark = " <- roofline kernel" if k == roof["kernel"] else ""
         print(f"{k:12s} {bpl:14.4g} {r['avg_launch_us']:10.1f} {avg if avg else nan:11.1f} {calls:6d} "
               f"{r['frac']:10.4f} {rf:12.4f} {vb:10.4f} {vr:12.4f}{mark}")

@@ -8,14 +8,17 @@ kernel families; a launcher of two kernels counts its calls once):
 
   insts_valu_per_launch   SQ_INSTS_VALU summed over the launcher's dispatches / calls: wave-level
                           VALU instructions, a property of the work (the same under stream overlap)
+  valu_cycles_per_launch  4 * SQ_ACTIVE_INST_VALU (quad-cycles) / calls: SIMD cycles the VALU was busy
+                          with the launch's instructions (multi-cycle ones counted in full)
   valu_busy_alone         4 * SQ_ACTIVE_INST_VALU (quad-cycles) / (1024 SIMDs * cycles), cycles =
                           duration * effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration,
                           MI355X_MICROARCH.md "DVFS give-back"): VALU-busy of the kernel running alone
   eff_clock_ghz           that effective clock
 
-bench.py turns insts_valu_per_launch into the live VALU-issue fraction of a launch: a wave64 VALU
-instruction holds a SIMD's issue for 2 cycles at best, so the chip issues at most
-1024 * 2.4 GHz / 2 = 1228.8 G wave-instructions/s (the 157 TF f32 vector peak / 128 flop).
+bench.py turns valu_cycles_per_launch into the live VALU-busy fraction of a launch (the VALU roofline:
+1024 SIMDs x 2.4 GHz of VALU cycles per second).  Every wave64 VALU instruction of these kernels
+counts 4 cycles (valu_cycles / insts = 4.0-4.2: none is packed f32, whose 2-lane form doubles the
+157 TF vector peak).
 
 usage: valu_pmc.py COUNTER_COLLECTION.csv CONFIG BATCH [out.json]
 """
@@ -60,6 +63,7 @@ def main():
         clk = g["GRBM_GUI_ACTIVE"] / XCDS / g["dur_ns"] if g.get("GRBM_GUI_ACTIVE") else 2.4
         busy = 4.0 * g["SQ_ACTIVE_INST_VALU"] / (SIMDS * g["dur_ns"] * clk)
         ent = {"calls": n, "avg_us_alone": g["dur_ns"] / n / 1e3, "insts_valu_per_launch": g["SQ_INSTS_VALU"] / n,
+               "valu_cycles_per_launch": 4.0 * g["SQ_ACTIVE_INST_VALU"] / n,
                "valu_busy_alone": busy, "eff_clock_ghz": clk,
                "wave_cycles_per_launch": g.get("SQ_WAVE_CYCLES", 0.0) * 4.0 / n}
         res["kernels"][key] = ent
