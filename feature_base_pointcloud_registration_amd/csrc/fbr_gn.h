@@ -124,12 +124,9 @@ __device__ __forceinline__ bool row_range(const MapGrid& m, int y, int z, int x0
 // absolute map index = sub (mod LPQ) (knn5_merge combines the lists).  A lane prunes with its own
 // 5th distance, which is never below the merged one (its list holds the 5 nearest of a subset),
 // so every point of the merged 5 nearest is still scanned by its lane.
-// kFlat only queues the rows: *nrow_out / *npts_out receive the rows queued and their point total,
-// and knn5_flat_scan walks them (possibly on another lane: gn_knn_block balances the lanes).
 template <int R, int RX, bool kFlat = false, bool kSparse = false, int LPQ = 1>
 __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
-                          float bound, Knn5& r, unsigned* ks, int2* rows = nullptr, int sub = 0, int* nrow_out = nullptr,
-                          int* npts_out = nullptr) {
+                          float bound, Knn5& r, unsigned* ks, int2* rows = nullptr, int sub = 0) {
   constexpr int K = 2 * R + 1;  // rows per side in y and z; RX = cells per side along x
 #pragma unroll
   for (int t = 0; t < 5; ++t) r.k[t] = kKnnEmpty;
@@ -139,8 +136,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
   if (!(fabsf(fx) < 1e7f && fabsf(fy) < 1e7f && fabsf(fz) < 1e7f)) return;
   const int cx = (int)fx - (int)m.g.origin[0], cy = (int)fy - (int)m.g.origin[1], cz = (int)fz - (int)m.g.origin[2];
   const int X = m.g.dims[0], Y = m.g.dims[1], Z = m.g.dims[2];
-  if (cx < -RX || cy < -R || cz < -R || cx >= X + RX || cy >= Y + R || cz >= Z + R) return;  // (kFlat: the caller
-                                                                                            // zeroed *nrow_out)
+  if (cx < -RX || cy < -R || cz < -R || cx >= X + RX || cy >= Y + R || cz >= Z + R) return;
   const int sgy = (sy - fy) >= 0.5f ? 1 : -1, sgz = (sz - fz) >= 0.5f ? 1 : -1;
   // squared per-axis lower bounds: y/z by visit rank, x by offset (negative / positive side)
   float ly2[K], lz2[K], lxm2[RX + 1], lxp2[RX + 1];
@@ -163,7 +159,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
   const float bx0 = bmin[0], by0 = bmin[1], bz0 = bmin[2], bx1 = bmax[0], by1 = bmax[1], bz1 = bmax[2];
   const float xlo = (fx - (float)RX) * cxs, xhi = (fx + (float)(RX + 1)) * cxs;  // row x extent (max)
   const bool xin = xlo >= bx0 && xhi <= bx1;
-  int nrow = 0, npts = 0;  // kFlat: rows queued, their points
+  int nrow = 0;  // kFlat: rows queued
 #pragma unroll
   for (int ksum = 0; ksum <= 2 * (K - 1); ++ksum) {
 #pragma unroll
@@ -200,10 +196,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       const float ylo = (fy + (float)oyk[ky]) * c, zlo = (fz + (float)ozk[kz]) * c;
       const bool inside = xin & (ylo >= by0) & (ylo + c <= by1) & (zlo >= bz0) & (zlo + c <= bz1);
       if constexpr (kFlat) {
-        if (e > b) {
-          rows[nrow++ * kResThreads] = make_int2(b, inside ? (int)((unsigned)e | 0x80000000u) : e);
-          npts += e - b;
-        }
+        if (e > b) rows[nrow++ * kResThreads] = make_int2(b, inside ? (int)((unsigned)e | 0x80000000u) : e);
         continue;
       }
       for (int i = LPQ == 1 ? b : b + ((sub - b) & (LPQ - 1)); i < e; i += LPQ) {
@@ -225,42 +218,31 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
     }
   }
   if constexpr (kFlat) {
-    *nrow_out = nrow;
-    *npts_out = npts;
-  }
-}
-
-// The point walk of a query whose rows knn5_grid<.., kFlat> queued (rows at stride kResThreads).
-__device__ __forceinline__ void knn5_flat_scan(const MapGrid& m, float qx, float qy, float qz, const float* bmin,
-                                               const float* bmax, const int2* rows, int nrow, Knn5& r, unsigned* ks) {
-#pragma unroll
-  for (int t = 0; t < 5; ++t) r.k[t] = kKnnEmpty;
-  const float bx0 = bmin[0], by0 = bmin[1], bz0 = bmin[2], bx1 = bmax[0], by1 = bmax[1], bz1 = bmax[2];
-  int j = 0, i = 0, e = 0;
-  bool inside = true;
-  while (true) {
-    if (i >= e) {  // next queued row (every queued row is non-empty)
-      if (j >= nrow) break;
-      const int2 q = rows[j++ * kResThreads];
-      i = q.x;
-      e = q.y & 0x7fffffff;
-      inside = q.y < 0;
-    }
-    const float4 p = m.pts[i++];
-    bool out = false;
-    if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
-    float dist = 0.0f, diff;
-    diff = qx - p.x; dist += diff * diff;  // flann::L2_Simple
-    diff = qy - p.y; dist += diff * diff;
-    diff = qz - p.z; dist += diff * diff;
-    const unsigned hi = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
-    FBR_KS(4, __int_as_float((int)hi) < knn_d(r.k[4]) ? 1 : 0);
+    int j = 0, i = 0, e = 0;
+    bool inside = true;
+    while (true) {
+      if (i >= e) {  // next queued row (every queued row is non-empty)
+        if (j >= nrow) break;
+        const int2 q = rows[j++ * kResThreads];
+        i = q.x;
+        e = q.y & 0x7fffffff;
+        inside = q.y < 0;
+      }
+      const float4 p = m.pts[i++];
+      bool out = false;
+      if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
+      float dist = 0.0f, diff;
+      diff = qx - p.x; dist += diff * diff;  // flann::L2_Simple
+      diff = qy - p.y; dist += diff * diff;
+      diff = qz - p.z; dist += diff * diff;
+      const unsigned hi = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
+      FBR_KS(4, __int_as_float((int)hi) < knn_d(r.k[4]) ? 1 : 0);
 #ifdef FBR_KNN_STATS
-    if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ks[7] += 1;  // one per wave iteration
+      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ks[7] += 1;  // one per wave iteration
 #endif
-    knn_insert(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
+      knn_insert(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
+    }
   }
-  (void)ks;
 }
 
 // Wide mode: the LPQ lanes of a query (consecutive lanes) exchange their lists in a butterfly and
@@ -476,109 +458,8 @@ __device__ __forceinline__ void res_reduce(double (*red)[28], int tid, const flo
 // flat): a workgroup covers 256 / LPQ queries of an item with LPQ lanes each, so a query's search
 // chain is LPQ times shorter; lane `sub` == 0 of each query writes the results.
 // One virtual workgroup v (item v / LPQ, query group v % LPQ) of the kNN pass (k_gn_knn's body).
-// LDS of the flat pass's lane balancing: each query's transformed point and queued row count, the
-// point-count histogram / scan, the balanced query order.
-struct KnnBalanceLds {
-  float4 q[kResThreads];
-  int hist[kResThreads];
-  int order[kResThreads];
-  int wsum[kResThreads / 64];
-};
-
-// Flat pass (kFlat, iterations >= 1) of one work item: every lane queues its own query's rows, then
-// the queries are dealt to the lanes in order of their queued point counts (a counting sort over
-// 256 buckets), so the 64 queries of a wave have similar walks and a wave no longer runs for its
-// one longest query while most lanes idle (the walk's lane efficiency was 0.44).  Each query's 5
-// nearest are a function of its own queued rows alone, so the lane that walks them does not matter.
-template <int R, int RX, bool kSparse>
-__device__ __forceinline__ void gn_knn_flat_item(const GnArgs& a, int it, int2 (*rows)[kResThreads], KnnBalanceLds& L) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int4 item = a.items[it];
-  const int job = item.x;
-  const GnState& g = a.gn[job];
-  if (!g.active) return;  // block-uniform
-  const bool corner = item.y == 0;
-  const MapGrid& mg = corner ? a.mc : a.ms;
-  int32_t* obase = a.nbr + (int64_t)it * 5 * kResThreads;
-  unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  int nrow = 0, npts = 0;
-  if (tid < item.w) {
-    const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
-    const float* T = g.T;
-    // pointAssociateToMap (:397-403)
-    const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
-    const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
-    const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
-    const int32_t* o = obase + tid;
-    float bound = __int_as_float(0x7f800000);
-    if (o[0] >= 0) {  // warm start: the previous iteration's neighbours of this query
-      float mx = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const float4 q = mg.by_id[o[k * kResThreads]];
-        float dist = 0.0f, diff;
-        diff = x0 - q.x; dist += diff * diff;
-        diff = y0 - q.y; dist += diff * diff;
-        diff = z0 - q.z; dist += diff * diff;
-        mx = fmaxf(mx, dist);
-      }
-      bound = mx;
-    }
-    Knn5 nn;
-    knn5_grid<R, RX, true, kSparse, 1>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks, &rows[0][tid], 0, &nrow, &npts);
-    L.q[tid] = make_float4(x0, y0, z0, __int_as_float(nrow));
-  }
-  // counting sort of the queries by queued points (256 buckets of 2 points)
-  const int bkt = min(npts >> 1, kResThreads - 1);
-  L.hist[tid] = 0;
-  __syncthreads();
-  const int rank = atomicAdd(&L.hist[bkt], 1);
-  __syncthreads();
-  const int v = L.hist[tid];
-  int inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(inc, o);
-    if (lane >= o) inc += y;
-  }
-  if (lane == 63) L.wsum[wave] = inc;
-  __syncthreads();
-  int base = 0;
-  for (int w = 0; w < wave; ++w) base += L.wsum[w];
-  L.hist[tid] = base + inc - v;  // exclusive prefix (every lane read its own bin above)
-  __syncthreads();
-  L.order[L.hist[bkt] + rank] = tid;
-  __syncthreads();
-  const int qs = L.order[tid];  // the query this lane walks
-  if (qs >= item.w) return;
-  const float4 qp = L.q[qs];
-  Knn5 nn;
-  knn5_flat_scan(mg, qp.x, qp.y, qp.z, g.crop_min, g.crop_max, &rows[0][qs], __float_as_int(qp.w), nn, ks);
-  const bool ok = nn.k[4] < kKnnEmpty;
-  int32_t* o = obase + qs;
-  const bool have_prev = o[0] >= 0;
-  bool same = have_prev && ok && a.fit_cache;
-  int32_t ids[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    ids[k] = knn_id(nn.k[k]);
-    same = same && ids[k] == o[k * kResThreads];
-  }
-#pragma unroll
-  for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? ids[k] : -1;
-  a.nsame[(int64_t)it * kResThreads + qs] = same ? 1 : 0;
-#ifdef FBR_KNN_STATS
-  ks[5] = ok;
-  ks[6] = corner;
-  ks[8] = have_prev;
-  ks[9] = same;
-  for (int k = 0; k < 10; ++k) atomicAdd(&a.knn_stats[k], (unsigned long long)ks[k]);
-#endif
-}
-
 template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ>
 __device__ __forceinline__ void gn_knn_block(const GnArgs& a, int v, int use_prev, double (*red)[28], int2* rows) {
-  static_assert(!kFlat, "the flat pass is gn_knn_flat_item");
   constexpr int QPB = kResThreads / LPQ;  // queries per workgroup
   const int sub = (int)threadIdx.x % LPQ;
   const int it = v / LPQ;
@@ -654,20 +535,11 @@ template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ = 1>
 __global__ void __launch_bounds__(kResThreads)
 k_gn_knn(GnArgs a, int use_prev) {
   static_assert(LPQ == 1 || (!kFused && !kFlat), "wide mode is the plain kNN pass");
-  static_assert(!kFlat || !kFused, "the flat pass is not fused");
   __shared__ double red[kFused ? kResThreads / 64 : 1][28];
   __shared__ int2 rows[kFlat ? (2 * R + 1) * (2 * R + 1) : 1][kResThreads];
   const int nitems = a.nitems[0];
-  if constexpr (kFlat) {
-    __shared__ KnnBalanceLds bal;
-    for (int v = blockIdx.x; v < nitems; v += gridDim.x) {
-      gn_knn_flat_item<R, RX, kSparse>(a, v, rows, bal);
-      __syncthreads();  // the next item reuses rows / bal
-    }
-  } else {
-    for (int v = blockIdx.x; v < nitems * LPQ; v += gridDim.x)
-      gn_knn_block<R, RX, kFused, kFlat, kSparse, LPQ>(a, v, use_prev, red, &rows[0][threadIdx.x]);
-  }
+  for (int v = blockIdx.x; v < nitems * LPQ; v += gridDim.x)
+    gn_knn_block<R, RX, kFused, kFlat, kSparse, LPQ>(a, v, use_prev, red, &rows[0][threadIdx.x]);
 }
 
 // pcl::getTransformation (x,y,z,roll,pitch,yaw) in float with glibc's sinf / cosf
