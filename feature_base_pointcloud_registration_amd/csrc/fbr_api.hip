@@ -1932,7 +1932,7 @@ int fbr_voxel_grid(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf, 
 extern "C" int fbr_diag_feature_stamps(fbr_ctx* c, unsigned long long* out /* [max_batch*n_scan][12] */) {
   if (!c) return FBR_ERR_INVALID_ARG;
   CK(hipSetDevice(c->dev));
-  const size_t n = (size_t)c->Bcap * c->H * 12;
+  const size_t n = (size_t)c->Bwork * c->H * 12;  // both launch slots (the first launch uses slot 0)
   if (!c->d_feat_stamps) {
     CK(hipMalloc(&c->d_feat_stamps, sizeof(unsigned long long) * n));
     CK(hipMemset(c->d_feat_stamps, 0, sizeof(unsigned long long) * n));

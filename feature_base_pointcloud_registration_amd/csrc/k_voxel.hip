@@ -1243,13 +1243,255 @@ __global__ void __launch_bounds__(64) k_voxel_ring_wave(VgRing A) {
   if (lane == 0) A.cnt_out[slot] = V;
 }
 
-// The wave-per-ring filter for the default order (FBR_VR_WAVE=1; default: the 512-thread kernel,
-// which measured faster: 407 vs 481 us per sequential 256-job launch, 97.4k vs 95.2k scans/s at
-// B = 1024, profiles/r04e_voxel_ring_wave_ab.txt, r04f_pipe_nsub_sweep.txt).
-bool vr_wave() {
-  static const bool v = [] {
+// ---- the per-ring surf filter, four waves per ring (default order) ----
+// k_voxel_ring_wave's algorithm with the memory round trips of a ring cut to about three: each of
+// the 4 waves loads a quarter of the ring's labels and points in one go (up to 8 steps of 64,
+// kept in registers for the key pass: one load per point), the run keys and starts are
+// compacted with workgroup prefixes, wave 0 sorts the runs in registers (R <= 512; above, the
+// four waves rank them by counting), and every thread sums about one voxel.  The one-wave kernel
+// needed 2.3x fewer VALU instructions than the 512-thread kernel (profiles/r04j_valu_*) but sat
+// on ~14 dependent round trips per ring (VALU-busy 0.26 alone, slower overall).
+template <int KQ>  // steps of 64 points per wave: 4 * 64 * KQ >= the ring capacity
+__global__ void __launch_bounds__(256) k_voxel_ring_q(VgRing A) {
+  constexpr int NW = 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ float mmx[NW][6];
+  __shared__ int cntw[NW], runw[NW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int slot = blockIdx.x, job = slot / A.H;
+  const int s = A.start_ring[slot], e = A.end_ring[slot];
+  float4* out = A.out + (int64_t)slot * A.stride_out;
+  if (e <= s) {
+    if (tid == 0) A.cnt_out[slot] = 0;
+    return;
+  }
+  int sp6[6], ep6[6];
+  bool all6 = true;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    sp6[j] = (s * (6 - j) + e * j) / 6;
+    ep6[j] = (s * (5 - j) + e * (j + 1)) / 6 - 1;
+    all6 = all6 && sp6[j] < ep6[j];
+  }
+  auto in_seg = [&](int k) {  // the non-empty segments [sp, ep] (:195-200), inside [s, e - 1]
+    if (all6) return k <= ep6[5];
+    bool in = false;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) in |= sp6[j] < ep6[j] && k >= sp6[j] && k <= ep6[j];
+    return in;
+  };
+  const float4* CL = A.cloud + (int64_t)job * A.HW + s;
+  const int8_t* LB = A.label + (int64_t)job * A.HW + s;
+  const int len = min(e - s, (int)A.cap);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  // ---- pass A: this wave's quarter [q0, q1) in one round of loads, kept in registers ----
+  const int qlen = (((len + NW - 1) / NW) + 63) & ~63;
+  const int q0 = min(len, w * qlen), q1 = min(len, q0 + qlen);
+  float4 pt[KQ];
+  bool cd[KQ];
+#pragma unroll
+  for (int u = 0; u < KQ; ++u) {
+    const int i = q0 + 64 * u + lane;
+    const bool ok = i < q1;
+    const int8_t lab = ok ? LB[i] : (int8_t)1;
+    pt[u] = ok ? CL[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    cd[u] = ok && lab <= 0;
+  }
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  int nw = 0;
+#pragma unroll
+  for (int u = 0; u < KQ; ++u) {
+    cd[u] = cd[u] && in_seg(s + q0 + 64 * u + lane);
+    if (cd[u]) {
+      const float v[3] = {pt[u].x, pt[u].y, pt[u].z};
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
+        mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
+      }
+    }
+    nw += __popcll(__ballot(cd[u]));
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+    for (int o = 32; o > 0; o >>= 1) {
+      const float a = __shfl_xor(mn[d], o), b = __shfl_xor(mx[d], o);
+      mn[d] = (a < mn[d]) ? a : mn[d];
+      mx[d] = (mx[d] < b) ? b : mx[d];
+    }
+  if (lane == 0) {
+    for (int d = 0; d < 3; ++d) {
+      mmx[w][d] = mn[d];
+      mmx[w][3 + d] = mx[d];
+    }
+    cntw[w] = nw;
+  }
+  __syncthreads();
+  int n = 0, base = 0;
+#pragma unroll
+  for (int ww = 0; ww < NW; ++ww) {
+    base += ww < w ? cntw[ww] : 0;
+    n += cntw[ww];
+  }
+  if (n == 0) {
+    if (tid == 0) A.cnt_out[slot] = 0;
+    return;
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    mn[d] = mmx[0][d];
+    mx[d] = mmx[0][3 + d];
+#pragma unroll
+    for (int ww = 1; ww < NW; ++ww) {
+      mn[d] = (mmx[ww][d] < mn[d]) ? mmx[ww][d] : mn[d];
+      mx[d] = (mx[d] < mmx[ww][3 + d]) ? mmx[ww][3 + d] : mx[d];
+    }
+  }
+  VgGrid G;
+  G.init(mn, mx, A.leaf, false);
+  const int cap = (int)A.cap;
+  uint32_t* kb = (uint32_t*)smem;             // [cap + 1] candidate keys, then run keys; then sid / vst (u16)
+  uint16_t* off = (uint16_t*)(kb + cap + 1);  // [cap] ring offset of the t-th candidate
+  uint16_t* rst = off + cap;                  // [cap + 1] first candidate of each run
+  // ---- pass B: keys in index order (or, on PCL's overflow, the candidates themselves) ----
+#pragma unroll
+  for (int u = 0; u < KQ; ++u) {
+    const uint64_t b = __ballot(cd[u]);
+    const int pos = base + __popcll(b & lt);
+    if (cd[u]) {
+      if (G.overflow) {
+        out[pos] = pt[u];  // PCL: "Leaf size is too small" -> output = input, in index order
+      } else {
+        kb[pos] = G.key(pt[u]);
+        off[pos] = (uint16_t)(q0 + 64 * u + lane);
+      }
+    }
+    base += __popcll(b);
+  }
+  if (G.overflow) {
+    if (tid == 0) A.cnt_out[slot] = n;
+    return;
+  }
+  __syncthreads();
+  // ---- pass C: run heads (keys read before the barrier, run keys written after it) ----
+  const int tq = (((n + NW - 1) / NW) + 63) & ~63;
+  const int t0w = min(n, w * tq), t1w = min(n, t0w + tq);
+  constexpr int KR = KQ;  // n <= len: each wave's share of candidates fits KR steps as well
+  uint32_t rk[KR];
+  uint64_t hb[KR];
+  int nr = 0;
+#pragma unroll
+  for (int u = 0; u < KR; ++u) {
+    const int t = t0w + 64 * u + lane;
+    const bool valid = t < t1w;
+    const uint32_t key = valid ? kb[t] : 0u;
+    const uint32_t prev = (valid && t > 0) ? kb[t - 1] : 0u;
+    rk[u] = key;
+    hb[u] = __ballot(valid && (t == 0 || key != prev));
+    nr += __popcll(hb[u]);
+  }
+  if (lane == 0) runw[w] = nr;
+  __syncthreads();
+  int R = 0, rq = 0;
+#pragma unroll
+  for (int ww = 0; ww < NW; ++ww) {
+    rq += ww < w ? runw[ww] : 0;
+    R += runw[ww];
+  }
+#pragma unroll
+  for (int u = 0; u < KR; ++u) {
+    if ((hb[u] >> lane) & 1ull) {
+      const int r = rq + __popcll(hb[u] & lt);
+      kb[r] = rk[u];
+      rst[r] = (uint16_t)(t0w + 64 * u + lane);
+    }
+    rq += __popcll(hb[u]);
+  }
+  if (tid == 0) rst[R] = (uint16_t)n;
+  __syncthreads();
+  // ---- sort the runs (stable by run id), voxel starts ----
+  uint16_t* sid = (uint16_t*)kb;  // [R]
+  uint16_t* vst = sid + cap + 1;  // [V + 1]
+  __shared__ int vcount;
+  if (R <= 512) {
+    if (w == 0) {
+      const int V = R <= 256 ? vr_sort_runs<4>(kb, R, sid, vst, lane) : vr_sort_runs<8>(kb, R, sid, vst, lane);
+      if (lane == 0) vcount = V;
+    }
+  } else {
+    // rank by counting over all 4 waves into the output slot, then wave 0 marks the voxels
+    uint64_t* scr = reinterpret_cast<uint64_t*>(out);
+    for (int r = tid; r < R; r += 256) {
+      const uint32_t key = kb[r];
+      int rank = 0;
+      for (int j = 0; j < R; ++j) {
+        const uint32_t kj = kb[j];
+        rank += (kj < key || (kj == key && j < r)) ? 1 : 0;
+      }
+      scr[rank] = ((uint64_t)key << 16) | (uint64_t)r;
+    }
+    __syncthreads();  // (also orders the global scratch writes before the reads below)
+    if (w == 0) {
+      int V = 0;
+      for (int g0 = 0; g0 < R; g0 += 64) {
+        const int g = g0 + lane;
+        const uint64_t x = g < R ? scr[g] : ~0ull;
+        const uint64_t px = (g > 0 && g < R) ? scr[g - 1] : ~0ull;
+        const bool hd = g < R && (g == 0 || (x >> 16) != (px >> 16));
+        const uint64_t b = __ballot(hd);
+        wave_lds_sync();
+        if (g < R) sid[g] = (uint16_t)(x & 0xFFFFull);
+        if (hd) vst[V + __popcll(b & lt)] = (uint16_t)g;
+        V += __popcll(b);
+      }
+      if (lane == 0) {
+        vst[V] = (uint16_t)R;
+        vcount = V;
+      }
+    }
+  }
+  __syncthreads();  // (the scratch reads above precede the emit's stores to the same slot)
+  const int V = vcount;
+  // ---- one thread per voxel: the float sum of its points in index order (runs in id order) ----
+  for (int vv = tid; vv < V; vv += 256) {
+    const int g0 = vst[vv], g1 = vst[vv + 1];
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    int cnt = 0;
+    for (int g = g0; g < g1; ++g) {
+      const int rid = sid[g];
+      const int ta = rst[rid], tb = rst[rid + 1];
+      for (int t = ta; t < tb; t += 8) {  // a run's points, 8 gathers in flight
+        float4 pp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pp[u] = CL[off[min(t + u, tb - 1)]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (t + u < tb) {
+            if (cnt == 0) {
+              c = pp[u];
+            } else {
+              c.x += pp[u].x;
+              c.y += pp[u].y;
+              c.z += pp[u].z;
+              c.w += pp[u].w;
+            }
+            ++cnt;
+          }
+      }
+    }
+    const float fc = (float)cnt;
+    out[vv] = make_float4(c.x / fc, c.y / fc, c.z / fc, c.w / fc);
+  }
+  if (tid == 0) A.cnt_out[slot] = V;
+}
+
+// The per-ring filter of the default order (FBR_VR_WAVE): 0 = the 512-thread kernel, 1 = one
+// wave per ring (2.3x fewer VALU instructions but latency-bound: 481 vs 407 us per sequential
+// 256-job launch, profiles/r04e_voxel_ring_wave_ab.txt, r04j_valu_*), 2 = four waves per ring.
+int vr_mode() {
+  static const int v = [] {
     const char* e = std::getenv("FBR_VR_WAVE");
-    return e ? std::atoi(e) != 0 : false;
+    return e ? std::atoi(e) : 2;
   }();
   return v;
 }
@@ -1278,9 +1520,11 @@ void launch_voxel_ring(hipStream_t s, const VgRing& a) {
   };
   if (a.exact) {
     go(std::true_type{});
-  } else if (vr_wave() && a.dbg == 0 && a.cap <= 4096) {
+  } else if (vr_mode() != 0 && a.dbg == 0 && a.cap <= 4096) {
     const size_t lds = (((size_t)a.cap + 1) * 4 + (size_t)a.cap * 2 + ((size_t)a.cap + 1) * 2 + 15) & ~(size_t)15;
-    fbr_launch(k_voxel_ring_wave, dim3(nseg), dim3(64), lds, s, a);
+    if (vr_mode() == 1) fbr_launch(k_voxel_ring_wave, dim3(nseg), dim3(64), lds, s, a);
+    else if (a.cap <= 4 * 64 * 8) fbr_launch(k_voxel_ring_q<8>, dim3(nseg), dim3(256), lds, s, a);
+    else fbr_launch(k_voxel_ring_q<16>, dim3(nseg), dim3(256), lds, s, a);
   } else {
     go(std::false_type{});
   }

@@ -662,11 +662,13 @@ def _adversarial_ring_scan(H, W, seed):
     return np.concatenate(pts)
 
 
-def test_wave_ring_filter_is_bit_identical_to_workgroup_kernel():
-    """The one-wave-per-ring surf VoxelGrid (k_voxel_ring_wave, register bitonic / counting-rank run
-    sorts) against the 512-thread kernel (FBR_VR_WAVE=0, child process): identical surf clouds,
-    labels and corners on C1 / C2 / C3 scans and on adversarial rings (every candidate its own
-    voxel), and within SURF_ULPS of the oracle."""
+@pytest.mark.parametrize("mode", ["0", "1"], ids=["workgroup-512", "one-wave"])
+def test_wave_ring_filter_is_bit_identical_to_workgroup_kernel(mode):
+    """The default four-waves-per-ring surf VoxelGrid (k_voxel_ring_q: register bitonic /
+    counting-rank run sorts) against the 512-thread kernel (FBR_VR_WAVE=0) and the one-wave kernel
+    (FBR_VR_WAVE=1), each in a child process: identical surf clouds, labels and corners on C1 / C2 /
+    C3 scans and on adversarial rings (every candidate its own voxel), and within SURF_ULPS of the
+    oracle."""
     import subprocess
     import sys
     cases = [("C1", synth.scan(synth.job(1)[0], 16, 1800, seed=1)),
@@ -682,7 +684,7 @@ def test_wave_ring_filter_is_bit_identical_to_workgroup_kernel():
             "    out += [f['label'].tobytes(), f['corner'].tobytes(), f['surf'].tobytes()]\n"
             "sys.stdout.buffer.write(b''.join(len(x).to_bytes(8, 'little') + x for x in out))"
             % (REPO, path, [c[0] for c in cases]))
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, FBR_VR_WAVE="0"),
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, FBR_VR_WAVE=mode),
                        timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     blob, ref = r.stdout, []
