@@ -19,11 +19,7 @@ namespace fbr {
 __host__ __device__ inline int32_t f2bits(float x) { return __builtin_bit_cast(int32_t, x); }
 __host__ __device__ inline float bits2f(int32_t i) { return __builtin_bit_cast(float, i); }
 
-// fdlibm s_atanf.c argument reduction + odd/even polynomial split.  The four reduction branches
-// (id 0..3) and the small-argument one (id -1) are computed as selects feeding ONE division
-// (num / den: each branch's own operands, so the same IEEE operation; x / 1 = x exactly for id -1):
-// across a wave the lanes fall into all five ranges, and the branchy form ran up to four division
-// sequences per wave.
+// fdlibm s_atanf.c argument reduction + odd/even polynomial split.
 __host__ __device__ inline float fd_atanf(float x) {
   const float atanhi0 = 4.6364760399e-01f, atanhi1 = 7.8539812565e-01f,
               atanhi2 = 9.8279368877e-01f, atanhi3 = 1.5707962513e+00f;
@@ -36,29 +32,33 @@ __host__ __device__ inline float fd_atanf(float x) {
   const float one = 1.0f;
   int32_t hx = f2bits(x);
   int32_t ix = hx & 0x7fffffff;
+  int id;
   if (ix >= 0x4c000000) {          // |x| >= 2^25
     if (ix > 0x7f800000) return x + x;  // NaN
     return hx > 0 ? atanhi3 + atanlo3 : -atanhi3 - atanlo3;
   }
-  const float ax = __builtin_fabsf(x);
-  // id: -1 |x| < 0.4375; 0 < 0.6875; 1 < 1.1875; 2 < 2.4375; 3 above
-  const int id = ix < 0x3ee00000 ? -1 : ix < 0x3f300000 ? 0 : ix < 0x3f980000 ? 1 : ix < 0x401c0000 ? 2 : 3;
-  const float n0 = 2.0f * ax - one, d0 = 2.0f + ax;     // id 0: (2x - 1) / (2 + x)
-  const float n1 = ax - one, d1 = ax + one;             // id 1: (x - 1) / (x + 1)
-  const float n2 = ax - 1.5f, d2 = one + 1.5f * ax;     // id 2: (x - 1.5) / (1 + 1.5x)
-  const float num = id < 0 ? x : id == 0 ? n0 : id == 1 ? n1 : id == 2 ? n2 : -1.0f;  // id 3: -1 / x
-  const float den = id < 0 ? one : id == 0 ? d0 : id == 1 ? d1 : id == 2 ? d2 : ax;
-  x = num / den;
+  if (ix < 0x3ee00000) {           // |x| < 0.4375
+    if (ix < 0x31000000) return x; // |x| < 2^-29
+    id = -1;
+  } else {
+    x = __builtin_fabsf(x);
+    if (ix < 0x3f980000) {         // |x| < 1.1875
+      if (ix < 0x3f300000) { id = 0; x = (2.0f * x - one) / (2.0f + x); }
+      else                 { id = 1; x = (x - one) / (x + one); }
+    } else {
+      if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (one + 1.5f * x); }
+      else                 { id = 3; x = -1.0f / x; }
+    }
+  }
   float z = x * x;
   float w = z * z;
   float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
   float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
-  const float small = x - x * (s1 + s2);
+  if (id < 0) return x - x * (s1 + s2);
   float hi = id == 0 ? atanhi0 : id == 1 ? atanhi1 : id == 2 ? atanhi2 : atanhi3;
   float lo = id == 0 ? atanlo0 : id == 1 ? atanlo1 : id == 2 ? atanlo2 : atanlo3;
   z = hi - ((x * (s1 + s2) - lo) - x);
-  const float big = hx < 0 ? -z : z;
-  return ix < 0x31000000 ? bits2f(hx) : (id < 0 ? small : big);  // |x| < 2^-29: x itself
+  return hx < 0 ? -z : z;
 }
 
 // fdlibm e_atan2f.c: atan2(y, x) in single precision.

@@ -33,13 +33,7 @@ __device__ __forceinline__ bool project_point(const fbr_point_xyzirt& q, int H, 
   if (rowIdn < 0 || rowIdn >= H) return false;
   float horizonAngle = (float)((double)(fd_atan2f(q.x, q.y) * 180.0f) / M_PI);
   float ang_res_x = (float)(360.0 / (double)(float)W);
-  // round(t / res) by a multiplication: |t * (1 / res) - t / res| < 1e-12 for |t / res| < 2^20, so
-  // the rounded values agree unless t / res lies within 1e-9 of a rounding boundary (k + 0.5),
-  // where the quotient itself is taken (NaN falls through to the quotient's NaN either way)
-  const double t = (double)horizonAngle - 90.0, res = (double)ang_res_x;
-  double u = t * (1.0 / res);
-  if (__builtin_fabs((u - floor(u)) - 0.5) < 1e-9 || !(__builtin_fabs(u) < 1048576.0)) u = t / res;
-  int columnIdn = x86_cvt(-round(u) + (double)(W / 2));
+  int columnIdn = x86_cvt(-round(((double)horizonAngle - 90.0) / (double)ang_res_x) + (double)(W / 2));
   if (columnIdn >= W) columnIdn -= W;
   if (columnIdn < 0 || columnIdn >= W) return false;
   // range = sqrtf(x^2 + y^2 + z^2) < 1.0 (:618-621): a correctly rounded sqrt is below 1 exactly
