@@ -856,13 +856,30 @@ class CopyPool {
   }
 
  private:
+  // Idle workers spin for spin_us (FBR_COPY_SPIN_US, default 1000 us) after an upload, so a
+  // pose-chained scan stream (one call every ~0.7 ms) finds them awake, then sleep on the
+  // condition variable; 0 = never spin (no host cores held between calls).
+  static int64_t spin_ns() {
+    static const int64_t v = [] {
+      const char* e = std::getenv("FBR_COPY_SPIN_US");
+      return (int64_t)(e ? std::max(0, std::atoi(e)) : 1000) * 1000;
+    }();
+    return v;
+  }
   void loop(int id) {
     uint64_t seen = 0;
     while (true) {
       uint64_t g = gen_.load();
-      for (int spin = 0; g == seen && spin < 100000; ++spin) {  // ~1 ms awake after an upload
-        __builtin_ia32_pause();
-        g = gen_.load();
+      if (g == seen && spin_ns() > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int spin = 0; g == seen; ++spin) {
+          __builtin_ia32_pause();
+          g = gen_.load();
+          if ((spin & 255) == 255 &&
+              std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() >
+                  spin_ns())
+            break;
+        }
       }
       if (g == seen) {
         std::unique_lock<std::mutex> l(mu_);
@@ -894,7 +911,7 @@ CopyPool& copy_pool() {
 // copy engine runs while the rest is still being copied (a 64x1800 scan is 2.6 MB).  The chunks
 // are disjoint, so their order on the stream does not matter; the caller enqueues the consumer
 // after this returns.
-hipError_t pinned_upload_async(void* d_dst, void* h_stage, const void* src, size_t bytes, hipStream_t st) {
+hipError_t pinned_upload_async(int dev, void* d_dst, void* h_stage, const void* src, size_t bytes, hipStream_t st) {
   constexpr size_t kChunk = 512 << 10;
   if (bytes <= kChunk) {
     std::memcpy(h_stage, src, bytes);
@@ -903,6 +920,7 @@ hipError_t pinned_upload_async(void* d_dst, void* h_stage, const void* src, size
   const size_t nchunk = (bytes + kChunk - 1) / kChunk;
   std::atomic<int> err{(int)hipSuccess};
   const std::function<void(int)> fn = [&](int p) {
+    if (p > 0) (void)hipSetDevice(dev);  // pool workers serve every context: the stream's device
     for (size_t k = (size_t)p; k < nchunk; k += CopyPool::kWorkers + 1) {
       const size_t b = k * kChunk, e = std::min(bytes, b + kChunk);
       std::memcpy((uint8_t*)h_stage + b, (const uint8_t*)src + b, e - b);
@@ -933,7 +951,7 @@ int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n) {
   c->no_time_call = false;
   if (n && pinned_upload()) {
     CK(fbr_sync(c->stream));  // staging free (a no-op after the previous call's result copy)
-    CK(pinned_upload_async(c->d_pts + job * c->NMAX, c->h_scan, pts, sizeof(fbr_point_xyzirt) * n, c->stream));
+    CK(pinned_upload_async(c->dev, c->d_pts + job * c->NMAX, c->h_scan, pts, sizeof(fbr_point_xyzirt) * n, c->stream));
   } else if (n) {
     CK(hipMemcpyAsync(c->d_pts + job * c->NMAX, pts, sizeof(fbr_point_xyzirt) * n, hipMemcpyHostToDevice, c->stream));
   }
@@ -965,7 +983,7 @@ int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags) {
     c->h_msg_cap = L.bytes;
   }
   if (L.bytes) {
-    CK(pinned_upload_async(c->d_msg, c->h_msg, msg->data, L.bytes, c->stream));
+    CK(pinned_upload_async(c->dev, c->d_msg, c->h_msg, msg->data, L.bytes, c->stream));
   }
   MsgDev D;
   D.n = L.n;

@@ -447,6 +447,10 @@ def test_c3_ouster_registration_matches_oracle():
         assert stats["status"][k] == so["status"] == 0 and stats["iterations"][k] == so["iterations"]
         for f in ("n_points", "n_corner", "n_corner_map", "n_surf_map"):
             assert stats[f][k] == so[f], f
+        # default mode: a per-ring centroid one ulp off (index-order sums) may move one of ~10^5
+        # queries across a gate (sqdist < 1, lambda ratio 3, s > 0.1, plane 0.2): at most one
+        # correspondence per job (the round-2 bench sample's C3 flip); exact mode below is equal
+        assert abs(int(stats["n_sel"][k]) - so["n_sel"]) <= 1, (stats["n_sel"][k], so["n_sel"])
         assert stats["n_corner_map"][k] + stats["n_surf_map"][k] > 450000  # ~500k-point local map
         assert_pose_close(poses[k], po)
         assert np.abs(poses[k][3:] - gt[3:]).max() < 0.05
