@@ -278,11 +278,17 @@ def main():
         cur = torch.cuda.current_stream()
         lid, sh = ctx.batch_export_ready(gather_buf.data_ptr(), cur.cuda_stream)
         if lid < 0:
-            return
+            return False
         if sh not in ext_streams:
             ext_streams[sh] = torch.cuda.ExternalStream(sh, device=f"cuda:{dev}")
         cur.wait_stream(ext_streams[sh])
         gathered[0] = shard.gather_records(dist, gather_buf, world)
+        return True
+
+    def gather_rest():  # after the last launch: every launch not yet gathered, in order
+        ctx.batch_flush()
+        while gather_ready():
+            pass
 
     def step():
         ctx.batch_launch()
@@ -299,8 +305,7 @@ def main():
     for _ in range(args.warmup):
         step()
     if dist is not None and args.backend == "nccl":
-        ctx.batch_flush()
-        gather_ready()
+        gather_rest()
     ctx.batch_wait()
     kernels = ["gn_knn", "gn_residual", "gn_solve", "project", "extract", "features", "voxel_ring", "concat",
                "voxel_scan", "gn_init", "crop", "gn_finalize"]
@@ -308,8 +313,7 @@ def main():
     ctx.set_profiling(True)
     step()
     if dist is not None and args.backend == "nccl":
-        ctx.batch_flush()
-        gather_ready()
+        gather_rest()
     ctx.batch_wait()
     ctx.set_profiling(False)
     prof = {k: ctx.kernel_time(k) for k in kernels}
@@ -328,9 +332,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    if dist is not None and args.backend == "nccl":  # the last launch's records
-        ctx.batch_flush()
-        gather_ready()
+    if dist is not None and args.backend == "nccl":  # the last launches' records
+        gather_rest()
     ctx.batch_wait()
     if dist is not None:
         torch.cuda.synchronize()

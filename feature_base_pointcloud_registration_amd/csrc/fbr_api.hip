@@ -139,16 +139,16 @@ struct fbr_ctx {
   int nsub_pref = 3;                  // sub-batches per batch launch (FBR_NSUB overrides): 3 unpipelined (at
                                       // B = 128: 2 -> 76.1k, 3 -> 78.5k, 4 -> 46.7k scans/s), 1 pipelined
   int H = 0, W = 0, Bcap = 0;
-  // Batch launches alternate between nslot work slots (2 unless FBR_PIPE=0 or max_batch = 1): the
-  // next launch's projection / features overlap the previous one's Gauss-Newton tail.  Work arrays
+  // Batch launches rotate over nslot work slots (FBR_PIPE, default 2; 1 when max_batch = 1): the
+  // next launch's projection / features overlap the previous ones' Gauss-Newton tails.  Work arrays
   // hold Bwork = nslot * Bcap jobs; inputs hold Bcap.
+  static constexpr int kMaxSlots = 3;
   int nslot = 1;
   int64_t Bwork = 0;
-  GnRun run[2];
+  GnRun run[kMaxSlots];
   int64_t launch_seq = 0;     // batch launches so far
   int last_slot = -1;         // slot of the latest launch (-1: none since the last stage)
-  int last_nsub[2] = {0, 0};  // sub-batches of each slot's latest launch
-  int64_t slot_launch[2] = {-1, -1};  // launch number of each slot's latest launch
+  int64_t slot_launch[kMaxSlots] = {-1, -1, -1};  // launch number of each slot's latest launch
   int64_t exported = -1;      // latest launch whose records fbr_batch_export_ready exported
   hipEvent_t ev_staged = nullptr;  // the staged inputs are on the device (recorded on stream)
   hipEvent_t ev_fork = nullptr;    // single-scan side-stream fork
@@ -726,12 +726,17 @@ int gn_run_finish(fbr_ctx* c, GnRun& r) {
 // Advance the batch launches in flight together (non-blocking passes; spin while neither can
 // progress) until run[target] is fully enqueued (target -1: every run).
 int advance_runs(fbr_ctx* c, int target) {
-  auto busy = [&] { return target < 0 ? (c->run[0].pending || c->run[1].pending) : c->run[target].pending; };
+  auto busy = [&] {
+    if (target >= 0) return c->run[target].pending;
+    for (int q = 0; q < fbr_ctx::kMaxSlots; ++q)
+      if (c->run[q].pending) return true;
+    return false;
+  };
   auto tw = std::chrono::steady_clock::now();
   bool waiting = false;
   while (busy()) {
     bool p = false;
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < fbr_ctx::kMaxSlots; ++s)
       if (c->run[s].pending) {
         const int rc = gn_run_pass(c, c->run[s], false, &p);
         if (rc) return rc;
@@ -755,7 +760,7 @@ int advance_runs(fbr_ctx* c, int target) {
 int batch_quiesce(fbr_ctx* c) {
   const int rc = advance_runs(c, -1);
   if (rc) return rc;
-  for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < fbr_ctx::kMaxSlots; ++s)
     for (int k = 0; k < c->run[s].nsub; ++k)
       if (c->run[s].subs[k].st != c->stream) CK(hipStreamWaitEvent(c->stream, c->xev[c->run[s].subs[k].k], 0));
   return FBR_OK;
@@ -1181,15 +1186,15 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   c->Bcap = p->max_batch;
   c->NMAX = p->max_points_per_scan;
   if (const char* e = std::getenv("FBR_NSUB")) c->nsub_pref = std::max(1, std::min(kMaxSub, std::atoi(e)));
-  static const bool pipe = [] {
+  static const int pipe = [] {  // launch slots (0 / 1: no pipelining)
     const char* e = std::getenv("FBR_PIPE");
-    return e ? std::atoi(e) != 0 : true;
+    return e ? std::max(1, std::min(fbr_ctx::kMaxSlots, std::atoi(e) <= 0 ? 1 : std::atoi(e))) : 2;
   }();
-  c->nslot = (pipe && p->max_batch > 1) ? 2 : 1;
+  c->nslot = p->max_batch > 1 ? pipe : 1;
   // Pipelined, one sub-batch per launch is best at every batch size (the two launches in flight
   // overlap as the sub-batches did): B = 128 / 256 / 1024 give 91.8k / 96.7k / 97.4k scans/s
   // against 83.2k / 93.1k / 96.7k with 3 sub-batches (profiles/r04f_pipe_nsub_sweep.txt).
-  if (c->nslot == 2) c->nsub_pref = std::getenv("FBR_NSUB") ? std::min(c->nsub_pref, kMaxSub / 2) : 1;
+  if (c->nslot > 1) c->nsub_pref = std::getenv("FBR_NSUB") ? std::min(c->nsub_pref, kMaxSub / c->nslot) : 1;
   c->Bwork = (int64_t)c->nslot * c->Bcap;
   const int64_t B = c->Bcap, Bw = c->Bwork, HW = c->HW, H = c->H;
   // streams of the sub-batches this context can use, per slot (each stream takes a hardware queue:
@@ -1622,7 +1627,7 @@ int fbr_batch_launch(fbr_ctx* c) {
   // alternate work slots with their own streams, and this call returns once the previous launch is
   // fully enqueued: this launch's projection and features run beside the previous one's GN tail.
   const int B = c->staged_B;
-  const int slot = c->nslot == 2 ? (int)(c->launch_seq & 1) : 0;
+  const int slot = (int)(c->launch_seq % c->nslot);
   int rc = advance_runs(c, slot);  // (already enqueued by the previous call: launches n-2 < n-1)
   if (rc) return rc;
   const int nsub = std::max(1, std::min({c->nsub_pref, kMaxSub / c->nslot, B / 8}));
@@ -1644,7 +1649,9 @@ int fbr_batch_launch(fbr_ctx* c) {
   c->slot_launch[slot] = c->launch_seq++;
   bool p = false;
   rc = gn_run_pass(c, c->run[slot], false, &p);  // the iterations that need no flag yet
-  if (!rc) rc = advance_runs(c, c->nslot == 2 ? slot ^ 1 : slot);
+  // return once launch n - (nslot - 1) is fully enqueued (its slot is launch_seq mod nslot now that
+  // launch_seq = n + 1; nslot = 1: this launch itself)
+  if (!rc) rc = advance_runs(c, (int)(c->launch_seq % c->nslot));
   debug_counters().batch_ns[0].fetch_add(
       std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
       std::memory_order_relaxed);
