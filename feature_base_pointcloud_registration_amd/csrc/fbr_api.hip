@@ -5,7 +5,8 @@
 //   memset owners -> k_project -> k_rowcount/k_compact        (imageProjection.cpp:583-670)
 //   -> k_features (per ring) -> k_voxel_grid (per ring surf)  (featureExtraction.h:109-294)
 //   -> k_concat -> k_voxel_grid x2 (downsampleCurrentScan)    (mapOptmization.h:981-993)
-//   -> k_gn_init -> [k_gn_residual -> k_gn_solve] x max_iter  (mapOptmization.h:1403-1442)
+//   -> k_gn_init -> [k_gn_knn -> k_gn_residual -> k_gn_solve] x max_iter
+//                                                             (mapOptmization.h:1403-1442)
 //   -> k_gn_finalize                                          (transformUpdate, :1444-1479)
 // with no host round trip between stages (converged jobs drop out on the device).
 #include <hip/hip_runtime.h>
@@ -139,7 +140,7 @@ struct fbr_ctx {
   int nsub_pref = 3;                  // sub-batches per batch launch (FBR_NSUB overrides): 3 unpipelined (at
                                       // B = 128: 2 -> 76.1k, 3 -> 78.5k, 4 -> 46.7k scans/s), 1 pipelined
   int H = 0, W = 0, Bcap = 0;
-  // Batch launches rotate over nslot work slots (FBR_PIPE, default 2; 1 when max_batch = 1): the
+  // Batch launches rotate over nslot work slots (FBR_PIPE, default 3; 1 when max_batch = 1): the
   // next launch's projection / features overlap the previous ones' Gauss-Newton tails.  Work arrays
   // hold Bwork = nslot * Bcap jobs; inputs hold Bcap.
   static constexpr int kMaxSlots = 3;
@@ -529,6 +530,11 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
     return e ? std::atoi(e) : 1;
   }();
   a.fit_cache = fit_cache;
+  static const int res_mfma = [] {  // opt-in: -3 % gn_residual, headline within noise
+    const char* e = std::getenv("FBR_RES_MFMA");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.res_mfma = res_mfma;
   a.iter_flags = c->d_iter_flags + (int64_t)sb.k * mi;
   a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 2 * mi;
   a.desk_mode = c->desk_any ? c->d_desk_mode + sb.in0 : nullptr;
@@ -1188,12 +1194,14 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   if (const char* e = std::getenv("FBR_NSUB")) c->nsub_pref = std::max(1, std::min(kMaxSub, std::atoi(e)));
   static const int pipe = [] {  // launch slots (0 / 1: no pipelining)
     const char* e = std::getenv("FBR_PIPE");
-    return e ? std::max(1, std::min(fbr_ctx::kMaxSlots, std::atoi(e) <= 0 ? 1 : std::atoi(e))) : 2;
+    return e ? std::max(1, std::min(fbr_ctx::kMaxSlots, std::atoi(e) <= 0 ? 1 : std::atoi(e))) : 3;
   }();
   c->nslot = p->max_batch > 1 ? pipe : 1;
   // Pipelined, one sub-batch per launch is best at every batch size (the two launches in flight
   // overlap as the sub-batches did): B = 128 / 256 / 1024 give 91.8k / 96.7k / 97.4k scans/s
-  // against 83.2k / 93.1k / 96.7k with 3 sub-batches (profiles/r04f_pipe_nsub_sweep.txt).
+  // against 83.2k / 93.1k / 96.7k with 3 sub-batches (profiles/r04f_pipe_nsub_sweep.txt).  Three
+  // slots (the default) against two: B = 128 / 256 96.8k / 100.1k vs 92.6k / 97.8k, B = 1024 equal
+  // (profiles/r04n_mfma_pipe_cell_ab.txt).
   if (c->nslot > 1) c->nsub_pref = std::getenv("FBR_NSUB") ? std::min(c->nsub_pref, kMaxSub / c->nslot) : 1;
   c->Bwork = (int64_t)c->nslot * c->Bcap;
   const int64_t B = c->Bcap, Bw = c->Bwork, HW = c->HW, H = c->H;

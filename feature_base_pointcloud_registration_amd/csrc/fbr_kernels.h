@@ -261,6 +261,7 @@ struct GnArgs {
   int8_t* fits;              // [max_items][256] fit cache state (0 none, 1 fitted, 2 rejected)
   int8_t* nsame;             // [max_items][256] 1: this iteration's neighbours equal the previous ones
   int fit_cache;             // reuse cached fits (FBR_FIT_CACHE, default 1)
+  int res_mfma;              // item partials on the matrix cores (FBR_RES_MFMA=1; default: the butterfly)
   unsigned long long* iter_flags;  // host-mapped [max_iter]: (generation << 32) | jobs still active
   int32_t* iter_cnt;         // [max_iter][2] active-job count / finished workgroups (zeroed per solve)
   const int32_t* desk_mode;  // [B] kDesk* bits or null (transformUpdate's IMU slerp, :1447-1474)

@@ -1,5 +1,5 @@
-// k_keyframe.hip — SURVEY §8(f) row 4: the LIO-SAM keyframe local map on the device, and a
-// device-side build of the kNN map grid.
+// k_keyframe.hip — SURVEY §8(f) row 4: the LIO-SAM keyframe local map on the device (the kNN
+// map grid over it is built by k_grid.hip's grid_build_device).
 //
 // Reference: /root/reference/src/mapOptmization.h
 //   extractCloud()        :909-955  transformPointCloud of every selected keyframe's corner / surf

@@ -99,8 +99,9 @@ __global__ void k_gn_init(GnArgs a) {
 __global__ void __launch_bounds__(kResThreads)
 k_gn_residual(GnArgs a) {
   __shared__ double red[kResThreads / 64][28];
+  __shared__ __attribute__((aligned(16))) float stage[kResThreads * 8];
   const int nitems = a.nitems[0];
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x) gn_residual_item(a, it, red);
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) gn_residual_item(a, it, red, stage);
 }
 
 

@@ -353,9 +353,9 @@ int fbr_debug_counters(long long* launches, long long* host_syncs, long long* fl
  * computes the per-job CropBox map statistics, which depend only on the guesses); launch enqueues
  * the whole path for the staged batch (asynchronous, inputs are not modified so it may be
  * re-launched); wait blocks; results copies the latest launch's poses/stats out.
- * Launches are pipelined two deep (unless FBR_PIPE=0 or max_batch = 1): consecutive launches use
- * alternate work buffers and streams, and fbr_batch_launch returns once the *previous* launch is
- * fully enqueued, leaving the tail of its own Gauss-Newton loop (whose length the device decides)
+ * Launches are pipelined three deep (FBR_PIPE = 1..3, default 3; 1 when max_batch = 1):
+ * consecutive launches rotate over the work buffers and streams of the launch slots, and
+ * fbr_batch_launch returns once the launch two before it is fully enqueued, leaving the tail of its own Gauss-Newton loop (whose length the device decides)
  * to the next launch / flush / wait call.  So launch n's projection and features run beside launch
  * n-1's last iterations.  The single-scan entry points (fbr_project, fbr_register*,
  * fbr_process_scan) share the device buffers and drop a staged batch (after enqueueing every

@@ -99,11 +99,19 @@ with api.Context(P) as ctx:
     ctx.batch_wait()
     p0, s0 = ctx.batch_results()
     ids = []
+
+    def drain():  # every launch whose records are ready, oldest first
+        while True:
+            lid = ctx.batch_export_ready(buf[min(len(ids), 3)].data_ptr())[0]
+            if lid < 0:
+                return
+            ids.append(lid)
+
     for k in range(3):
         ctx.batch_launch()
-        ids.append(ctx.batch_export_ready(buf[k].data_ptr())[0])
+        drain()
     ctx.batch_flush()
-    ids.append(ctx.batch_export_ready(buf[3].data_ptr())[0])
+    drain()
     again = ctx.batch_export_ready(buf[3].data_ptr())[0]
     ctx.batch_wait()
     p1, s1 = ctx.batch_results()
@@ -116,19 +124,20 @@ print(json.dumps({"ids": ids, "again": again,
 """
 
 
-def test_pipelined_launches_are_bit_identical_and_export_in_order():
-    """Consecutive fbr_batch_launch calls run two deep (alternate work slots and streams; a launch
-    returns once the previous one is fully enqueued).  Every launch of the same staged batch gives
-    the same bytes, and fbr_batch_export_ready hands out every launch's records, in launch order.
+@pytest.mark.parametrize("pipe", ["2", "3"])
+def test_pipelined_launches_are_bit_identical_and_export_in_order(pipe):
+    """Consecutive fbr_batch_launch calls run FBR_PIPE deep (rotating work slots and streams; a
+    launch returns once the launch pipe - 1 before it is fully enqueued).  Every launch of the same
+    staged batch gives the same bytes, and fbr_batch_export_ready hands out every launch's records
+    once, in launch order (-1 while the oldest unexported launch is still being enqueued).
     (Child process: torch, which allocates the export buffers, must initialise HIP first.)"""
     import json
     import subprocess
     import sys
     from conftest import REPO
     r = subprocess.run([sys.executable, "-c", _PIPE_CHILD % {"repo": REPO}], capture_output=True, text=True,
-                       timeout=300, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+                       timeout=300, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", FBR_PIPE=pipe))
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    # after launch n returns, launch n-1 is the latest fully enqueued one (launch 0 was waited for)
     assert d["ids"] == [0, 1, 2, 3] and d["again"] == -1, d
     assert d["same_results"] and d["exports_equal"] == [True] * 4 and d["status_ok"] == 24, d
