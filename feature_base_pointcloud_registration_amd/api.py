@@ -167,6 +167,19 @@ def batch_times(reset=False):
     return tuple(x * 1e-9 for x in v)
 
 
+def knn_tile_stats(reset=False):
+    """Wave-tile kNN counters since the last reset: (queries, tile-served queries, tile loads,
+    points loaded into tiles, tile failures, of which: box too large, load too long, too many
+    points), or None unless FBR_KNN_TILE_STATS=1 -- diagnostic (fbr_diag_knn_tile_stats,
+    k_knn_tile.hip)."""
+    f = lib().fbr_diag_knn_tile_stats
+    f.restype, f.argtypes = ctypes.c_int, [_VP, ctypes.c_int]
+    v = (ctypes.c_ulonglong * 8)()
+    if f(v, int(reset)) != 0:
+        return None
+    return tuple(int(x) for x in v)
+
+
 def selftest_math(a, b):
     """Device sqrt(|a|), a/b, atan2f(a,b), a*b+b*a-a, sinf(a), cosf(a) (see fbr_selftest_math)."""
     a = np.ascontiguousarray(a, np.float32)

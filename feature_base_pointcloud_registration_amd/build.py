@@ -18,7 +18,7 @@ REPO = os.path.dirname(HERE)
 OBJ = os.path.join(HERE, "build")
 
 HIP_SOURCES = ["k_project.hip", "k_features.hip", "k_voxel.hip", "k_register.hip", "k_knn_r1.hip", "k_knn_r1f.hip",
-               "k_knn_r2.hip", "k_knn_r2f.hip", "k_knn_r4.hip", "k_knn_r4f.hip", "k_keyframe.hip", "k_grid.hip",
+               "k_knn_r2.hip", "k_knn_r2f.hip", "k_knn_r4.hip", "k_knn_r4f.hip", "k_knn_tile.hip", "k_keyframe.hip", "k_grid.hip",
                "k_selftest.hip", "fbr_api.hip"]
 HOST_SOURCES = ["fbr_pcd.cpp", "fbr_msg.cpp", "fbr_imu.cpp"]  # host-only C++ in the same library (PCD, PointCloud2, IMU)
 ARCH = os.environ.get("FBR_OFFLOAD_ARCH", "gfx950")

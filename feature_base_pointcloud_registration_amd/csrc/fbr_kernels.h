@@ -274,6 +274,8 @@ struct GnArgs {
 #ifdef FBR_KNN_STATS
 unsigned long long* knn_stats_buffer();
 #endif
+// iterations >= 1 on dense maps: the wave-tile search (k_knn_tile.hip); false = not applicable
+bool launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int use_prev);
 void launch_gn_init(hipStream_t s, const GnArgs& a);
 // fused: kNN + residual row + item partial in one launch (launch_gn_residual is then skipped)
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fused);

@@ -252,6 +252,7 @@ void launch_gn_knn_f(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
 
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fused) {
   const int use_prev = iter > 0;  // nbr holds this launch's previous iteration
+  if (!fused && launch_gn_knn_tile(s, a, grid, use_prev)) return;  // dense maps: LDS tiles (k_knn_tile.hip)
   if (fused) launch_gn_knn_f<true>(s, a, grid, use_prev);
   else launch_gn_knn_f<false>(s, a, grid, use_prev);
 }

@@ -404,23 +404,27 @@ def test_full_size_batch_properties(c2_map):
 
 
 # ------------------------------------------------------------------------------- C3 / C5 configs
-def _cfg_batch_in_child(cfg, scans, guesses, env):
+def _cfg_batch_in_child(cfg, scans, guesses, env, tile_stats=False):
     """Poses (B, 6) and REG_STATS records of a batch of `cfg` scans registered in a child process
-    with extra environment knobs (read once per process), against the config's map."""
+    with extra environment knobs (read once per process), against the config's map (tile_stats:
+    also the child's api.knn_tile_stats(), FBR_KNN_TILE_STATS=1)."""
     import subprocess
     import sys
     from feature_base_pointcloud_registration_amd.fbr_types import REG_STATS
     n = len(scans)
     path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_child_%s_jobs.npz" % cfg)
     np.savez(path, *scans, guesses=np.asarray(guesses, np.float32))
+    tail = " + np.array(api.knn_tile_stats(), np.uint64).tobytes()" if tile_stats else ""
     code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api, synth; "
             "d = np.load(%r); scans = [d['arr_%%d' %% k] for k in range(%d)]; "
             "c = api.Context(synth.config_params(%r, max_batch=%d)); c.set_map(*synth.config_map(%r)); "
-            "p, s = c.process_batch(scans, d['guesses']); sys.stdout.buffer.write(p.tobytes() + s.tobytes())"
-            % (REPO, path, n, cfg, n, cfg))
+            "p, s = c.process_batch(scans, d['guesses']); sys.stdout.buffer.write(p.tobytes() + s.tobytes()%s)"
+            % (REPO, path, n, cfg, n, cfg, tail))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, **env), timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     poses = np.frombuffer(r.stdout[:n * 24], np.float32).reshape(n, 6)
+    if tile_stats:
+        return poses, np.frombuffer(r.stdout[n * 24:-64], REG_STATS), np.frombuffer(r.stdout[-64:], np.uint64)
     return poses, np.frombuffer(r.stdout[n * 24:], REG_STATS)
 
 
@@ -455,6 +459,25 @@ def test_c3_ouster_registration_matches_oracle():
         assert_pose_close(poses[k], po)
         assert np.abs(poses[k][3:] - gt[3:]).max() < 0.05
         assert_exact_order_bitwise(pe[k], se[k], po, so)
+
+
+def test_knn_tile_is_bit_identical_to_global_search():
+    """Dense maps from the second Gauss-Newton iteration on: the LDS wave-tile search
+    (k_knn_tile.hip) against the global grid search (FBR_KNN_TILE=0), each in a child process:
+    identical poses and stats bytes on C3 jobs, and most queries served from the tiles.  C3's
+    neighbours are ~0.2 m away, beyond the default tile reach (one 0.125 m cell, sized for C5), so
+    the tiles here have 0.25 m cells and a two-cell reach (fine cells spanning two global x cells:
+    fine_to_global's s < 0 branch)."""
+    jobs = synth.make_jobs("C3", 3, base_seed=5100)
+    scans, guesses = [j[0] for j in jobs], np.stack([j[1] for j in jobs])
+    p0, s0 = _cfg_batch_in_child("C3", scans, guesses, {"FBR_KNN_TILE": "0"})
+    p1, s1, ts = _cfg_batch_in_child("C3", scans, guesses, {"FBR_KNN_TILE": "1", "FBR_KNN_TILE_STATS": "1",
+                                                            "FBR_KNN_TILE_CELL": "0.25", "FBR_KNN_TILE_REACH": "2"},
+                                     tile_stats=True)
+    assert p0.tobytes() == p1.tobytes() and s0.tobytes() == s1.tobytes()
+    assert (s1["status"] == 0).all()
+    queries, served = int(ts[0]), int(ts[1])
+    assert queries > 0 and served > 0.5 * queries, ts
 
 
 def test_c5_dense_scan_matches_oracle():

@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Wave-tile kNN counters (k_knn_tile.hip) and wall time of one batch: usage
+tile_probe.py CONFIG B [REPEAT].  Run with FBR_KNN_TILE_STATS=1 (and the FBR_KNN_TILE_* knobs)."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: F401  (HIP runtime first, as bench.py)
+
+from feature_base_pointcloud_registration_amd import api, synth  # noqa: E402
+
+cfg, B = sys.argv[1], int(sys.argv[2])
+rep = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+jobs = synth.make_jobs(cfg, B, base_seed=9100)
+with api.Context(synth.config_params(cfg, max_batch=B)) as c:
+    c.set_map(*synth.config_map(cfg))
+    scans, guesses = [j[0] for j in jobs], np.stack([j[1] for j in jobs])
+    c.process_batch(scans, guesses)
+    api.knn_tile_stats(reset=True)
+    t = time.perf_counter()
+    for _ in range(rep):
+        p, s = c.process_batch(scans, guesses)
+    dt = (time.perf_counter() - t) / rep
+    ts = api.knn_tile_stats()
+keys = ["queries", "served", "loads", "loaded_pts", "fails", "fail_box", "fail_load", "fail_pts"]
+print(json.dumps({"cfg": cfg, "B": B, "env": {k: v for k, v in os.environ.items() if k.startswith("FBR_KNN")},
+                  "s_per_batch": round(dt, 4), "status_ok": int((s["status"] == 0).sum()),
+                  "iters": float(s["iterations"].mean()),
+                  "tile": dict(zip(keys, ts)) if ts else None}))
