@@ -72,14 +72,114 @@ __device__ __forceinline__ void fine_to_global(int f0, int f1, int s, int& g0, i
   }
 }
 
-// sx / sy: log2(inv_f / inv_x), log2(inv_f / inv_cell) (fine_to_global).
+// Load the map points of fine-cell box [X0, X0 + Dx) x [Y0, Y0 + Dy) x [Z0, Z0 + Dz) that lie
+// inside the CropBox into T, counting-sorted by fine cell (T.cs[c] = end of cell c).  Wave-uniform
+// result: false when the box, its global rows or its points exceed the tile.
+template <int PTS, int CELLS>
+__device__ bool tile_build(TileLds<PTS, CELLS>& T, const MapGrid& mg, int X0, int Y0, int Z0, int Dx, int Dy, int Dz,
+                           float inv_f, int sx, int sy, const float* bmin, const float* bmax,
+                           unsigned long long* tile_stats) {
+  const int lane = threadIdx.x;
+  const bool small = Dx <= CELLS && Dy <= CELLS && Dz <= CELLS && (int64_t)Dx * Dy * Dz <= CELLS;
+  const int ncell = small ? Dx * Dy * Dz : CELLS + 1;
+  // global cells holding the box (fine_to_global: x by sx, y and z by sy)
+  int ax, bx, ay, by, az, bz;
+  fine_to_global(X0, X0 + Dx - 1, sx, ax, bx);
+  fine_to_global(Y0, Y0 + Dy - 1, sy, ay, by);
+  fine_to_global(Z0, Z0 + Dz - 1, sy, az, bz);
+  const int gx0 = max(ax - (int)mg.g.origin[0], 0), gx1 = min(bx - (int)mg.g.origin[0], mg.g.dims[0] - 1);
+  const int gy0 = max(ay - (int)mg.g.origin[1], 0), gy1 = min(by - (int)mg.g.origin[1], mg.g.dims[1] - 1);
+  const int gz0 = max(az - (int)mg.g.origin[2], 0), gz1 = min(bz - (int)mg.g.origin[2], mg.g.dims[2] - 1);
+  const int ny = gy1 - gy0 + 1, nz = gz1 - gz0 + 1;
+  const int nrows = (gx0 <= gx1 && ny > 0 && nz > 0) ? ny * nz : 0;
+  if (!(ncell <= CELLS && nrows <= kTileLoadRows)) {
+    if (tile_stats && lane == 0) atomicAdd(&tile_stats[5], 1ull);
+    return false;
+  }
+  int len = 0;
+  if (lane < nrows) {
+    const int y = gy0 + lane % ny, z = gz0 + lane / ny;
+    const int rowbase = (z * mg.g.dims[1] + y) * mg.g.dims[0];
+    const int b = mg.cell_start[rowbase + gx0], e = mg.cell_start[rowbase + gx1 + 1];
+    T.rows[lane] = make_int2(b, e);
+    len = e - b;
+  }
+  int inc = len;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(inc, off);
+    if (lane >= off) inc += y;
+  }
+  if (lane < nrows) T.rpre[lane + 1] = inc;
+  if (lane == 0) T.rpre[0] = 0;
+  const int L = __shfl(inc, 63);
+  if (L > kTileLoadMax) {
+    if (tile_stats && lane == 0) atomicAdd(&tile_stats[6], 1ull);
+    return false;
+  }
+  for (int c = lane; c < ncell; c += 64) T.cs[c] = 0u;
+  __syncthreads();
+  const float bx0 = bmin[0], by0 = bmin[1], bz0 = bmin[2], bx1 = bmax[0], by1 = bmax[1], bz1 = bmax[2];
+  // pass 1: per-cell counts of the points inside the box and the CropBox
+  int j = 0;
+  for (int t = lane; t < L; t += 64) {
+    while (T.rpre[j + 1] <= t) ++j;
+    const float4 q = mg.pts[T.rows[j].x + (t - T.rpre[j])];
+    const int cx = fine(q.x, inv_f) - X0, cy = fine(q.y, inv_f) - Y0, cz = fine(q.z, inv_f) - Z0;
+    const bool in = (unsigned)cx < (unsigned)Dx && (unsigned)cy < (unsigned)Dy && (unsigned)cz < (unsigned)Dz &&
+                    !((q.x < bx0) | (q.y < by0) | (q.z < bz0) | (q.x > bx1) | (q.y > by1) | (q.z > bz1));
+    if (in) atomicAdd(&T.cs[cx + Dx * (cy + Dy * cz)], 1u);
+  }
+  __syncthreads();
+  // exclusive starts, 64 cells per step (a wave scan plus the running carry)
+  uint32_t carry = 0;
+  for (int c0 = 0; c0 < ncell; c0 += 64) {
+    const int c = c0 + lane;
+    const uint32_t n = c < ncell ? T.cs[c] : 0u;
+    uint32_t incs = n;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(incs, off);
+      if (lane >= off) incs += y;
+    }
+    if (c < ncell) T.cs[c] = carry + incs - n;
+    carry += __shfl(incs, 63);
+  }
+  if (carry > (uint32_t)PTS) {
+    if (tile_stats && lane == 0) atomicAdd(&tile_stats[7], 1ull);
+    __syncthreads();
+    return false;
+  }
+  const uint32_t total = carry;
+  __syncthreads();
+  // pass 2: scatter (cs[c] ends as the end of cell c)
+  j = 0;
+  for (int t = lane; t < L; t += 64) {
+    while (T.rpre[j + 1] <= t) ++j;
+    const float4 q = mg.pts[T.rows[j].x + (t - T.rpre[j])];
+    const int cx = fine(q.x, inv_f) - X0, cy = fine(q.y, inv_f) - Y0, cz = fine(q.z, inv_f) - Z0;
+    const bool in = (unsigned)cx < (unsigned)Dx && (unsigned)cy < (unsigned)Dy && (unsigned)cz < (unsigned)Dz &&
+                    !((q.x < bx0) | (q.y < by0) | (q.z < bz0) | (q.x > bx1) | (q.y > by1) | (q.z > bz1));
+    if (in) T.pts[atomicAdd(&T.cs[cx + Dx * (cy + Dy * cz)], 1u)] = q;
+  }
+  __syncthreads();
+  if (tile_stats && lane == 0) {
+    atomicAdd(&tile_stats[2], 1ull);
+    atomicAdd(&tile_stats[3], (unsigned long long)total);
+  }
+  return true;
+}
+
+// sx / sy: log2(inv_f / inv_x), log2(inv_f / inv_cell) (fine_to_global).  Clusters: the eligible
+// lanes are served in up to kRounds tiles, each around the lowest still-pending lane (the anchor):
+// lanes whose bound box lies within `span` fine cells of the anchor's join its tile, so one far
+// query (Morton order jumps between octree blocks) does not blow up the box of the others.
 // tile_stats (diagnostic, may be null): [queries, tile-served, tile loads, points loaded, tile
 // fails, of which: box over CELLS cells or kTileLoadRows rows, load over kTileLoadMax, over PTS].
 template <int R, int RX, int PTS, int CELLS>
-__global__ void __launch_bounds__(64) k_gn_knn_tile(GnArgs a, float inv_f, int sx, int sy, float rmax2,
-                                                   unsigned long long* tile_stats) {
+__global__ void __launch_bounds__(64) k_gn_knn_tile(GnArgs a, float inv_f, int sx, int sy, float rmax2, int span,
+                                                   int rounds, unsigned long long* tile_stats) {
   static_assert(CELLS % 64 == 0 && CELLS <= 4096, "cell starts: CELLS / 64 per lane");
-  constexpr int kTileCells = CELLS, kTilePts = PTS, CPL = CELLS / 64;
   __shared__ TileLds<PTS, CELLS> T;
   const int lane = threadIdx.x;
   const int nitems = a.nitems[0];
@@ -94,12 +194,11 @@ __global__ void __launch_bounds__(64) k_gn_knn_tile(GnArgs a, float inv_f, int s
     const bool has_q = tid < item.w;
     // ---- the query, its previous neighbours and bound (gn_knn_block's arithmetic) ----
     float x0 = 0.0f, y0 = 0.0f, z0 = 0.0f, bound = __int_as_float(0x7f800000);
-    float4 p = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     int32_t oid[5] = {-1, -1, -1, -1, -1};
     int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
     bool have_prev = false;
     if (has_q) {
-      p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
+      const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
       const float* Tm = g.T;
       x0 = Tm[0] * p.x + Tm[1] * p.y + Tm[2] * p.z + Tm[3];
       y0 = Tm[4] * p.x + Tm[5] * p.y + Tm[6] * p.z + Tm[7];
@@ -121,7 +220,7 @@ __global__ void __launch_bounds__(64) k_gn_knn_tile(GnArgs a, float inv_f, int s
         bound = mx;
       }
     }
-    bool el = has_q && have_prev && bound <= rmax2;
+    const bool el = has_q && have_prev && bound <= rmax2;
     int lx0 = 0, lx1 = -1, ly0 = 0, ly1 = -1, lz0 = 0, lz1 = -1;
     if (el) {
       const float r_up = sqrtf(bound) * 1.0078125f + 1e-6f * (1.0f + fabsf(x0) + fabsf(y0) + fabsf(z0));
@@ -129,140 +228,55 @@ __global__ void __launch_bounds__(64) k_gn_knn_tile(GnArgs a, float inv_f, int s
       ly0 = fine(y0 - r_up, inv_f); ly1 = fine(y0 + r_up, inv_f);
       lz0 = fine(z0 - r_up, inv_f); lz1 = fine(z0 + r_up, inv_f);
     }
-    const float bx0 = g.crop_min[0], by0 = g.crop_min[1], bz0 = g.crop_min[2];
-    const float bx1 = g.crop_max[0], by1 = g.crop_max[1], bz1 = g.crop_max[2];
     Knn5 nn;
 #pragma unroll
     for (int t = 0; t < 5; ++t) nn.k[t] = kKnnEmpty;
-    bool tile_ok = __ballot(el) != 0ull;
-    // ---- the wave's tile box (fine cells) and its global rows ----
-    int X0 = 0, Y0 = 0, Z0 = 0, Dx = 0, Dy = 0, ncell = 0;
-    if (tile_ok) {
+    bool served = false;
+    uint64_t pending = __ballot(el);
+    for (int rd = 0; rd < rounds && pending; ++rd) {
+      // ---- this round's cluster and its tile box (fine cells) ----
+      const int an = __ffsll((unsigned long long)pending) - 1;
+      const int ax0 = __shfl(lx0, an), ax1 = __shfl(lx1, an), ay0 = __shfl(ly0, an), ay1 = __shfl(ly1, an);
+      const int az0 = __shfl(lz0, an), az1 = __shfl(lz1, an);
+      const bool mine = ((pending >> lane) & 1ull) && lx0 >= ax0 - span && lx1 <= ax1 + span && ly0 >= ay0 - span &&
+                        ly1 <= ay1 + span && lz0 >= az0 - span && lz1 <= az1 + span;
+      const uint64_t cl = __ballot(mine);  // holds the anchor
+      pending &= ~cl;
       const int big = 0x3fffffff;
-      X0 = wave_min_i(el ? lx0 : big); Y0 = wave_min_i(el ? ly0 : big); Z0 = wave_min_i(el ? lz0 : big);
-      const int X1 = wave_max_i(el ? lx1 : -big), Y1 = wave_max_i(el ? ly1 : -big), Z1 = wave_max_i(el ? lz1 : -big);
-      Dx = X1 - X0 + 1;
-      Dy = Y1 - Y0 + 1;
-      const int Dz = Z1 - Z0 + 1;
-      const bool small = Dx <= kTileCells && Dy <= kTileCells && Dz <= kTileCells;
-      ncell = small && (int64_t)Dx * Dy * Dz <= kTileCells ? Dx * Dy * Dz : kTileCells + 1;
-      // global cells holding the box (the fine cells nest in them; x: sx, y and z: sy)
-      int ax, bx, ay, by, az, bz;
-      fine_to_global(X0, X1, sx, ax, bx);
-      fine_to_global(Y0, Y1, sy, ay, by);
-      fine_to_global(Z0, Z1, sy, az, bz);
-      const int gx0 = max(ax - (int)mg.g.origin[0], 0), gx1 = min(bx - (int)mg.g.origin[0], mg.g.dims[0] - 1);
-      const int gy0 = max(ay - (int)mg.g.origin[1], 0), gy1 = min(by - (int)mg.g.origin[1], mg.g.dims[1] - 1);
-      const int gz0 = max(az - (int)mg.g.origin[2], 0), gz1 = min(bz - (int)mg.g.origin[2], mg.g.dims[2] - 1);
-      const int ny = gy1 - gy0 + 1, nz = gz1 - gz0 + 1;
-      const int nrows = (gx0 <= gx1 && ny > 0 && nz > 0) ? ny * nz : 0;
-      tile_ok = ncell <= kTileCells && nrows <= kTileLoadRows;
-      if (!tile_ok && tile_stats && lane == 0) atomicAdd(&tile_stats[5], 1ull);
-      if (tile_ok) {
-        int len = 0;
-        if (lane < nrows) {
-          const int y = gy0 + lane % ny, z = gz0 + lane / ny;
-          const int rowbase = (z * mg.g.dims[1] + y) * mg.g.dims[0];
-          const int b = mg.cell_start[rowbase + gx0], e = mg.cell_start[rowbase + gx1 + 1];
-          T.rows[lane] = make_int2(b, e);
-          len = e - b;
-        }
-        int inc = len;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          const int y = __shfl_up(inc, off);
-          if (lane >= off) inc += y;
-        }
-        if (lane < nrows) T.rpre[lane + 1] = inc;
-        if (lane == 0) T.rpre[0] = 0;
-        const int L = __shfl(inc, 63);
-        tile_ok = L <= kTileLoadMax;
-        if (!tile_ok && tile_stats && lane == 0) atomicAdd(&tile_stats[6], 1ull);
-        for (int c = lane; c < ncell; c += 64) T.cs[c] = 0u;
-        __syncthreads();
-        // ---- pass 1: per-cell counts of the points inside the box and the CropBox ----
-        if (tile_ok) {
-          int j = 0;
-          for (int t = lane; t < L; t += 64) {
-            while (T.rpre[j + 1] <= t) ++j;
-            const float4 q = mg.pts[T.rows[j].x + (t - T.rpre[j])];
-            const int cx = fine(q.x, inv_f) - X0, cy = fine(q.y, inv_f) - Y0, cz = fine(q.z, inv_f) - Z0;
-            const bool in = (unsigned)cx < (unsigned)Dx && (unsigned)cy < (unsigned)Dy && (unsigned)cz < (unsigned)Dz &&
-                            !((q.x < bx0) | (q.y < by0) | (q.z < bz0) | (q.x > bx1) | (q.y > by1) | (q.z > bz1));
-            if (in) atomicAdd(&T.cs[cx + Dx * (cy + Dy * cz)], 1u);
+      const int X0 = wave_min_i(mine ? lx0 : big), Y0 = wave_min_i(mine ? ly0 : big), Z0 = wave_min_i(mine ? lz0 : big);
+      const int Dx = wave_max_i(mine ? lx1 : -big) - X0 + 1, Dy = wave_max_i(mine ? ly1 : -big) - Y0 + 1;
+      const int Dz = wave_max_i(mine ? lz1 : -big) - Z0 + 1;
+      if (!tile_build(T, mg, X0, Y0, Z0, Dx, Dy, Dz, inv_f, sx, sy, g.crop_min, g.crop_max, tile_stats)) {
+        if (tile_stats && lane == 0) atomicAdd(&tile_stats[4], 1ull);
+        continue;  // the cluster's lanes take the global search
+      }
+      // ---- the tile search: the lane's fine rows (y, z), each one contiguous x-cell range ----
+      if (mine) {
+        served = true;
+        const int nyr = ly1 - ly0 + 1, nr = nyr * (lz1 - lz0 + 1);
+        int r = 0, i = 0, e = 0;
+        while (true) {
+          if (i >= e) {
+            if (r >= nr) break;
+            const int y = ly0 + r % nyr - Y0, z = lz0 + r / nyr - Z0;
+            const int base = Dx * (y + Dy * z);
+            const int ca = base + (lx0 - X0), cb = base + (lx1 - X0);
+            i = ca ? (int)T.cs[ca - 1] : 0;
+            e = (int)T.cs[cb];
+            ++r;
+            continue;
           }
-          __syncthreads();
-          // exclusive starts (CPL cells per lane)
-          uint32_t loc[CPL], sum = 0;
-#pragma unroll
-          for (int k = 0; k < CPL; ++k) {
-            const int c = lane * CPL + k;
-            loc[k] = c < ncell ? T.cs[c] : 0u;
-            sum += loc[k];
-          }
-          uint32_t incs = sum;
-#pragma unroll
-          for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incs, off);
-            if (lane >= off) incs += y;
-          }
-          const uint32_t total = __shfl(incs, 63);
-          tile_ok = total <= (uint32_t)kTilePts;
-          if (!tile_ok && tile_stats && lane == 0) atomicAdd(&tile_stats[7], 1ull);
-          uint32_t run = incs - sum;
-          __syncthreads();
-#pragma unroll
-          for (int k = 0; k < CPL; ++k) {
-            const int c = lane * CPL + k;
-            if (c < ncell) T.cs[c] = run;
-            run += loc[k];
-          }
-          __syncthreads();
-          // ---- pass 2: scatter (cs[c] ends as the end of cell c) ----
-          if (tile_ok) {
-            j = 0;
-            for (int t = lane; t < L; t += 64) {
-              while (T.rpre[j + 1] <= t) ++j;
-              const float4 q = mg.pts[T.rows[j].x + (t - T.rpre[j])];
-              const int cx = fine(q.x, inv_f) - X0, cy = fine(q.y, inv_f) - Y0, cz = fine(q.z, inv_f) - Z0;
-              const bool in = (unsigned)cx < (unsigned)Dx && (unsigned)cy < (unsigned)Dy && (unsigned)cz < (unsigned)Dz &&
-                              !((q.x < bx0) | (q.y < by0) | (q.z < bz0) | (q.x > bx1) | (q.y > by1) | (q.z > bz1));
-              if (in) T.pts[atomicAdd(&T.cs[cx + Dx * (cy + Dy * cz)], 1u)] = q;
-            }
-            __syncthreads();
-          }
-          if (tile_stats && lane == 0) {
-            atomicAdd(&tile_stats[2], 1ull);
-            atomicAdd(&tile_stats[3], (unsigned long long)total);
-          }
+          const float4 q = T.pts[i++];
+          float dist = 0.0f, diff;
+          diff = x0 - q.x; dist += diff * diff;  // flann::L2_Simple
+          diff = y0 - q.y; dist += diff * diff;
+          diff = z0 - q.z; dist += diff * diff;
+          knn_insert(nn, ((unsigned long long)(unsigned)__float_as_int(dist) << 32) | (unsigned)__float_as_int(q.w));
         }
       }
-      if (!tile_ok && tile_stats && lane == 0) atomicAdd(&tile_stats[4], 1ull);
+      __syncthreads();  // the next round rebuilds the tile
     }
-    // ---- the tile search: the lane's fine rows (y, z), each one contiguous x-cell range ----
-    const bool served = tile_ok && el;
-    if (served) {
-      const int nyr = ly1 - ly0 + 1, nr = nyr * (lz1 - lz0 + 1);
-      int r = 0, i = 0, e = 0;
-      while (true) {
-        if (i >= e) {
-          if (r >= nr) break;
-          const int y = ly0 + r % nyr - Y0, z = lz0 + r / nyr - Z0;
-          const int base = Dx * (y + Dy * z);
-          const int ca = base + (lx0 - X0), cb = base + (lx1 - X0);
-          i = ca ? (int)T.cs[ca - 1] : 0;
-          e = (int)T.cs[cb];
-          ++r;
-          continue;
-        }
-        const float4 q = T.pts[i++];
-        float dist = 0.0f, diff;
-        diff = x0 - q.x; dist += diff * diff;  // flann::L2_Simple
-        diff = y0 - q.y; dist += diff * diff;
-        diff = z0 - q.z; dist += diff * diff;
-        knn_insert(nn, ((unsigned long long)(unsigned)__float_as_int(dist) << 32) | (unsigned)__float_as_int(q.w));
-      }
-    } else if (has_q) {  // the global search
+    if (has_q && !served) {  // the global search
       unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       knn5_grid<R, RX, false, false, 1>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
       (void)ks;
@@ -330,10 +344,21 @@ bool launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int use_prev) 
     const char* e = std::getenv("FBR_KNN_TILE_CAP");
     return e ? std::max(0, std::min(2, std::atoi(e))) : 1;
   }();
+  static const int span = [] {  // cluster reach around the anchor's box, fine cells (FBR_KNN_TILE_SPAN)
+    const char* e = std::getenv("FBR_KNN_TILE_SPAN");
+    return e ? std::max(0, std::atoi(e)) : 3;
+  }();
+  static const int rounds = [] {  // tiles per wave (FBR_KNN_TILE_ROUNDS)
+    const char* e = std::getenv("FBR_KNN_TILE_ROUNDS");
+    return e ? std::max(1, std::min(64, std::atoi(e))) : 4;
+  }();
   unsigned long long* st = knn_tile_stats_buffer();
-  if (cap == 0) fbr_launch((k_gn_knn_tile<2, 8, 512, 512>), dim3(g4), dim3(64), 0, s, a, inv_f, sx, sy, rmax2, st);
-  else if (cap == 1) fbr_launch((k_gn_knn_tile<2, 8, 1024, 1024>), dim3(g4), dim3(64), 0, s, a, inv_f, sx, sy, rmax2, st);
-  else fbr_launch((k_gn_knn_tile<2, 8, 2048, 2048>), dim3(g4), dim3(64), 0, s, a, inv_f, sx, sy, rmax2, st);
+  if (cap == 0)
+    fbr_launch((k_gn_knn_tile<2, 8, 512, 512>), dim3(g4), dim3(64), 0, s, a, inv_f, sx, sy, rmax2, span, rounds, st);
+  else if (cap == 1)
+    fbr_launch((k_gn_knn_tile<2, 8, 1024, 1024>), dim3(g4), dim3(64), 0, s, a, inv_f, sx, sy, rmax2, span, rounds, st);
+  else
+    fbr_launch((k_gn_knn_tile<2, 8, 2048, 2048>), dim3(g4), dim3(64), 0, s, a, inv_f, sx, sy, rmax2, span, rounds, st);
   return true;
 }
 
