@@ -190,6 +190,7 @@ struct fbr_ctx {
   float* d_fitc = nullptr;     // [max_items][6][256] per-query fit cache (k_gn_residual)
   int8_t* d_fits = nullptr;    // [max_items][256]
   int8_t* d_nsame = nullptr;   // [max_items][256]
+  int32_t* d_fb_list = nullptr; // [max_items][256] wave-tile kNN: queries left to the grid search
   unsigned long long* h_iter_flags = nullptr;  // host-mapped, written by k_gn_solve
   unsigned long long* d_iter_flags = nullptr;  // its device address
   unsigned long long gn_gen = 0;
@@ -536,7 +537,8 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   }();
   a.res_mfma = res_mfma;
   a.iter_flags = c->d_iter_flags + (int64_t)sb.k * mi;
-  a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 2 * mi;
+  a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 3 * mi;  // [2 * mi] solve counters, [mi] fallback counts
+  a.fb_list = c->d_fb_list + ib * 256;
   a.desk_mode = c->desk_any ? c->d_desk_mode + sb.in0 : nullptr;
   a.desk = c->desk_any ? c->d_desk + sb.in0 : nullptr;
   a.nocrop = c->map_nocrop ? 1 : 0;
@@ -1242,7 +1244,8 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_nbr, (int64_t)c->max_items * 5 * 256) ||
               dalloc(&c->d_fitc, (int64_t)c->max_items * 6 * 256) || dalloc(&c->d_fits, (int64_t)c->max_items * 256) ||
               dalloc(&c->d_nsame, (int64_t)c->max_items * 256) ||
-              dalloc(&c->d_iter_cnt, kMaxSub * 2 * std::max(1, p->max_iterations)) ||
+              dalloc(&c->d_iter_cnt, kMaxSub * 3 * std::max(1, p->max_iterations)) ||
+              dalloc(&c->d_fb_list, (int64_t)c->max_items * 256) ||
               dalloc(&c->d_feat_scratch, Bw * H * feat_slot_bytes(c->W)) ||
               hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * kMaxSub * std::max(1, p->max_iterations),
                             hipHostMallocMapped) != hipSuccess ||
@@ -1283,7 +1286,7 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring, c->d_surf_ring_cnt, c->d_ring_box,
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
-                  c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_fitc, c->d_fits, c->d_nsame, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
+                  c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_fitc, c->d_fits, c->d_nsame, c->d_fb_list, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
                   c->d_desk, c->d_desk_mode, c->d_rowmin, c->d_choff,
                   c->d_kf_c, c->d_kf_s, c->d_kraw_c, c->d_kraw_s, c->d_kds_c, c->d_kds_s, c->d_kf_segs, c->d_bounds};
   for (void* p : ptrs)

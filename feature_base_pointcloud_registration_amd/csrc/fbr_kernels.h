@@ -263,7 +263,9 @@ struct GnArgs {
   int fit_cache;             // reuse cached fits (FBR_FIT_CACHE, default 1)
   int res_mfma;              // item partials on the matrix cores (FBR_RES_MFMA=1; default: the butterfly)
   unsigned long long* iter_flags;  // host-mapped [max_iter]: (generation << 32) | jobs still active
-  int32_t* iter_cnt;         // [max_iter][2] active-job count / finished workgroups (zeroed per solve)
+  int32_t* iter_cnt;         // [max_iter][2] active-job count / finished workgroups, then [max_iter]
+                             // wave-tile kNN fallback counts (zeroed by k_gn_init)
+  int32_t* fb_list;          // [max_items][256] wave-tile kNN: query slots left to the grid search
   const int32_t* desk_mode;  // [B] kDesk* bits or null (transformUpdate's IMU slerp, :1447-1474)
   const fbr_deskew_table* desk;  // [B]
   int nocrop;                // 1: keyframe local map, no CropBox (scan2MapOptimization on it)
@@ -275,7 +277,7 @@ struct GnArgs {
 unsigned long long* knn_stats_buffer();
 #endif
 // iterations >= 1 on dense maps: the wave-tile search (k_knn_tile.hip); false = not applicable
-bool launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int use_prev);
+bool launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int iter);
 void launch_gn_init(hipStream_t s, const GnArgs& a);
 // fused: kNN + residual row + item partial in one launch (launch_gn_residual is then skipped)
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fused);

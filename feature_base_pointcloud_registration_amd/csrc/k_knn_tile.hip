@@ -18,8 +18,9 @@
 //     cells in LDS (<= 512 points, <= 512 cells: 10 KB);
 //   * each query then walks only the fine cells of its own bound box, out of LDS, with no CropBox
 //     test per point (the tile holds in-box points only): ~6-25 points instead of ~140.
-// Lanes whose bound is missing (no previous neighbours), too large (> one fine cell), or whose tile
-// does not fit, run the global search (knn5_grid) instead.
+// Lanes whose bound is missing (no previous neighbours), too large (> `reach` fine cells), or whose
+// tile does not fit, are queued (fb_list) and a second launch runs the global search (knn5_grid)
+// on the queue, so they do not hold up the waves the tiles serve.
 //
 // Exactness.  The scanned set of every query still contains every crop-box point whose computed d2
 // is <= bound: a point with fl(q - p)^2 summed <= bound has |q_x - p_x| <= sqrt(bound) (1 + 2^-22)
@@ -177,8 +178,8 @@ __device__ bool tile_build(TileLds<PTS, CELLS>& T, const MapGrid& mg, int X0, in
 // tile_stats (diagnostic, may be null): [queries, tile-served, tile loads, points loaded, tile
 // fails, of which: box over CELLS cells or kTileLoadRows rows, load over kTileLoadMax, over PTS].
 template <int R, int RX, int PTS, int CELLS>
-__global__ void __launch_bounds__(64) k_gn_knn_tile(GnArgs a, float inv_f, int sx, int sy, float rmax2, int span,
-                                                   int rounds, unsigned long long* tile_stats) {
+__global__ void __launch_bounds__(64) k_gn_knn_tile(GnArgs a, int iter, float inv_f, int sx, int sy, float rmax2,
+                                                   int span, int rounds, unsigned long long* tile_stats) {
   static_assert(CELLS % 64 == 0 && CELLS <= 4096, "cell starts: CELLS / 64 per lane");
   __shared__ TileLds<PTS, CELLS> T;
   const int lane = threadIdx.x;
@@ -276,10 +277,14 @@ __global__ void __launch_bounds__(64) k_gn_knn_tile(GnArgs a, float inv_f, int s
       }
       __syncthreads();  // the next round rebuilds the tile
     }
-    if (has_q && !served) {  // the global search
-      unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      knn5_grid<R, RX, false, false, 1>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
-      (void)ks;
+    // queries not served here are queued for the grid search (k_gn_knn_list), one atomic per wave
+    const bool fb = has_q && !served;
+    const uint64_t fbm = __ballot(fb);
+    if (fbm) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&a.iter_cnt[2 * max(1, a.max_iter) + iter], __popcll(fbm));
+      base = __shfl(base, 0);
+      if (fb) a.fb_list[base + __popcll(fbm & ((1ull << lane) - 1ull))] = it * kResThreads + tid;
     }
     if (tile_stats) {
       const uint64_t hq = __ballot(has_q), sv = __ballot(served);
@@ -288,10 +293,10 @@ __global__ void __launch_bounds__(64) k_gn_knn_tile(GnArgs a, float inv_f, int s
         atomicAdd(&tile_stats[1], (unsigned long long)__popcll(sv));
       }
     }
-    if (has_q) {
+    if (served) {
       const bool ok = nn.k[4] < kKnnEmpty;
       int32_t ids[5];
-      bool same = have_prev && ok && a.fit_cache;
+      bool same = ok && a.fit_cache;
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
         ids[k] = knn_id(nn.k[k]);
@@ -302,6 +307,62 @@ __global__ void __launch_bounds__(64) k_gn_knn_tile(GnArgs a, float inv_f, int s
       a.nsame[(int64_t)it * kResThreads + tid] = same ? 1 : 0;
     }
     __syncthreads();  // the next virtual block reuses the tile
+  }
+}
+
+// The grid search (knn5_grid, gn_knn_block's per-query body) for the query slots the tile kernel
+// queued (fb_list[0, count), it * 256 + slot, in arrival order: each query's result depends on the
+// query only).  Lanes take consecutive list entries.
+template <int R, int RX>
+__global__ void __launch_bounds__(256) k_gn_knn_list(GnArgs a, int iter) {
+  const int n = a.iter_cnt[2 * max(1, a.max_iter) + iter];
+  for (int q = blockIdx.x * 256 + threadIdx.x; q < n; q += gridDim.x * 256) {
+    const int id = a.fb_list[q];
+    const int it = id / kResThreads, tid = id % kResThreads;
+    const int4 item = a.items[it];
+    const int job = item.x;
+    const GnState& g = a.gn[job];
+    const bool corner = item.y == 0;
+    const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
+    const float* T = g.T;
+    const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
+    const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
+    const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
+    const MapGrid& mg = corner ? a.mc : a.ms;
+    int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
+    float bound = __int_as_float(0x7f800000);
+    int32_t oid[5] = {-1, -1, -1, -1, -1};
+    const bool have_prev = o[0] >= 0;
+    if (have_prev) {
+      float mx = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) oid[k] = o[k * kResThreads];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const float4 m = mg.by_id[oid[k]];
+        float dist = 0.0f, diff;
+        diff = x0 - m.x; dist += diff * diff;
+        diff = y0 - m.y; dist += diff * diff;
+        diff = z0 - m.z; dist += diff * diff;
+        mx = fmaxf(mx, dist);
+      }
+      bound = mx;
+    }
+    Knn5 nn;
+    unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    knn5_grid<R, RX, false, false, 1>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
+    (void)ks;
+    const bool ok = nn.k[4] < kKnnEmpty;
+    int32_t ids[5];
+    bool same = have_prev && ok && a.fit_cache;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      ids[k] = knn_id(nn.k[k]);
+      same = same && ids[k] == oid[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? ids[k] : -1;
+    a.nsame[(int64_t)it * kResThreads + tid] = same ? 1 : 0;
   }
 }
 
@@ -326,8 +387,8 @@ static float knn_tile_inv() {
 
 unsigned long long* knn_tile_stats_buffer();
 
-bool launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
-  if (!use_prev || !knn_tile_enabled() || a.mc.g.sparse || a.ms.g.sparse) return false;
+bool launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int iter) {
+  if (iter <= 0 || !knn_tile_enabled() || a.mc.g.sparse || a.ms.g.sparse) return false;
   const float inv_x = a.mc.g.inv_x, inv = a.mc.g.inv_cell;
   if (inv_x != 8.0f || inv != 2.0f) return false;  // instantiated for the dense-map cells (R = 2, RX = 8)
   const float inv_f = knn_tile_inv();
@@ -354,11 +415,12 @@ bool launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int use_prev) 
   }();
   unsigned long long* st = knn_tile_stats_buffer();
   if (cap == 0)
-    fbr_launch((k_gn_knn_tile<2, 8, 512, 512>), dim3(g4), dim3(64), 0, s, a, inv_f, sx, sy, rmax2, span, rounds, st);
+    fbr_launch((k_gn_knn_tile<2, 8, 512, 512>), dim3(g4), dim3(64), 0, s, a, iter, inv_f, sx, sy, rmax2, span, rounds, st);
   else if (cap == 1)
-    fbr_launch((k_gn_knn_tile<2, 8, 1024, 1024>), dim3(g4), dim3(64), 0, s, a, inv_f, sx, sy, rmax2, span, rounds, st);
+    fbr_launch((k_gn_knn_tile<2, 8, 1024, 1024>), dim3(g4), dim3(64), 0, s, a, iter, inv_f, sx, sy, rmax2, span, rounds, st);
   else
-    fbr_launch((k_gn_knn_tile<2, 8, 2048, 2048>), dim3(g4), dim3(64), 0, s, a, inv_f, sx, sy, rmax2, span, rounds, st);
+    fbr_launch((k_gn_knn_tile<2, 8, 2048, 2048>), dim3(g4), dim3(64), 0, s, a, iter, inv_f, sx, sy, rmax2, span, rounds, st);
+  fbr_launch((k_gn_knn_list<2, 8>), dim3(std::max(1, grid)), dim3(256), 0, s, a, iter);
   return true;
 }
 

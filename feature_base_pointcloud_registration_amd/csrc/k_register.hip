@@ -41,7 +41,7 @@ namespace fbr {
 __global__ void k_gn_init(GnArgs a) {
   __shared__ int32_t scan[1024];
   const int tid = threadIdx.x;
-  for (int i = tid; i < 2 * max(1, a.max_iter); i += 1024) a.iter_cnt[i] = 0;  // k_gn_solve's counters
+  for (int i = tid; i < 3 * max(1, a.max_iter); i += 1024) a.iter_cnt[i] = 0;  // k_gn_solve's + fallback counters
   int base = 0;
   for (int j0 = 0; j0 < a.B; j0 += 1024) {
     const int job = j0 + tid;
@@ -252,7 +252,7 @@ void launch_gn_knn_f(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
 
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fused) {
   const int use_prev = iter > 0;  // nbr holds this launch's previous iteration
-  if (!fused && launch_gn_knn_tile(s, a, grid, use_prev)) return;  // dense maps: LDS tiles (k_knn_tile.hip)
+  if (!fused && launch_gn_knn_tile(s, a, grid, iter)) return;  // dense maps: LDS tiles (k_knn_tile.hip)
   if (fused) launch_gn_knn_f<true>(s, a, grid, use_prev);
   else launch_gn_knn_f<false>(s, a, grid, use_prev);
 }
