@@ -168,10 +168,9 @@ def batch_times(reset=False):
 
 
 def knn_tile_stats(reset=False):
-    """Wave-tile kNN counters since the last reset: (queries, tile-served queries, tile loads,
-    points loaded into tiles, tile failures, of which: box too large, load too long, too many
-    points), or None unless FBR_KNN_TILE_STATS=1 -- diagnostic (fbr_diag_knn_tile_stats,
-    k_knn_tile.hip)."""
+    """Block-tile kNN counters since the last reset: (queries, binned queries, tiles built, points
+    in tiles, points scanned by the tile loads, tiles over capacity, 0, 0), or None unless
+    FBR_KNN_TILE_STATS=1 -- diagnostic (fbr_diag_knn_tile_stats, k_knn_tile.hip)."""
     f = lib().fbr_diag_knn_tile_stats
     f.restype, f.argtypes = ctypes.c_int, [_VP, ctypes.c_int]
     v = (ctypes.c_ulonglong * 8)()

@@ -190,7 +190,10 @@ struct fbr_ctx {
   float* d_fitc = nullptr;     // [max_items][6][256] per-query fit cache (k_gn_residual)
   int8_t* d_fits = nullptr;    // [max_items][256]
   int8_t* d_nsame = nullptr;   // [max_items][256]
-  int32_t* d_fb_list = nullptr; // [max_items][256] wave-tile kNN: queries left to the grid search
+  // block-tile kNN (k_knn_tile.hip), allocated by build_map_grids when the map's grids take it:
+  int32_t* d_fb_list = nullptr;  // [3][max_items][256] queued / binned query slots, query blocks
+  int32_t* d_bin = nullptr;      // [kMaxSub][3][bin_nb] per-block counts, cursors, non-empty list
+  int64_t bin_nb = 0, bin_nb_c = 0;
   unsigned long long* h_iter_flags = nullptr;  // host-mapped, written by k_gn_solve
   unsigned long long* d_iter_flags = nullptr;  // its device address
   unsigned long long gn_gen = 0;
@@ -537,8 +540,16 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   }();
   a.res_mfma = res_mfma;
   a.iter_flags = c->d_iter_flags + (int64_t)sb.k * mi;
-  a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 3 * mi;  // [2 * mi] solve counters, [mi] fallback counts
-  a.fb_list = c->d_fb_list + ib * 256;
+  a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 4 * mi;  // [2 * mi] solve, [mi] queued, [mi] blocks
+  if (c->d_bin) {
+    const int64_t slots = (int64_t)c->max_items * 256;
+    a.fb_list = c->d_fb_list + ib * 256;
+    a.bin_list = c->d_fb_list + slots + ib * 256;
+    a.qblk = c->d_fb_list + 2 * slots + ib * 256;
+    a.bin = c->d_bin + (int64_t)sb.k * 3 * c->bin_nb;
+    a.nb_c = (int)c->bin_nb_c;
+    a.nb_s = (int)(c->bin_nb - c->bin_nb_c);
+  }
   a.desk_mode = c->desk_any ? c->d_desk_mode + sb.in0 : nullptr;
   a.desk = c->desk_any ? c->d_desk + sb.in0 : nullptr;
   a.nocrop = c->map_nocrop ? 1 : 0;
@@ -1114,6 +1125,26 @@ int build_map_grids(fbr_ctx* c, const float4* d_corner, int64_t nc, const float4
   if (!rc) rc = grid_build_device(c->stream, c->arena, d_surf, ns, invx, inv, c->grid_c.g.sparse != 0, c->grid_s);
   if (!rc && c->grid_s.g.sparse && !c->grid_c.g.sparse)
     rc = grid_build_device(c->stream, c->arena, d_corner, nc, invx, inv, true, c->grid_c);
+  // block-tile kNN buffers (dense 0.5 m x 0.125 m grids only): per-block arrays for every stream
+  // a sub-batch may run on, zeroed once (k_bin_tile re-zeroes the counts it used)
+  (void)hipFree(c->d_bin);
+  c->d_bin = nullptr;
+  c->bin_nb = c->bin_nb_c = 0;
+  if (!rc && knn_tile_applies(c->grid_c.g, c->grid_s.g)) {
+    c->bin_nb_c = knn_tile_blocks(c->grid_c.g);
+    c->bin_nb = c->bin_nb_c + knn_tile_blocks(c->grid_s.g);
+    const int64_t slots = (int64_t)c->max_items * 256;
+    const bool ok = c->bin_nb < (int64_t)1 << 30 &&
+                    (c->d_fb_list || hipMalloc(&c->d_fb_list, sizeof(int32_t) * 3 * slots) == hipSuccess) &&
+                    hipMalloc(&c->d_bin, sizeof(int32_t) * kMaxSub * 3 * c->bin_nb) == hipSuccess &&
+                    hipMemsetAsync(c->d_bin, 0, sizeof(int32_t) * kMaxSub * 3 * c->bin_nb, c->stream) == hipSuccess;
+    if (!ok) {  // the grid search serves every query
+      (void)hipGetLastError();
+      (void)hipFree(c->d_bin);
+      c->d_bin = nullptr;
+      c->bin_nb = c->bin_nb_c = 0;
+    }
+  }
   return rc;
 }
 
@@ -1244,8 +1275,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_nbr, (int64_t)c->max_items * 5 * 256) ||
               dalloc(&c->d_fitc, (int64_t)c->max_items * 6 * 256) || dalloc(&c->d_fits, (int64_t)c->max_items * 256) ||
               dalloc(&c->d_nsame, (int64_t)c->max_items * 256) ||
-              dalloc(&c->d_iter_cnt, kMaxSub * 3 * std::max(1, p->max_iterations)) ||
-              dalloc(&c->d_fb_list, (int64_t)c->max_items * 256) ||
+              dalloc(&c->d_iter_cnt, kMaxSub * 4 * std::max(1, p->max_iterations)) ||
               dalloc(&c->d_feat_scratch, Bw * H * feat_slot_bytes(c->W)) ||
               hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * kMaxSub * std::max(1, p->max_iterations),
                             hipHostMallocMapped) != hipSuccess ||
@@ -1286,7 +1316,7 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring, c->d_surf_ring_cnt, c->d_ring_box,
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
-                  c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_fitc, c->d_fits, c->d_nsame, c->d_fb_list, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
+                  c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_fitc, c->d_fits, c->d_nsame, c->d_fb_list, c->d_bin, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
                   c->d_desk, c->d_desk_mode, c->d_rowmin, c->d_choff,
                   c->d_kf_c, c->d_kf_s, c->d_kraw_c, c->d_kraw_s, c->d_kds_c, c->d_kds_s, c->d_kf_segs, c->d_bounds};
   for (void* p : ptrs)

@@ -264,8 +264,13 @@ struct GnArgs {
   int res_mfma;              // item partials on the matrix cores (FBR_RES_MFMA=1; default: the butterfly)
   unsigned long long* iter_flags;  // host-mapped [max_iter]: (generation << 32) | jobs still active
   int32_t* iter_cnt;         // [max_iter][2] active-job count / finished workgroups, then [max_iter]
-                             // wave-tile kNN fallback counts (zeroed by k_gn_init)
-  int32_t* fb_list;          // [max_items][256] wave-tile kNN: query slots left to the grid search
+                             // queued-query and [max_iter] non-empty-block counts of the block
+                             // tiles (k_knn_tile.hip; all zeroed by k_gn_init)
+  int32_t* fb_list;          // block tiles: [max_items][256] query slots left to the grid search
+  int32_t* bin_list;         // block tiles: [max_items][256] binned query slots, by block
+  int32_t* qblk;             // block tiles: [max_items][256] block of each query slot (-1: none)
+  int32_t* bin;              // block tiles: [3][nb_c + nb_s] counts, cursors, non-empty list; null: off
+  int nb_c, nb_s;            // blocks of the corner / surf grids
   const int32_t* desk_mode;  // [B] kDesk* bits or null (transformUpdate's IMU slerp, :1447-1474)
   const fbr_deskew_table* desk;  // [B]
   int nocrop;                // 1: keyframe local map, no CropBox (scan2MapOptimization on it)
@@ -278,6 +283,8 @@ unsigned long long* knn_stats_buffer();
 #endif
 // iterations >= 1 on dense maps: the wave-tile search (k_knn_tile.hip); false = not applicable
 bool launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int iter);
+bool knn_tile_applies(const GridDesc& gc, const GridDesc& gs);
+int64_t knn_tile_blocks(const GridDesc& g);
 void launch_gn_init(hipStream_t s, const GnArgs& a);
 // fused: kNN + residual row + item partial in one launch (launch_gn_residual is then skipped)
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fused);

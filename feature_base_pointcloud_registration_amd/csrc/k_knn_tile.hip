@@ -1,426 +1,432 @@
-// k_knn_tile.hip — LDS-staged map tiles for the neighbour search on dense maps (north_star: "LDS-
-// staged map tiles for the neighbour search"; BASELINE configs[2] / configs[4]).
+// k_knn_tile.hip — query-binned LDS map tiles for the neighbour search on dense maps (north_star:
+// "LDS-staged map tiles for the neighbour search"; BASELINE configs[2] / configs[4]).
 //
 // Reference: /root/reference/src/mapOptmization.h:1143 (surf kdtree->nearestKSearch(pointSel, 5)),
 // :1022 (corner), :1413-1414 (the per-scan KD-tree builds on the cropped local maps).
 //
 // The global grid (k_grid.hip) has 0.5 m y/z x 0.125 m x cells on dense maps.  At C5's density
-// (mapping leaves 0.05 m: ~400 map points per m^2 of surface) a query's pruned search still walks
+// (mapping leaves 0.05 m, ~400 map points per m^2 of surface) a query's pruned search still walks
 // ~140 points, because a grid row is 0.5 m x 0.5 m in cross-section; finer global cells need
-// 4x-16x more rows per query and measured 2-6x slower.  From the second
-// Gauss-Newton iteration on, every query knows an upper bound of its 5th-neighbour distance (its
-// previous neighbours, `bound` in knn5_grid), typically ~0.05 m on these maps.  So:
-//   * one 64-lane workgroup serves 64 consecutive queries of a work item (Morton order: a compact
-//     patch of the scan);
-//   * the wave's tile box is the union of its queries' bound boxes in FINE cells (0.125 m cubes);
-//   * the tile is loaded once from the global grid rows that overlap the box (coalesced), keeping
-//     only the points inside the box and inside the job's CropBox, and counting-sorted into the fine
-//     cells in LDS (<= 512 points, <= 512 cells: 10 KB);
-//   * each query then walks only the fine cells of its own bound box, out of LDS, with no CropBox
-//     test per point (the tile holds in-box points only): ~6-25 points instead of ~140.
-// Lanes whose bound is missing (no previous neighbours), too large (> `reach` fine cells), or whose
-// tile does not fit, are queued (fb_list) and a second launch runs the global search (knn5_grid)
-// on the queue, so they do not hold up the waves the tiles serve.
+// 4-16x more unrolled rows per query and measured 2-6x slower.  From the second
+// Gauss-Newton iteration on, every query knows an upper bound of its 5th-neighbour distance (the
+// distance to its previous neighbours, `bound` in knn5_grid), mostly below 0.125 m on these maps.
+// The jobs of a batch share the map, so the queries of all jobs are binned by map block:
+//   k_bin_count    one lane per query: bound, block (0.5 m cube = 4 x 4 x 4 fine 0.125 m cells of
+//                  the grid) when the query's bound box stays within its block +- one fine cell,
+//                  else the query is queued for the grid search (fb_list); per-block counts and the
+//                  list of non-empty blocks;
+//   k_bin_scan     one workgroup: exclusive scan of the non-empty blocks' counts -> cursors;
+//   k_bin_scatter  one lane per binned query: its slot in its block's run of the query list;
+//   k_bin_tile     one workgroup per non-empty block: the map points of the block +- one fine cell
+//                  (6^3 fine cells, from 9 global rows) are loaded once into LDS, counting-sorted by
+//                  fine cell, and every query of the block (all jobs) walks only the fine cells of
+//                  its own bound box: ~10-30 points instead of ~140, each an LDS read;
+//   k_gn_knn_list  the grid search for the queued queries.
+// Queries of different jobs share a tile, so a job's CropBox is tested per point unless the tile
+// lies inside it (then never).
 //
 // Exactness.  The scanned set of every query still contains every crop-box point whose computed d2
 // is <= bound: a point with fl(q - p)^2 summed <= bound has |q_x - p_x| <= sqrt(bound) (1 + 2^-22)
 // per axis, and the box edge fl(q_x - r_up) with r_up = sqrtf(bound) * (1 + 2^-7) + 1e-6 (1 + |q|)
-// stays below p_x (the margins exceed every rounding involved), so floor(p_x * inv_f), an exact
+// stays below p_x (the margins exceed every rounding involved), so floor(p_x * 8), an exact
 // power-of-two scaling, lies in the query's cell range.  The 5-NN list (5 smallest (d2, index)
 // keys with d2 < 1.0) is a function of the scanned set once that set holds the true 5 nearest, so
-// the neighbours are bit-identical to the global search's (`test_knn_tile_is_bit_identical`).
+// the neighbours are bit-identical to the grid search's (`test_knn_tile_is_bit_identical...`).
 #include "fbr_gn.h"
 
 namespace fbr {
 
 namespace {
-constexpr int kTileLoadRows = 16;  // global grid rows a tile may be loaded from
-constexpr int kTileLoadMax = 8192; // points a tile load may scan
+constexpr int kBinThreads = 256;
+constexpr int kTilePts = 2048;     // map points per block tile (32 KB)
+constexpr int kTileSide = 6;       // fine cells per side: the block's 4 + one on each side
+constexpr int kTileCells = kTileSide * kTileSide * kTileSide;
+constexpr float kFineInv = 8.0f;   // fine cell 0.125 m (= the grid's x cell; 4 per y / z cell)
 }  // namespace
 
-// PTS map points, CELLS fine cells per wave tile
-template <int PTS, int CELLS>
-struct TileLds {
-  float4 pts[PTS];                // the tile's points, by fine cell (w = map index bits)
-  uint32_t cs[CELLS];             // per-cell counts -> starts -> ends (cs[c] = end of cell c)
-  int2 rows[kTileLoadRows];       // global point ranges of the tile load
-  int rpre[kTileLoadRows + 1];    // their running lengths
+struct BinTileLds {
+  float4 pts[kTilePts];               // the tile's points, by fine cell (w = map index bits)
+  uint32_t cs[kTileCells];            // per-cell counts -> starts -> ends (cs[c] = end of cell c)
+  int2 rows[9];                       // the 3 x 3 global rows of the load
+  int rpre[10];                       // their running lengths
+  uint32_t wsum[kBinThreads / 64];
 };
 
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
-  return v;
-}
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
-  return v;
-}
+__device__ __forceinline__ int fine8(float x) { return (int)floorf(x * kFineInv); }
 
-// Fine-cell coordinate of a metric coordinate (inv_f a power of two: the product is exact).
-__device__ __forceinline__ int fine(float x, float inv_f) { return (int)floorf(x * inv_f); }
-
-// Global cells [g0, g1] covering fine cells [f0, f1] (s = log2(global cell / fine cell): 2^s fine
-// cells nest in a global cell when s >= 0, a fine cell spans 2^-s global cells when s < 0).
-__device__ __forceinline__ void fine_to_global(int f0, int f1, int s, int& g0, int& g1) {
-  if (s >= 0) {
-    g0 = f0 >> s;  // arithmetic shift: floor
-    g1 = f1 >> s;
-  } else {
-    g0 = f0 * (1 << -s);
-    g1 = (f1 + 1) * (1 << -s) - 1;
-  }
-}
-
-// Load the map points of fine-cell box [X0, X0 + Dx) x [Y0, Y0 + Dy) x [Z0, Z0 + Dz) that lie
-// inside the CropBox into T, counting-sorted by fine cell (T.cs[c] = end of cell c).  Wave-uniform
-// result: false when the box, its global rows or its points exceed the tile.
-template <int PTS, int CELLS>
-__device__ bool tile_build(TileLds<PTS, CELLS>& T, const MapGrid& mg, int X0, int Y0, int Z0, int Dx, int Dy, int Dz,
-                           float inv_f, int sx, int sy, const float* bmin, const float* bmax,
-                           unsigned long long* tile_stats) {
-  const int lane = threadIdx.x;
-  const bool small = Dx <= CELLS && Dy <= CELLS && Dz <= CELLS && (int64_t)Dx * Dy * Dz <= CELLS;
-  const int ncell = small ? Dx * Dy * Dz : CELLS + 1;
-  // global cells holding the box (fine_to_global: x by sx, y and z by sy)
-  int ax, bx, ay, by, az, bz;
-  fine_to_global(X0, X0 + Dx - 1, sx, ax, bx);
-  fine_to_global(Y0, Y0 + Dy - 1, sy, ay, by);
-  fine_to_global(Z0, Z0 + Dz - 1, sy, az, bz);
-  const int gx0 = max(ax - (int)mg.g.origin[0], 0), gx1 = min(bx - (int)mg.g.origin[0], mg.g.dims[0] - 1);
-  const int gy0 = max(ay - (int)mg.g.origin[1], 0), gy1 = min(by - (int)mg.g.origin[1], mg.g.dims[1] - 1);
-  const int gz0 = max(az - (int)mg.g.origin[2], 0), gz1 = min(bz - (int)mg.g.origin[2], mg.g.dims[2] - 1);
-  const int ny = gy1 - gy0 + 1, nz = gz1 - gz0 + 1;
-  const int nrows = (gx0 <= gx1 && ny > 0 && nz > 0) ? ny * nz : 0;
-  if (!(ncell <= CELLS && nrows <= kTileLoadRows)) {
-    if (tile_stats && lane == 0) atomicAdd(&tile_stats[5], 1ull);
-    return false;
-  }
-  int len = 0;
-  if (lane < nrows) {
-    const int y = gy0 + lane % ny, z = gz0 + lane / ny;
-    const int rowbase = (z * mg.g.dims[1] + y) * mg.g.dims[0];
-    const int b = mg.cell_start[rowbase + gx0], e = mg.cell_start[rowbase + gx1 + 1];
-    T.rows[lane] = make_int2(b, e);
-    len = e - b;
-  }
-  int inc = len;
+// The query of slot (it, tid) at the job's current pose and its warm-start bound (the largest
+// distance to its previous 5 neighbours; +inf without them): gn_knn_block's arithmetic.
+struct BinQuery {
+  float x0, y0, z0, bound;
+  int32_t oid[5];
+  bool have_prev;
+};
+__device__ __forceinline__ void bin_query(const GnArgs& a, int it, int tid, const int4& item, const GnState& g,
+                                          BinQuery& q) {
+  const int job = item.x;
+  const bool corner = item.y == 0;
+  const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
+  const float* T = g.T;
+  q.x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
+  q.y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
+  q.z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
+  const int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
+  q.have_prev = o[0] >= 0;
+  q.bound = __int_as_float(0x7f800000);
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int y = __shfl_up(inc, off);
-    if (lane >= off) inc += y;
-  }
-  if (lane < nrows) T.rpre[lane + 1] = inc;
-  if (lane == 0) T.rpre[0] = 0;
-  const int L = __shfl(inc, 63);
-  if (L > kTileLoadMax) {
-    if (tile_stats && lane == 0) atomicAdd(&tile_stats[6], 1ull);
-    return false;
-  }
-  for (int c = lane; c < ncell; c += 64) T.cs[c] = 0u;
-  __syncthreads();
-  const float bx0 = bmin[0], by0 = bmin[1], bz0 = bmin[2], bx1 = bmax[0], by1 = bmax[1], bz1 = bmax[2];
-  // pass 1: per-cell counts of the points inside the box and the CropBox
-  int j = 0;
-  for (int t = lane; t < L; t += 64) {
-    while (T.rpre[j + 1] <= t) ++j;
-    const float4 q = mg.pts[T.rows[j].x + (t - T.rpre[j])];
-    const int cx = fine(q.x, inv_f) - X0, cy = fine(q.y, inv_f) - Y0, cz = fine(q.z, inv_f) - Z0;
-    const bool in = (unsigned)cx < (unsigned)Dx && (unsigned)cy < (unsigned)Dy && (unsigned)cz < (unsigned)Dz &&
-                    !((q.x < bx0) | (q.y < by0) | (q.z < bz0) | (q.x > bx1) | (q.y > by1) | (q.z > bz1));
-    if (in) atomicAdd(&T.cs[cx + Dx * (cy + Dy * cz)], 1u);
-  }
-  __syncthreads();
-  // exclusive starts, 64 cells per step (a wave scan plus the running carry)
-  uint32_t carry = 0;
-  for (int c0 = 0; c0 < ncell; c0 += 64) {
-    const int c = c0 + lane;
-    const uint32_t n = c < ncell ? T.cs[c] : 0u;
-    uint32_t incs = n;
+  for (int k = 0; k < 5; ++k) q.oid[k] = -1;
+  if (q.have_prev) {
+    const float4* by_id = corner ? a.mc.by_id : a.ms.by_id;
+    float mx = 0.0f;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t y = __shfl_up(incs, off);
-      if (lane >= off) incs += y;
-    }
-    if (c < ncell) T.cs[c] = carry + incs - n;
-    carry += __shfl(incs, 63);
-  }
-  if (carry > (uint32_t)PTS) {
-    if (tile_stats && lane == 0) atomicAdd(&tile_stats[7], 1ull);
-    __syncthreads();
-    return false;
-  }
-  const uint32_t total = carry;
-  __syncthreads();
-  // pass 2: scatter (cs[c] ends as the end of cell c)
-  j = 0;
-  for (int t = lane; t < L; t += 64) {
-    while (T.rpre[j + 1] <= t) ++j;
-    const float4 q = mg.pts[T.rows[j].x + (t - T.rpre[j])];
-    const int cx = fine(q.x, inv_f) - X0, cy = fine(q.y, inv_f) - Y0, cz = fine(q.z, inv_f) - Z0;
-    const bool in = (unsigned)cx < (unsigned)Dx && (unsigned)cy < (unsigned)Dy && (unsigned)cz < (unsigned)Dz &&
-                    !((q.x < bx0) | (q.y < by0) | (q.z < bz0) | (q.x > bx1) | (q.y > by1) | (q.z > bz1));
-    if (in) T.pts[atomicAdd(&T.cs[cx + Dx * (cy + Dy * cz)], 1u)] = q;
-  }
-  __syncthreads();
-  if (tile_stats && lane == 0) {
-    atomicAdd(&tile_stats[2], 1ull);
-    atomicAdd(&tile_stats[3], (unsigned long long)total);
-  }
-  return true;
-}
-
-// sx / sy: log2(inv_f / inv_x), log2(inv_f / inv_cell) (fine_to_global).  Clusters: the eligible
-// lanes are served in up to kRounds tiles, each around the lowest still-pending lane (the anchor):
-// lanes whose bound box lies within `span` fine cells of the anchor's join its tile, so one far
-// query (Morton order jumps between octree blocks) does not blow up the box of the others.
-// tile_stats (diagnostic, may be null): [queries, tile-served, tile loads, points loaded, tile
-// fails, of which: box over CELLS cells or kTileLoadRows rows, load over kTileLoadMax, over PTS].
-template <int R, int RX, int PTS, int CELLS>
-__global__ void __launch_bounds__(64) k_gn_knn_tile(GnArgs a, int iter, float inv_f, int sx, int sy, float rmax2,
-                                                   int span, int rounds, unsigned long long* tile_stats) {
-  static_assert(CELLS % 64 == 0 && CELLS <= 4096, "cell starts: CELLS / 64 per lane");
-  __shared__ TileLds<PTS, CELLS> T;
-  const int lane = threadIdx.x;
-  const int nitems = a.nitems[0];
-  for (int v = blockIdx.x; v < nitems * 4; v += gridDim.x) {
-    const int it = v >> 2, tid = (v & 3) * 64 + lane;
-    const int4 item = a.items[it];
-    const int job = item.x;
-    const GnState& g = a.gn[job];
-    if (!g.active) continue;  // block-uniform
-    const bool corner = item.y == 0;
-    const MapGrid& mg = corner ? a.mc : a.ms;
-    const bool has_q = tid < item.w;
-    // ---- the query, its previous neighbours and bound (gn_knn_block's arithmetic) ----
-    float x0 = 0.0f, y0 = 0.0f, z0 = 0.0f, bound = __int_as_float(0x7f800000);
-    int32_t oid[5] = {-1, -1, -1, -1, -1};
-    int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
-    bool have_prev = false;
-    if (has_q) {
-      const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
-      const float* Tm = g.T;
-      x0 = Tm[0] * p.x + Tm[1] * p.y + Tm[2] * p.z + Tm[3];
-      y0 = Tm[4] * p.x + Tm[5] * p.y + Tm[6] * p.z + Tm[7];
-      z0 = Tm[8] * p.x + Tm[9] * p.y + Tm[10] * p.z + Tm[11];
-      have_prev = o[0] >= 0;
-      if (have_prev) {
-        float mx = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) oid[k] = o[k * kResThreads];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const float4 q = mg.by_id[oid[k]];
-          float dist = 0.0f, diff;
-          diff = x0 - q.x; dist += diff * diff;
-          diff = y0 - q.y; dist += diff * diff;
-          diff = z0 - q.z; dist += diff * diff;
-          mx = fmaxf(mx, dist);
-        }
-        bound = mx;
-      }
-    }
-    const bool el = has_q && have_prev && bound <= rmax2;
-    int lx0 = 0, lx1 = -1, ly0 = 0, ly1 = -1, lz0 = 0, lz1 = -1;
-    if (el) {
-      const float r_up = sqrtf(bound) * 1.0078125f + 1e-6f * (1.0f + fabsf(x0) + fabsf(y0) + fabsf(z0));
-      lx0 = fine(x0 - r_up, inv_f); lx1 = fine(x0 + r_up, inv_f);
-      ly0 = fine(y0 - r_up, inv_f); ly1 = fine(y0 + r_up, inv_f);
-      lz0 = fine(z0 - r_up, inv_f); lz1 = fine(z0 + r_up, inv_f);
-    }
-    Knn5 nn;
-#pragma unroll
-    for (int t = 0; t < 5; ++t) nn.k[t] = kKnnEmpty;
-    bool served = false;
-    uint64_t pending = __ballot(el);
-    for (int rd = 0; rd < rounds && pending; ++rd) {
-      // ---- this round's cluster and its tile box (fine cells) ----
-      const int an = __ffsll((unsigned long long)pending) - 1;
-      const int ax0 = __shfl(lx0, an), ax1 = __shfl(lx1, an), ay0 = __shfl(ly0, an), ay1 = __shfl(ly1, an);
-      const int az0 = __shfl(lz0, an), az1 = __shfl(lz1, an);
-      const bool mine = ((pending >> lane) & 1ull) && lx0 >= ax0 - span && lx1 <= ax1 + span && ly0 >= ay0 - span &&
-                        ly1 <= ay1 + span && lz0 >= az0 - span && lz1 <= az1 + span;
-      const uint64_t cl = __ballot(mine);  // holds the anchor
-      pending &= ~cl;
-      const int big = 0x3fffffff;
-      const int X0 = wave_min_i(mine ? lx0 : big), Y0 = wave_min_i(mine ? ly0 : big), Z0 = wave_min_i(mine ? lz0 : big);
-      const int Dx = wave_max_i(mine ? lx1 : -big) - X0 + 1, Dy = wave_max_i(mine ? ly1 : -big) - Y0 + 1;
-      const int Dz = wave_max_i(mine ? lz1 : -big) - Z0 + 1;
-      if (!tile_build(T, mg, X0, Y0, Z0, Dx, Dy, Dz, inv_f, sx, sy, g.crop_min, g.crop_max, tile_stats)) {
-        if (tile_stats && lane == 0) atomicAdd(&tile_stats[4], 1ull);
-        continue;  // the cluster's lanes take the global search
-      }
-      // ---- the tile search: the lane's fine rows (y, z), each one contiguous x-cell range ----
-      if (mine) {
-        served = true;
-        const int nyr = ly1 - ly0 + 1, nr = nyr * (lz1 - lz0 + 1);
-        int r = 0, i = 0, e = 0;
-        while (true) {
-          if (i >= e) {
-            if (r >= nr) break;
-            const int y = ly0 + r % nyr - Y0, z = lz0 + r / nyr - Z0;
-            const int base = Dx * (y + Dy * z);
-            const int ca = base + (lx0 - X0), cb = base + (lx1 - X0);
-            i = ca ? (int)T.cs[ca - 1] : 0;
-            e = (int)T.cs[cb];
-            ++r;
-            continue;
-          }
-          const float4 q = T.pts[i++];
-          float dist = 0.0f, diff;
-          diff = x0 - q.x; dist += diff * diff;  // flann::L2_Simple
-          diff = y0 - q.y; dist += diff * diff;
-          diff = z0 - q.z; dist += diff * diff;
-          knn_insert(nn, ((unsigned long long)(unsigned)__float_as_int(dist) << 32) | (unsigned)__float_as_int(q.w));
-        }
-      }
-      __syncthreads();  // the next round rebuilds the tile
-    }
-    // queries not served here are queued for the grid search (k_gn_knn_list), one atomic per wave
-    const bool fb = has_q && !served;
-    const uint64_t fbm = __ballot(fb);
-    if (fbm) {
-      int base = 0;
-      if (lane == 0) base = atomicAdd(&a.iter_cnt[2 * max(1, a.max_iter) + iter], __popcll(fbm));
-      base = __shfl(base, 0);
-      if (fb) a.fb_list[base + __popcll(fbm & ((1ull << lane) - 1ull))] = it * kResThreads + tid;
-    }
-    if (tile_stats) {
-      const uint64_t hq = __ballot(has_q), sv = __ballot(served);
-      if (lane == 0) {
-        atomicAdd(&tile_stats[0], (unsigned long long)__popcll(hq));
-        atomicAdd(&tile_stats[1], (unsigned long long)__popcll(sv));
-      }
-    }
-    if (served) {
-      const bool ok = nn.k[4] < kKnnEmpty;
-      int32_t ids[5];
-      bool same = ok && a.fit_cache;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        ids[k] = knn_id(nn.k[k]);
-        same = same && ids[k] == oid[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? ids[k] : -1;
-      a.nsame[(int64_t)it * kResThreads + tid] = same ? 1 : 0;
-    }
-    __syncthreads();  // the next virtual block reuses the tile
-  }
-}
-
-// The grid search (knn5_grid, gn_knn_block's per-query body) for the query slots the tile kernel
-// queued (fb_list[0, count), it * 256 + slot, in arrival order: each query's result depends on the
-// query only).  Lanes take consecutive list entries.
-template <int R, int RX>
-__global__ void __launch_bounds__(256) k_gn_knn_list(GnArgs a, int iter) {
-  const int n = a.iter_cnt[2 * max(1, a.max_iter) + iter];
-  for (int q = blockIdx.x * 256 + threadIdx.x; q < n; q += gridDim.x * 256) {
-    const int id = a.fb_list[q];
-    const int it = id / kResThreads, tid = id % kResThreads;
-    const int4 item = a.items[it];
-    const int job = item.x;
-    const GnState& g = a.gn[job];
-    const bool corner = item.y == 0;
-    const float4 p = corner ? a.cornerDS[job * a.capc + item.z + tid] : a.surfDS[job * a.caps + item.z + tid];
-    const float* T = g.T;
-    const float x0 = T[0] * p.x + T[1] * p.y + T[2] * p.z + T[3];
-    const float y0 = T[4] * p.x + T[5] * p.y + T[6] * p.z + T[7];
-    const float z0 = T[8] * p.x + T[9] * p.y + T[10] * p.z + T[11];
-    const MapGrid& mg = corner ? a.mc : a.ms;
-    int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
-    float bound = __int_as_float(0x7f800000);
-    int32_t oid[5] = {-1, -1, -1, -1, -1};
-    const bool have_prev = o[0] >= 0;
-    if (have_prev) {
-      float mx = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) oid[k] = o[k * kResThreads];
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const float4 m = mg.by_id[oid[k]];
-        float dist = 0.0f, diff;
-        diff = x0 - m.x; dist += diff * diff;
-        diff = y0 - m.y; dist += diff * diff;
-        diff = z0 - m.z; dist += diff * diff;
-        mx = fmaxf(mx, dist);
-      }
-      bound = mx;
-    }
-    Knn5 nn;
-    unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    knn5_grid<R, RX, false, false, 1>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks);
-    (void)ks;
-    const bool ok = nn.k[4] < kKnnEmpty;
-    int32_t ids[5];
-    bool same = have_prev && ok && a.fit_cache;
+    for (int k = 0; k < 5; ++k) q.oid[k] = o[k * kResThreads];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-      ids[k] = knn_id(nn.k[k]);
-      same = same && ids[k] == oid[k];
+      const float4 m = by_id[q.oid[k]];
+      float dist = 0.0f, diff;
+      diff = q.x0 - m.x; dist += diff * diff;
+      diff = q.y0 - m.y; dist += diff * diff;
+      diff = q.z0 - m.z; dist += diff * diff;
+      mx = fmaxf(mx, dist);
     }
-#pragma unroll
-    for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? ids[k] : -1;
-    a.nsame[(int64_t)it * kResThreads + tid] = same ? 1 : 0;
+    q.bound = mx;
   }
 }
 
-// FBR_KNN_TILE: 1 serves iterations >= 1 on dense 0.5 m x 0.125 m grids from wave tiles; 0 (the
-// default until the tiles measure faster) keeps the global search.  FBR_KNN_TILE_CELL: the fine cell (m, power of two, default 0.125);
-// FBR_KNN_TILE_REACH: the largest bound served, in fine cells (default 1).
-static bool knn_tile_enabled() {
+// Fine-cell bound box of a query (absolute fine coordinates).
+__device__ __forceinline__ void bin_box(const BinQuery& q, int* lo, int* hi) {
+  const float r_up = sqrtf(q.bound) * 1.0078125f + 1e-6f * (1.0f + fabsf(q.x0) + fabsf(q.y0) + fabsf(q.z0));
+  lo[0] = fine8(q.x0 - r_up); hi[0] = fine8(q.x0 + r_up);
+  lo[1] = fine8(q.y0 - r_up); hi[1] = fine8(q.y0 + r_up);
+  lo[2] = fine8(q.z0 - r_up); hi[2] = fine8(q.z0 + r_up);
+}
+
+// Blocks of a map grid along x (4 x cells each); y / z: one per grid cell.
+__device__ __forceinline__ int bin_nbx(const MapGrid& m) { return (m.g.dims[0] + 3) >> 2; }
+
+// The query's result: the neighbour map indices (slot 0 = -1: no correspondence) and the
+// same-as-previous flag of the fit cache.
+__device__ __forceinline__ void bin_write(const GnArgs& a, int it, int tid, const BinQuery& q, const Knn5& nn) {
+  int32_t* o = a.nbr + (int64_t)it * 5 * kResThreads + tid;
+  const bool ok = nn.k[4] < kKnnEmpty;
+  int32_t ids[5];
+  bool same = q.have_prev && ok && a.fit_cache;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    ids[k] = knn_id(nn.k[k]);
+    same = same && ids[k] == q.oid[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) o[k * kResThreads] = ok ? ids[k] : -1;
+  a.nsame[(int64_t)it * kResThreads + tid] = same ? 1 : 0;
+}
+
+// Per-sub counters in iter_cnt: [2 mi] solve, [mi] queued queries, [mi] non-empty blocks.
+__device__ __forceinline__ int32_t* fb_count(const GnArgs& a, int iter) {
+  return a.iter_cnt + 2 * max(1, a.max_iter) + iter;
+}
+__device__ __forceinline__ int32_t* ne_count(const GnArgs& a, int iter) {
+  return a.iter_cnt + 3 * max(1, a.max_iter) + iter;
+}
+
+// Queue the flagged lanes' slots for the grid search (one atomic per wave).
+__device__ __forceinline__ void queue_fallback(const GnArgs& a, int iter, bool fb, int v) {
+  const uint64_t m = __ballot(fb);
+  if (!m) return;
+  const int lane = threadIdx.x & 63, lead = __ffsll((unsigned long long)m) - 1;
+  int base = 0;
+  if (lane == lead) base = atomicAdd(fb_count(a, iter), __popcll(m));
+  base = __shfl(base, lead);
+  if (fb) a.fb_list[base + __popcll(m & ((1ull << lane) - 1ull))] = v;
+}
+
+// tile_stats (diagnostic, may be null): [queries, binned queries, tiles built, points in tiles,
+// points scanned by the tile loads, tiles over capacity].
+__global__ void __launch_bounds__(kBinThreads) k_bin_count(GnArgs a, int iter, float rmax2,
+                                                          unsigned long long* tile_stats) {
+  const int nitems = a.nitems[0];
+  const int nb_c = a.nb_c;
+  int32_t* cnt = a.bin;
+  int32_t* ne = a.bin + 2 * (a.nb_c + a.nb_s);
+  for (int64_t v0 = (int64_t)blockIdx.x * kBinThreads; v0 < (int64_t)nitems * kResThreads;
+       v0 += (int64_t)gridDim.x * kBinThreads) {
+    const int v = (int)v0 + (int)threadIdx.x;  // kBinThreads == kResThreads: v < nitems * 256
+    const int it = v / kResThreads, tid = v % kResThreads;
+    const int4 item = a.items[it];
+    const GnState& g = a.gn[item.x];
+    const bool has_q = g.active && tid < item.w;
+    int blk = -1;
+    if (has_q) {
+      BinQuery q;
+      bin_query(a, it, tid, item, g, q);
+      if (q.have_prev && q.bound <= rmax2) {
+        const bool corner = item.y == 0;
+        const MapGrid& mg = corner ? a.mc : a.ms;
+        int lo[3], hi[3];
+        bin_box(q, lo, hi);
+        const int ox = (int)mg.g.origin[0], oy = (int)mg.g.origin[1], oz = (int)mg.g.origin[2];
+        // the block of the query's fine cell (grid-relative: x cells / 4, y / z cells)
+        const int bx = (fine8(q.x0) - ox) >> 2, by = (fine8(q.y0) >> 2) - oy, bz = (fine8(q.z0) >> 2) - oz;
+        const int nbx = bin_nbx(mg);
+        const bool in_grid = bx >= 0 && bx < nbx && by >= 0 && by < mg.g.dims[1] && bz >= 0 && bz < mg.g.dims[2];
+        const int fx0 = 4 * bx + ox, fy0 = 4 * (by + oy), fz0 = 4 * (bz + oz);  // the block's first fine cells
+        const bool fits = lo[0] >= fx0 - 1 && hi[0] <= fx0 + 4 && lo[1] >= fy0 - 1 && hi[1] <= fy0 + 4 &&
+                          lo[2] >= fz0 - 1 && hi[2] <= fz0 + 4;
+        if (in_grid && fits) blk = (corner ? 0 : nb_c) + (bz * mg.g.dims[1] + by) * nbx + bx;
+      }
+    }
+    a.qblk[v] = blk;
+    if (blk >= 0 && atomicAdd(&cnt[blk], 1) == 0) ne[atomicAdd(ne_count(a, iter), 1)] = blk;
+    queue_fallback(a, iter, has_q && blk < 0, v);
+    if (tile_stats) {
+      const uint64_t hq = __ballot(has_q), bq = __ballot(blk >= 0);
+      if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&tile_stats[0], (unsigned long long)__popcll(hq));
+        atomicAdd(&tile_stats[1], (unsigned long long)__popcll(bq));
+      }
+    }
+  }
+}
+
+// Exclusive scan of the non-empty blocks' counts (one 1024-thread workgroup): cur[b] = first slot.
+__global__ void __launch_bounds__(1024) k_bin_scan(GnArgs a, int iter) {
+  __shared__ int32_t wsum[16];
+  const int n = *ne_count(a, iter);
+  const int32_t* cnt = a.bin;
+  int32_t* cur = a.bin + (a.nb_c + a.nb_s);
+  const int32_t* ne = a.bin + 2 * (a.nb_c + a.nb_s);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int carry = 0;
+  for (int i0 = 0; i0 < n; i0 += 1024) {
+    const int i = i0 + tid;
+    const int b = i < n ? ne[i] : -1;
+    const int c = b >= 0 ? cnt[b] : 0;
+    int inc = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(inc, off);
+      if (lane >= off) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    int pre = carry, tot = 0;
+    for (int k = 0; k < 16; ++k) {
+      if (k < w) pre += wsum[k];
+      tot += wsum[k];
+    }
+    if (b >= 0) cur[b] = pre + inc - c;
+    carry += tot;
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(kBinThreads) k_bin_scatter(GnArgs a) {
+  const int nitems = a.nitems[0];
+  int32_t* cur = a.bin + (a.nb_c + a.nb_s);
+  for (int64_t v = (int64_t)blockIdx.x * kBinThreads + threadIdx.x; v < (int64_t)nitems * kResThreads;
+       v += (int64_t)gridDim.x * kBinThreads) {
+    const int b = a.qblk[v];
+    if (b >= 0) a.bin_list[atomicAdd(&cur[b], 1)] = (int32_t)v;
+  }
+}
+
+// One workgroup per non-empty block: load its tile, serve its queries (every job's).
+template <int R, int RX>
+__global__ void __launch_bounds__(kBinThreads) k_bin_tile(GnArgs a, int iter, unsigned long long* tile_stats) {
+  __shared__ BinTileLds T;
+  const int n_ne = *ne_count(a, iter);
+  int32_t* cnt = a.bin;
+  const int32_t* cur = a.bin + (a.nb_c + a.nb_s);
+  const int32_t* ne = a.bin + 2 * (a.nb_c + a.nb_s);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = blockIdx.x; i < n_ne; i += gridDim.x) {
+    const int b = ne[i];
+    const bool corner = b < a.nb_c;
+    const MapGrid& mg = corner ? a.mc : a.ms;
+    const int lb = corner ? b : b - a.nb_c;
+    const int nbx = bin_nbx(mg), Y = mg.g.dims[1];
+    const int bx = lb % nbx, by = (lb / nbx) % Y, bz = lb / (nbx * Y);
+    const int nq = cnt[b], q0 = cur[b] - nq;  // the scatter advanced cur to the run's end
+    const int ox = (int)mg.g.origin[0], oy = (int)mg.g.origin[1], oz = (int)mg.g.origin[2];
+    const int X0 = 4 * bx + ox - 1, Y0 = 4 * (by + oy) - 1, Z0 = 4 * (bz + oz) - 1;  // tile fine box origin
+    // ---- load: the 3 x 3 global rows around the block, x cells 4 bx - 1 .. 4 bx + 4 ----
+    const int gx0 = max(4 * bx - 1, 0), gx1 = min(4 * bx + 4, mg.g.dims[0] - 1);
+    if (tid < 9) {
+      const int y = by - 1 + tid % 3, z = bz - 1 + tid / 3;
+      int bb = 0, ee = 0;
+      if (y >= 0 && y < Y && z >= 0 && z < mg.g.dims[2] && gx0 <= gx1) {
+        const int rowbase = (z * Y + y) * mg.g.dims[0];
+        bb = mg.cell_start[rowbase + gx0];
+        ee = mg.cell_start[rowbase + gx1 + 1];
+      }
+      T.rows[tid] = make_int2(bb, ee);
+    }
+    for (int c = tid; c < kTileCells; c += kBinThreads) T.cs[c] = 0u;
+    __syncthreads();
+    if (tid == 0) {
+      int s = 0;
+      T.rpre[0] = 0;
+      for (int r = 0; r < 9; ++r) T.rpre[r + 1] = (s += T.rows[r].y - T.rows[r].x);
+    }
+    __syncthreads();
+    const int L = T.rpre[9];
+    // pass 1: counts per fine cell (every point of the box: the CropBox is per query)
+    for (int t = tid; t < L; t += kBinThreads) {
+      int j = 0;
+      while (T.rpre[j + 1] <= t) ++j;
+      const float4 p = mg.pts[T.rows[j].x + (t - T.rpre[j])];
+      const int cx = fine8(p.x) - X0, cy = fine8(p.y) - Y0, cz = fine8(p.z) - Z0;
+      if ((unsigned)cx < (unsigned)kTileSide && (unsigned)cy < (unsigned)kTileSide && (unsigned)cz < (unsigned)kTileSide)
+        atomicAdd(&T.cs[cx + kTileSide * (cy + kTileSide * cz)], 1u);
+    }
+    __syncthreads();
+    // exclusive starts over the 216 cells (one per thread)
+    {
+      const uint32_t c = tid < kTileCells ? T.cs[tid] : 0u;
+      uint32_t inc = c;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off);
+        if (lane >= off) inc += y;
+      }
+      if (lane == 63) T.wsum[w] = inc;
+      __syncthreads();
+      uint32_t pre = 0;
+      for (int k = 0; k < w; ++k) pre += T.wsum[k];
+      if (tid < kTileCells) T.cs[tid] = pre + inc - c;
+    }
+    __syncthreads();
+    const uint32_t total = T.wsum[0] + T.wsum[1] + T.wsum[2] + T.wsum[3];
+    const bool tile_ok = total <= (uint32_t)kTilePts;
+    if (tile_ok) {
+      // pass 2: scatter (cs[c] ends as the end of cell c)
+      for (int t = tid; t < L; t += kBinThreads) {
+        int j = 0;
+        while (T.rpre[j + 1] <= t) ++j;
+        const float4 p = mg.pts[T.rows[j].x + (t - T.rpre[j])];
+        const int cx = fine8(p.x) - X0, cy = fine8(p.y) - Y0, cz = fine8(p.z) - Z0;
+        if ((unsigned)cx < (unsigned)kTileSide && (unsigned)cy < (unsigned)kTileSide && (unsigned)cz < (unsigned)kTileSide)
+          T.pts[atomicAdd(&T.cs[cx + kTileSide * (cy + kTileSide * cz)], 1u)] = p;
+      }
+    }
+    __syncthreads();
+    if (tile_stats && tid == 0) {
+      atomicAdd(&tile_stats[2], 1ull);
+      atomicAdd(&tile_stats[3], (unsigned long long)total);
+      atomicAdd(&tile_stats[4], (unsigned long long)L);
+      if (!tile_ok) atomicAdd(&tile_stats[5], 1ull);
+    }
+    // ---- the block's queries, one per lane ----
+    const float fc = 1.0f / kFineInv;
+    for (int k0 = 0; k0 < nq; k0 += kBinThreads) {
+      const int k = k0 + tid;
+      if (k < nq) {
+        const int v = a.bin_list[q0 + k];
+        const int it = v / kResThreads, qt = v % kResThreads;
+        const int4 item = a.items[it];
+        const GnState& g = a.gn[item.x];
+        BinQuery q;
+        bin_query(a, it, qt, item, g, q);
+        Knn5 nn;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) nn.k[t] = kKnnEmpty;
+        if (tile_ok) {
+          int lo[3], hi[3];
+          bin_box(q, lo, hi);  // within the tile (k_bin_count checked it, same arithmetic)
+          const float bx0 = g.crop_min[0], by0 = g.crop_min[1], bz0 = g.crop_min[2];
+          const float bx1 = g.crop_max[0], by1 = g.crop_max[1], bz1 = g.crop_max[2];
+          // the tile inside the job's CropBox: no per-point test (edges exact: multiples of 1/8)
+          const bool inside = (float)X0 * fc >= bx0 && (float)(X0 + kTileSide) * fc <= bx1 && (float)Y0 * fc >= by0 &&
+                              (float)(Y0 + kTileSide) * fc <= by1 && (float)Z0 * fc >= bz0 &&
+                              (float)(Z0 + kTileSide) * fc <= bz1;
+          const int nyr = hi[1] - lo[1] + 1, nr = nyr * (hi[2] - lo[2] + 1);
+          int r = 0, ii = 0, e = 0;
+          while (true) {
+            if (ii >= e) {
+              if (r >= nr) break;
+              const int y = lo[1] + r % nyr - Y0, z = lo[2] + r / nyr - Z0;
+              const int base = kTileSide * (y + kTileSide * z);
+              const int ca = base + (lo[0] - X0), cb = base + (hi[0] - X0);
+              ii = ca ? (int)T.cs[ca - 1] : 0;
+              e = (int)T.cs[cb];
+              ++r;
+              continue;
+            }
+            const float4 p = T.pts[ii++];
+            bool out = false;
+            if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
+            float dist = 0.0f, diff;
+            diff = q.x0 - p.x; dist += diff * diff;  // flann::L2_Simple
+            diff = q.y0 - p.y; dist += diff * diff;
+            diff = q.z0 - p.z; dist += diff * diff;
+            const unsigned hb = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
+            knn_insert(nn, ((unsigned long long)hb << 32) | (unsigned)__float_as_int(p.w));
+          }
+        } else {  // the tile did not fit: the grid search
+          unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+          knn5_grid<R, RX, false, false, 1>(mg, q.x0, q.y0, q.z0, g.crop_min, g.crop_max, q.bound, nn, ks);
+          (void)ks;
+        }
+        bin_write(a, it, qt, q, nn);
+      }
+    }
+    __syncthreads();
+    if (tid == 0) cnt[b] = 0;  // the next iteration's counts start from zero
+  }
+}
+
+// The grid search (knn5_grid, gn_knn_block's per-query body) for the query slots k_bin_count
+// queued (fb_list[0, count): it * 256 + slot, in arrival order; each query's result depends on the
+// query only).
+template <int R, int RX>
+__global__ void __launch_bounds__(256) k_gn_knn_list(GnArgs a, int iter) {
+  const int n = *fb_count(a, iter);
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+    const int v = a.fb_list[k];
+    const int it = v / kResThreads, tid = v % kResThreads;
+    const int4 item = a.items[it];
+    const GnState& g = a.gn[item.x];
+    BinQuery q;
+    bin_query(a, it, tid, item, g, q);
+    Knn5 nn;
+    unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    knn5_grid<R, RX, false, false, 1>(item.y == 0 ? a.mc : a.ms, q.x0, q.y0, q.z0, g.crop_min, g.crop_max, q.bound,
+                                      nn, ks);
+    (void)ks;
+    bin_write(a, it, tid, q, nn);
+  }
+}
+
+// FBR_KNN_TILE: 1 (default) serves iterations >= 1 on dense 0.5 m x 0.125 m grids from the block
+// tiles; 0 keeps the grid search for every query.
+bool knn_tile_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("FBR_KNN_TILE");
-    return e ? std::atoi(e) != 0 : false;
+    return e ? std::atoi(e) != 0 : true;
   }();
   return v;
 }
-static float knn_tile_inv() {
-  static const float v = [] {
-    const char* e = std::getenv("FBR_KNN_TILE_CELL");
-    const float c = e ? std::strtof(e, nullptr) : 0.125f;
-    return c > 0.0f ? std::exp2(-std::round(std::log2(c))) : 8.0f;
-  }();
-  return v;
+
+// The tiles apply to dense grids of 0.5 m y/z x 0.125 m x cells (the k_gn_knn<2, 8> layout).
+bool knn_tile_applies(const GridDesc& gc, const GridDesc& gs) {
+  return knn_tile_enabled() && !gc.sparse && !gs.sparse && gc.inv_x == 8.0f && gc.inv_cell == 2.0f &&
+         gs.inv_x == 8.0f && gs.inv_cell == 2.0f;
 }
+
+int64_t knn_tile_blocks(const GridDesc& g) { return (int64_t)((g.dims[0] + 3) / 4) * g.dims[1] * g.dims[2]; }
 
 unsigned long long* knn_tile_stats_buffer();
 
 bool launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int iter) {
-  if (iter <= 0 || !knn_tile_enabled() || a.mc.g.sparse || a.ms.g.sparse) return false;
-  const float inv_x = a.mc.g.inv_x, inv = a.mc.g.inv_cell;
-  if (inv_x != 8.0f || inv != 2.0f) return false;  // instantiated for the dense-map cells (R = 2, RX = 8)
-  const float inv_f = knn_tile_inv();
-  if (inv_f < 0.5f || inv_f > 64.0f) return false;
-  const int sx = (int)std::lround(std::log2(inv_f / inv_x)), sy = (int)std::lround(std::log2(inv_f / inv));
-  static const float reach = [] {
-    const char* e = std::getenv("FBR_KNN_TILE_REACH");
-    const float r = e ? std::strtof(e, nullptr) : 1.0f;
-    return r > 0.0f ? std::min(r, 4.0f) : 1.0f;
-  }();
-  const float rmax2 = reach * reach / (inv_f * inv_f);  // bound boxes up to `reach` fine cells
-  const int g4 = (int)std::min<int64_t>((int64_t)grid * 4, 1 << 20);
-  static const int cap = [] {  // tile capacity (FBR_KNN_TILE_CAP): 0 512 points / 512 cells, 1 1024 / 1024, 2 2048 / 2048
-    const char* e = std::getenv("FBR_KNN_TILE_CAP");
-    return e ? std::max(0, std::min(2, std::atoi(e))) : 1;
-  }();
-  static const int span = [] {  // cluster reach around the anchor's box, fine cells (FBR_KNN_TILE_SPAN)
-    const char* e = std::getenv("FBR_KNN_TILE_SPAN");
-    return e ? std::max(0, std::atoi(e)) : 3;
-  }();
-  static const int rounds = [] {  // tiles per wave (FBR_KNN_TILE_ROUNDS)
-    const char* e = std::getenv("FBR_KNN_TILE_ROUNDS");
-    return e ? std::max(1, std::min(64, std::atoi(e))) : 4;
-  }();
+  if (iter <= 0 || !a.bin || !knn_tile_applies(a.mc.g, a.ms.g)) return false;
+  const float rmax2 = 1.0f / (kFineInv * kFineInv);  // bounds up to one fine cell
+  const int gq = std::max(1, std::min(grid, 16384));
   unsigned long long* st = knn_tile_stats_buffer();
-  if (cap == 0)
-    fbr_launch((k_gn_knn_tile<2, 8, 512, 512>), dim3(g4), dim3(64), 0, s, a, iter, inv_f, sx, sy, rmax2, span, rounds, st);
-  else if (cap == 1)
-    fbr_launch((k_gn_knn_tile<2, 8, 1024, 1024>), dim3(g4), dim3(64), 0, s, a, iter, inv_f, sx, sy, rmax2, span, rounds, st);
-  else
-    fbr_launch((k_gn_knn_tile<2, 8, 2048, 2048>), dim3(g4), dim3(64), 0, s, a, iter, inv_f, sx, sy, rmax2, span, rounds, st);
-  fbr_launch((k_gn_knn_list<2, 8>), dim3(std::max(1, grid)), dim3(256), 0, s, a, iter);
+  fbr_launch(k_bin_count, dim3(gq), dim3(kBinThreads), 0, s, a, iter, rmax2, st);
+  fbr_launch(k_bin_scan, dim3(1), dim3(1024), 0, s, a, iter);
+  fbr_launch(k_bin_scatter, dim3(gq), dim3(kBinThreads), 0, s, a);
+  fbr_launch((k_bin_tile<2, 8>), dim3(gq), dim3(kBinThreads), 0, s, a, iter, st);
+  fbr_launch((k_gn_knn_list<2, 8>), dim3(gq), dim3(256), 0, s, a, iter);
   return true;
 }
 
@@ -439,9 +445,8 @@ unsigned long long* knn_tile_stats_buffer() {
 
 }  // namespace fbr
 
-// [queries, tile-served queries, tile loads, points loaded into tiles, tile failures, of which box
-// too large / load too long / too many points] since the last reset; -1 when the counters are off
-// (FBR_KNN_TILE_STATS unset).
+// [queries, binned queries, tiles built, points in tiles, points scanned by the tile loads, tiles
+// over capacity, 0, 0] since the last reset; -1 when the counters are off (FBR_KNN_TILE_STATS unset).
 extern "C" int fbr_diag_knn_tile_stats(unsigned long long* out, int reset) {
   unsigned long long* p = fbr::knn_tile_stats_buffer();
   if (!p) return -1;

@@ -41,7 +41,7 @@ namespace fbr {
 __global__ void k_gn_init(GnArgs a) {
   __shared__ int32_t scan[1024];
   const int tid = threadIdx.x;
-  for (int i = tid; i < 3 * max(1, a.max_iter); i += 1024) a.iter_cnt[i] = 0;  // k_gn_solve's + fallback counters
+  for (int i = tid; i < 4 * max(1, a.max_iter); i += 1024) a.iter_cnt[i] = 0;  // k_gn_solve's + block-tile counters
   int base = 0;
   for (int j0 = 0; j0 < a.B; j0 += 1024) {
     const int job = j0 + tid;

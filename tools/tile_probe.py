@@ -26,7 +26,7 @@ with api.Context(synth.config_params(cfg, max_batch=B)) as c:
         p, s = c.process_batch(scans, guesses)
     dt = (time.perf_counter() - t) / rep
     ts = api.knn_tile_stats()
-keys = ["queries", "served", "loads", "loaded_pts", "fails", "fail_box", "fail_load", "fail_pts"]
+keys = ["queries", "binned", "tiles", "tile_pts", "load_scanned", "tile_overflow", "_6", "_7"]
 print(json.dumps({"cfg": cfg, "B": B, "env": {k: v for k, v in os.environ.items() if k.startswith("FBR_KNN")},
                   "s_per_batch": round(dt, 4), "status_ok": int((s["status"] == 0).sum()),
                   "iters": float(s["iterations"].mean()),
