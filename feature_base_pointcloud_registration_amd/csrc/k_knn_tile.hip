@@ -397,12 +397,13 @@ __global__ void __launch_bounds__(256) k_gn_knn_list(GnArgs a, int iter) {
   }
 }
 
-// FBR_KNN_TILE: 1 (default) serves iterations >= 1 on dense 0.5 m x 0.125 m grids from the block
-// tiles; 0 keeps the grid search for every query.
+// FBR_KNN_TILE: 1 serves iterations >= 1 on dense 0.5 m x 0.125 m grids from the block tiles; 0
+// (the default: the tiles measured slower than the grid search) keeps the grid
+// search for every query.
 bool knn_tile_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("FBR_KNN_TILE");
-    return e ? std::atoi(e) != 0 : true;
+    return e ? std::atoi(e) != 0 : false;
   }();
   return v;
 }

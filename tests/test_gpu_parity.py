@@ -463,7 +463,7 @@ def test_c3_ouster_registration_matches_oracle():
 
 def test_knn_tile_is_bit_identical_to_global_search():
     """Dense maps from the second Gauss-Newton iteration on: the query-binned LDS block tiles
-    (k_knn_tile.hip, the default) against the grid search for every query (FBR_KNN_TILE=0), each in a
+    (k_knn_tile.hip, FBR_KNN_TILE=1) against the grid search for every query (FBR_KNN_TILE=0), each in a
     child process: identical poses and stats bytes on two C5 jobs (a ~5.8M-point map shared by
     both jobs' queries), with most queries binned into tiles."""
     gts = [synth.job(s) for s in (11, 12)]
