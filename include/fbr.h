@@ -376,8 +376,9 @@ int fbr_batch_results(fbr_ctx* ctx, float* poses_out /* [n_jobs][6] */,
  * memory of the ctx's device, [n_jobs][8] x 4 B) — the payload of the cross-GPU pose all-gather. */
 int fbr_batch_export(fbr_ctx* ctx, void* device_dst);
 /* Pipelined form: export the records of the oldest launch not yet exported, if it is fully
- * enqueued (after fbr_batch_launch n: launch n-1; after fbr_batch_flush: the latest), without
- * waiting for the launch in flight; launches are exported in launch order.  The copy runs on that launch's stream after it, and after the
+ * enqueued (after fbr_batch_launch n: at least launch n - (FBR_PIPE - 1); after fbr_batch_flush:
+ * every launch), without waiting for the launches in flight; launches are exported in launch
+ * order, each once.  The copy runs on that launch's stream after it, and after the
  * work queued so far on `wait_stream` (a HIP stream of the caller still reading device_dst, or
  * NULL); *export_stream receives the stream to wait on before reading device_dst, *launch_id the
  * launch number (0, 1, ... since the context was created), or -1 (nothing to export: no copy). */
