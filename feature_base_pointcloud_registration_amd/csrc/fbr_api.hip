@@ -880,13 +880,15 @@ class CopyPool {
   }
 
  private:
-  // Idle workers spin for spin_us (FBR_COPY_SPIN_US, default 1000 us) after an upload, so a
-  // pose-chained scan stream (one call every ~0.7 ms) finds them awake, then sleep on the
-  // condition variable; 0 = never spin (no host cores held between calls).
+  // Idle workers spin for spin_us (FBR_COPY_SPIN_US, default 5000 us) after an upload, so a
+  // pose-chained scan stream (one call every ~0.7-0.9 ms, the caller's own work between calls
+  // included) finds them awake, then sleep on the condition variable; 0 = never spin (no host
+  // cores held between calls).  With 1000 us, calls that came a little late found the workers
+  // asleep and the futex wake-up put ms-scale outliers into the upload (p99 0.81 -> 3.9 ms).
   static int64_t spin_ns() {
     static const int64_t v = [] {
       const char* e = std::getenv("FBR_COPY_SPIN_US");
-      return (int64_t)(e ? std::max(0, std::atoi(e)) : 1000) * 1000;
+      return (int64_t)(e ? std::max(0, std::atoi(e)) : 5000) * 1000;
     }();
     return v;
   }
@@ -944,7 +946,11 @@ hipError_t pinned_upload_async(int dev, void* d_dst, void* h_stage, const void* 
   const size_t nchunk = (bytes + kChunk - 1) / kChunk;
   std::atomic<int> err{(int)hipSuccess};
   const std::function<void(int)> fn = [&](int p) {
-    if (p > 0) (void)hipSetDevice(dev);  // pool workers serve every context: the stream's device
+    thread_local int cur_dev = -1;  // pool workers serve every context: the stream's device
+    if (p > 0 && cur_dev != dev) {
+      (void)hipSetDevice(dev);
+      cur_dev = dev;
+    }
     for (size_t k = (size_t)p; k < nchunk; k += CopyPool::kWorkers + 1) {
       const size_t b = k * kChunk, e = std::min(bytes, b + kChunk);
       std::memcpy((uint8_t*)h_stage + b, (const uint8_t*)src + b, e - b);
