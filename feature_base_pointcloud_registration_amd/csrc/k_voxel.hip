@@ -30,6 +30,7 @@
 #include "fbr_kernels.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -688,6 +689,158 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
     total = vg_sort_emit<T, uint32_t, 9, false>(kb, vb, n, G.nbits, hist, wsum, in, out);
   }
   if (tid == 0) S.cnt_out[seg] = total;
+}
+
+// Few segments (single-scan calls: one corner and one surf cloud) leave all but two CUs idle in
+// k_voxel_grid_ip.  Here P workgroups share a segment (block = seg * P + part): each computes the
+// grid and a histogram of the keys' top bits over the whole cloud (the same in every part), keeps
+// the points of its key range (the bins between the n * part / P and n * (part + 1) / P quantiles)
+// in index order, sorts them in LDS and emits their voxels.  Equal keys share a bin, so every voxel
+// lies in one part, and the parts' key ranges are ascending: part p's voxels go after the voxels of
+// parts < p.  Each part publishes its voxel count as (gen << 32 | count) in flags[block], then reads
+// the lower parts' counts (decoupled look-back: a lower block was dispatched earlier, so it runs to
+// completion; the wait is bounded anyway, and gives up with a zero count rather than hang).  Same
+// output as k_voxel_grid_ip (`test_split_voxel_grid_is_bit_identical`).  Default-order mode only.
+template <int T, int KPL>
+__global__ void __launch_bounds__(T) k_voxel_grid_split(VgArgs A, int P, unsigned long long* flags, unsigned gen) {
+  constexpr int NW = T / 64, LCAP = T * KPL;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int blk = blockIdx.x, part = blk % P;
+  int seg = blk / P;
+  const bool second = seg >= A.s[0].nseg;
+  const VgSet S = second ? A.s[1] : A.s[0];
+  if (second) seg -= A.s[0].nseg;
+  uint32_t* hist = (uint32_t*)smem;  // [NW + 1][256] in-place sort counters; 1024 key bins before
+  uint32_t* wsum = hist + (NW + 1) * 512;
+  float* mm = (float*)(wsum + NW);
+  int* misc = (int*)(mm + NW * 6);
+  const int n = (int)min((int64_t)S.cnt_in[seg], S.cap);
+  const float4* in = S.in + (int64_t)seg * S.stride_in;
+  float4* out = S.out + (int64_t)seg * S.stride_out;
+  if (n <= 0) {
+    if (tid == 0 && part == 0) S.cnt_out[seg] = 0;
+    return;
+  }
+  float mn[3], mx[3];
+  vg_seg_bounds<T>(S, seg, n, in, mn, mx, mm);
+  VgGrid G;
+  G.init(mn, mx, S.leaf, S.morton != 0);
+  if (G.overflow) {  // PCL's "leaf size too small": output = input
+    if (part == 0) {
+      for (int i = tid; i < n; i += T) out[i] = in[i];
+      if (tid == 0) S.cnt_out[seg] = n;
+    }
+    return;
+  }
+  if (n > LCAP) {  // over the LDS capacity: part 0 alone, k_voxel_grid_ip's global-scratch path
+    if (part != 0) return;
+    uint32_t* sc = S.scratch + (int64_t)seg * kVgScratch * S.cap;
+    uint32_t* kb[2] = {sc, sc + S.cap};
+    uint32_t* vb[2] = {sc + 2 * S.cap, sc + 3 * S.cap};
+    for (int i = tid; i < n; i += T) {
+      kb[0][i] = G.key(in[i]);
+      vb[0][i] = (uint32_t)i;
+    }
+    __syncthreads();
+    const int total = vg_sort_emit<T, uint32_t, 9, false>(kb, vb, n, G.nbits, hist, wsum, in, out);
+    if (tid == 0) S.cnt_out[seg] = total;
+    return;
+  }
+  // ---- key histogram over the top hb bits (every part computes the same) ----
+  const int hb = min(10, G.nbits), sh = G.nbits - hb, nbin = 1 << hb;
+  for (int b = tid; b < nbin; b += T) hist[b] = 0u;
+  __syncthreads();
+  for (int i = tid; i < n; i += T) atomicAdd(&hist[G.key(in[i]) >> sh], 1u);
+  __syncthreads();
+  // this part's bin range [b0, b1): the first bins whose inclusive prefix exceeds n * part / P
+  // and n * (part + 1) / P (inclusive scan over the bins, one bin per thread, T >= 1024)
+  {
+    const uint32_t c = tid < nbin ? hist[tid] : 0u;
+    uint32_t inc = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(inc, off);
+      if (lane >= off) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int k = 0; k < w; ++k) pre += wsum[k];
+    inc += pre;  // inclusive prefix of bin tid
+    const uint32_t lo = (uint32_t)(((int64_t)n * part) / P), hi = (uint32_t)(((int64_t)n * (part + 1)) / P);
+    // bin tid starts the range of part q when inc(tid - 1) <= n q / P < inc(tid): the bins of
+    // part q are those whose exclusive prefix lies in [n q / P, n (q + 1) / P) -- every bin lands in
+    // exactly one part, in order
+    const uint32_t ex = inc - c;
+    const bool mine = tid < nbin && c > 0 && ex >= lo && (part == P - 1 || ex < hi);
+    __syncthreads();
+    if (tid == 0) { misc[0] = nbin; misc[1] = -1; }
+    __syncthreads();
+    if (mine) atomicMin(&misc[0], tid);
+    if (mine) atomicMax(&misc[1], tid);
+    __syncthreads();
+  }
+  const int b0 = misc[0], b1 = misc[1];  // empty range: b0 = nbin, b1 = -1
+  // ---- this part's points in index order (block-wide ordered compaction) ----
+  unsigned char* q = smem + ((((unsigned char*)(misc + 4) - smem) + 15) & ~15);
+  FBR_LDS_AS uint32_t* keys = (FBR_LDS_AS uint32_t*)q;
+  FBR_LDS_AS uint16_t* vals = (FBR_LDS_AS uint16_t*)((FBR_LDS_AS uint32_t*)q + LCAP);
+  int nk = 0;
+  for (int i0 = 0; i0 < n; i0 += T) {
+    const int i = i0 + tid;
+    uint32_t key = 0;
+    bool keep = false;
+    if (i < n) {
+      key = G.key(in[i]);
+      const int b = (int)(key >> sh);
+      keep = b >= b0 && b <= b1;
+    }
+    const uint64_t m = __ballot(keep);
+    if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    int pre = nk, tot = 0;
+    for (int k = 0; k < NW; ++k) {
+      if (k < w) pre += (int)wsum[k];
+      tot += (int)wsum[k];
+    }
+    if (keep) {
+      const int pos = pre + __popcll(m & ((1ull << lane) - 1ull));
+      keys[pos] = key;
+      vals[pos] = (uint16_t)i;
+    }
+    nk += tot;
+    __syncthreads();
+  }
+  if (nk > 0) vg_radix_sort_inplace<T, KPL>(keys, vals, nk, G.nbits, hist, wsum);
+  // ---- voxel count, publish, look back ----
+  int heads = 0;
+  for (int i = tid; i < nk; i += T) heads += (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+  for (int off = 32; off > 0; off >>= 1) heads += __shfl_xor(heads, off);
+  __syncthreads();
+  if (lane == 0) wsum[w] = (uint32_t)heads;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t V = 0;
+    for (int k = 0; k < NW; ++k) V += wsum[k];
+    __hip_atomic_store(&flags[blk], ((unsigned long long)gen << 32) | V, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t off = 0;
+    for (int j = blk - part; j < blk; ++j) {
+      unsigned long long f = 0;
+      for (int spin = 0; spin < (1 << 24); ++spin) {
+        f = __hip_atomic_load(&flags[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(f >> 32) == gen) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      off += (unsigned)(f >> 32) == gen ? (uint32_t)f : 0u;
+    }
+    misc[2] = (int)off;
+    misc[3] = (int)V;
+  }
+  __syncthreads();
+  const int off = misc[2], V = misc[3];
+  if (nk > 0) vg_emit<T, true>(keys, vals, nk, hist, wsum, in, out + off);
+  if (tid == 0 && part == P - 1) S.cnt_out[seg] = off + V;
 }
 
 // Per-ring front end (featureExtraction.h:279-292): the surf candidates of (job, ring) are the
@@ -1563,6 +1716,16 @@ size_t voxel_lds_bytes(const VgArgs& a, int threads, bool lds_mode) {
 }
 
 constexpr int kVgIpKpl = 18;  // k_voxel_grid_ip: segments up to 1024 * 18 points sort in LDS
+constexpr int kVgSplitSlots = 16;   // k_voxel_grid_split: segments x parts per launch
+constexpr int kVgSplitRing = 1024;  // flag regions: a launch's own region (concurrent launches)
+int vg_split() {
+  static const int v = [] {
+    const char* e = std::getenv("FBR_VG_SPLIT");
+    const int p = e ? std::atoi(e) : 4;
+    return p < 2 ? 1 : std::min(p, 8);
+  }();
+  return v;
+}
 
 void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
   const int nseg = a.s[0].nseg + a.s[1].nseg;
@@ -1571,6 +1734,24 @@ void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
   for (int k = 0; k < 2; ++k)
     if (a.s[k].nseg > 0) cap = std::max<int64_t>(cap, a.s[k].cap);
   const bool exact = a.s[0].exact || a.s[1].exact;  // both sets share vg_exact()
+  // few segments (single-scan calls): P workgroups per segment (FBR_VG_SPLIT = P, default 4; 1 off)
+  const int P = vg_split();
+  if (!exact && P > 1 && cap > kVgLdsCap && vg_inplace() && nseg * P <= kVgSplitSlots) {
+    static unsigned long long* flags = [] {
+      unsigned long long* f = nullptr;
+      if (hipMalloc(&f, sizeof(unsigned long long) * kVgSplitSlots * kVgSplitRing) != hipSuccess) return (unsigned long long*)nullptr;
+      if (hipMemset(f, 0, sizeof(unsigned long long) * kVgSplitSlots * kVgSplitRing) != hipSuccess) return (unsigned long long*)nullptr;
+      return f;
+    }();
+    static std::atomic<unsigned> gen{0};
+    if (flags) {
+      const unsigned g = gen.fetch_add(1) + 1;  // never 0 (the zeroed flags)
+      const size_t lds = voxel_lds_bytes(a, 1024, false) + (size_t)1024 * kVgIpKpl * (sizeof(uint32_t) + sizeof(uint16_t));
+      fbr_launch((k_voxel_grid_split<1024, kVgIpKpl>), dim3(nseg * P), dim3(1024), lds, s, a, P,
+                 flags + (size_t)(g % kVgSplitRing) * kVgSplitSlots, g);
+      return;
+    }
+  }
   auto go = [&](auto ex) {
     constexpr bool E = decltype(ex)::value;
     if (cap <= kVgLdsCap) {

@@ -578,6 +578,75 @@ def test_voxel_grid_inplace_lds_sort_matches_global_scratch_kernel():
     assert r.stdout == b"".join(outs[n].tobytes() for n in clouds)
 
 
+def test_split_voxel_grid_is_bit_identical():
+    """Few-segment VoxelGrids (single-scan calls, fbr_voxel_grid) run on P workgroups per segment
+    (k_voxel_grid_split: key-range parts, decoupled look-back for the output offsets).  Its bytes
+    equal the one-workgroup kernel's (FBR_VG_SPLIT=1, child process) on uniform, clustered,
+    single-voxel and tiny clouds and across the LDS capacity, and a pose-chained C2 scan stream
+    gives the same poses."""
+    import subprocess
+    import sys
+    rng = np.random.default_rng(33)
+    clouds = {}
+    for name, n in (("uniform", 9000), ("cap", 18432), ("over", 18433), ("tiny", 4100), ("one_voxel", 6000),
+                    ("clustered", 15000)):
+        pts = np.zeros(n, POINT_XYZI)
+        if name == "one_voxel":
+            pts["x"], pts["y"], pts["z"] = rng.uniform(1.01, 1.39, n), rng.uniform(2.01, 2.39, n), rng.uniform(0.01, 0.39, n)
+        elif name == "clustered":
+            c = rng.integers(0, 5, n)
+            pts["x"] = rng.normal(c * 7.0, 0.3, n)
+            pts["y"] = rng.normal(c * -3.0, 0.3, n)
+            pts["z"] = rng.normal(0, 0.2, n)
+        else:
+            pts["x"], pts["y"] = rng.uniform(-30, 30, n), rng.uniform(-30, 30, n)
+            pts["z"] = rng.normal(0, 0.4, n) + (rng.random(n) < 0.3) * rng.uniform(0, 6, n)
+        pts["intensity"] = rng.uniform(0, 255, n)
+        clouds[name] = pts
+    with api.Context(default_params(16, 900)) as ctx:
+        outs = {k: ctx.voxel_grid(p, 0.4) for k, p in clouds.items()}
+    for k, p in clouds.items():
+        assert len(outs[k]) == len(O.voxel_grid(p, 0.4)), k
+    assert len(outs["one_voxel"]) == 1
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_vg_split_in.npz")
+    np.savez(path, **clouds)
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api; "
+            "from feature_base_pointcloud_registration_amd.fbr_types import default_params; "
+            "c = api.Context(default_params(16, 900)); d = np.load(%r); "
+            "sys.stdout.buffer.write(b''.join(c.voxel_grid(d[k], 0.4).tobytes() for k in %r))"
+            % (REPO, path, list(clouds)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, FBR_VG_SPLIT="1"),
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout == b"".join(outs[k].tobytes() for k in clouds)
+    # the single-scan path (mapping DS of one corner and one surf cloud) on a pose-chained stream
+    P = default_params(64, 1800)
+    cmap, smap = synth.config_map("C2")
+    traj = synth.trajectory(7, 4)
+    scans = [synth.scan(p, 64, 1800, seed=700 + k) for k, p in enumerate(traj)]
+    spath = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_vg_split_scans.npz")
+    np.savez(spath, *scans)
+    _, guess = synth.job(7)
+    poses = []
+    with api.Context(P) as ctx:
+        ctx.set_map(cmap, smap)
+        pose = guess.copy()
+        for k, sc in enumerate(scans):
+            pose, _ = ctx.process_scan(sc, 0.1 * k, pose)
+            poses.append(pose.copy())
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api, synth; "
+            "from feature_base_pointcloud_registration_amd.fbr_types import default_params; "
+            "d = np.load(%r); c = api.Context(default_params(64, 1800)); c.set_map(*synth.config_map('C2')); "
+            "pose = np.array(%r, np.float32); out = []\n"
+            "for k in range(%d):\n"
+            "    pose, _ = c.process_scan(d['arr_%%d' %% k], 0.1 * k, pose); out.append(pose.copy())\n"
+            "sys.stdout.buffer.write(np.stack(out).tobytes())" % (REPO, spath, [float(x) for x in guess], len(scans)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, FBR_VG_SPLIT="1"),
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout == np.stack(poses).astype(np.float32).tobytes()
+
+
 # ------------------------------------------------------------------------------- map grids
 def _c2_batch_in_child(jobs, env, sparse):
     """Poses + stats bytes of `jobs` (C2) registered in a child process with extra environment
