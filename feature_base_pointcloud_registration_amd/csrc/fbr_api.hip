@@ -868,6 +868,16 @@ class CopyPool {
   }
   void run(const std::function<void(int)>& fn) {
     std::lock_guard<std::mutex> serial(run_mu_);  // one upload at a time (contexts may share it)
+    // adaptive spin: twice the smoothed interval between uploads, within [0.2, spin_ns()] ms
+    const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::steady_clock::now().time_since_epoch()).count();
+    if (last_run_ns_ > 0) {
+      const double dt = (double)(now - last_run_ns_);
+      ema_ns_ = ema_ns_ > 0.0 ? 0.8 * ema_ns_ + 0.2 * dt : dt;
+      const int64_t cap = spin_ns();
+      spin_cur_.store(std::min<int64_t>(cap, std::max<int64_t>(std::min<int64_t>(cap, 200000), (int64_t)(2.0 * ema_ns_))));
+    }
+    last_run_ns_ = now;
     fn_ = &fn;
     pending_.store(kWorkers);
     {
@@ -880,11 +890,12 @@ class CopyPool {
   }
 
  private:
-  // Idle workers spin for spin_us (FBR_COPY_SPIN_US, default 5000 us) after an upload, so a
-  // pose-chained scan stream (one call every ~0.7-0.9 ms, the caller's own work between calls
-  // included) finds them awake, then sleep on the condition variable; 0 = never spin (no host
-  // cores held between calls).  With 1000 us, calls that came a little late found the workers
-  // asleep and the futex wake-up put ms-scale outliers into the upload (p99 0.81 -> 3.9 ms).
+  // Idle workers spin after an upload for twice the smoothed interval between uploads, at least
+  // 0.2 ms and at most spin_us (FBR_COPY_SPIN_US, default 5000 us), so a pose-chained scan stream
+  // (one call every ~0.7-0.9 ms, the caller's own work included) finds them awake while a sensor-
+  // rate stream (a scan every 100 ms) holds the cores for at most 5 % of the time; then they sleep
+  // on the condition variable.  0 = never spin.  A fixed 1000 us spin let late calls find the
+  // workers asleep, and the futex wake-up put ms-scale outliers into the upload (p99 3.9 ms).
   static int64_t spin_ns() {
     static const int64_t v = [] {
       const char* e = std::getenv("FBR_COPY_SPIN_US");
@@ -896,14 +907,14 @@ class CopyPool {
     uint64_t seen = 0;
     while (true) {
       uint64_t g = gen_.load();
-      if (g == seen && spin_ns() > 0) {
+      const int64_t spin = spin_cur_.load();
+      if (g == seen && spin > 0) {
         const auto t0 = std::chrono::steady_clock::now();
-        for (int spin = 0; g == seen; ++spin) {
+        for (int k = 0; g == seen; ++k) {
           __builtin_ia32_pause();
           g = gen_.load();
-          if ((spin & 255) == 255 &&
-              std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() >
-                  spin_ns())
+          if ((k & 255) == 255 &&
+              std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() > spin)
             break;
         }
       }
@@ -925,6 +936,9 @@ class CopyPool {
   std::atomic<int> pending_{0};
   const std::function<void(int)>* fn_ = nullptr;
   std::atomic<bool> stop_{false};
+  std::atomic<int64_t> spin_cur_{spin_ns()};
+  int64_t last_run_ns_ = 0;
+  double ema_ns_ = 0.0;
 };
 
 CopyPool& copy_pool() {
