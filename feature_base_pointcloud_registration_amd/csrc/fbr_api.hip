@@ -868,14 +868,14 @@ class CopyPool {
   }
   void run(const std::function<void(int)>& fn) {
     std::lock_guard<std::mutex> serial(run_mu_);  // one upload at a time (contexts may share it)
-    // adaptive spin: twice the smoothed interval between uploads, within [0.2, spin_ns()] ms
+    // adaptive spin: 4x the smoothed interval between uploads, within [1 ms, spin_ns()]
     const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
                             std::chrono::steady_clock::now().time_since_epoch()).count();
     if (last_run_ns_ > 0) {
       const double dt = (double)(now - last_run_ns_);
       ema_ns_ = ema_ns_ > 0.0 ? 0.8 * ema_ns_ + 0.2 * dt : dt;
       const int64_t cap = spin_ns();
-      spin_cur_.store(std::min<int64_t>(cap, std::max<int64_t>(std::min<int64_t>(cap, 200000), (int64_t)(2.0 * ema_ns_))));
+      spin_cur_.store(std::min<int64_t>(cap, std::max<int64_t>(std::min<int64_t>(cap, 1000000), (int64_t)(4.0 * ema_ns_))));
     }
     last_run_ns_ = now;
     fn_ = &fn;
@@ -890,8 +890,8 @@ class CopyPool {
   }
 
  private:
-  // Idle workers spin after an upload for twice the smoothed interval between uploads, at least
-  // 0.2 ms and at most spin_us (FBR_COPY_SPIN_US, default 5000 us), so a pose-chained scan stream
+  // Idle workers spin after an upload for 4x the smoothed interval between uploads, at least 1 ms
+  // and at most spin_us (FBR_COPY_SPIN_US, default 5000 us), so a pose-chained scan stream
   // (one call every ~0.7-0.9 ms, the caller's own work included) finds them awake while a sensor-
   // rate stream (a scan every 100 ms) holds the cores for at most 5 % of the time; then they sleep
   // on the condition variable.  0 = never spin.  A fixed 1000 us spin let late calls find the

@@ -1641,12 +1641,16 @@ __global__ void __launch_bounds__(256) k_voxel_ring_q(VgRing A) {
 // The per-ring filter of the default order (FBR_VR_WAVE): 0 = the 512-thread kernel, 1 = one
 // wave per ring (2.3x fewer VALU instructions but latency-bound: 481 vs 407 us per sequential
 // 256-job launch, profiles/r04e_voxel_ring_wave_ab.txt, r04j_valu_*), 2 = four waves per ring.
-int vr_mode() {
+// FBR_VR_WAVE: 0 the 512-thread kernel, 1 one wave per ring, 2 four waves per ring; unset: four
+// waves per ring, except launches of at most 256 rings (single scans), where the 512-thread kernel
+// finishes a ring sooner (C2 single scan: 19.8 vs 34.3 us, profiles/r04u_latency_scan_timeline.txt)
+// and the chip has room for the extra threads.
+int vr_mode(int nseg) {
   static const int v = [] {
     const char* e = std::getenv("FBR_VR_WAVE");
-    return e ? std::atoi(e) : 2;
+    return e ? std::atoi(e) : -1;
   }();
-  return v;
+  return v >= 0 ? v : (nseg <= 256 ? 0 : 2);
 }
 
 size_t voxel_ring_lds_bytes(const VgRing& a, int threads, int kpt) {
@@ -1673,9 +1677,9 @@ void launch_voxel_ring(hipStream_t s, const VgRing& a) {
   };
   if (a.exact) {
     go(std::true_type{});
-  } else if (vr_mode() != 0 && a.dbg == 0 && a.cap <= 4096) {
+  } else if (vr_mode(nseg) != 0 && a.dbg == 0 && a.cap <= 4096) {
     const size_t lds = (((size_t)a.cap + 1) * 4 + (size_t)a.cap * 2 + ((size_t)a.cap + 1) * 2 + 15) & ~(size_t)15;
-    if (vr_mode() == 1) fbr_launch(k_voxel_ring_wave, dim3(nseg), dim3(64), lds, s, a);
+    if (vr_mode(nseg) == 1) fbr_launch(k_voxel_ring_wave, dim3(nseg), dim3(64), lds, s, a);
     else if (a.cap <= 4 * 64 * 8) fbr_launch(k_voxel_ring_q<8>, dim3(nseg), dim3(256), lds, s, a);
     else fbr_launch(k_voxel_ring_q<16>, dim3(nseg), dim3(256), lds, s, a);
   } else {

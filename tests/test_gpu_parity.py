@@ -592,7 +592,7 @@ def test_split_voxel_grid_is_bit_identical():
                     ("clustered", 15000)):
         pts = np.zeros(n, POINT_XYZI)
         if name == "one_voxel":
-            pts["x"], pts["y"], pts["z"] = rng.uniform(1.01, 1.39, n), rng.uniform(2.01, 2.39, n), rng.uniform(0.01, 0.39, n)
+            pts["x"], pts["y"], pts["z"] = rng.uniform(0.81, 1.19, n), rng.uniform(2.01, 2.39, n), rng.uniform(0.01, 0.39, n)
         elif name == "clustered":
             c = rng.integers(0, 5, n)
             pts["x"] = rng.normal(c * 7.0, 0.3, n)
@@ -756,13 +756,13 @@ def _adversarial_ring_scan(H, W, seed):
     return np.concatenate(pts)
 
 
-@pytest.mark.parametrize("mode", ["0", "1"], ids=["workgroup-512", "one-wave"])
+@pytest.mark.parametrize("mode", ["2", "1"], ids=["four-waves", "one-wave"])
 def test_wave_ring_filter_is_bit_identical_to_workgroup_kernel(mode):
-    """The default four-waves-per-ring surf VoxelGrid (k_voxel_ring_q: register bitonic /
-    counting-rank run sorts) against the 512-thread kernel (FBR_VR_WAVE=0) and the one-wave kernel
-    (FBR_VR_WAVE=1), each in a child process: identical surf clouds, labels and corners on C1 / C2 /
-    C3 scans and on adversarial rings (every candidate its own voxel), and within SURF_ULPS of the
-    oracle."""
+    """The per-ring surf VoxelGrid kernels: the four-waves-per-ring kernel (k_voxel_ring_q, register
+    bitonic / counting-rank run sorts; FBR_VR_WAVE=2, the batch default) and the one-wave kernel
+    (FBR_VR_WAVE=1), each in a child process, against the 512-thread kernel (the default for single
+    scans, in process): identical surf clouds, labels and corners on C1 / C2 / C3 scans and on
+    adversarial rings (every candidate its own voxel), and within SURF_ULPS of the oracle."""
     import subprocess
     import sys
     cases = [("C1", synth.scan(synth.job(1)[0], 16, 1800, seed=1)),
