@@ -115,7 +115,7 @@ struct Sub {
 };
 
 // The Gauss-Newton iterations of one launch that the host has still to enqueue.  The host stays
-// kLag iterations ahead of each sub-batch and stops once its k_gn_solve reports that no job is
+// `lag` (gn_lag) iterations ahead of each sub-batch and stops once its k_gn_solve reports that no job is
 // active (flags in host-mapped memory), so a launch's tail cannot be enqueued before the device
 // has run most of it; two launches in flight are advanced together (fbr_batch_launch).
 struct GnRun {
@@ -126,7 +126,8 @@ struct GnRun {
   Sub subs[kMaxSub];
   GnArgs a[kMaxSub];
   bool live[kMaxSub] = {}, watch[kMaxSub] = {}, done[kMaxSub] = {};
-  int active[kMaxSub] = {};  // jobs still iterating kLag iterations ago (an upper bound now)
+  int lag = 2;               // gn_lag: iterations enqueued ahead of the latest flag read
+  int active[kMaxSub] = {};  // jobs still iterating `lag` iterations ago (an upper bound now)
   int it[kMaxSub] = {};      // next iteration to enqueue
   long polls[kMaxSub] = {};  // unanswered flag reads of the current wait
 };
@@ -651,7 +652,18 @@ int gn_tail_div() {
   return v;
 }
 
-constexpr int kLag = 2;  // iterations the host enqueues ahead of a sub-batch's latest flag
+// Iterations the host enqueues ahead of a sub-batch's latest flag (FBR_GN_LAG): 2 for batches; 3
+// for runs of at most 2 jobs (single scans), whose iterations are short enough (~40 us) that
+// waiting for the flag two iterations back left a ~5.7 us gap before every iteration from the
+// third on, while the extra iteration enqueued after convergence costs ~8 us (its workgroups exit
+// at once: no job is active).
+int gn_lag(int jobs) {
+  static const int v = [] {
+    const char* e = std::getenv("FBR_GN_LAG");
+    return e ? std::max(1, std::min(8, std::atoi(e))) : 0;
+  }();
+  return v ? v : (jobs <= 2 ? 3 : 2);
+}
 
 void gn_run_start(fbr_ctx* c, GnRun& r, const Sub* subs, int nsub, bool trace) {
   r = GnRun{};
@@ -659,6 +671,9 @@ void gn_run_start(fbr_ctx* c, GnRun& r, const Sub* subs, int nsub, bool trace) {
   r.trace = trace;
   r.nsub = nsub;
   r.gen = ++c->gn_gen;
+  int jobs = 0;
+  for (int k = 0; k < nsub; ++k) jobs += subs[k].B;
+  r.lag = gn_lag(jobs);
   for (int k = 0; k < nsub; ++k) {
     r.subs[k] = subs[k];
     r.a[k] = gn_args(c, subs[k], trace);
@@ -679,8 +694,8 @@ int gn_run_pass(fbr_ctx* c, GnRun& r, bool block, bool* progress) {
     if (r.done[k]) continue;
     const Sub& sb = r.subs[k];
     const int it = r.it[k];
-    if (r.live[k] && it < c->P.max_iterations && r.watch[k] && it >= kLag) {
-      volatile unsigned long long* f = c->h_iter_flags + (int64_t)sb.k * mi + (it - kLag);
+    if (r.live[k] && it < c->P.max_iterations && r.watch[k] && it >= r.lag) {
+      volatile unsigned long long* f = c->h_iter_flags + (int64_t)sb.k * mi + (it - r.lag);
       unsigned long long v = *f;
       const auto tspin = std::chrono::steady_clock::now();
       while ((v >> 32) != g32) {
