@@ -652,17 +652,16 @@ int gn_tail_div() {
   return v;
 }
 
-// Iterations the host enqueues ahead of a sub-batch's latest flag (FBR_GN_LAG): 2 for batches; 3
-// for runs of at most 2 jobs (single scans), whose iterations are short enough (~40 us) that
-// waiting for the flag two iterations back left a ~5.7 us gap before every iteration from the
-// third on, while the extra iteration enqueued after convergence costs ~8 us (its workgroups exit
-// at once: no job is active).
+// Iterations the host enqueues ahead of a sub-batch's latest flag (FBR_GN_LAG, default 2).  Three
+// for single scans (~40 us iterations, a ~5.7 us host gap before each from the third on) measured
+// no better: C2 latency p50 0.719 / 0.746 ms against 0.716 / 0.716 with 2 (profiles/r04v_*).
 int gn_lag(int jobs) {
   static const int v = [] {
     const char* e = std::getenv("FBR_GN_LAG");
     return e ? std::max(1, std::min(8, std::atoi(e))) : 0;
   }();
-  return v ? v : (jobs <= 2 ? 3 : 2);
+  (void)jobs;
+  return v ? v : 2;
 }
 
 void gn_run_start(fbr_ctx* c, GnRun& r, const Sub* subs, int nsub, bool trace) {
