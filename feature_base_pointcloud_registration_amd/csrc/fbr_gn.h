@@ -821,13 +821,23 @@ inline bool knn_flat() {
   return v;
 }
 
+// Flat row queue for the 0.5 m cells of dense maps too (FBR_KNN_FLAT_R2=1; 25 rows x 256 lanes of
+// int2 = 50 KB of LDS per workgroup).
+inline bool knn_flat_r2() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_KNN_FLAT_R2");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+
 template <int R, bool F>
 void launch_gn_knn_r(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
   if constexpr (!F) {
     if (knn_lpq(a.B) == 8) return launch_gn_knn_rl<R, F, false, 8>(s, a, grid, use_prev);
   }
-  if constexpr (R == 1 && !F) {
-    if (use_prev && knn_flat()) return launch_gn_knn_rl<R, F, true>(s, a, grid, use_prev);
+  if constexpr (R <= 2 && !F) {
+    if (use_prev && knn_flat() && (R == 1 || knn_flat_r2())) return launch_gn_knn_rl<R, F, true>(s, a, grid, use_prev);
   }
   launch_gn_knn_rl<R, F, false>(s, a, grid, use_prev);
 }
