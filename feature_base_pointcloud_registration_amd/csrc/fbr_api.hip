@@ -429,7 +429,7 @@ int stage_project(fbr_ctx* c, const Sub& sb) {
     desk = DeskArgs{c->d_desk_mode + i0, c->d_desk + i0, c->d_rowmin + j0 * c->H};
   int32_t* owner = c->d_owner + j0 * c->HW;  // all kEmptyOwner: set at fbr_create, reset by k_compact
   TIMED_ON(c, sb.st, "project", launch_project(sb.st, c->d_pts + i0 * c->NMAX, c->d_nin + i0, c->NMAX, sb.B, c->H,
-                                               c->W, owner));
+                                               c->W, owner, c->d_err + j0));
   TIMED_ON(c, sb.st, "extract",
            launch_extract(sb.st, c->d_pts + i0 * c->NMAX, c->NMAX, owner, sb.B, c->H, c->W, c->d_rowcnt + j0 * c->H,
                           c->d_choff + j0 * c->H * (c->W / 32 + 1),
@@ -438,7 +438,8 @@ int stage_project(fbr_ctx* c, const Sub& sb) {
   return FBR_OK;
 }
 
-int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode) {
+// err_clear: stage_project has just cleared the jobs' feature-capacity flags (k_project).
+int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode, bool err_clear = false) {
   const int64_t j0 = sb.j0, HW = c->HW, H = c->H;
   FeatArgs a{};
   a.B = sb.B;
@@ -467,7 +468,7 @@ int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode) {
   feat_caps(c->W, a);
   a.gscratch = c->d_feat_scratch + j0 * H * a.gslot_bytes;
   a.stamps = c->d_feat_stamps ? c->d_feat_stamps + j0 * H * 12 : nullptr;
-  CK(hipMemsetAsync(c->d_err + j0, 0, sizeof(int32_t) * sb.B, sb.st));
+  if (!err_clear) CK(hipMemsetAsync(c->d_err + j0, 0, sizeof(int32_t) * sb.B, sb.st));
   TIMED_ON(c, sb.st, "features", launch_features(sb.st, a));
   VgRing v{};
   v.cloud = a.cloud;
@@ -1586,7 +1587,7 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
   const auto t0 = std::chrono::steady_clock::now();
   c->crop_join = false;
   int rc = stage_project(c, single_sub(c));
-  if (!rc) rc = stage_features(c, single_sub(c), true);
+  if (!rc) rc = stage_features(c, single_sub(c), true, true);
   if (rc) return rc;
   c->have_projection = true;
   fbr_reg_stats st;
@@ -1715,7 +1716,7 @@ int fbr_batch_launch(fbr_ctx* c) {
   }
   for (int k = 0; k < nsub && !rc; ++k) {
     rc = stage_project(c, subs[k]);
-    if (!rc) rc = stage_features(c, subs[k], false);
+    if (!rc) rc = stage_features(c, subs[k], false, true);
     if (!rc) rc = register_prepare(c, subs[k], false);
   }
   if (rc) return rc;

@@ -61,11 +61,14 @@ constexpr int kProjThreads = 256, kProjPPT = 8, kProjChunk = kProjThreads * kPro
 // 8 waves per SIMD hide the atomic latency.
 __global__ void __launch_bounds__(kProjThreads)
 k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ nin, int64_t nmax, int H, int W,
-          int tile_log2, int32_t* __restrict__ owner) {
+          int tile_log2, int32_t* __restrict__ owner, int32_t* __restrict__ err) {
   extern __shared__ int32_t tile[];  // [H][1 << tile_log2]
   __shared__ int32_t cellk[kProjChunk];
   __shared__ int red[2][kProjThreads / 64];
   const int job = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // the job's feature-capacity flags start clear (k_features ORs into them; this saves the
+  // single-scan path a 6 us fill dispatch on its critical path)
+  if (err && blockIdx.x == 0 && tid == 0) err[job] = 0;
   const int tcols = 1 << tile_log2, tcells = H << tile_log2;
   const int64_t n = nin[job];
   const fbr_point_xyzirt* P = pts + (int64_t)job * nmax;
@@ -398,14 +401,14 @@ void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int 
 }
 
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
-                    int W, int32_t* owner) {
+                    int W, int32_t* owner, int32_t* err) {
   int blocks = (int)((nmax + kProjChunk - 1) / kProjChunk);
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
   int tile_log2 = 6;  // 64 columns, shrunk so the tile stays <= 32 KB
   while (tile_log2 > 3 && ((int64_t)H << tile_log2) > 8192) --tile_log2;
   const size_t lds = sizeof(int32_t) * ((size_t)H << tile_log2);
-  fbr_launch(k_project, dim3(blocks, B), dim3(kProjThreads), lds, s, pts, nin, nmax, H, W, tile_log2, owner);
+  fbr_launch(k_project, dim3(blocks, B), dim3(kProjThreads), lds, s, pts, nin, nmax, H, W, tile_log2, owner, err);
 }
 
 // Compaction tile size in cells (FBR_COMPACT_CELLS: 512, 1024 or 2048).
