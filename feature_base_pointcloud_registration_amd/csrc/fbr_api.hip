@@ -154,6 +154,7 @@ struct fbr_ctx {
   int64_t exported = -1;      // latest launch whose records fbr_batch_export_ready exported
   hipEvent_t ev_staged = nullptr;  // the staged inputs are on the device (recorded on stream)
   hipEvent_t ev_fork = nullptr;    // single-scan side-stream fork
+  hipEvent_t ev_guess = nullptr;   // single-scan guess copied (side stream)
   hipEvent_t ev_ext = nullptr;     // a caller's stream, waited on before an export (fbr_batch_export_ready)
   int items_per_job = 0;
   int64_t HW = 0, NMAX = 0;
@@ -1283,6 +1284,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   }
   if (!sfail) sfail = hipEventCreateWithFlags(&c->ev_staged, hipEventDisableTiming) != hipSuccess ||
                      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+                     hipEventCreateWithFlags(&c->ev_guess, hipEventDisableTiming) != hipSuccess ||
                      hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming) != hipSuccess;
   if (sfail) {
     fbr_destroy(c);
@@ -1389,6 +1391,7 @@ int fbr_destroy(fbr_ctx* c) {
   }
   if (c->ev_staged) (void)hipEventDestroy(c->ev_staged);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_guess) (void)hipEventDestroy(c->ev_guess);
   if (c->ev_ext) (void)hipEventDestroy(c->ev_ext);
   delete c;
   return FBR_OK;
@@ -1586,25 +1589,31 @@ namespace {
 int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stats* stats) {
   const auto t0 = std::chrono::steady_clock::now();
   c->crop_join = false;
-  int rc = stage_project(c, single_sub(c));
+  const bool run = stamp - c->time_last >= c->P.mapping_process_interval;  // mapOptmization.h:279
+  if (run && !c->has_map) return FBR_ERR_NO_MAP;
+  int rc = FBR_OK;
+  if (run) {
+    // the guess and the CropBox statistics (which depend only on it) go on a side stream forked
+    // before the front end, so neither the 24-B copy nor its dispatch gap sits between the
+    // features and the mapping DS; the registration waits for the copy, copy_results joins the rest
+    CK(hipEventRecord(c->ev_fork, c->stream));
+    CK(hipStreamWaitEvent(c->xstream[1], c->ev_fork, 0));
+    CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->xstream[1]));
+    CK(hipEventRecord(c->ev_guess, c->xstream[1]));
+    rc = crop_stats(c, Sub{0, 1, 0, c->xstream[1], true});
+    if (rc) return rc;
+    CK(hipMemcpyAsync(c->h_crop, c->d_cropcnt, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, c->xstream[1]));
+    c->crop_join = true;
+  }
+  rc = stage_project(c, single_sub(c));
   if (!rc) rc = stage_features(c, single_sub(c), true, true);
   if (rc) return rc;
   c->have_projection = true;
   fbr_reg_stats st;
   std::memset(&st, 0, sizeof(st));
-  const bool run = stamp - c->time_last >= c->P.mapping_process_interval;  // mapOptmization.h:279
-  if (run && !c->has_map) return FBR_ERR_NO_MAP;
   float pose[6];
   if (run) {
-    CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->stream));
-    // the CropBox statistics depend only on the guess: a side stream computes them while the
-    // registration runs, and copy_results joins it
-    CK(hipEventRecord(c->ev_fork, c->stream));
-    CK(hipStreamWaitEvent(c->xstream[1], c->ev_fork, 0));
-    rc = crop_stats(c, Sub{0, 1, 0, c->xstream[1], true});
-    if (rc) return rc;
-    CK(hipMemcpyAsync(c->h_crop, c->d_cropcnt, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, c->xstream[1]));
-    c->crop_join = true;
+    CK(hipStreamWaitEvent(c->stream, c->ev_guess, 0));
     c->crop_cached = true;
     rc = stage_register(c, single_sub(c), false);
     c->crop_cached = false;
