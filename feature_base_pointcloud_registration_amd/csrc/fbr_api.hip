@@ -161,6 +161,7 @@ struct fbr_ctx {
   // inputs
   fbr_point_xyzirt* d_pts = nullptr;
   int64_t* d_nin = nullptr;
+  int64_t single_n = -1;  // the single-scan path's point count (k_project's argument, no copy)
   float* d_guess = nullptr;
   // projection
   int32_t *d_owner = nullptr, *d_rowcnt = nullptr, *d_col = nullptr, *d_start = nullptr, *d_end = nullptr,
@@ -430,7 +431,7 @@ int stage_project(fbr_ctx* c, const Sub& sb) {
     desk = DeskArgs{c->d_desk_mode + i0, c->d_desk + i0, c->d_rowmin + j0 * c->H};
   int32_t* owner = c->d_owner + j0 * c->HW;  // all kEmptyOwner: set at fbr_create, reset by k_compact
   TIMED_ON(c, sb.st, "project", launch_project(sb.st, c->d_pts + i0 * c->NMAX, c->d_nin + i0, c->NMAX, sb.B, c->H,
-                                               c->W, owner, c->d_err + j0));
+                                               c->W, owner, c->d_err + j0, sb.stream_mode ? c->single_n : -1));
   TIMED_ON(c, sb.st, "extract",
            launch_extract(sb.st, c->d_pts + i0 * c->NMAX, c->NMAX, owner, sb.B, c->H, c->W, c->d_rowcnt + j0 * c->H,
                           c->d_choff + j0 * c->H * (c->W / 32 + 1),
@@ -1015,8 +1016,8 @@ int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n) {
   } else if (n) {
     CK(hipMemcpyAsync(c->d_pts + job * c->NMAX, pts, sizeof(fbr_point_xyzirt) * n, hipMemcpyHostToDevice, c->stream));
   }
-  *c->h_nin = n;
-  CK(hipMemcpyAsync(c->d_nin + job, c->h_nin, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+  c->single_n = n;  // k_project takes it as an argument (no 8-B copy ahead of it on the stream)
+  (void)job;
   return FBR_OK;
 }
 
@@ -1052,8 +1053,7 @@ int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags) {
   D.point_step = L.point_step;
   for (int k = 0; k < kMsgFields; ++k) D.off[k] = L.off[k];
   TIMED(c, "unpack_msg", launch_unpack_msg(c->stream, c->d_msg, D, c->d_pts));
-  *c->h_nin = L.n;
-  CK(hipMemcpyAsync(c->d_nin, c->h_nin, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+  c->single_n = L.n;
   if (msg_flags) *msg_flags = L.flags;
   c->no_time_call = (L.flags & FBR_MSG_NO_TIME) != 0;
   return FBR_OK;

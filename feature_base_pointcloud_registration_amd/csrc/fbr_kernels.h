@@ -67,7 +67,7 @@ inline int64_t ingest_region_bytes(int64_t nmax) { return ((2 * nmax + 15) & ~(i
 void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, fbr_point_xyzirt* out);
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
                     int W, int32_t* owner,
-                    int32_t* err);
+                    int32_t* err, int64_t n_single = -1);
 // Optional IMU deskew of the kept points (deskewPoint, imageProjection.cpp:545-580): desk_mode
 // [B] (kDesk* bits, fbr_imu.h) and desk [B] tables, both null when no job deskews; rowmin [B][H]
 // receives each row's minimum owner (the scan's first deskewed point is the minimum over rows).

@@ -61,7 +61,7 @@ constexpr int kProjThreads = 256, kProjPPT = 8, kProjChunk = kProjThreads * kPro
 // 8 waves per SIMD hide the atomic latency.
 __global__ void __launch_bounds__(kProjThreads)
 k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ nin, int64_t nmax, int H, int W,
-          int tile_log2, int32_t* __restrict__ owner, int32_t* __restrict__ err) {
+          int tile_log2, int32_t* __restrict__ owner, int32_t* __restrict__ err, int64_t n_single) {
   extern __shared__ int32_t tile[];  // [H][1 << tile_log2]
   __shared__ int32_t cellk[kProjChunk];
   __shared__ int red[2][kProjThreads / 64];
@@ -70,7 +70,7 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
   // single-scan path a 6 us fill dispatch on its critical path)
   if (err && blockIdx.x == 0 && tid == 0) err[job] = 0;
   const int tcols = 1 << tile_log2, tcells = H << tile_log2;
-  const int64_t n = nin[job];
+  const int64_t n = n_single >= 0 ? n_single : nin[job];  // single scans: the count as an argument
   const fbr_point_xyzirt* P = pts + (int64_t)job * nmax;
   int32_t* O = owner + (int64_t)job * H * W;
   for (int64_t base = (int64_t)blockIdx.x * kProjChunk; base < n; base += (int64_t)gridDim.x * kProjChunk) {
@@ -401,14 +401,15 @@ void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int 
 }
 
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
-                    int W, int32_t* owner, int32_t* err) {
+                    int W, int32_t* owner, int32_t* err, int64_t n_single) {
   int blocks = (int)((nmax + kProjChunk - 1) / kProjChunk);
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
   int tile_log2 = 6;  // 64 columns, shrunk so the tile stays <= 32 KB
   while (tile_log2 > 3 && ((int64_t)H << tile_log2) > 8192) --tile_log2;
   const size_t lds = sizeof(int32_t) * ((size_t)H << tile_log2);
-  fbr_launch(k_project, dim3(blocks, B), dim3(kProjThreads), lds, s, pts, nin, nmax, H, W, tile_log2, owner, err);
+  fbr_launch(k_project, dim3(blocks, B), dim3(kProjThreads), lds, s, pts, nin, nmax, H, W, tile_log2, owner, err,
+             n_single);
 }
 
 // Compaction tile size in cells (FBR_COMPACT_CELLS: 512, 1024 or 2048).
