@@ -870,7 +870,9 @@ int copy_stats(fbr_ctx* c, int B, fbr_reg_stats* stats) { return copy_results(c,
 // scans find them awake), then sleep on the condition variable.
 class CopyPool {
  public:
-  static constexpr int kWorkers = 7;  // + the caller: 8 host copies of a single-scan upload
+  // + the caller: 4 host copies of a single-scan upload (7 workers and 256 KB chunks measured
+  // slower: latency p50 0.72 -> 0.75 ms, profiles/r04z_latency_8_copiers.txt)
+  static constexpr int kWorkers = 3;
   CopyPool() {
     for (int t = 1; t <= kWorkers; ++t) th_.emplace_back([this, t] { loop(t); });
   }
@@ -963,13 +965,13 @@ CopyPool& copy_pool() {
   return *pool;
 }
 
-// Host bytes -> pinned staging -> device, pipelined: the participants copy 256 KB chunks
+// Host bytes -> pinned staging -> device, pipelined: the participants copy 512 KB chunks
 // round-robin and each enqueues its chunk's DMA on `st` as soon as the chunk is staged, so the
 // copy engine runs while the rest is still being copied (a 64x1800 scan is 2.6 MB).  The chunks
 // are disjoint, so their order on the stream does not matter; the caller enqueues the consumer
 // after this returns.
 hipError_t pinned_upload_async(int dev, void* d_dst, void* h_stage, const void* src, size_t bytes, hipStream_t st) {
-  constexpr size_t kChunk = 256 << 10;  // ~10 chunks of a 2.6 MB C2 scan over 8 participants
+  constexpr size_t kChunk = 512 << 10;
   if (bytes <= kChunk) {
     std::memcpy(h_stage, src, bytes);
     return hipMemcpyAsync(d_dst, h_stage, bytes, hipMemcpyHostToDevice, st);
