@@ -99,6 +99,8 @@ struct Ingest {
   // Compact records (no deskew tables set: `time` is never read): per scan the rings (u16) and
   // xyzi (f32 x 4), 18 B per point instead of 24, expanded on the device by k_expand_scans.
   uint8_t* d_stage = nullptr;        // [Bcap][ingest_region_bytes(NMAX)]
+  int64_t* d_nin = nullptr;          // [2][Bcap] point counts of the staged scans (copy stream)
+  int64_t* h_nin = nullptr;          // [2][Bcap] pinned
   bool compact_used = false;         // the last fbr_process_batch used compact records
 };
 
@@ -1371,6 +1373,8 @@ int fbr_destroy(fbr_ctx* c) {
   if (c->ing.h_stage) (void)hipHostFree(c->ing.h_stage);
   if (c->ing.d_pts_slot[1]) (void)hipFree(c->ing.d_pts_slot[1]);
   if (c->ing.d_stage) (void)hipFree(c->ing.d_stage);
+  if (c->ing.d_nin) (void)hipFree(c->ing.d_nin);
+  if (c->ing.h_nin) (void)hipHostFree(c->ing.h_nin);
   for (auto& e : c->ing.up_ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ing.chunk_ev)
@@ -1844,6 +1848,8 @@ int ingest_init(fbr_ctx* c) {
   g.d_pts_slot[0] = c->d_pts;
   if (dalloc(&g.d_pts_slot[1], (int64_t)c->Bcap * c->NMAX)) return FBR_ERR_HIP;
   if (dalloc(&g.d_stage, (int64_t)c->Bcap * ingest_region_bytes(c->NMAX))) return FBR_ERR_HIP;
+  if (dalloc(&g.d_nin, 2 * (int64_t)c->Bcap)) return FBR_ERR_HIP;
+  CK(hipHostMalloc((void**)&g.h_nin, sizeof(int64_t) * 2 * c->Bcap, hipHostMallocDefault));
   return FBR_OK;
 }
 
@@ -1866,8 +1872,14 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
   // compact records unless a deskew table may read the per-point time (deskewPoint, :545-580)
   const bool compact = ingest_compact_enabled() && !c->desk_any;
   g.compact_used = compact;
-  const int64_t ring_bytes = (2 * c->NMAX + 15) & ~(int64_t)15, region = ingest_region_bytes(c->NMAX);
-  auto host_bytes = [&](int64_t n) { return compact ? ring_bytes + 16 * n : n * (int64_t)sizeof(fbr_point_xyzirt); };
+  const int64_t region = ingest_region_bytes(c->NMAX);
+  const int rb = c->H <= 256 ? 1 : 2;  // ring bytes per point (u8 for sensors of <= 256 rings)
+  auto host_bytes = [&](int64_t n) { return compact ? (16 + rb) * n : n * (int64_t)sizeof(fbr_point_xyzirt); };
+  if (compact) {  // the counts for k_expand_scans, on the copy stream (slot's half of the pinned array)
+    for (int jj = 0; jj < B; ++jj) g.h_nin[(int64_t)slot * c->Bcap + jj] = n_in[jj];
+    CK(hipMemcpyAsync(g.d_nin + (int64_t)slot * c->Bcap, g.h_nin + (int64_t)slot * c->Bcap, sizeof(int64_t) * B,
+                      hipMemcpyHostToDevice, g.cstream));
+  }
   std::vector<int64_t> off;
   for (int j = 0; j < B;) {
     const int k = g.next_chunk;
@@ -1893,15 +1905,18 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
           continue;
         }
         const fbr_point_xyzirt* src = scans[jj];
-        uint16_t* rr = reinterpret_cast<uint16_t*>(base + off[jj - j]);
-        float* xyzi = reinterpret_cast<float*>(base + off[jj - j] + ring_bytes);
+        float* xyzi = reinterpret_cast<float*>(base + off[jj - j]);
+        uint8_t* rr = base + off[jj - j] + 16 * n;
         for (int64_t i = 0; i < n; ++i) {
-          rr[i] = src[i].ring;
           xyzi[4 * i] = src[i].x;
           xyzi[4 * i + 1] = src[i].y;
           xyzi[4 * i + 2] = src[i].z;
           xyzi[4 * i + 3] = src[i].intensity;
         }
+        if (rb == 1)
+          for (int64_t i = 0; i < n; ++i) rr[i] = (uint8_t)src[i].ring;
+        else
+          for (int64_t i = 0; i < n; ++i) reinterpret_cast<uint16_t*>(rr)[i] = src[i].ring;
       }
     };
     std::vector<std::thread> th;
@@ -1922,7 +1937,8 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
     for (int jj = j; jj < j1; ++jj) g.h2d_bytes += (double)(n_in[jj] ? host_bytes(n_in[jj]) : 0);
     j = j1;
   }
-  if (compact) launch_expand_scans(g.cstream, g.d_stage, c->NMAX, B, dst);  // stream order: after the copies
+  if (compact)  // stream order: after the copies
+    launch_expand_scans(g.cstream, g.d_stage, c->NMAX, B, g.d_nin + (int64_t)slot * c->Bcap, rb, dst);
   CK(hipEventRecord(g.up_ev[slot], g.cstream));
   return FBR_OK;
 }

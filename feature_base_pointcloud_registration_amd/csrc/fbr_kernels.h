@@ -61,10 +61,12 @@ struct MsgDev {
   int32_t off[6];
 };
 void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_point_xyzirt* out);
-// Compact ingest records (fbr_process_batch without deskew tables) -> the scan buffer: job j's
-// staging region is [ring u16 x nmax, padded to 16 B][xyzi f32 x 4 x nmax] (ingest_region_bytes).
-inline int64_t ingest_region_bytes(int64_t nmax) { return ((2 * nmax + 15) & ~(int64_t)15) + 16 * nmax; }
-void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, fbr_point_xyzirt* out);
+// Compact ingest records (fbr_process_batch without deskew tables): job j's staging region holds
+// its n points packed, [x, y, z, intensity f32 x n][ring x n], the rings as u8 when the sensor has
+// at most 256 rings (rb = 1), else u16 (rb = 2); regions are ingest_region_bytes(nmax) apart.
+inline int64_t ingest_region_bytes(int64_t nmax) { return (18 * nmax + 15) & ~(int64_t)15; }
+void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, const int64_t* nin, int rb,
+                         fbr_point_xyzirt* out);
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
                     int W, int32_t* owner,
                     int32_t* err, int64_t n_single = -1);

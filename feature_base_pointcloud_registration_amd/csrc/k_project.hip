@@ -373,16 +373,19 @@ void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_
 
 // K0' k_expand_scans: the compact ingest records of fbr_process_batch (no deskew: the reference
 // never reads `time` on this path, imageProjection.cpp:189-191) -> the 24-B scan buffer.  Job j's
-// staging region is [ring u16 x nmax, padded to 16 B][x, y, z, intensity f32 x nmax]; time = 0.
-// HBM-bound: 18 B read + 24 B written per point slot.
+// staging region (ingest_region_bytes apart) holds its n points packed: xyzi (f32 x 4) x n, then
+// the rings x n (u8 when rb = 1, u16 when rb = 2); time = 0.  Slots past n are not written
+// (k_project reads n points).  HBM-bound: 16 + rb B read + 24 B written per point.
 __global__ void __launch_bounds__(256)
-k_expand_scans(const uint8_t* __restrict__ stage, int64_t nmax, int64_t region, fbr_point_xyzirt* __restrict__ out) {
+k_expand_scans(const uint8_t* __restrict__ stage, int64_t nmax, int64_t region, const int64_t* __restrict__ nin,
+               int rb, fbr_point_xyzirt* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= nmax) return;
   const int64_t job = blockIdx.y;
+  const int64_t n = min(nin[job], nmax);
+  if (i >= n) return;
   const uint8_t* r = stage + job * region;
-  const uint16_t ring = reinterpret_cast<const uint16_t*>(r)[i];
-  const float4 p = reinterpret_cast<const float4*>(r + ((2 * nmax + 15) & ~(int64_t)15))[i];
+  const float4 p = reinterpret_cast<const float4*>(r)[i];
+  const uint16_t ring = rb == 1 ? (uint16_t)r[16 * n + i] : reinterpret_cast<const uint16_t*>(r + 16 * n)[i];
   fbr_point_xyzirt q;
   q.x = p.x;
   q.y = p.y;
@@ -394,10 +397,11 @@ k_expand_scans(const uint8_t* __restrict__ stage, int64_t nmax, int64_t region, 
   out[job * nmax + i] = q;
 }
 
-void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, fbr_point_xyzirt* out) {
+void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, const int64_t* nin, int rb,
+                         fbr_point_xyzirt* out) {
   if (B <= 0 || nmax <= 0) return;
-  const int64_t region = ((2 * nmax + 15) & ~(int64_t)15) + 16 * nmax;
-  fbr_launch(k_expand_scans, dim3((unsigned)((nmax + 255) / 256), B), dim3(256), 0, s, stage, nmax, region, out);
+  fbr_launch(k_expand_scans, dim3((unsigned)((nmax + 255) / 256), B), dim3(256), 0, s, stage, nmax,
+             ingest_region_bytes(nmax), nin, rb, out);
 }
 
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
