@@ -156,7 +156,6 @@ struct fbr_ctx {
   int64_t exported = -1;      // latest launch whose records fbr_batch_export_ready exported
   hipEvent_t ev_staged = nullptr;  // the staged inputs are on the device (recorded on stream)
   hipEvent_t ev_fork = nullptr;    // single-scan side-stream fork
-  hipEvent_t ev_guess = nullptr;   // single-scan guess copied (side stream)
   hipEvent_t ev_ext = nullptr;     // a caller's stream, waited on before an export (fbr_batch_export_ready)
   int items_per_job = 0;
   int64_t HW = 0, NMAX = 0;
@@ -210,6 +209,7 @@ struct fbr_ctx {
   bool crop_cached = false;  // d_cropcnt holds the staged batch's CropBox statistics
   bool crop_join = false;    // single scan: copy_results takes the CropBox counts from h_crop (side stream)
   int32_t* h_crop = nullptr;  // pinned [2]: the single-scan CropBox counts
+  float* h_guess = nullptr;   // pinned [6]: the single-scan guess (queue_guess)
   int max_items = 0;
   float* d_pose_out = nullptr;
   fbr_reg_stats* d_stats = nullptr;
@@ -1011,11 +1011,23 @@ bool pinned_upload() {
 // A single scan into job slot `job` with no host synchronisation of its own: a copy from pageable
 // memory returns once the runtime has staged the source, and the pinned staging buffer is only
 // rewritten by the next call, after this call's results came back.
-int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n) {
+// A single-scan call at `stamp` registers (the mapping_process_interval gate, mapOptmization.h:279).
+bool will_register(const fbr_ctx* c, double stamp) { return stamp - c->time_last >= c->P.mapping_process_interval; }
+
+// The registration guess of a single-scan call, queued on the stream ahead of the scan's chunks
+// (pinned, so the 24-B DMA runs while the host still copies the first chunk).
+hipError_t queue_guess(fbr_ctx* c, const float* guess) {
+  if (!guess) return hipSuccess;
+  std::memcpy(c->h_guess, guess, sizeof(float) * 6);
+  return hipMemcpyAsync(c->d_guess, c->h_guess, sizeof(float) * 6, hipMemcpyHostToDevice, c->stream);
+}
+
+int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n, const float* guess = nullptr) {
   if (n < 0 || n > c->NMAX) return FBR_ERR_CAPACITY;
   c->no_time_call = false;
+  CK(fbr_sync(c->stream));  // staging free (a no-op after the previous call's result copy)
+  CK(queue_guess(c, guess));
   if (n && pinned_upload()) {
-    CK(fbr_sync(c->stream));  // staging free (a no-op after the previous call's result copy)
     CK(pinned_upload_async(c->dev, c->d_pts + job * c->NMAX, c->h_scan, pts, sizeof(fbr_point_xyzirt) * n, c->stream));
   } else if (n) {
     CK(hipMemcpyAsync(c->d_pts + job * c->NMAX, pts, sizeof(fbr_point_xyzirt) * n, hipMemcpyHostToDevice, c->stream));
@@ -1027,12 +1039,13 @@ int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n) {
 
 // The raw PointCloud2 goes to HBM as it is; k_unpack_msg writes job 0's scan buffer
 // (cachePointCloud's fromROSMsg, imageProjection.cpp:253, on the device).
-int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags) {
+int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags, const float* guess = nullptr) {
   MsgLayout L;
   int rc = resolve_msg(msg, &L);
   if (rc) return rc;
   if (L.n > c->NMAX) return FBR_ERR_CAPACITY;
   CK(fbr_sync(c->stream));  // staging free (a no-op after the previous call's result copy)
+  CK(queue_guess(c, guess));
   if (L.bytes > c->msg_cap) {
     if (c->d_msg) CK(hipFree(c->d_msg));
     c->d_msg = nullptr;
@@ -1288,7 +1301,6 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   }
   if (!sfail) sfail = hipEventCreateWithFlags(&c->ev_staged, hipEventDisableTiming) != hipSuccess ||
                      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-                     hipEventCreateWithFlags(&c->ev_guess, hipEventDisableTiming) != hipSuccess ||
                      hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming) != hipSuccess;
   if (sfail) {
     fbr_destroy(c);
@@ -1328,7 +1340,8 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               hipHostMalloc((void**)&c->h_scan, sizeof(fbr_point_xyzirt) * std::max<int64_t>(c->NMAX, 1),
                             hipHostMallocDefault) != hipSuccess ||
               hipHostMalloc((void**)&c->h_nin, sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
-              hipHostMalloc((void**)&c->h_crop, sizeof(int32_t) * 2, hipHostMallocDefault) != hipSuccess;
+              hipHostMalloc((void**)&c->h_crop, sizeof(int32_t) * 2, hipHostMallocDefault) != hipSuccess ||
+              hipHostMalloc((void**)&c->h_guess, sizeof(float) * 6, hipHostMallocDefault) != hipSuccess;
   if (fail) {
     fbr_destroy(c);
     return FBR_ERR_HIP;
@@ -1366,7 +1379,7 @@ int fbr_destroy(fbr_ctx* c) {
   free_grid(c->grid_c);
   free_grid(c->grid_s);
   arena_free(c->arena);
-  for (void* h : {(void*)c->h_result, (void*)c->h_scan, (void*)c->h_nin, (void*)c->h_msg, (void*)c->h_crop})
+  for (void* h : {(void*)c->h_result, (void*)c->h_scan, (void*)c->h_nin, (void*)c->h_msg, (void*)c->h_crop, (void*)c->h_guess})
     if (h) (void)hipHostFree(h);
   if (c->d_result) (void)hipFree(c->d_result);
   if (c->ing.cstream) (void)fbr_sync(c->ing.cstream);
@@ -1397,7 +1410,6 @@ int fbr_destroy(fbr_ctx* c) {
   }
   if (c->ev_staged) (void)hipEventDestroy(c->ev_staged);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  if (c->ev_guess) (void)hipEventDestroy(c->ev_guess);
   if (c->ev_ext) (void)hipEventDestroy(c->ev_ext);
   delete c;
   return FBR_OK;
@@ -1569,7 +1581,7 @@ int fbr_process_scan(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, d
   CK(hipSetDevice(c->dev));
   int rc = drop_staged_batch(c);
   if (rc) return rc;
-  rc = upload_scan(c, 0, points, n_in);
+  rc = upload_scan(c, 0, points, n_in, will_register(c, stamp) ? pose_inout : nullptr);
   if (rc) return rc;
   host_time(0, t0);
   rc = process_uploaded(c, stamp, pose_inout, stats);
@@ -1583,7 +1595,7 @@ int fbr_process_msg(fbr_ctx* c, const fbr_pointcloud2* msg, double stamp, float 
   CK(hipSetDevice(c->dev));
   int rc = drop_staged_batch(c);
   if (rc) return rc;
-  rc = upload_msg(c, msg, msg_flags);
+  rc = upload_msg(c, msg, msg_flags, will_register(c, stamp) ? pose_inout : nullptr);
   if (rc) return rc;
   return process_uploaded(c, stamp, pose_inout, stats);
 }
@@ -1599,13 +1611,11 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
   if (run && !c->has_map) return FBR_ERR_NO_MAP;
   int rc = FBR_OK;
   if (run) {
-    // the guess and the CropBox statistics (which depend only on it) go on a side stream forked
-    // before the front end, so neither the 24-B copy nor its dispatch gap sits between the
-    // features and the mapping DS; the registration waits for the copy, copy_results joins the rest
+    // the guess went to the device ahead of the scan (queue_guess); the CropBox statistics, which
+    // depend only on it, run on a side stream forked here, beside the front end, and copy_results
+    // joins them
     CK(hipEventRecord(c->ev_fork, c->stream));
     CK(hipStreamWaitEvent(c->xstream[1], c->ev_fork, 0));
-    CK(hipMemcpyAsync(c->d_guess, pose_inout, sizeof(float) * 6, hipMemcpyHostToDevice, c->xstream[1]));
-    CK(hipEventRecord(c->ev_guess, c->xstream[1]));
     rc = crop_stats(c, Sub{0, 1, 0, c->xstream[1], true});
     if (rc) return rc;
     CK(hipMemcpyAsync(c->h_crop, c->d_cropcnt, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, c->xstream[1]));
@@ -1619,7 +1629,6 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
   std::memset(&st, 0, sizeof(st));
   float pose[6];
   if (run) {
-    CK(hipStreamWaitEvent(c->stream, c->ev_guess, 0));
     c->crop_cached = true;
     rc = stage_register(c, single_sub(c), false);
     c->crop_cached = false;
