@@ -160,6 +160,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
   const float xlo = (fx - (float)RX) * cxs, xhi = (fx + (float)(RX + 1)) * cxs;  // row x extent (max)
   const bool xin = xlo >= bx0 && xhi <= bx1;
   int nrow = 0;  // kFlat: rows queued
+  int total = 0;  // kFlat: points queued
 #pragma unroll
   for (int ksum = 0; ksum <= 2 * (K - 1); ++ksum) {
 #pragma unroll
@@ -197,6 +198,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       const bool inside = xin & (ylo >= by0) & (ylo + c <= by1) & (zlo >= bz0) & (zlo + c <= bz1);
       if constexpr (kFlat) {
         if (e > b) rows[nrow++ * kResThreads] = make_int2(b, inside ? (int)((unsigned)e | 0x80000000u) : e);
+        total += e - b;
         continue;
       }
       for (int i = LPQ == 1 ? b : b + ((sub - b) & (LPQ - 1)); i < e; i += LPQ) {
@@ -218,12 +220,14 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
     }
   }
   if constexpr (kFlat) {
-    int j = 0, i = 0, e = 0;
-    bool inside = true;
-    while (true) {
-      if (i >= e) {  // next queued row (every queued row is non-empty)
-        if (j >= nrow) break;
-        const int2 q = rows[j++ * kResThreads];
+    // counted walk: one trip per queued point (the lane's total), the row advance a short branch
+    // (a while loop that tests for the next row first: +16 % per dispatch, r04ae)
+    int2 q = rows[0];  // unread when nothing is queued
+    int j = 0, i = q.x, e = q.y & 0x7fffffff;
+    bool inside = q.y < 0;
+    for (int t = 0; t < total; ++t) {
+      if (i == e) {  // next queued row (every queued row is non-empty)
+        q = rows[++j * kResThreads];
         i = q.x;
         e = q.y & 0x7fffffff;
         inside = q.y < 0;
@@ -831,13 +835,23 @@ inline bool knn_flat_r2() {
   return v;
 }
 
+// Flat row queue in iteration 0 too (FBR_KNN_FLAT0=1): no warm-start bound, so every row within
+// distance 1 is queued and walked without the per-row pruning of the 5th distance.
+inline bool knn_flat0() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_KNN_FLAT0");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+
 template <int R, bool F>
 void launch_gn_knn_r(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
   if constexpr (!F) {
     if (knn_lpq(a.B) == 8) return launch_gn_knn_rl<R, F, false, 8>(s, a, grid, use_prev);
   }
   if constexpr (R <= 2 && !F) {
-    if (use_prev && knn_flat() && (R == 1 || knn_flat_r2())) return launch_gn_knn_rl<R, F, true>(s, a, grid, use_prev);
+    if ((use_prev || knn_flat0()) && knn_flat() && (R == 1 || knn_flat_r2())) return launch_gn_knn_rl<R, F, true>(s, a, grid, use_prev);
   }
   launch_gn_knn_rl<R, F, false>(s, a, grid, use_prev);
 }
