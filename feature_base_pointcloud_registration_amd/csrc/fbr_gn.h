@@ -226,12 +226,23 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
     int j = 0, i = q.x, e = q.y & 0x7fffffff;
     bool inside = q.y < 0;
     for (int t = 0; t < total; ++t) {
+#ifdef FBR_KNN_ROW_SEL
+      // A/B build (tools/gpu_r04am.sh): the next row's entry read every trip, the advance as
+      // selects instead of a branch
+      const int2 qn = rows[min(j + 1, nrow - 1) * kResThreads];
+      const bool adv = i == e;
+      i = adv ? qn.x : i;
+      e = adv ? (qn.y & 0x7fffffff) : e;
+      inside = adv ? qn.y < 0 : inside;
+      j += adv ? 1 : 0;
+#else
       if (i == e) {  // next queued row (every queued row is non-empty)
         q = rows[++j * kResThreads];
         i = q.x;
         e = q.y & 0x7fffffff;
         inside = q.y < 0;
       }
+#endif
       const float4 p = m.pts[i++];
       bool out = false;
       if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
