@@ -36,10 +36,25 @@ WORKLOAD = {"C1": "VLP-16-style scans, local corner+surf map",
             "C3": "Ouster-style scans, ~500k-pt local corner+surf map (mapping leaves 0.1/0.2)",
             "C5": "dense scans, ~5.8M-pt map inside the crop box (mapping leaves 0.05)"}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU roof: 1024 SIMDs at 2.4 GHz (peak engine clock) = 2457.6 G SIMD-cycles/s; the VALU-busy cycles
-# of a launch come from SQ_ACTIVE_INST_VALU (quad-cycles, tools/valu_pmc.py).  On gfx950 every
-# wave64 VALU instruction of these kernels counts 4 cycles (none is packed f32)
-VALU_PEAK_GCYC = 1024 * 2.4
+# VALU roof: wave-level VALU instructions per second.  MI355X_MICROARCH.md: a wave64 VALU instruction
+# occupies a SIMD-32 for 2 cycles, 1024 SIMDs x 2.4 GHz / 2 = 1228.8 G instr/s; measured on the box
+# (fbr_valu_peak, tools/valu_calib.py -> profiles/valu_calib.json): 1079 G instr/s of independent
+# v_fma_f32 at 8 waves per SIMD (2.26 cycles per instruction at the 2.38 GHz effective clock), ~490
+# with one wave per SIMD.  The measured peak is the roof.  (SQ_ACTIVE_INST_VALU counts one
+# quad-cycle per VALU instruction whatever the issue rate -- the calibration's PMC pass -- so it is
+# an instruction count, not busy time.)
+VALU_PEAK_GINST_SPEC = 1024 * 2.4 / 2.0
+
+
+def valu_peak_ginst():
+    try:
+        with open(os.path.join(REPO, "profiles", "valu_calib.json")) as f:
+            return float(json.load(f)["measured_peak_ginst_per_s"]), "profiles/valu_calib.json (measured v_fma_f32)"
+    except Exception:
+        return VALU_PEAK_GINST_SPEC, "MI355X_MICROARCH.md (2 cycles per wave64 VALU instruction)"
+
+
+VALU_PEAK_GINST, VALU_PEAK_SOURCE = valu_peak_ginst()
 
 # Algorithmic bytes per unit for each kernel family: the minimal HBM traffic the kernel's job needs
 # (DESIGN.md §4 holds the same table; every model is <= the FETCH/WRITE counter bytes).  Units per
@@ -116,6 +131,8 @@ def parse():
                          "events): every kernel (default), only the roofline kernel, or none")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "hbm_traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from rocprofv3 PMC passes")
+    ap.add_argument("--sq-json", default=os.path.join(REPO, "profiles", "sq_decomp.json"),
+                    help="per-kernel wave-state / instruction-mix decomposition (tools/sq_decomp.py)")
     ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "valu_pmc.json"),
                     help="per-launch VALU instructions of every kernel from a rocprofv3 SQ pass (tools/valu_pmc.py)")
     return ap.parse_args()
@@ -405,17 +422,27 @@ def main():
         r = dict(bytes_per_launch=bpl, avg_launch_us=round(avg_s * 1e6, 3), launches_per_step=lps,
                  achieved_GBps=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
                  ms_per_step=round(ms / max(steps_measured, 1), 4), live=live)
-        if k in valu and avg_s > 0:  # the launch's VALU cycles / instructions over its live duration
-            cpl, ipl = valu[k].get("valu_cycles_per_launch"), valu[k]["insts_valu_per_launch"]
+        if k in valu and avg_s > 0:  # the launch's wave-level VALU instructions over its live duration
+            ipl = valu[k]["insts_valu_per_launch"]
             r["valu_insts_per_launch"] = ipl
-            if cpl:
-                r["valu_cycles_per_launch"] = cpl
-                r["valu_achieved_gcyc_s"] = round(cpl / avg_s / 1e9, 2)
-                r["valu_frac"] = round(cpl / avg_s / 1e9 / VALU_PEAK_GCYC, 5)
-            r["valu_busy_alone"] = round(valu[k]["valu_busy_alone"], 4)
+            r["valu_achieved_ginst_s"] = round(ipl / avg_s / 1e9, 2)
+            r["valu_frac"] = round(ipl / avg_s / 1e9 / VALU_PEAK_GINST, 5)
+            if valu[k].get("avg_us_alone"):  # the same against the SQ pass's own (serialised) duration
+                r["valu_frac_alone"] = round(ipl / (valu[k]["avg_us_alone"] * 1e-6) / 1e9 / VALU_PEAK_GINST, 4)
         return r
 
     kroof = {k: kernel_roofline(k) for k in modelled}
+    # what each kernel's waves wait on (SQ passes of the same config and batch, tools/sq_decomp.py)
+    if os.path.exists(args.sq_json):
+        try:
+            with open(args.sq_json) as f:
+                sj = json.load(f)
+            if sj.get("config") == cfg and sj.get("batch") == B:
+                for k, e in sj["kernels"].items():
+                    if k in kroof:
+                        kroof[k]["wave_state_alone"] = {kk: round(v, 3) for kk, v in e["wave_state"].items()}
+        except Exception:
+            pass
     bytes_per_launch, launches_per_step = kroof[dom]["bytes_per_launch"], kroof[dom]["launches_per_step"]
     avg_launch_s, achieved, live = kroof[dom]["avg_launch_us"] * 1e-6, kroof[dom]["achieved_GBps"], kroof[dom]["live"]
     # the roof the dominant kernel is closer to: VALU issue when its VALU fraction exceeds its HBM one
@@ -462,12 +489,14 @@ def main():
         "roofline": {
             "bound": "valu" if valu_bound else "hbm",
             "kernel": dom,
-            "achieved": kroof[dom]["valu_achieved_gcyc_s"] if valu_bound else round(achieved, 2),
-            "peak": VALU_PEAK_GCYC if valu_bound else HBM_PEAK_GBS,
-            "unit": "G VALU-busy SIMD-cycles/s" if valu_bound else "GB/s",
+            "achieved": kroof[dom]["valu_achieved_ginst_s"] if valu_bound else round(achieved, 2),
+            "peak": round(VALU_PEAK_GINST, 2) if valu_bound else HBM_PEAK_GBS,
+            "unit": "G wave64 VALU instr/s" if valu_bound else "GB/s",
             "frac": kroof[dom]["valu_frac"] if valu_bound else round(achieved / HBM_PEAK_GBS, 5),
             "valu_frac": kroof[dom].get("valu_frac"),
-            "valu_busy_alone": kroof[dom].get("valu_busy_alone"),
+            "valu_frac_alone": kroof[dom].get("valu_frac_alone"),
+            "valu_peak_source": VALU_PEAK_SOURCE,
+            "valu_peak_spec_ginst_s": VALU_PEAK_GINST_SPEC,
             "hbm_achieved_GBps": round(achieved, 2),
             "hbm_frac": round(achieved / HBM_PEAK_GBS, 5),
             "valu_source": os.path.relpath(args.valu_json, REPO) if valu else None,

@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = [
     "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math", "fbr_selftest_eigen6", "fbr_selftest_eig_certified", "fbr_selftest_voxel_order", "fbr_selftest_radix_sort",
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
     "fbr_msg_to_points", "fbr_points_to_msg_data", "fbr_project_msg", "fbr_process_msg",
-    "fbr_imu_convert", "fbr_imu_deskew_info", "fbr_set_deskew", "fbr_stream_copy_bandwidth",
+    "fbr_imu_convert", "fbr_imu_deskew_info", "fbr_set_deskew", "fbr_stream_copy_bandwidth", "fbr_valu_peak",
     "fbr_keyframe_params_default", "fbr_keyframes_add", "fbr_keyframes_set_pose", "fbr_keyframes_count",
     "fbr_keyframes_reset", "fbr_extract_surrounding_keyframes",
 ]
@@ -110,6 +110,7 @@ def lib():
             "fbr_imu_deskew_info": (ctypes.c_int, [_VP, _I64, ctypes.c_double, ctypes.c_double, _VP, _VP]),
             "fbr_set_deskew": (ctypes.c_int, [_VP, _VP, ctypes.c_int]),
             "fbr_stream_copy_bandwidth": (ctypes.c_int, [ctypes.c_int, _I64, ctypes.c_int, _VP]),
+            "fbr_valu_peak": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _VP, _VP]),
             "fbr_keyframe_params_default": (None, [_VP]),
             "fbr_keyframes_add": (ctypes.c_int, [_VP, _VP, _VP, _I64, _VP, _I64]),
             "fbr_keyframes_set_pose": (ctypes.c_int, [_VP, _I64, _VP]),
@@ -230,6 +231,15 @@ def stream_copy_bandwidth(device=0, nbytes=2 << 30, iters=20):
     g = ctypes.c_double()
     _check(lib().fbr_stream_copy_bandwidth(device, nbytes, iters, ctypes.byref(g)), "fbr_stream_copy_bandwidth")
     return g.value
+
+
+def valu_peak(device=0, waves_per_simd=4, kind=0, iters=4096, reps=5):
+    """(wave-level VALU G instr/s, ms per launch) of the fbr_valu_peak probe: kind 0 v_fma_f32,
+    1 v_add_u32, 2 v_pk_fma_f32, waves_per_simd waves on every SIMD."""
+    g, ms = ctypes.c_double(), ctypes.c_double()
+    _check(lib().fbr_valu_peak(device, waves_per_simd, kind, iters, reps, ctypes.byref(g), ctypes.byref(ms)),
+           "fbr_valu_peak")
+    return g.value, ms.value
 
 
 def affine_from_pose(pose):

@@ -400,7 +400,7 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
       launch_voxel_grid(c->stream, a);
       int32_t nout = 0;
       if (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-          fbr_sync(c->stream) != hipSuccess) {
+          fbr_sync(c->stream) != hipSuccess || nout < 0) {
         rc = FBR_ERR_HIP;
       } else {
         out.resize(nout);
@@ -572,7 +572,9 @@ int drop_staged_batch(fbr_ctx* c) {
   c->staged_B = 0;
   c->crop_cached = false;
   c->last_slot = -1;
-  c->exported = -1;
+  // launch ids only grow: every launch made so far belongs to the dropped batch (or its slot was
+  // overwritten by a single-scan call), so fbr_batch_export_ready must never hand one of them out
+  c->exported = c->launch_seq - 1;
   return rc;
 }
 
@@ -615,6 +617,7 @@ int register_prepare(fbr_ctx* c, const Sub& sb, bool trace) {
       v.s[k].box_stride = (int64_t)c->H * kRingBox;
     }
   }
+  v.err = c->d_err + j0;  // a failed split look-back flags the job (FBR_REG_FEATURE_CAPACITY / error)
   TIMED_ON(c, sb.st, "voxel_scan", launch_voxel_grid(sb.st, v));
   GnArgs a = gn_args(c, sb, trace);
   if (trace) CK(hipMemsetAsync(a.trace, 0, sizeof(float) * sb.B * c->P.max_iterations * 6, sb.st));
@@ -1158,9 +1161,9 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
     } else {
       launch_voxel_grid(c->stream, a);
       if (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-          fbr_sync(c->stream) != hipSuccess)
+          fbr_sync(c->stream) != hipSuccess || nout < 0)
         rc = FBR_ERR_HIP;
-      *n_out = nout;
+      *n_out = rc ? 0 : nout;
     }
   }
   (void)hipFree(d_cnt);
@@ -1789,7 +1792,8 @@ int fbr_batch_export(fbr_ctx* c, void* device_dst) {
   const int rc = batch_quiesce(c);
   if (rc) return rc;
   const int64_t w0 = (int64_t)c->last_slot * c->Bcap;
-  launch_export_records(c->stream, c->staged_B, c->d_pose_out + w0 * 6, c->d_stats + w0, (float*)device_dst);
+  launch_export_records(c->stream, c->staged_B, c->d_pose_out + w0 * 6, c->d_stats + w0, c->d_err + w0, c->d_guess,
+                        (float*)device_dst);
   CK(hipGetLastError());
   c->exported = c->slot_launch[c->last_slot];
   return FBR_OK;
@@ -1816,7 +1820,8 @@ int fbr_batch_export_ready(fbr_ctx* c, void* device_dst, void* wait_stream, void
     CK(hipStreamWaitEvent(st, c->ev_ext, 0));
   }
   const int64_t w0 = (int64_t)s * c->Bcap;
-  launch_export_records(st, c->staged_B, c->d_pose_out + w0 * 6, c->d_stats + w0, (float*)device_dst);
+  launch_export_records(st, c->staged_B, c->d_pose_out + w0 * 6, c->d_stats + w0, c->d_err + w0, c->d_guess,
+                        (float*)device_dst);
   CK(hipGetLastError());
   c->exported = c->slot_launch[s];
   *export_stream = (void*)st;
@@ -1882,7 +1887,9 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
   const bool compact = ingest_compact_enabled() && !c->desk_any;
   g.compact_used = compact;
   const int64_t region = ingest_region_bytes(c->NMAX);
-  const int rb = c->H <= 256 ? 1 : 2;  // ring bytes per point (u8 for sensors of <= 256 rings)
+  // ring bytes per point: u8 for sensors of < 256 rings, where every out-of-range ring (>= H, which
+  // projectPointCloud drops, imageProjection.cpp:599) is stored as 255, still out of range
+  const int rb = c->H < 256 ? 1 : 2;
   auto host_bytes = [&](int64_t n) { return compact ? (16 + rb) * n : n * (int64_t)sizeof(fbr_point_xyzirt); };
   if (compact) {  // the counts for k_expand_scans, on the copy stream (slot's half of the pinned array)
     for (int jj = 0; jj < B; ++jj) g.h_nin[(int64_t)slot * c->Bcap + jj] = n_in[jj];
@@ -1923,7 +1930,7 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
           xyzi[4 * i + 3] = src[i].intensity;
         }
         if (rb == 1)
-          for (int64_t i = 0; i < n; ++i) rr[i] = (uint8_t)src[i].ring;
+          for (int64_t i = 0; i < n; ++i) rr[i] = src[i].ring < c->H ? (uint8_t)src[i].ring : (uint8_t)255;
         else
           for (int64_t i = 0; i < n; ++i) reinterpret_cast<uint16_t*>(rr)[i] = src[i].ring;
       }

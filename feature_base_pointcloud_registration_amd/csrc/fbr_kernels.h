@@ -137,7 +137,12 @@ constexpr int64_t kVgScratch = 5;
 bool vg_exact();
 struct VgArgs {
   VgSet s[2];                // segments of set 0, then of set 1 (set 1 may be empty)
+  // per-segment error words (segment j of either set = job j; may be null): k_voxel_grid_split ORs
+  // kVgErrLookback into them when its bounded look-back gives up (the segment's count is then 0;
+  // with err null it is -1, which the single-cloud callers report as FBR_ERR_HIP)
+  int32_t* err = nullptr;
 };
+constexpr int32_t kVgErrLookback = 16;
 constexpr int64_t kVgLdsCap = 4096;  // segments up to this size sort entirely in LDS
 void launch_voxel_grid(hipStream_t s, const VgArgs& a);
 
@@ -308,7 +313,8 @@ void launch_pack_results(hipStream_t s, int B, int with_reg, const float* pose_o
                          const int32_t* nvalid, const int32_t* ncorner, const int32_t* nsurf, const int32_t* cropcnt,
                          const int32_t* err, const float* guess, JobResult* out);
 // laserCloud{Corner,Surf}FromMapDSNum: CropBox counts of the global map per job.
-void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, float* dst);
+void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, const int32_t* err,
+                           const float* guess, float* dst);
 void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* map_pts, int64_t n, int which,
                        int32_t* counts /* [B][2] */);
 

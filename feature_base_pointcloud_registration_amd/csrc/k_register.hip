@@ -183,13 +183,17 @@ __global__ void k_crop_count(GnArgs a, const float4* pts, int64_t n, int which, 
     if (c[j]) atomicAdd(&counts[2 * j + which], c[j]);
 }
 
-// 32-byte pose record per job {pose[6], iterations, status} for the cross-GPU gather.
-__global__ void k_export_records(int B, const float* pose_out, const fbr_reg_stats* stats, float* dst) {
+// 32-byte pose record per job {pose[6], iterations, status} for the cross-GPU gather.  A job over the
+// feature capacity gets the same record fbr_batch_results reports for it (k_pack_results): its guess,
+// 0 iterations, FBR_REG_FEATURE_CAPACITY.
+__global__ void k_export_records(int B, const float* pose_out, const fbr_reg_stats* stats, const int32_t* err,
+                                 const float* guess, float* dst) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= B) return;
-  for (int k = 0; k < 6; ++k) dst[8 * j + k] = pose_out[6 * j + k];
-  dst[8 * j + 6] = __int_as_float(stats[j].iterations);
-  dst[8 * j + 7] = __int_as_float(stats[j].status);
+  const bool cap = err[j] != 0;
+  for (int k = 0; k < 6; ++k) dst[8 * j + k] = cap ? guess[6 * j + k] : pose_out[6 * j + k];
+  dst[8 * j + 6] = __int_as_float(cap ? 0 : stats[j].iterations);
+  dst[8 * j + 7] = __int_as_float(cap ? FBR_REG_FEATURE_CAPACITY : stats[j].status);
 }
 
 __global__ void k_pack_results(int B, int with_reg, const float* pose_out, const fbr_reg_stats* stats,
@@ -229,8 +233,9 @@ void launch_pack_results(hipStream_t s, int B, int with_reg, const float* pose_o
              cropcnt, err, guess, out);
 }
 
-void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, float* dst) {
-  fbr_launch(k_export_records, dim3((B + 63) / 64), dim3(64), 0, s, B, pose_out, stats, dst);
+void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, const int32_t* err,
+                           const float* guess, float* dst) {
+  fbr_launch(k_export_records, dim3((B + 63) / 64), dim3(64), 0, s, B, pose_out, stats, err, guess, dst);
 }
 
 void launch_gn_init(hipStream_t s, const GnArgs& a) { fbr_launch(k_gn_init, dim3(1), dim3(1024), 0, s, a); }

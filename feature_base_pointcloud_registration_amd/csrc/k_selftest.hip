@@ -260,3 +260,102 @@ extern "C" int fbr_stream_copy_bandwidth(int hip_device, int64_t bytes, int iter
   (void)hipFree(b);
   return rc;
 }
+
+// VALU issue-rate probe (measurement helper for the VALU roofline, bench.py / tools/valu_calib.py):
+// every lane runs 8 independent dependency chains of one VALU instruction for `iters` rounds, written
+// as inline asm so the compiler can neither pack (SLP) nor drop them.  kind 0: v_fma_f32, 1:
+// v_add_u32, 2: v_pk_fma_f32 (2 lanes of f32 per slot).  The grid is n_cu * waves_per_simd
+// workgroups of 256 threads (4 waves: one per SIMD), so every SIMD holds waves_per_simd waves.
+namespace fbr {
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <int KIND>
+__global__ void __launch_bounds__(256) k_valu_peak(float* out, int iters, float a, float b) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if constexpr (KIND == 0) {
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = (float)(t + u);
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[u]) : "v"(a), "v"(b));
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += x[u];
+    out[t] = s;
+  } else if constexpr (KIND == 1) {
+    uint32_t x[8];
+    const uint32_t ia = __float_as_uint(a);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = (uint32_t)(t + u);
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) asm volatile("v_add_u32 %0, %1, %0" : "+v"(x[u]) : "v"(ia));
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += x[u];
+    out[t] = (float)s;
+  } else {
+    f32x2 x[8];
+    f32x2 va = {a, a}, vb = {b, b};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = f32x2{(float)(t + u), (float)(t - u)};
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(x[u]) : "v"(va), "v"(vb));
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += x[u].x + x[u].y;
+    out[t] = s;
+  }
+}
+}  // namespace fbr
+
+// Wave-level VALU instructions per second of the probe above (32 per lane per round, timed with HIP
+// events over `reps` launches after one warm-up launch).
+extern "C" int fbr_valu_peak(int hip_device, int waves_per_simd, int kind, int iters, int reps, double* ginst_per_s,
+                             double* ms_per_launch) {
+  if (waves_per_simd < 1 || waves_per_simd > 8 || kind < 0 || kind > 2 || iters <= 0 || reps <= 0 || !ginst_per_s)
+    return FBR_ERR_INVALID_ARG;
+  if (hipSetDevice(hip_device) != hipSuccess) return FBR_ERR_NO_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, hip_device) != hipSuccess) return FBR_ERR_HIP;
+  const int blocks = prop.multiProcessorCount * waves_per_simd;
+  float* out = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = FBR_OK;
+  if (hipMalloc(&out, sizeof(float) * 256 * blocks) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+      hipEventCreate(&e1) != hipSuccess) {
+    rc = FBR_ERR_HIP;
+  } else {
+    auto launch = [&]() {
+      if (kind == 0) hipLaunchKernelGGL(fbr::k_valu_peak<0>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0000001f, 0.5f);
+      else if (kind == 1) hipLaunchKernelGGL(fbr::k_valu_peak<1>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0000001f, 0.5f);
+      else hipLaunchKernelGGL(fbr::k_valu_peak<2>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0000001f, 0.5f);
+    };
+    launch();
+    (void)hipEventRecord(e0, 0);
+    for (int k = 0; k < reps; ++k) launch();
+    (void)hipEventRecord(e1, 0);
+    float ms = 0.0f;
+    if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess || ms <= 0.0f) {
+      rc = FBR_ERR_HIP;
+    } else {
+      const double waves = 4.0 * blocks;
+      *ginst_per_s = waves * 32.0 * iters * reps / (ms * 1e-3) / 1e9;
+      if (ms_per_launch) *ms_per_launch = ms / reps;
+    }
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(out);
+  return rc;
+}

@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <cstdlib>
 #include <type_traits>
 
@@ -825,6 +826,7 @@ __global__ void __launch_bounds__(T) k_voxel_grid_split(VgArgs A, int P, unsigne
     for (int k = 0; k < NW; ++k) V += wsum[k];
     __hip_atomic_store(&flags[blk], ((unsigned long long)gen << 32) | V, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t off = 0;
+    bool lost = false;
     for (int j = blk - part; j < blk; ++j) {
       unsigned long long f = 0;
       for (int spin = 0; spin < (1 << 24); ++spin) {
@@ -832,15 +834,21 @@ __global__ void __launch_bounds__(T) k_voxel_grid_split(VgArgs A, int P, unsigne
         if ((unsigned)(f >> 32) == gen) break;
         __builtin_amdgcn_s_sleep(2);
       }
-      off += (unsigned)(f >> 32) == gen ? (uint32_t)f : 0u;
+      if ((unsigned)(f >> 32) == gen) off += (uint32_t)f;
+      else lost = true;
     }
+    // a lower part never published (the wait is a safety bound, it does not happen when the lower
+    // blocks run): the offsets are unknown, so the segment is reported failed, never short
+    if (lost && A.err) atomicOr(&A.err[seg], kVgErrLookback);
     misc[2] = (int)off;
     misc[3] = (int)V;
+    misc[1] = lost ? 1 : 0;
   }
   __syncthreads();
   const int off = misc[2], V = misc[3];
-  if (nk > 0) vg_emit<T, true>(keys, vals, nk, hist, wsum, in, out + off);
-  if (tid == 0 && part == P - 1) S.cnt_out[seg] = off + V;
+  const bool lost = misc[1] != 0;
+  if (nk > 0 && !lost) vg_emit<T, true>(keys, vals, nk, hist, wsum, in, out + off);
+  if (tid == 0 && part == P - 1) S.cnt_out[seg] = lost ? (A.err ? 0 : -1) : off + V;
 }
 
 // Per-ring front end (featureExtraction.h:279-292): the surf candidates of (job, ring) are the
@@ -1722,6 +1730,7 @@ size_t voxel_lds_bytes(const VgArgs& a, int threads, bool lds_mode) {
 constexpr int kVgIpKpl = 18;  // k_voxel_grid_ip: segments up to 1024 * 18 points sort in LDS
 constexpr int kVgSplitSlots = 16;   // k_voxel_grid_split: segments x parts per launch
 constexpr int kVgSplitRing = 1024;  // flag regions: a launch's own region (concurrent launches)
+constexpr int kVgSplitMaxDevices = 64;
 int vg_split() {
   static const int v = [] {
     const char* e = std::getenv("FBR_VG_SPLIT");
@@ -1741,12 +1750,23 @@ void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
   // few segments (single-scan calls): P workgroups per segment (FBR_VG_SPLIT = P, default 4; 1 off)
   const int P = vg_split();
   if (!exact && P > 1 && cap > kVgLdsCap && vg_inplace() && nseg * P <= kVgSplitSlots) {
-    static unsigned long long* flags = [] {
-      unsigned long long* f = nullptr;
-      if (hipMalloc(&f, sizeof(unsigned long long) * kVgSplitSlots * kVgSplitRing) != hipSuccess) return (unsigned long long*)nullptr;
-      if (hipMemset(f, 0, sizeof(unsigned long long) * kVgSplitSlots * kVgSplitRing) != hipSuccess) return (unsigned long long*)nullptr;
-      return f;
-    }();
+    // look-back flags of the current device (agent-scope atomics must stay on the device that runs
+    // the kernel: contexts on several GPUs in one process each get their own)
+    static std::mutex mu;
+    static unsigned long long* dev_flags[kVgSplitMaxDevices] = {};
+    static bool dev_failed[kVgSplitMaxDevices] = {};
+    int dev = -1;
+    unsigned long long* flags = nullptr;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kVgSplitMaxDevices) {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!dev_flags[dev] && !dev_failed[dev]) {
+        unsigned long long* f = nullptr;
+        const size_t bytes = sizeof(unsigned long long) * kVgSplitSlots * kVgSplitRing;
+        if (hipMalloc(&f, bytes) == hipSuccess && hipMemset(f, 0, bytes) == hipSuccess) dev_flags[dev] = f;
+        else dev_failed[dev] = true;  // the one-workgroup kernel below serves this device
+      }
+      flags = dev_flags[dev];
+    }
     static std::atomic<unsigned> gen{0};
     if (flags) {
       const unsigned g = gen.fetch_add(1) + 1;  // never 0 (the zeroed flags)

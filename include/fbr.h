@@ -433,6 +433,12 @@ int fbr_selftest_radix_sort(int64_t n, int nbits, int variant, uint32_t* keys_in
  * write counted), averaged over `iters` launches (the STREAM-copy figure bench.py reports next to
  * the 8 TB/s spec peak). */
 int fbr_stream_copy_bandwidth(int hip_device, int64_t bytes, int iters, double* gbps);
+/* Measurement helper: the VALU issue roof.  Every SIMD holds waves_per_simd (1..8) waves, each lane
+ * running 8 independent chains of one VALU instruction (kind 0 v_fma_f32, 1 v_add_u32, 2
+ * v_pk_fma_f32) for 32 * iters instructions; *ginst_per_s = wave-level instructions per second over
+ * `reps` launches, *ms_per_launch (optional) the launch time (tools/valu_calib.py). */
+int fbr_valu_peak(int hip_device, int waves_per_simd, int kind, int iters, int reps, double* ginst_per_s,
+                  double* ms_per_launch);
 
 /* pcl::getTransformation / pcl::getTranslationAndEulerAngles (row-major 4x4 float). */
 void fbr_affine_from_pose(const float pose[6], float m[16]);

@@ -7,7 +7,7 @@ kernel trace reports the same per-dispatch durations.  This script takes a commi
 the bench's average launch time next to rocprofv3's and the HBM fraction each gives for the
 bench's algorithmic bytes per launch (bench.py kernel_bytes / DESIGN.md §4), and, where the line
 carries them, the VALU-issue fraction each gives for the bench's VALU instructions per launch
-(rocprofv3 SQ pass, tools/valu_pmc.py).
+(rocprofv3 SQ pass, tools/valu_pmc.py) against the measured issue peak (profiles/valu_calib.json).
 
 usage: roofline_check.py KERNEL_STATS.csv BENCH.json [--peak 8000]
 """
@@ -46,7 +46,7 @@ def main():
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import KERNEL_SYMBOLS as symbols
-    from bench import VALU_PEAK_GCYC
+    from bench import VALU_PEAK_GINST
     print(f"{'kernel':12s} {'bytes/launch':>14s} {'bench us':>10s} {'rocprof us':>11s} {'calls':>6s} "
           f"{'bench frac':>10s} {'rocprof frac':>12s} {'bench valu':>10s} {'rocprof valu':>12s}")
     nan = float("nan")
@@ -55,7 +55,7 @@ def main():
         bpl = r["bytes_per_launch"]
         rf = bpl / (avg * 1e-6) / 1e9 / a.peak if avg else nan
         vb = r.get("valu_frac", nan)
-        vr = r["valu_cycles_per_launch"] / (avg * 1e-6) / 1e9 / VALU_PEAK_GCYC if avg and "valu_cycles_per_launch" in r else nan
+        vr = r["valu_insts_per_launch"] / (avg * 1e-6) / 1e9 / VALU_PEAK_GINST if avg and "valu_insts_per_launch" in r else nan
         mark = " <- roofline kernel" if k == roof["kernel"] else ""
         print(f"{k:12s} {bpl:14.4g} {r['avg_launch_us']:10.1f} {avg if avg else nan:11.1f} {calls:6d} "
               f"{r['frac']:10.4f} {rf:12.4f} {vb:10.4f} {vr:12.4f}{mark}")

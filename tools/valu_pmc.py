@@ -8,17 +8,14 @@ kernel families; a launcher of two kernels counts its calls once):
 
   insts_valu_per_launch   SQ_INSTS_VALU summed over the launcher's dispatches / calls: wave-level
                           VALU instructions, a property of the work (the same under stream overlap)
-  valu_cycles_per_launch  4 * SQ_ACTIVE_INST_VALU (quad-cycles) / calls: SIMD cycles the VALU was busy
-                          with the launch's instructions (multi-cycle ones counted in full)
-  valu_busy_alone         4 * SQ_ACTIVE_INST_VALU (quad-cycles) / (1024 SIMDs * cycles), cycles =
-                          duration * effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration,
-                          MI355X_MICROARCH.md "DVFS give-back"): VALU-busy of the kernel running alone
-  eff_clock_ghz           that effective clock
+  valu_issue_alone        those instructions / the serialised duration / the measured issue peak
+                          (profiles/valu_calib.json: 1079 G wave64 instr/s of v_fma_f32)
+  eff_clock_ghz           GRBM_GUI_ACTIVE / 8 XCDs / duration (MI355X_MICROARCH.md "DVFS give-back")
 
-bench.py turns valu_cycles_per_launch into the live VALU-busy fraction of a launch (the VALU roofline:
-1024 SIMDs x 2.4 GHz of VALU cycles per second).  Every wave64 VALU instruction of these kernels
-counts 4 cycles (valu_cycles / insts = 4.0-4.2: none is packed f32, whose 2-lane form doubles the
-157 TF vector peak).
+bench.py turns insts_valu_per_launch into the live VALU fraction of a launch.  SQ_ACTIVE_INST_VALU
+is not busy time: the calibration's PMC pass shows it counts exactly one quad-cycle per wave64 VALU
+instruction at every issue rate (1, 2, 4, 8 waves per SIMD), while the SIMD issues one every ~2.3
+cycles with two or more waves; round 4 priced 4 x ACTIVE_INST_VALU as busy cycles, twice the truth.
 
 usage: valu_pmc.py COUNTER_COLLECTION.csv CONFIG BATCH [out.json]
 """
@@ -33,6 +30,7 @@ NAMES = {"gn_knn": [r"k_gn_knn"], "gn_residual": [r"k_gn_residual"], "features":
          "project": [r"k_project\b"], "extract": [r"k_compact", r"k_rowcount"], "gn_solve": [r"k_gn_solve"]}
 SIMDS = 1024
 XCDS = 8
+CALIB = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))), "profiles", "valu_calib.json")
 
 
 def main():
@@ -52,22 +50,25 @@ def main():
         for k, v in d.items():
             agg[key][k] += v
         calls[key][i] += 1
-    res = {"config": cfg, "batch": batch, "simds": SIMDS, "peak_issue_ginst_per_s": SIMDS * 2.4 / 2.0,
-           "source": path, "kernels": {}}
-    print(f"{'kernel':12s} {'calls':>6s} {'avg us':>9s} {'VALU inst/launch':>17s} {'busy alone':>10s} {'clk GHz':>8s}")
+    peak = 1024 * 2.4 / 2.0
+    try:
+        peak = json.load(open(CALIB))["measured_peak_ginst_per_s"]
+    except Exception:
+        pass
+    res = {"config": cfg, "batch": batch, "simds": SIMDS, "valu_peak_ginst_per_s": peak, "source": path, "kernels": {}}
+    print(f"{'kernel':12s} {'calls':>6s} {'avg us':>9s} {'VALU inst/launch':>17s} {'issue alone':>11s} {'clk GHz':>8s}")
     for key in NAMES:
         g = agg.get(key)
         if not g or "SQ_INSTS_VALU" not in g:
             continue
         n = max(calls[key].values())
         clk = g["GRBM_GUI_ACTIVE"] / XCDS / g["dur_ns"] if g.get("GRBM_GUI_ACTIVE") else 2.4
-        busy = 4.0 * g["SQ_ACTIVE_INST_VALU"] / (SIMDS * g["dur_ns"] * clk)
+        issue = g["SQ_INSTS_VALU"] / (g["dur_ns"] * 1e-9) / 1e9 / peak
         ent = {"calls": n, "avg_us_alone": g["dur_ns"] / n / 1e3, "insts_valu_per_launch": g["SQ_INSTS_VALU"] / n,
-               "valu_cycles_per_launch": 4.0 * g["SQ_ACTIVE_INST_VALU"] / n,
-               "valu_busy_alone": busy, "eff_clock_ghz": clk,
+               "valu_issue_alone": issue, "eff_clock_ghz": clk,
                "wave_cycles_per_launch": g.get("SQ_WAVE_CYCLES", 0.0) * 4.0 / n}
         res["kernels"][key] = ent
-        print(f"{key:12s} {n:6d} {ent['avg_us_alone']:9.1f} {ent['insts_valu_per_launch']:17.4g} {busy:10.3f} {clk:8.2f}")
+        print(f"{key:12s} {n:6d} {ent['avg_us_alone']:9.1f} {ent['insts_valu_per_launch']:17.4g} {issue:11.3f} {clk:8.2f}")
     if out:
         with open(out, "w") as f:
             json.dump(res, f, indent=1)
