@@ -120,7 +120,7 @@ def parse():
                     help="worker threads of the all-cores CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--exact-line", type=int, default=1,
-                    help="rank 0 at N=1: a child run with FBR_VG_EXACT=1 (PCL's point order inside voxels, "
+                    help="rank 0 at N=1: a second context with exact_voxel_order = 1 (PCL's point order inside voxels, "
                          "bit-identical poses) reports its throughput and parity block; 0 disables")
     ap.add_argument("--deskew", action="store_true",
                     help="enable the IMU deskew path (SURVEY 8f row 3): one imuDeskewInfo table per job")
@@ -220,22 +220,38 @@ def latency_line(cfg, corner_map, surf_map, n, cpu_scans=0):
     return out
 
 
-def exact_line(args):
-    """The same workload with FBR_VG_EXACT=1 in a child process (the knob is read once per process):
-    every VoxelGrid sums a voxel's points in std::sort's order (csrc/fbr_introsort.h), so the poses
-    equal the oracle's bit for bit.  B = 256 jobs, its parity block over the oracle sample."""
-    import subprocess
-    cmd = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--batch", "256", "--steps", "5",
-           "--warmup", "2", "--latency", "0", "--ingest", "0", "--profile", "off", "--exact-line", "0",
-           "--cpu-sample", str(args.cpu_sample), "--pmc-json", "none"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=dict(os.environ, FBR_VG_EXACT="1"))
-    if r.returncode != 0:
-        return {"error": r.stderr[-500:]}
-    d = json.loads(r.stdout.strip().splitlines()[-1])
-    return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"], "jobs_per_step": 256,
-            "path": "FBR_VG_EXACT=1: std::sort's partition phase emulated in every VoxelGrid (per-ring, mapping DS, "
-                    "start-up map), then the stable radix sort",
-            "parity_vs_ref": d.get("parity_vs_ref"), "pose_rmse_vs_ref": d.get("pose_rmse_vs_ref")}
+def exact_line(cfg, corner_map, surf_map, scans, guesses, ref=None, ref_iters=None, ref_nsel=None, B=256, steps=5):
+    """The same workload on a second context with fbr_params.exact_voxel_order = 1 (in this process,
+    beside the default-mode context): every VoxelGrid sums a voxel's points in std::sort's order
+    (csrc/fbr_introsort.h), so the poses equal the oracle's bit for bit.  B = 256 jobs; its parity
+    block over the oracle sample of the main line (the same first jobs)."""
+    from feature_base_pointcloud_registration_amd import api, synth
+    B = min(B, len(scans))
+    P = synth.config_params(cfg, max_batch=B, exact_voxel_order=1)
+    with api.Context(P) as c:
+        c.set_map(corner_map, surf_map)
+        c.batch_stage(scans[:B], guesses[:B])
+        for _ in range(2):
+            c.batch_launch()
+        c.batch_wait()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            c.batch_launch()
+        c.batch_wait()
+        dt = time.perf_counter() - t0
+        poses, stats = c.batch_results()
+    out = {"value": round(B * steps / dt, 3), "unit": "scans/s", "ms_per_step": round(1e3 * dt / steps, 4),
+           "jobs_per_step": B,
+           "path": "fbr_params.exact_voxel_order = 1: std::sort's partition phase emulated in every VoxelGrid "
+                   "(per-ring, mapping DS, start-up map), then the stable radix sort"}
+    if ref is not None:
+        S = min(len(ref), B)
+        out["parity_vs_ref"] = {
+            "n": S, "iterations_equal": int((stats["iterations"][:S] == ref_iters[:S]).sum()),
+            "n_sel_equal": int((stats["n_sel"][:S] == ref_nsel[:S]).sum()),
+            "pose_bit_equal": int((poses[:S].view(np.int32) == ref[:S].view(np.int32)).all(axis=1).sum())}
+        out["pose_max_abs_diff_vs_ref"] = float(np.abs(poses[:S].astype(np.float64) - ref[:S]).max())
+    return out
 
 
 def main():
@@ -594,8 +610,8 @@ def main():
         result["cpu_baseline_all_cores"] = {
             "value": round(S / cpu_all_s, 3), "unit": "scans/s", "cores": nth, "kind": "port",
             "sample": f"the same {S} jobs, {nth} independent single-threaded jobs at a time"}
-    if world == 1 and args.exact_line and not args.no_cpu_baseline and os.environ.get("FBR_VG_EXACT", "0") == "0":
-        result["exact_voxel_order"] = exact_line(args)
+    if world == 1 and args.exact_line and not args.no_cpu_baseline:
+        result["exact_voxel_order"] = exact_line(cfg, corner_map, surf_map, scans, guesses, ref, ref_iters, ref_nsel)
     print(json.dumps(result), flush=True)
     ctx.close()
     if dist is not None:

@@ -36,6 +36,7 @@ EXPORTED_SYMBOLS = [
     "fbr_imu_convert", "fbr_imu_deskew_info", "fbr_set_deskew", "fbr_stream_copy_bandwidth", "fbr_valu_peak",
     "fbr_keyframe_params_default", "fbr_keyframes_add", "fbr_keyframes_set_pose", "fbr_keyframes_count",
     "fbr_keyframes_reset", "fbr_extract_surrounding_keyframes",
+    "fbr_comm_unique_id", "fbr_comm_create", "fbr_comm_destroy", "fbr_batch_allgather",
 ]
 
 
@@ -117,6 +118,10 @@ def lib():
             "fbr_keyframes_count": (ctypes.c_int, [_VP, _VP]),
             "fbr_keyframes_reset": (ctypes.c_int, [_VP]),
             "fbr_extract_surrounding_keyframes": (ctypes.c_int, [_VP, ctypes.c_double, _VP, _VP, _VP, _VP]),
+            "fbr_comm_unique_id": (ctypes.c_int, [_VP]),
+            "fbr_comm_create": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+            "fbr_comm_destroy": (ctypes.c_int, [_VP]),
+            "fbr_batch_allgather": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -557,6 +562,20 @@ class Context:
                                             ctypes.byref(st), ctypes.byref(lid)), "fbr_batch_export_ready")
         return lid.value, st.value or 0
 
+    def diag_ring_filter(self, kernel):
+        """Diagnostic: the per-ring surf filter kernel of this context (-1 by launch size, 0 the
+        512-thread kernel, 2 four waves per ring; fbr_diag_ring_filter)."""
+        f = lib().fbr_diag_ring_filter
+        f.restype, f.argtypes = ctypes.c_int, [_VP, ctypes.c_int]
+        _check(f(self._h, int(kernel)), "fbr_diag_ring_filter")
+
+    def diag_force_capacity_error(self, job):
+        """Diagnostic: batch job `job` of the following launches is reported as over the feature
+        capacity (fbr_diag_force_capacity_error); job < 0 clears it."""
+        f = lib().fbr_diag_force_capacity_error
+        f.restype, f.argtypes = ctypes.c_int, [_VP, ctypes.c_int]
+        _check(f(self._h, int(job)), "fbr_diag_force_capacity_error")
+
     def batch_bytes(self):
         t, g = ctypes.c_double(), ctypes.c_double()
         _check(lib().fbr_batch_bytes(self._h, ctypes.byref(t), ctypes.byref(g)), "fbr_batch_bytes")
@@ -583,7 +602,39 @@ class Context:
         return out[:n.value].copy()
 
 
-__all__ = ["Context", "FbrError", "FbrParams", "default_params", "lib", "device_count",
+def comm_unique_id():
+    """fbr_comm_unique_id: the 128-byte RCCL id rank 0 makes and hands to the other ranks."""
+    buf = (ctypes.c_uint8 * 128)()
+    _check(lib().fbr_comm_unique_id(buf), "fbr_comm_unique_id")
+    return bytes(buf)
+
+
+class Comm:
+    """The pose-record communicator of one rank (fbr_comm_create): RCCL over the context's device.
+    allgather(launch_id, recv_ptr) all-gathers that launch's 32-B records of every rank into the
+    device buffer recv_ptr ([nranks][max_jobs][8] f32) and returns the HIP stream to wait on."""
+
+    def __init__(self, ctx, uid, nranks, rank, max_jobs):
+        self._h = _VP()
+        idb = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        _check(lib().fbr_comm_create(ctypes.byref(self._h), ctx._h, idb, int(nranks), int(rank), int(max_jobs)),
+               "fbr_comm_create")
+        self._ctx = ctx
+        self.nranks, self.rank, self.max_jobs = int(nranks), int(rank), int(max_jobs)
+
+    def allgather(self, launch_id, recv_ptr):
+        st = _VP()
+        _check(lib().fbr_batch_allgather(self._ctx._h, self._h, int(launch_id), ctypes.c_void_p(recv_ptr),
+                                         ctypes.byref(st)), "fbr_batch_allgather")
+        return st.value or 0
+
+    def close(self):
+        if self._h:
+            _check(lib().fbr_comm_destroy(self._h), "fbr_comm_destroy")
+            self._h = _VP()
+
+
+__all__ = ["Context", "Comm", "comm_unique_id", "FbrError", "FbrParams", "default_params", "lib", "device_count",
            "affine_from_pose", "pose_from_affine", "pcd_read", "pcd_write", "msg_to_points", "points_to_msg", "PointCloud2",
            "imu_convert", "imu_deskew_info",
            "EXPORTED_SYMBOLS"]

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <dlfcn.h>
 #include <functional>
 #include <map>
 #include <mutex>
@@ -154,6 +155,9 @@ struct fbr_ctx {
   int last_slot = -1;         // slot of the latest launch (-1: none since the last stage)
   int64_t slot_launch[kMaxSlots] = {-1, -1, -1};  // launch number of each slot's latest launch
   int64_t exported = -1;      // latest launch whose records fbr_batch_export_ready exported
+  int64_t first_valid = 0;    // launches below this id belong to a dropped batch (fbr_batch_allgather)
+  int diag_err_job = -1;      // diagnostic (fbr_diag_force_capacity_error): batch job flagged over capacity
+  int diag_ring_filter = -1;  // diagnostic (fbr_diag_ring_filter): per-ring surf filter kernel, -1 = by size
   hipEvent_t ev_staged = nullptr;  // the staged inputs are on the device (recorded on stream)
   hipEvent_t ev_fork = nullptr;    // single-scan side-stream fork
   hipEvent_t ev_ext = nullptr;     // a caller's stream, waited on before an export (fbr_batch_export_ready)
@@ -374,7 +378,7 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
         hipMemcpyAsync(d_cnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
       rc = FBR_ERR_HIP;
     } else if (large) {
-      rc = voxel_grid_large(c->stream, c->arena, d_in, n, leaf, 0, d_out, d_cnt + 1);
+      rc = voxel_grid_large(c->stream, c->arena, d_in, n, leaf, 0, c->P.exact_voxel_order ? 1 : 0, d_out, d_cnt + 1);
       int32_t nout = 0;
       if (!rc && (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
                   fbr_sync(c->stream) != hipSuccess))
@@ -396,7 +400,7 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
       a.s[0].scratch = d_sc;
       a.s[0].leaf = leaf;
       a.s[0].nseg = 1;
-      a.s[0].exact = vg_exact() ? 1 : 0;
+      a.s[0].exact = c->P.exact_voxel_order ? 1 : 0;
       launch_voxel_grid(c->stream, a);
       int32_t nout = 0;
       if (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
@@ -474,6 +478,8 @@ int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode, bool err_clear =
   a.stamps = c->d_feat_stamps ? c->d_feat_stamps + j0 * H * 12 : nullptr;
   if (!err_clear) CK(hipMemsetAsync(c->d_err + j0, 0, sizeof(int32_t) * sb.B, sb.st));
   TIMED_ON(c, sb.st, "features", launch_features(sb.st, a));
+  if (!stream_mode && c->diag_err_job >= sb.in0 && c->diag_err_job < sb.in0 + sb.B)
+    CK(hipMemsetD32Async((hipDeviceptr_t)(c->d_err + j0 + (c->diag_err_job - sb.in0)), 1, 1, sb.st));
   VgRing v{};
   v.cloud = a.cloud;
   v.label = a.label;
@@ -488,8 +494,9 @@ int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode, bool err_clear =
   v.stride_out = c->W;
   v.cnt_out = c->d_surf_ring_cnt + j0 * H;
   v.dbg = std::getenv("FBR_VR_DBG") ? std::atoi(std::getenv("FBR_VR_DBG")) : 0;
-  v.exact = vg_exact() ? 1 : 0;
+  v.exact = c->P.exact_voxel_order ? 1 : 0;
   v.stamps = a.stamps;
+  v.kernel = c->diag_ring_filter;
   TIMED_ON(c, sb.st, "voxel_ring", launch_voxel_ring(sb.st, v));
   TIMED_ON(c, sb.st, "concat",
            launch_concat(sb.st, sb.B, c->H, c->W, a.corner_slot, a.corner_cnt, v.out, v.cnt_out,
@@ -575,6 +582,7 @@ int drop_staged_batch(fbr_ctx* c) {
   // launch ids only grow: every launch made so far belongs to the dropped batch (or its slot was
   // overwritten by a single-scan call), so fbr_batch_export_ready must never hand one of them out
   c->exported = c->launch_seq - 1;
+  c->first_valid = c->launch_seq;
   return rc;
 }
 
@@ -605,10 +613,10 @@ int register_prepare(fbr_ctx* c, const Sub& sb, bool trace) {
   VgArgs v{};
   const int64_t ccap = std::min<int64_t>(HW, (int64_t)kCornerPerRing * c->H);
   v.s[0] = VgSet{c->d_surf_all + j0 * HW, HW, c->d_nsurf + j0, HW, c->d_surfDS + j0 * HW, HW, c->d_nsds + j0,
-                 c->d_vg_scratch + j0 * kVgScratch * HW, c->P.mapping_surf_leaf_size, sb.B, 1, vg_exact() ? 1 : 0};
+                 c->d_vg_scratch + j0 * kVgScratch * HW, c->P.mapping_surf_leaf_size, sb.B, 1, c->P.exact_voxel_order ? 1 : 0};
   v.s[1] = VgSet{c->d_corner_all + j0 * HW, HW, c->d_ncorner + j0, ccap, c->d_cornerDS + j0 * HW, HW, c->d_ncds + j0,
                  c->d_vg_scratch + c->Bwork * kVgScratch * HW + j0 * kVgScratch * ccap, c->P.mapping_corner_leaf_size,
-                 sb.B, 1, vg_exact() ? 1 : 0};
+                 sb.B, 1, c->P.exact_voxel_order ? 1 : 0};
   if (c->ring_box_valid) {  // the clouds' bounds from k_concat: the filter reads each cloud twice, not 3 times
     const float* rb = c->d_ring_box + j0 * c->H * kRingBox;
     for (int k = 0; k < 2; ++k) {
@@ -1132,7 +1140,7 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
   if (n >= vg_large_min()) {
     int32_t nout = 0;
     if (dalloc(&d_cnt, 1)) return FBR_ERR_HIP;
-    rc = voxel_grid_large(c->stream, c->arena, d_in, n, leaf, 0, d_out, d_cnt);
+    rc = voxel_grid_large(c->stream, c->arena, d_in, n, leaf, 0, c->P.exact_voxel_order ? 1 : 0, d_out, d_cnt);
     if (!rc && (hipMemcpyAsync(&nout, d_cnt, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
                 fbr_sync(c->stream) != hipSuccess))
       rc = FBR_ERR_HIP;
@@ -1155,7 +1163,7 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
     a.s[0].scratch = d_sc;
     a.s[0].leaf = leaf;
     a.s[0].nseg = 1;
-    a.s[0].exact = vg_exact() ? 1 : 0;
+    a.s[0].exact = c->P.exact_voxel_order ? 1 : 0;
     if (hipMemcpyAsync(d_cnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
       rc = FBR_ERR_HIP;
     } else {
@@ -1281,10 +1289,8 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
   c->Bcap = p->max_batch;
   c->NMAX = p->max_points_per_scan;
   if (const char* e = std::getenv("FBR_NSUB")) c->nsub_pref = std::max(1, std::min(kMaxSub, std::atoi(e)));
-  static const int pipe = [] {  // launch slots (0 / 1: no pipelining)
-    const char* e = std::getenv("FBR_PIPE");
-    return e ? std::max(1, std::min(fbr_ctx::kMaxSlots, std::atoi(e) <= 0 ? 1 : std::atoi(e))) : 3;
-  }();
+  // launch slots (fbr_params.pipeline_depth: 0 = the default 3)
+  const int pipe = p->pipeline_depth <= 0 ? 3 : std::min(fbr_ctx::kMaxSlots, p->pipeline_depth);
   c->nslot = p->max_batch > 1 ? pipe : 1;
   // Pipelined, one sub-batch per launch is best at every batch size (the two launches in flight
   // overlap as the sub-batches did): B = 128 / 256 / 1024 give 91.8k / 96.7k / 97.4k scans/s
@@ -1829,6 +1835,126 @@ int fbr_batch_export_ready(fbr_ctx* c, void* device_dst, void* wait_stream, void
   return FBR_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// RCCL pose gather.  librccl is opened on first use (dlopen, RTLD_LOCAL): a host
+// that never builds a communicator does not need it, and a process that already holds RCCL (torch)
+// shares the loaded copy through its soname.  Only the types come from the header.
+// ---------------------------------------------------------------------------------------------
+}  // extern "C" (reopened below)
+#include <rccl/rccl.h>
+namespace {
+struct RcclApi {
+  bool ok = false;
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+};
+const RcclApi& rccl() {
+  static const RcclApi api = [] {
+    RcclApi a;
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+    if (!h) return a;
+    a.get_unique_id = (decltype(a.get_unique_id))dlsym(h, "ncclGetUniqueId");
+    a.comm_init_rank = (decltype(a.comm_init_rank))dlsym(h, "ncclCommInitRank");
+    a.comm_destroy = (decltype(a.comm_destroy))dlsym(h, "ncclCommDestroy");
+    a.all_gather = (decltype(a.all_gather))dlsym(h, "ncclAllGather");
+    a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.all_gather;
+    return a;
+  }();
+  return api;
+}
+}  // namespace
+
+struct fbr_comm {
+  ncclComm_t nc = nullptr;
+  int dev = 0, nranks = 0, rank = 0, max_jobs = 0;
+  float* send = nullptr;  // [max_jobs][8] this rank's padded records
+};
+
+extern "C" {
+
+int fbr_comm_unique_id(uint8_t id_out[FBR_COMM_ID_BYTES]) {
+  static_assert(FBR_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
+  if (!id_out) return FBR_ERR_INVALID_ARG;
+  if (!rccl().ok) return FBR_ERR_UNSUPPORTED;
+  ncclUniqueId id;
+  if (rccl().get_unique_id(&id) != ncclSuccess) return FBR_ERR_HIP;
+  std::memcpy(id_out, id.internal, FBR_COMM_ID_BYTES);
+  return FBR_OK;
+}
+
+int fbr_comm_create(fbr_comm** out, fbr_ctx* c, const uint8_t id[FBR_COMM_ID_BYTES], int nranks, int rank,
+                    int max_jobs_per_rank) {
+  if (!out || !c || !id || nranks < 1 || rank < 0 || rank >= nranks || max_jobs_per_rank < 1) return FBR_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (!rccl().ok) return FBR_ERR_UNSUPPORTED;
+  CK(hipSetDevice(c->dev));
+  fbr_comm* m = new fbr_comm();
+  m->dev = c->dev;
+  m->nranks = nranks;
+  m->rank = rank;
+  m->max_jobs = max_jobs_per_rank;
+  ncclUniqueId uid;
+  std::memcpy(uid.internal, id, FBR_COMM_ID_BYTES);
+  if (hipMalloc((void**)&m->send, sizeof(float) * 8 * (size_t)max_jobs_per_rank) != hipSuccess) {
+    delete m;
+    return FBR_ERR_HIP;
+  }
+  // blocks until every rank has joined (bootstrap over the id's socket)
+  if (rccl().comm_init_rank(&m->nc, nranks, uid, rank) != ncclSuccess) {
+    (void)hipFree(m->send);
+    delete m;
+    return FBR_ERR_HIP;
+  }
+  *out = m;
+  return FBR_OK;
+}
+
+int fbr_comm_destroy(fbr_comm* m) {
+  if (!m) return FBR_ERR_INVALID_ARG;
+  (void)hipSetDevice(m->dev);
+  int rc = FBR_OK;
+  if (m->nc && rccl().comm_destroy(m->nc) != ncclSuccess) rc = FBR_ERR_HIP;
+  (void)hipFree(m->send);
+  delete m;
+  return rc;
+}
+
+int fbr_batch_allgather(fbr_ctx* c, fbr_comm* m, int64_t launch_id, void* recv, void** done_stream) {
+  if (!c || !m || !recv) return FBR_ERR_INVALID_ARG;
+  if (done_stream) *done_stream = nullptr;
+  if (m->dev != c->dev) return FBR_ERR_INVALID_ARG;
+  if (c->staged_B <= 0 || c->launch_seq == 0) return FBR_ERR_STATE;
+  if (c->staged_B > m->max_jobs) return FBR_ERR_CAPACITY;
+  if (launch_id < 0) launch_id = c->launch_seq - 1;
+  if (launch_id < c->first_valid || launch_id >= c->launch_seq) return FBR_ERR_STATE;
+  int s = -1;
+  for (int q = 0; q < c->nslot; ++q)
+    if (c->slot_launch[q] == launch_id) s = q;
+  if (s < 0) return FBR_ERR_STATE;  // its slot has been reused by a later launch
+  CK(hipSetDevice(c->dev));
+  int rc = advance_runs(c, s);  // the launch fully enqueued (the host follows its GN flags)
+  if (rc) return rc;
+  const GnRun& r = c->run[s];
+  hipStream_t st = r.subs[0].st;
+  for (int k = 1; k < r.nsub; ++k) CK(hipStreamWaitEvent(st, c->xev[r.subs[k].k], 0));
+  const int64_t w0 = (int64_t)s * c->Bcap;
+  if (c->staged_B < m->max_jobs)  // padding records: zeros
+    CK(hipMemsetAsync(m->send + 8 * (int64_t)c->staged_B, 0, sizeof(float) * 8 * (m->max_jobs - c->staged_B), st));
+  launch_export_records(st, c->staged_B, c->d_pose_out + w0 * 6, c->d_stats + w0, c->d_err + w0, c->d_guess, m->send);
+  CK(hipGetLastError());
+  if (rccl().all_gather(m->send, recv, (size_t)8 * m->max_jobs, ncclFloat32, m->nc, st) != ncclSuccess) return FBR_ERR_HIP;
+  if (done_stream) *done_stream = (void*)st;
+  else {
+    CK(hipEventRecord(c->ev_ext, st));
+    CK(hipStreamWaitEvent(c->stream, c->ev_ext, 0));
+  }
+  return FBR_OK;
+}
+
 int fbr_batch_bytes(fbr_ctx* c, double* bytes_total, double* bytes_gn) {
   if (!c) return FBR_ERR_INVALID_ARG;
   if (c->last_iters.empty()) return FBR_ERR_STATE;
@@ -2052,6 +2178,25 @@ extern "C" int fbr_diag_batch_times(long long* out2, int reset) {
     if (out2) out2[k] = d.batch_ns[k].load();
     if (reset) d.batch_ns[k] = 0;
   }
+  return FBR_OK;
+}
+
+// Diagnostic: the per-ring surf filter kernel of this context's default-order launches: -1 by
+// launch size (four waves per ring above 256 rings, else the 512-thread kernel), 0 the 512-thread
+// kernel, 2 four waves per ring -- so a test can compare the two on the same scans.
+extern "C" int fbr_diag_ring_filter(fbr_ctx* c, int kernel) {
+  if (!c || (kernel != -1 && kernel != 0 && kernel != 2)) return FBR_ERR_INVALID_ARG;
+  c->diag_ring_filter = kernel;
+  return FBR_OK;
+}
+
+// Diagnostic: batch job `job` of the following launches is treated as over the feature capacity
+// (as if k_features had flagged it), so the tests can check how fbr_batch_results and the exported
+// records report such a job (no valid scan reaches the capacity: a ring holds at most W points);
+// job < 0 clears it.
+extern "C" int fbr_diag_force_capacity_error(fbr_ctx* c, int job) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  c->diag_err_job = job < 0 ? -1 : job;
   return FBR_OK;
 }
 

@@ -226,23 +226,12 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
     int j = 0, i = q.x, e = q.y & 0x7fffffff;
     bool inside = q.y < 0;
     for (int t = 0; t < total; ++t) {
-#ifdef FBR_KNN_ROW_SEL
-      // A/B build (tools/gpu_r04am.sh): the next row's entry read every trip, the advance as
-      // selects instead of a branch
-      const int2 qn = rows[min(j + 1, nrow - 1) * kResThreads];
-      const bool adv = i == e;
-      i = adv ? qn.x : i;
-      e = adv ? (qn.y & 0x7fffffff) : e;
-      inside = adv ? qn.y < 0 : inside;
-      j += adv ? 1 : 0;
-#else
       if (i == e) {  // next queued row (every queued row is non-empty)
         q = rows[++j * kResThreads];
         i = q.x;
         e = q.y & 0x7fffffff;
         inside = q.y < 0;
       }
-#endif
       const float4 p = m.pts[i++];
       bool out = false;
       if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
@@ -836,33 +825,15 @@ inline bool knn_flat() {
   return v;
 }
 
-// Flat row queue for the 0.5 m cells of dense maps too (FBR_KNN_FLAT_R2=1; 25 rows x 256 lanes of
-// int2 = 50 KB of LDS per workgroup).
-inline bool knn_flat_r2() {
-  static const bool v = [] {
-    const char* e = std::getenv("FBR_KNN_FLAT_R2");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
-}
-
-// Flat row queue in iteration 0 too (FBR_KNN_FLAT0=1): no warm-start bound, so every row within
-// distance 1 is queued and walked without the per-row pruning of the 5th distance.
-inline bool knn_flat0() {
-  static const bool v = [] {
-    const char* e = std::getenv("FBR_KNN_FLAT0");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
-}
-
 template <int R, bool F>
 void launch_gn_knn_r(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
   if constexpr (!F) {
     if (knn_lpq(a.B) == 8) return launch_gn_knn_rl<R, F, false, 8>(s, a, grid, use_prev);
   }
-  if constexpr (R <= 2 && !F) {
-    if ((use_prev || knn_flat0()) && knn_flat() && (R == 1 || knn_flat_r2())) return launch_gn_knn_rl<R, F, true>(s, a, grid, use_prev);
+  // flat queue for the 1 m cells from iteration 1 (round 4 measured it slower in iteration 0, with
+  // no warm-start bound, and for the 0.5 m cells, whose 25-row queue costs occupancy)
+  if constexpr (R == 1 && !F) {
+    if (use_prev && knn_flat()) return launch_gn_knn_rl<R, F, true>(s, a, grid, use_prev);
   }
   launch_gn_knn_rl<R, F, false>(s, a, grid, use_prev);
 }

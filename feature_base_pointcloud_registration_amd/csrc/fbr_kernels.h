@@ -122,7 +122,8 @@ struct VgSet {               // nseg segments of one cloud family, one leaf size
   float leaf;
   int nseg;
   int morton;                // 1: emit voxels in Morton order of (i,j,k) instead of PCL key order
-  int exact;                 // 1: PCL's point order inside voxels (std::sort's, fbr_introsort.h)
+  int exact;                 // 1: PCL's point order inside voxels (std::sort's, fbr_introsort.h;
+                             // fbr_params.exact_voxel_order), 0: index order
   // Optional precomputed bounds (k_concat's ring boxes): segment seg's box k at
   // box + seg * box_stride + k * kRingBox, k < box_n, each {min xyz, max xyz}; null: from the points
   const float* box;
@@ -132,9 +133,6 @@ struct VgSet {               // nseg segments of one cloud family, one leaf size
 // Per-point u32 slots of a VoxelGrid segment's global scratch: keys / indices ping-pong (4) and
 // the std::sort emulation's frame lists (1).
 constexpr int64_t kVgScratch = 5;
-// FBR_VG_EXACT=1: sum a voxel's points in std::sort's order (PCL's), bit-identical centroids;
-// default 0: index order (centroids to float rounding)
-bool vg_exact();
 struct VgArgs {
   VgSet s[2];                // segments of set 0, then of set 1 (set 1 may be empty)
   // per-segment error words (segment j of either set = job j; may be null): k_voxel_grid_split ORs
@@ -184,8 +182,8 @@ inline void arena_free(DevArena& a) {
 
 // One large cloud on the whole device (rocprim stable radix sort); *d_nout gets the voxel count.
 constexpr int64_t kVgLargeMin = 32768;  // below this the one-workgroup kernel is faster
-int voxel_grid_large(hipStream_t s, DevArena& ar, const float4* in, int64_t n, float leaf, int morton, float4* out,
-                     int32_t* d_nout);
+int voxel_grid_large(hipStream_t s, DevArena& ar, const float4* in, int64_t n, float leaf, int morton, int exact,
+                     float4* out, int32_t* d_nout);
 
 // Per-ring surf filter reading the projected cloud + label mask directly (no candidate copy).
 struct VgRing {
@@ -201,6 +199,8 @@ struct VgRing {
   int64_t stride_out;
   int32_t* cnt_out;          // [B*H]
   int dbg;                   // diagnostic phase cut (FBR_VR_DBG; 0 = full kernel)
+  int kernel = -1;           // default order: -1 by launch size, 0 the 512-thread kernel, 2 four waves
+                             // per ring (fbr_diag_ring_filter: tests compare the two)
   int exact;                 // 1: PCL's point order inside voxels (std::sort's, fbr_introsort.h)
   unsigned long long* stamps;  // diagnostic builds (FBR_VR_STAMPS) only: [B*H][12]
 };

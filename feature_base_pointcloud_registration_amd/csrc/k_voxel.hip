@@ -290,10 +290,17 @@ __device__ int vg_radix_sort(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, 
 // 8-bit digits (hist holds (NW + 1) * 256 counters).  Ends with a barrier.  Always inlined: with
 // two callers (the exact and default kernels) the compiler outlined it, and the call frame put
 // 80 B per lane in scratch (spilled on every call: ~50 MB of writes per B = 1024 launch).
-// kLeader (diagnostic, fbr_selftest_radix_sort only): per-wave digit counts by the lowest lane of
-// each digit's ballot peer group instead of LDS atomics (round 3's variant).
-template <int T, int KPL, bool kLeader = false>
-__device__ __attribute__((always_inline)) void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint16_t* vals, int n, int nbits,
+// kLeader (diagnostic, fbr_selftest_radix_sort only): 1 = per-wave digit counts by the lowest lane
+// of each digit's ballot peer group instead of LDS atomics; 2 = that, plus round 3's wave-uniform
+// early exit (`if (c0 + 64 * k >= c1) break;`) in the count and scatter loops: the exact form that
+// mis-sorted in round 3.
+#ifdef FBR_VG_IP_NOINLINE  // diagnostic build: round 3's outlined call (with a call frame), for the replay
+#define FBR_VG_IP_INLINE __attribute__((noinline))
+#else
+#define FBR_VG_IP_INLINE __attribute__((always_inline))
+#endif
+template <int T, int KPL, int kLeader = 0>
+__device__ FBR_VG_IP_INLINE void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint16_t* vals, int n, int nbits,
                                       uint32_t* hist, uint32_t* wsum) {
   constexpr int NW = T / 64, NB = 256, PER = NB * NW / T;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -314,9 +321,11 @@ __device__ __attribute__((always_inline)) void vg_radix_sort_inplace(FBR_LDS_AS 
     }
     for (int b = tid; b < tot; b += T) hist[(b % NW) * NB + b / NW] = 0u;
     __syncthreads();  // every wave holds its chunk: the scatter below may overwrite any position
-    if constexpr (kLeader) {
+    if constexpr (kLeader != 0) {
 #pragma unroll
       for (int k = 0; k < KPL; ++k) {
+        if constexpr (kLeader == 2)
+          if (c0 + 64 * k >= c1) break;  // wave-uniform
         const bool valid = c0 + 64 * k + lane < c1;
         const uint32_t d = (kr[k] >> shift) & dmask;
         uint64_t peers = __ballot(valid);
@@ -361,6 +370,8 @@ __device__ __attribute__((always_inline)) void vg_radix_sort_inplace(FBR_LDS_AS 
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < KPL; ++k) {
+      if constexpr (kLeader == 2)
+        if (c0 + 64 * k >= c1) break;  // wave-uniform: the rest of the chunk is empty
       const bool valid = c0 + 64 * k + lane < c1;
       const uint32_t d = (kr[k] >> shift) & dmask;
       uint64_t peers = __ballot(valid);
@@ -661,8 +672,8 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
       }
     }
     FBR_VG_STAMP(2);
-#ifdef FBR_VG_IP_LEADER  // diagnostic build (tools/gpu_leader.sh): round 3's ballot-leader digit counts
-    vg_radix_sort_inplace<T, KPL, true>(keys, vals, n, G.nbits, hist, wsum);
+#ifdef FBR_VG_IP_LEADER  // diagnostic build: round 3's ballot-leader digit counts (1), or its exact form (2)
+    vg_radix_sort_inplace<T, KPL, FBR_VG_IP_LEADER>(keys, vals, n, G.nbits, hist, wsum);
 #else
     vg_radix_sort_inplace<T, KPL>(keys, vals, n, G.nbits, hist, wsum);
 #endif
@@ -1101,18 +1112,7 @@ k_voxel_ring(VgRing A) {
 #undef VR_TS_PTR
 }
 
-// ---- the per-ring surf filter, one wave per ring (default order) ----
-// The same filter as k_voxel_ring for the index-order sums, without workgroup barriers: one wave
-// owns a (job, ring).  A ring holds ~1.5k candidates in ~230 runs of equal keys (C2), so the
-// 512-thread kernel above spent most of its cycles in barriers and 3-pass radix sorts of a few
-// hundred keys.  Here: pass A (labels + points: min / max and the candidate count), pass B (keys,
-// compacted in index order into LDS), pass C (run heads: run keys in place, run starts), then a
-// register bitonic sort of the (key << 16 | run id) values (run ids are in index order, so equal
-// keys keep it: the stable order), voxel heads by one lane exchange, and one lane per voxel sums
-// the voxel's points in index order.  Rings with more than 512 runs (none on the synthetic C2 / C3 /
-// C5 scans: at most ~460) rank their runs by counting into the ring's output slot (global scratch)
-// instead.  Output bytes are identical to
-// k_voxel_ring's default mode.
+// ---- register helpers of the four-wave per-ring surf filter (k_voxel_ring_q below) ----
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
   const uint32_t lo = __shfl_xor((uint32_t)x, m), hi = __shfl_xor((uint32_t)(x >> 32), m);
   return ((uint64_t)hi << 32) | lo;
@@ -1198,220 +1198,16 @@ __device__ int vr_sort_runs(const uint32_t* kb, int R, uint16_t* sid, uint16_t* 
   return V;
 }
 
-// More than 512 runs: rank by counting (stable by run id), the sorted values staged in the ring's
-// output slot (global; it is written by the emit only after this).
-__device__ int vr_sort_runs_count(const uint32_t* kb, int R, uint16_t* sid, uint16_t* vst, uint64_t* scr, int lane) {
-  for (int r = lane; r < R; r += 64) {
-    const uint32_t key = kb[r];
-    int rank = 0;
-    for (int j = 0; j < R; ++j) {
-      const uint32_t kj = kb[j];
-      rank += (kj < key || (kj == key && j < r)) ? 1 : 0;
-    }
-    scr[rank] = ((uint64_t)key << 16) | (uint64_t)r;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  int V = 0;
-  for (int g0 = 0; g0 < R; g0 += 64) {
-    const int g = g0 + lane;
-    const uint64_t x = g < R ? scr[g] : ~0ull;
-    const uint64_t px = (g > 0 && g < R) ? scr[g - 1] : ~0ull;
-    const bool hd = g < R && (g == 0 || (x >> 16) != (px >> 16));
-    const uint64_t b = __ballot(hd);
-    wave_lds_sync();  // (sid may alias kb entries read above: all reads of kb are done)
-    if (g < R) sid[g] = (uint16_t)(x & 0xFFFFull);
-    if (hd) vst[V + __popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)g;
-    V += __popcll(b);
-  }
-  if (lane == 0) vst[V] = (uint16_t)R;
-  wave_lds_sync();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // scratch reads done before the emit's stores
-  return V;
-}
-
-__global__ void __launch_bounds__(64) k_voxel_ring_wave(VgRing A) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int lane = threadIdx.x;
-  const int slot = blockIdx.x, job = slot / A.H;
-  const int s = A.start_ring[slot], e = A.end_ring[slot];
-  float4* out = A.out + (int64_t)slot * A.stride_out;
-  if (e <= s) {
-    if (lane == 0) A.cnt_out[slot] = 0;
-    return;
-  }
-  int sp6[6], ep6[6];
-  bool all6 = true;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    sp6[j] = (s * (6 - j) + e * j) / 6;
-    ep6[j] = (s * (5 - j) + e * (j + 1)) / 6 - 1;
-    all6 = all6 && sp6[j] < ep6[j];
-  }
-  // candidates: the ring's non-empty segments [sp, ep] (:195-200) with cloudLabel <= 0, which lie
-  // in [s, e - 1] (segment j ends at sp_{j+1} - 1, segment 5 at e - 1)
-  auto in_seg = [&](int k) {
-    if (all6) return k <= ep6[5];
-    bool in = false;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) in |= sp6[j] < ep6[j] && k >= sp6[j] && k <= ep6[j];
-    return in;
-  };
-  const float4* CL = A.cloud + (int64_t)job * A.HW + s;
-  const int8_t* LB = A.label + (int64_t)job * A.HW + s;
-  const int len = min(e - s, (int)A.cap);
-  const uint64_t lt = (1ull << lane) - 1ull;
-  // ---- pass A: min / max of the candidates and their count.  Steps go in groups of kG with
-  // every label and point load of the group issued before the first use (one memory round trip
-  // per group, not per step: a lone wave has no other waves of its ring to hide latency behind) ----
-  constexpr int kG = 8;
-  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-  int n = 0;
-  for (int i0 = 0; i0 < len; i0 += 64 * kG) {
-    int8_t lab[kG];
-    float4 pt[kG];
-#pragma unroll
-    for (int u = 0; u < kG; ++u) {
-      const int i = i0 + 64 * u + lane;
-      const bool ok = i < len;
-      lab[u] = ok ? LB[i] : (int8_t)1;
-      pt[u] = ok ? CL[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < kG; ++u) {
-      const int i = i0 + 64 * u + lane;
-      const bool cd = i < len && lab[u] <= 0 && in_seg(s + i);
-      if (cd) {
-        const float v[3] = {pt[u].x, pt[u].y, pt[u].z};
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          mn[d] = (v[d] < mn[d]) ? v[d] : mn[d];
-          mx[d] = (mx[d] < v[d]) ? v[d] : mx[d];
-        }
-      }
-      n += __popcll(__ballot(cd));
-    }
-  }
-  if (n == 0) {
-    if (lane == 0) A.cnt_out[slot] = 0;
-    return;
-  }
-#pragma unroll
-  for (int d = 0; d < 3; ++d)
-    for (int o = 32; o > 0; o >>= 1) {
-      const float a = __shfl_xor(mn[d], o), b = __shfl_xor(mx[d], o);
-      mn[d] = (a < mn[d]) ? a : mn[d];
-      mx[d] = (mx[d] < b) ? b : mx[d];
-    }
-  VgGrid G;
-  G.init(mn, mx, A.leaf, false);
-  const int cap = (int)A.cap;
-  uint32_t* kb = (uint32_t*)smem;           // [cap + 1] candidate keys, then run keys; then sid / vst (u16)
-  uint16_t* off = (uint16_t*)(kb + cap + 1);  // [cap] ring offset of the t-th candidate
-  uint16_t* rst = off + cap;                // [cap + 1] first candidate of each run
-  // ---- pass B: keys in index order (or, on PCL's overflow, the candidates themselves) ----
-  int base = 0;
-  for (int i0 = 0; i0 < len; i0 += 64 * kG) {
-    int8_t lab[kG];
-    float4 pt[kG];
-#pragma unroll
-    for (int u = 0; u < kG; ++u) {
-      const int i = i0 + 64 * u + lane;
-      const bool ok = i < len;
-      lab[u] = ok ? LB[i] : (int8_t)1;
-      pt[u] = ok ? CL[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < kG; ++u) {
-      const int i = i0 + 64 * u + lane;
-      const bool cd = i < len && lab[u] <= 0 && in_seg(s + i);
-      const uint64_t b = __ballot(cd);
-      const int pos = base + __popcll(b & lt);
-      if (cd) {
-        if (G.overflow) {
-          out[pos] = pt[u];  // PCL: "Leaf size is too small" -> output = input, in index order
-        } else {
-          kb[pos] = G.key(pt[u]);
-          off[pos] = (uint16_t)i;
-        }
-      }
-      base += __popcll(b);
-    }
-  }
-  if (G.overflow) {
-    if (lane == 0) A.cnt_out[slot] = n;
-    return;
-  }
-  wave_lds_sync();
-  // ---- pass C: runs of equal keys in index order (run r's key goes to kb[r] <= its head t: a
-  // later step never reads an overwritten key, and r == t rewrites the same value) ----
-  int R = 0;
-  for (int t0 = 0; t0 < n; t0 += 64) {
-    const int t = t0 + lane;
-    const bool valid = t < n;
-    const uint32_t key = valid ? kb[t] : 0u;
-    const uint32_t prev = (valid && t > 0) ? kb[t - 1] : 0u;
-    const bool head = valid && (t == 0 || key != prev);
-    const uint64_t hb = __ballot(head);
-    wave_lds_sync();
-    if (head) {
-      const int r = R + __popcll(hb & lt);
-      kb[r] = key;
-      rst[r] = (uint16_t)t;
-    }
-    R += __popcll(hb);
-    wave_lds_sync();
-  }
-  if (lane == 0) rst[R] = (uint16_t)n;
-  wave_lds_sync();
-  // ---- sort the runs (stable by run id), voxel starts ----
-  uint16_t* sid = (uint16_t*)kb;  // [R]
-  uint16_t* vst = sid + cap + 1;  // [V + 1]
-  int V;
-  if (R <= 256) V = vr_sort_runs<4>(kb, R, sid, vst, lane);
-  else if (R <= 512) V = vr_sort_runs<8>(kb, R, sid, vst, lane);
-  else V = vr_sort_runs_count(kb, R, sid, vst, reinterpret_cast<uint64_t*>(out), lane);
-  // ---- one lane per voxel: the float sum of its points in index order (runs in id order) ----
-  for (int vv = lane; vv < V; vv += 64) {
-    const int g0 = vst[vv], g1 = vst[vv + 1];
-    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
-    int cnt = 0;
-    for (int g = g0; g < g1; ++g) {
-      const int rid = sid[g];
-      const int t0 = rst[rid], t1 = rst[rid + 1];
-      for (int t = t0; t < t1; t += 8) {  // a run's points, 8 gathers in flight
-        float4 pp[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) pp[u] = CL[off[min(t + u, t1 - 1)]];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (t + u < t1) {
-            if (cnt == 0) {
-              c = pp[u];
-            } else {
-              c.x += pp[u].x;
-              c.y += pp[u].y;
-              c.z += pp[u].z;
-              c.w += pp[u].w;
-            }
-            ++cnt;
-          }
-      }
-    }
-    const float fc = (float)cnt;
-    out[vv] = make_float4(c.x / fc, c.y / fc, c.z / fc, c.w / fc);
-  }
-  if (lane == 0) A.cnt_out[slot] = V;
-}
-
 // ---- the per-ring surf filter, four waves per ring (default order) ----
-// k_voxel_ring_wave's algorithm with the memory round trips of a ring cut to about three: each of
-// the 4 waves loads a quarter of the ring's labels and points in one go (up to 8 steps of 64,
-// kept in registers for the key pass: one load per point), the run keys and starts are
-// compacted with workgroup prefixes, wave 0 sorts the runs in registers (R <= 512; above, the
-// four waves rank them by counting), and every thread sums about one voxel.  The one-wave kernel
-// needed 2.3x fewer VALU instructions than the 512-thread kernel (profiles/r04j_valu_*) but sat
-// on ~14 dependent round trips per ring (VALU-busy 0.26 alone, slower overall).
+// The same filter as k_voxel_ring for the index-order sums with a ring's memory round trips cut to
+// about three: each of the 4 waves loads a quarter of the ring's labels and points in one go (up
+// to 8 steps of 64, kept in registers for the key pass: one load per point), the run keys and
+// starts are compacted with workgroup prefixes, wave 0 sorts the (key << 16 | run id) values in
+// registers (R <= 512; run ids are in index order, so equal keys keep it: the stable order; above,
+// the four waves rank them by counting), and every thread sums about one voxel in index order.  A
+// ring holds ~1.5k candidates in ~230 runs of equal keys (C2).  (Round 4 also measured one wave
+// per ring: 2.3x fewer VALU instructions than the 512-thread kernel but ~14 dependent round trips
+// per ring, slower overall; removed in round 5.)
 template <int KQ>  // steps of 64 points per wave: 4 * 64 * KQ >= the ring capacity
 __global__ void __launch_bounds__(256) k_voxel_ring_q(VgRing A) {
   constexpr int NW = 4;
@@ -1646,20 +1442,10 @@ __global__ void __launch_bounds__(256) k_voxel_ring_q(VgRing A) {
   if (tid == 0) A.cnt_out[slot] = V;
 }
 
-// The per-ring filter of the default order (FBR_VR_WAVE): 0 = the 512-thread kernel, 1 = one
-// wave per ring (2.3x fewer VALU instructions but latency-bound: 481 vs 407 us per sequential
-// 256-job launch, profiles/r04e_voxel_ring_wave_ab.txt, r04j_valu_*), 2 = four waves per ring.
-// FBR_VR_WAVE: 0 the 512-thread kernel, 1 one wave per ring, 2 four waves per ring; unset: four
-// waves per ring, except launches of at most 256 rings (single scans), where the 512-thread kernel
-// finishes a ring sooner (C2 single scan: 19.8 vs 34.3 us, profiles/r04u_latency_scan_timeline.txt)
-// and the chip has room for the extra threads.
-int vr_mode(int nseg) {
-  static const int v = [] {
-    const char* e = std::getenv("FBR_VR_WAVE");
-    return e ? std::atoi(e) : -1;
-  }();
-  return v >= 0 ? v : (nseg <= 256 ? 0 : 2);
-}
+// The per-ring filter of the default order: four waves per ring, except launches of at most 256
+// rings (single scans), where the 512-thread kernel finishes a ring sooner (C2 single scan: 19.8 vs
+// 34.3 us, profiles/r04u_latency_scan_timeline.txt) and the chip has room for the extra threads.
+bool vr_four_waves(int nseg) { return nseg > 256; }
 
 size_t voxel_ring_lds_bytes(const VgRing& a, int threads, int kpt) {
   const int nw = threads / 64;
@@ -1685,24 +1471,13 @@ void launch_voxel_ring(hipStream_t s, const VgRing& a) {
   };
   if (a.exact) {
     go(std::true_type{});
-  } else if (vr_mode(nseg) != 0 && a.dbg == 0 && a.cap <= 4096) {
+  } else if ((a.kernel < 0 ? vr_four_waves(nseg) : a.kernel == 2) && a.dbg == 0 && a.cap <= 4096) {
     const size_t lds = (((size_t)a.cap + 1) * 4 + (size_t)a.cap * 2 + ((size_t)a.cap + 1) * 2 + 15) & ~(size_t)15;
-    if (vr_mode(nseg) == 1) fbr_launch(k_voxel_ring_wave, dim3(nseg), dim3(64), lds, s, a);
-    else if (a.cap <= 4 * 64 * 8) fbr_launch(k_voxel_ring_q<8>, dim3(nseg), dim3(256), lds, s, a);
+    if (a.cap <= 4 * 64 * 8) fbr_launch(k_voxel_ring_q<8>, dim3(nseg), dim3(256), lds, s, a);
     else fbr_launch(k_voxel_ring_q<16>, dim3(nseg), dim3(256), lds, s, a);
   } else {
     go(std::false_type{});
   }
-}
-
-// PCL's point order inside voxels (FBR_VG_EXACT=1): bit-identical centroids, hence poses, at
-// about half the batch throughput; off by default.
-bool vg_exact() {
-  static const bool v = [] {
-    const char* e = std::getenv("FBR_VG_EXACT");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
 }
 
 // In-place LDS sort of the mapping-DS segments (FBR_VG_INPLACE=0: the global-scratch kernel).
@@ -1746,7 +1521,7 @@ void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
   int64_t cap = 0;
   for (int k = 0; k < 2; ++k)
     if (a.s[k].nseg > 0) cap = std::max<int64_t>(cap, a.s[k].cap);
-  const bool exact = a.s[0].exact || a.s[1].exact;  // both sets share vg_exact()
+  const bool exact = a.s[0].exact || a.s[1].exact;  // both sets share the context's mode
   // few segments (single-scan calls): P workgroups per segment (FBR_VG_SPLIT = P, default 4; 1 off)
   const int P = vg_split();
   if (!exact && P > 1 && cap > kVgLdsCap && vg_inplace() && nseg * P <= kVgSplitSlots) {
@@ -1881,7 +1656,8 @@ void launch_concat(hipStream_t s, int B, int H, int W, const float4* corner_slot
 // product's configurations of the wave-chunk sorts ----
 // variant 0: vg_radix_sort<512, u16, 8, LDS> (per-ring filter), 1: vg_radix_sort<256, u16, 9, LDS>
 // (per-segment LDS kernel), 2: vg_radix_sort<1024, u32, 9, global> (global-scratch kernel),
-// 3: vg_radix_sort_inplace<1024, 18> (mapping DS), 4: the same with ballot-leader digit counts.
+// 3: vg_radix_sort_inplace<1024, 18> (mapping DS), 4: the same with ballot-leader digit counts,
+// 5: round 3's rejected form (ballot-leader counts + wave-uniform early exits).
 template <int T, typename V, int MAXD, bool KV_LDS>
 __global__ void __launch_bounds__(T) k_selftest_radix(uint32_t* keys, uint32_t* vals, uint32_t* scratch, int n, int nbits) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1915,7 +1691,7 @@ __global__ void __launch_bounds__(T) k_selftest_radix(uint32_t* keys, uint32_t* 
   }
 }
 
-template <bool kLeader>
+template <int kLeader>
 __global__ void __launch_bounds__(1024) k_selftest_radix_ip(uint32_t* keys, uint32_t* vals, int n, int nbits) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NW = 16, LCAP = 1024 * kVgIpKpl;
@@ -1944,8 +1720,8 @@ __global__ void __launch_bounds__(1024) k_selftest_radix_ip(uint32_t* keys, uint
 // each sorted position.
 extern "C" int fbr_selftest_radix_sort(int64_t n, int nbits, int variant, uint32_t* keys_inout, uint32_t* perm) {
   using namespace fbr;
-  const int64_t lcap[5] = {4096, 4096, 1 << 20, 1024 * kVgIpKpl, 1024 * kVgIpKpl};
-  if (n < 0 || variant < 0 || variant > 4 || n > lcap[variant] || nbits < 1 || nbits > 32 || (n && (!keys_inout || !perm)))
+  const int64_t lcap[6] = {4096, 4096, 1 << 20, 1024 * kVgIpKpl, 1024 * kVgIpKpl, 1024 * kVgIpKpl};
+  if (n < 0 || variant < 0 || variant > 5 || n > lcap[variant] || nbits < 1 || nbits > 32 || (n && (!keys_inout || !perm)))
     return FBR_ERR_INVALID_ARG;
   if (n == 0) return FBR_OK;
   uint32_t *dk = nullptr, *dv = nullptr, *ds = nullptr;
@@ -1971,8 +1747,9 @@ extern "C" int fbr_selftest_radix_sort(int64_t n, int nbits, int variant, uint32
         break;
       default: {
         const size_t lds = hdr(1024) + (size_t)1024 * kVgIpKpl * 6;
-        if (variant == 3) hipLaunchKernelGGL(k_selftest_radix_ip<false>, dim3(1), dim3(1024), lds, 0, dk, dv, nn, nbits);
-        else hipLaunchKernelGGL(k_selftest_radix_ip<true>, dim3(1), dim3(1024), lds, 0, dk, dv, nn, nbits);
+        if (variant == 3) hipLaunchKernelGGL(k_selftest_radix_ip<0>, dim3(1), dim3(1024), lds, 0, dk, dv, nn, nbits);
+        else if (variant == 4) hipLaunchKernelGGL(k_selftest_radix_ip<1>, dim3(1), dim3(1024), lds, 0, dk, dv, nn, nbits);
+        else hipLaunchKernelGGL(k_selftest_radix_ip<2>, dim3(1), dim3(1024), lds, 0, dk, dv, nn, nbits);
       }
     }
     if (hipGetLastError() != hipSuccess || hipMemcpy(keys_inout, dk, 4 * n, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -2098,8 +1875,8 @@ k_vgl_emit(const float4* __restrict__ in, int64_t n, const VglState* __restrict_
   }
 }
 
-int voxel_grid_large(hipStream_t s, DevArena& ar, const float4* in, int64_t n, float leaf, int morton, float4* out,
-                     int32_t* d_nout) {
+int voxel_grid_large(hipStream_t s, DevArena& ar, const float4* in, int64_t n, float leaf, int morton, int exact,
+                     float4* out, int32_t* d_nout) {
   if (n <= 0) return hipMemsetAsync(d_nout, 0, sizeof(int32_t), s) == hipSuccess ? FBR_OK : FBR_ERR_HIP;
   if (n > (int64_t)INT32_MAX) return FBR_ERR_CAPACITY;
   const size_t N = (size_t)n;
@@ -2132,7 +1909,6 @@ int voxel_grid_large(hipStream_t s, DevArena& ar, const float4* in, int64_t n, f
   if (ok(hipMemsetD32Async((hipDeviceptr_t)mm, 0xFFFFFFFFu, 3, s)) && ok(hipMemsetD32Async((hipDeviceptr_t)(mm + 3), 0u, 3, s))) {
     fbr_launch(k_vgl_minmax, dim3(grid), dim3(256), 0, s, in, n, mm);
     fbr_launch(k_vgl_grid, dim3(1), dim3(1), 0, s, mm, leaf, morton, st);
-    const int exact = vg_exact() ? 1 : 0;
     fbr_launch(k_vgl_keys, dim3(grid), dim3(256), 0, s, in, n, st, exact, k0, v0);
     if (exact) {  // scratch: head / vox (positions) and k1 / v1 (frame lists), all free until the sort
       fbr_launch(k_vgl_isort, dim3(1), dim3(1024), 0, s, k0, v0, (int32_t*)head, (int32_t*)vox, (int*)k1, (int*)v1,

@@ -80,7 +80,9 @@ class FbrParams(ctypes.Structure):
         ("max_iterations", ctypes.c_int32),
         ("max_points_per_scan", ctypes.c_int32),
         ("max_batch", ctypes.c_int32),
-        ("reserved_", ctypes.c_int32 * 4),
+        ("exact_voxel_order", ctypes.c_int32),
+        ("pipeline_depth", ctypes.c_int32),
+        ("reserved_", ctypes.c_int32 * 2),
     ]
 
 

@@ -27,7 +27,8 @@
 extern "C" {
 #endif
 
-#define FBR_ABI_VERSION 2  /* 2: fbr_selftest_math writes 6 floats per element (was 4) */
+#define FBR_ABI_VERSION 3  /* 3: fbr_params.exact_voxel_order / pipeline_depth (were reserved_[0..1]);
+                              2: fbr_selftest_math writes 6 floats per element (was 4) */
 
 /* ---- status codes ------------------------------------------------------------------------- */
 #define FBR_OK 0
@@ -84,7 +85,14 @@ typedef struct fbr_params {
   int32_t max_iterations;            /* 30 Gauss-Newton iterations   mapOptmization.h:1417 */
   int32_t max_points_per_scan;       /* device capacity: raw points per scan               */
   int32_t max_batch;                 /* device capacity: scans per device batch            */
-  int32_t reserved_[4];
+  int32_t exact_voxel_order;         /* 0: every VoxelGrid sums a voxel's points in index order
+                                        (centroids to float rounding, the fast default); 1: in
+                                        std::sort's order, as PCL does (bit-identical centroids and
+                                        poses vs the oracle, ~0.45x the batch throughput)        */
+  int32_t pipeline_depth;            /* batch launch slots 1..3 (0 = default 3; forced to 1 when
+                                        max_batch = 1): launch n's front end overlaps the
+                                        Gauss-Newton tails of up to depth-1 launches before it    */
+  int32_t reserved_[2];
 } fbr_params;
 
 /* Per-scan registration statistics. */
@@ -384,6 +392,32 @@ int fbr_batch_export(fbr_ctx* ctx, void* device_dst);
  * launch number (0, 1, ... since the context was created), or -1 (nothing to export: no copy). */
 int fbr_batch_export_ready(fbr_ctx* ctx, void* device_dst, void* wait_stream, void** export_stream,
                            int64_t* launch_id);
+/* ---- multi-GPU pose gather ---------------------------------------------------
+ * Scans shard across the GPUs of a node: one process (and one ctx) per GPU, each registering its
+ * own contiguous block of jobs against its replica of the map; nothing is exchanged on the data
+ * path.  The only collective is the all-gather of the 32-B pose records {pose[6] f32, iterations
+ * i32, status i32} over RCCL (xGMI), after each launch.  librccl is loaded on the first call
+ * (FBR_ERR_UNSUPPORTED if it cannot be); a one-GPU host never needs it.
+ *   rank 0:     fbr_comm_unique_id(id), then hands id to the other ranks (any out-of-band channel);
+ *   every rank: fbr_comm_create(&comm, ctx, id, nranks, rank, max_jobs_per_rank)  (blocks until
+ *               all ranks joined), then per launch fbr_batch_allgather(ctx, comm, launch_id, recv,
+ *               &stream) with the same launch_id on every rank. */
+#define FBR_COMM_ID_BYTES 128
+typedef struct fbr_comm fbr_comm;
+int fbr_comm_unique_id(uint8_t id_out[FBR_COMM_ID_BYTES]);
+int fbr_comm_create(fbr_comm** out, fbr_ctx* ctx, const uint8_t id[FBR_COMM_ID_BYTES], int nranks, int rank,
+                    int max_jobs_per_rank);
+int fbr_comm_destroy(fbr_comm* comm);
+/* Collective (every rank, same launch_id; -1 = the latest launch): the records of that launch of
+ * every rank into recv = [nranks][max_jobs_per_rank][8] x 4 B (device memory of the ctx's device;
+ * rank r's block holds its staged jobs in order, then zero records).  Records follow
+ * fbr_batch_results (a job over the feature capacity: its guess, FBR_REG_FEATURE_CAPACITY).  The
+ * launch is first enqueued to its end (the host follows its GN flags); the export and the
+ * all-gather then run on that launch's stream, returned in *done_stream (wait on it before reading
+ * recv), or, with done_stream NULL, joined into the ctx stream.  The launch must still own its work
+ * slot (one of the last FBR_PIPE launches of the staged batch): FBR_ERR_STATE otherwise. */
+int fbr_batch_allgather(fbr_ctx* ctx, fbr_comm* comm, int64_t launch_id, void* recv, void** done_stream);
+
 /* Sum of the per-scan algorithmic byte counts of the last completed batch (roofline input). */
 int fbr_batch_bytes(fbr_ctx* ctx, double* bytes_total, double* bytes_gn);
 
@@ -425,7 +459,8 @@ int fbr_selftest_voxel_order(int64_t n, const uint32_t* keys, int lds, uint32_t*
  * `nbits` significant), one workgroup: variant 0 = the per-ring filter's LDS sort (512 threads,
  * 8-bit digits, n <= 4096), 1 = the per-segment LDS sort (256 threads, 9-bit digits, n <= 4096),
  * 2 = the global-scratch sort (1024 threads), 3 = the mapping DS's in-place LDS sort (1024 x 18),
- * 4 = variant 3 with ballot-leader digit counts (round 3's rejected form).  keys_inout receives
+ * 4 = variant 3 with ballot-leader digit counts, 5 = variant 4 with round 3's wave-uniform early
+ * exits in its count and scatter loops (the exact form round 3 reverted).  keys_inout receives
  * the sorted keys, perm the source index of every sorted position. */
 int fbr_selftest_radix_sort(int64_t n, int nbits, int variant, uint32_t* keys_inout, uint32_t* perm);
 

@@ -55,6 +55,26 @@ def probe_lib():
     return build_probe("host_probe")
 
 
+def build_shard_demo():
+    """Compile tests/native/shard_demo.cpp (a native host sharding a C4 batch over processes, the
+    pose records all-gathered over RCCL through the C-ABI) with the host compiler against
+    libfbr_hip.so and the HIP runtime (device memory for the gathered records)."""
+    from feature_base_pointcloud_registration_amd import api
+    src = os.path.join(NATIVE, "shard_demo.cpp")
+    out_dir = os.path.join(NATIVE, "build")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, "shard_demo")
+    lib = api.lib_path()
+    deps = [src, lib, os.path.join(REPO, "include", "fbr.h")]
+    if not os.path.exists(out) or any(os.path.getmtime(d) > os.path.getmtime(out) for d in deps):
+        libdir = os.path.dirname(lib)
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include",
+                               "-I", os.path.join(REPO, "include"), "-o", out, src, "-L", libdir,
+                               "-l:" + os.path.basename(lib), "-L/opt/rocm/lib", "-lamdhip64",
+                               "-Wl,-rpath," + libdir, "-Wl,-rpath,/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib"])
+    return out
+
+
 def has_gpu():
     try:
         from feature_base_pointcloud_registration_amd import api

@@ -89,7 +89,7 @@ from feature_base_pointcloud_registration_amd import api, shard, synth
 from feature_base_pointcloud_registration_amd.fbr_types import default_params
 H, W = synth.CONFIGS["C2"][:2]
 B = 24
-P = default_params(H, W, max_batch=B)
+P = default_params(H, W, max_batch=B, pipeline_depth=%(pipe)d)
 jobs = synth.make_jobs("C2", B, base_seed=6000)
 buf = torch.zeros((4, B * shard.RECORD_FLOATS), dtype=torch.float32, device="cuda:0")
 with api.Context(P) as ctx:
@@ -115,29 +115,65 @@ with api.Context(P) as ctx:
     again = ctx.batch_export_ready(buf[3].data_ptr())[0]
     ctx.batch_wait()
     p1, s1 = ctx.batch_results()
+    # re-stage a different, smaller batch with job 5 over the feature capacity (diagnostic hook): the
+    # launches of the old batch are never handed out again, and the new launch's exported records
+    # carry what fbr_batch_results reports for every job (the capacity job: its guess, status 3)
+    torch.cuda.synchronize()
+    ex0 = [buf[k].cpu().numpy().copy() for k in range(4)]
+    jobs2 = synth.make_jobs("C2", 16, base_seed=7000)
+    g2 = np.stack([j[1] for j in jobs2]).astype(np.float32)
+    ctx.diag_force_capacity_error(5)
+    ctx.batch_stage([j[0] for j in jobs2], g2)
+    buf.zero_()
+    ctx.batch_launch()
+    ids2 = []
+    while True:
+        lid = ctx.batch_export_ready(buf[0].data_ptr())[0]
+        if lid < 0:
+            break
+        ids2.append(lid)
+    ctx.batch_flush()
+    while True:
+        lid = ctx.batch_export_ready(buf[0].data_ptr())[0]
+        if lid < 0:
+            break
+        ids2.append(lid)
+    ctx.batch_wait()
+    p2, s2 = ctx.batch_results()
+    ctx.diag_force_capacity_error(-1)
 torch.cuda.synchronize()
 rec0 = shard.encode_records(p0, s0["iterations"], s0["status"])
-print(json.dumps({"ids": ids, "again": again,
+rec2 = shard.encode_records(p2, s2["iterations"], s2["status"])
+print(json.dumps({"ids": ids, "again": again, "ids_restaged": ids2,
                   "same_results": bool(np.array_equal(p0.view(np.int32), p1.view(np.int32)) and np.array_equal(s0, s1)),
-                  "exports_equal": [bool(np.array_equal(buf[k].cpu().numpy().view(np.int32), rec0.view(np.int32))) for k in range(4)],
-                  "status_ok": int((s0["status"] == 0).sum())}))
+                  "exports_equal": [bool(np.array_equal(ex0[k].view(np.int32), rec0.view(np.int32))) for k in range(4)],
+                  "status_ok": int((s0["status"] == 0).sum()),
+                  "restaged_export_equal": bool(np.array_equal(buf[0, :16 * shard.RECORD_FLOATS].cpu().numpy().view(np.int32),
+                                                               rec2.view(np.int32))),
+                  "cap_status": int(s2["status"][5]), "cap_pose_is_guess": bool(np.array_equal(p2[5], g2[5])),
+                  "others_ok": int((np.delete(s2["status"], 5) == 0).sum())}))
 """
 
 
-@pytest.mark.parametrize("pipe", ["2", "3"])
+@pytest.mark.parametrize("pipe", [2, 3])
 def test_pipelined_launches_are_bit_identical_and_export_in_order(pipe):
-    """Consecutive fbr_batch_launch calls run FBR_PIPE deep (rotating work slots and streams; a
+    """Consecutive fbr_batch_launch calls run fbr_params.pipeline_depth deep (rotating work slots and streams; a
     launch returns once the launch pipe - 1 before it is fully enqueued).  Every launch of the same
     staged batch gives the same bytes, and fbr_batch_export_ready hands out every launch's records
-    once, in launch order (-1 while the oldest unexported launch is still being enqueued).
+    once, in launch order (-1 while the oldest unexported launch is still being enqueued).  After a
+    re-stage only the new batch's launch is handed out, and its records report a job over the
+    feature capacity as fbr_batch_results does (guess + FBR_REG_FEATURE_CAPACITY).
     (Child process: torch, which allocates the export buffers, must initialise HIP first.)"""
     import json
     import subprocess
     import sys
     from conftest import REPO
-    r = subprocess.run([sys.executable, "-c", _PIPE_CHILD % {"repo": REPO}], capture_output=True, text=True,
-                       timeout=300, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", FBR_PIPE=pipe))
+    r = subprocess.run([sys.executable, "-c", _PIPE_CHILD % {"repo": REPO, "pipe": pipe}], capture_output=True,
+                       text=True, timeout=300, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["ids"] == [0, 1, 2, 3] and d["again"] == -1, d
     assert d["same_results"] and d["exports_equal"] == [True] * 4 and d["status_ok"] == 24, d
+    # after a re-stage only the new launch is exported, once, with the capacity rule applied
+    assert d["ids_restaged"] == [4], d
+    assert d["restaged_export_equal"] and d["cap_status"] == 3 and d["cap_pose_is_guess"] and d["others_ok"] == 15, d

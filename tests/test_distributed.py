@@ -132,3 +132,71 @@ def test_bench_rccl_path_one_rank(tmp_path):
     res = json.loads(line)
     assert res["n_gpus"] == 1 and res["value"] > 0 and res["registration_status_ok"] == 16
     assert res["records_check"] == {"jobs": 16, "mismatched_words": 0}
+
+
+# ------------------------------------------------------------------ native RCCL path (no torch)
+def _write_shard_input(path, H, W, cmap, smap, jobs):
+    import struct
+    with open(path, "wb") as f:
+        f.write(struct.pack("<iiiqq", H, W, len(jobs), len(cmap), len(smap)))
+        f.write(np.ascontiguousarray(cmap).tobytes())
+        f.write(np.ascontiguousarray(smap).tobytes())
+        for pts, guess, _ in jobs:
+            f.write(np.asarray(guess, np.float32).tobytes())
+            f.write(struct.pack("<q", len(pts)))
+            f.write(np.ascontiguousarray(pts).tobytes())
+
+
+def test_native_shard_demo_builds_and_reports_no_device(tmp_path):
+    """CPU: the native sharding host (tests/native/shard_demo.cpp: fork one process per rank, fbr_comm_*
+    + fbr_batch_allgather over RCCL) builds against the C-ABI; without a GPU fbr_create fails in the
+    rank process and the demo exits 3."""
+    import subprocess
+    from conftest import build_shard_demo, has_gpu
+    from feature_base_pointcloud_registration_amd import synth
+    if has_gpu():
+        pytest.skip("a GPU is visible")
+    exe = build_shard_demo()
+    H, W = 16, 1800
+    inp = tmp_path / "in.bin"
+    _write_shard_input(inp, H, W, *synth.config_map("C1"), synth.make_jobs("C1", 2, base_seed=90))
+    r = subprocess.run([exe, str(inp), str(tmp_path / "out.bin"), "--ranks", "2"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 3, (r.returncode, r.stderr)
+    assert "fbr_create" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_native_rccl_allgather_world1_matches_batch_results(tmp_path):
+    """GPU, world 1 (RCCL refuses two ranks on one device, and the box has one): the native host
+    stages a C2 batch, runs three pipelined launches and all-gathers each launch's records through
+    fbr_comm_create / fbr_batch_allgather; the gathered records equal the rank's fbr_batch_results
+    (checked inside the demo, exit 4 otherwise) and an in-process run of the same jobs, bit for
+    bit, and a job over the feature capacity is not involved (every status 0)."""
+    import subprocess
+    from conftest import build_shard_demo
+    from feature_base_pointcloud_registration_amd import api, shard, synth
+    from feature_base_pointcloud_registration_amd.fbr_types import default_params
+    exe = build_shard_demo()
+    H, W = synth.CONFIGS["C2"][:2]
+    cmap, smap = synth.config_map("C2")
+    jobs = synth.make_jobs("C2", 12, base_seed=4100)
+    inp, out = tmp_path / "in.bin", tmp_path / "out.bin"
+    _write_shard_input(inp, H, W, cmap, smap, jobs)
+    r = subprocess.run([exe, str(inp), str(out), "--ranks", "1", "--launches", "3"], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+    rec = np.fromfile(out, np.float32)
+    assert rec.shape == (12 * shard.RECORD_FLOATS,)
+    P = default_params(H, W, max_batch=12, max_points_per_scan=max(len(j[0]) for j in jobs))
+    with api.Context(P) as ctx:
+        ctx.set_map(cmap, smap)
+        ctx.batch_stage([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
+        ctx.batch_launch()
+        ctx.batch_wait()
+        p, s = ctx.batch_results()
+    mine = shard.encode_records(p, s["iterations"], s["status"])
+    assert np.array_equal(rec.view(np.int32), mine.view(np.int32))
+    _, iters, status = shard.decode_records(rec)
+    assert (status == 0).all() and (iters > 0).all()

@@ -360,6 +360,34 @@ def test_batch_matches_single_and_oracle(c2_map):
         assert_pose_close(poses[k], po)
 
 
+def test_process_batch_drops_out_of_range_rings_like_staged_path(c2_map):
+    """fbr_process_batch packs rings as u8 for sensors of < 256 rings: a ring >= N_SCAN (256, 260,
+    65535 ...) must still be dropped (imageProjection.cpp:599), not wrap into a valid row.  The
+    compact-ingest results equal fbr_batch_stage's 24-byte path bit for bit."""
+    H, W = synth.CONFIGS["C2"][:2]
+    P = default_params(H, W, max_batch=4)
+    jobs = synth.make_jobs("C2", 4, base_seed=80)
+    scans = []
+    rng = np.random.default_rng(80)
+    for pts, _, _ in jobs:
+        pts = pts.copy()
+        idx = rng.choice(len(pts), 4000, replace=False)
+        pts["ring"][idx] = rng.choice(np.array([H, 255, 256, 260, 300, 511, 65535], np.uint16), len(idx))
+        scans.append(pts)
+    guesses = np.stack([j[1] for j in jobs])
+    with api.Context(P) as ctx:
+        ctx.set_map(*c2_map)
+        pb, sb = ctx.process_batch(scans, guesses)
+        ctx.batch_stage(scans, guesses)
+        ctx.batch_launch()
+        ctx.batch_wait()
+        ps, ss = ctx.batch_results()
+    assert np.array_equal(pb.view(np.int32), ps.view(np.int32))
+    assert np.array_equal(sb, ss)
+    assert (sb["status"] == 0).all()
+    assert (sb["n_points"] < np.array([len(s) for s in scans]) - 3000).all()  # the 4000 are gone
+
+
 def test_batch_tail_mode_matches_oracle(c2_map):
     """24 jobs = 3 sub-batches of 8: each sub-batch's last iterating job runs its final Gauss-Newton
     iterations in tail mode (fused kNN + residual launch, fbr_api.hip gn_tail_div); every pose and
@@ -428,8 +456,16 @@ def _cfg_batch_in_child(cfg, scans, guesses, env, tile_stats=False):
     return poses, np.frombuffer(r.stdout[n * 24:], REG_STATS)
 
 
+def _cfg_batch_exact(cfg, scans, guesses):
+    """Poses and stats of a batch of `cfg` scans on a context with exact_voxel_order = 1 (PCL's point
+    order inside voxels), in this process."""
+    with api.Context(synth.config_params(cfg, max_batch=len(scans), exact_voxel_order=1)) as c:
+        c.set_map(*synth.config_map(cfg))
+        return c.process_batch(scans, np.asarray(guesses, np.float32))
+
+
 def assert_exact_order_bitwise(pose, stats, po, so):
-    """FBR_VG_EXACT=1 run against the oracle: the same correspondence count in the final
+    """exact_voxel_order = 1 run against the oracle: the same correspondence count in the final
     iteration, the same iterations and the pose's bits."""
     assert (int(stats["iterations"]), int(stats["n_sel"]), int(stats["status"])) == (so["iterations"], so["n_sel"], so["status"])
     assert np.array_equal(np.asarray(pose, np.float32).view(np.uint32), np.asarray(po, np.float32).view(np.uint32)), (pose, po)
@@ -444,8 +480,8 @@ def test_c3_ouster_registration_matches_oracle():
     with api.Context(P) as ctx:
         ctx.set_map(cmap, smap)
         poses, stats = ctx.process_batch([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
-    # the same jobs with PCL's in-voxel point order (FBR_VG_EXACT=1): bit-identical to the oracle
-    pe, se = _cfg_batch_in_child("C3", [j[0] for j in jobs], np.stack([j[1] for j in jobs]), {"FBR_VG_EXACT": "1"})
+    # the same jobs with PCL's in-voxel point order (exact_voxel_order = 1): bit-identical to the oracle
+    pe, se = _cfg_batch_exact("C3", [j[0] for j in jobs], np.stack([j[1] for j in jobs]))
     for k, (pts, guess, gt) in enumerate(jobs):
         po, so = O.Stream(P).process_scan(m, pts, 0.0, guess, n_threads=8)
         assert stats["status"][k] == so["status"] == 0 and stats["iterations"][k] == so["iterations"]
@@ -501,9 +537,9 @@ def test_c5_dense_scan_matches_oracle():
     assert sg["n_corner_map"] + sg["n_surf_map"] > 5000000
     assert_pose_close(pg, po)
     assert np.abs(pg[3:] - gt[3:]).max() < 0.05
-    # PCL's in-voxel point order (FBR_VG_EXACT=1, child process): the dense scan's feature clouds
-    # take the global-scratch VoxelGrid, and the pose and correspondence count equal the oracle's
-    pe, se = _cfg_batch_in_child("C5", [pts], np.asarray(guess, np.float32)[None], {"FBR_VG_EXACT": "1"})
+    # PCL's in-voxel point order (exact_voxel_order = 1): the dense scan's feature clouds take the
+    # global-scratch VoxelGrid, and the pose and correspondence count equal the oracle's
+    pe, se = _cfg_batch_exact("C5", [pts], np.asarray(guess, np.float32)[None])
     assert_exact_order_bitwise(pe[0], se[0], po, so)
 
 
@@ -686,26 +722,41 @@ def test_sparse_grid_registration_is_bit_identical_to_dense(c2_map):
 
 
 def test_exact_voxel_order_gives_bit_identical_poses(c2_map):
-    """FBR_VG_EXACT=1 (child process): every VoxelGrid sums a voxel's points in std::sort's order
+    """exact_voxel_order = 1: every VoxelGrid sums a voxel's points in std::sort's order
     (csrc/fbr_introsort.h), so the per-ring, mapping-DS and start-up map centroids are PCL's bit for
     bit, and the registered poses equal the oracle's (the reference algorithm with the host's
-    libstdc++ std::sort) exactly, not just within POSE_TOL."""
+    libstdc++ std::sort) exactly, not just within POSE_TOL.  The mode is per context: an exact and a
+    default context live side by side in this process, their launches interleaved, and the default
+    one returns what a default context alone returns."""
     jobs = synth.make_jobs("C2", 8, base_seed=620)
-    out = _c2_batch_in_child(jobs, {"FBR_VG_EXACT": "1"}, False)
-    poses = np.frombuffer(out[:8 * 6 * 4], np.float32).reshape(8, 6)
     H, W = synth.CONFIGS["C2"][:2]
+    scans, guesses = [j[0] for j in jobs], np.stack([j[1] for j in jobs])
+    with api.Context(default_params(H, W, max_batch=8, exact_voxel_order=1)) as ce, \
+            api.Context(default_params(H, W, max_batch=8)) as cd:
+        ce.set_map(*c2_map)
+        cd.set_map(*c2_map)
+        ce.batch_stage(scans, guesses)
+        cd.batch_stage(scans, guesses)
+        ce.batch_launch()
+        cd.batch_launch()
+        ce.batch_wait()
+        cd.batch_wait()
+        poses, _ = ce.batch_results()
+        pd, sd = cd.batch_results()
+    assert pd.tobytes() + sd.tobytes() == _c2_batch_here(c2_map, jobs)
     P = default_params(H, W)
     m = O.Map(P, *c2_map)
     for k, (pts, guess, _) in enumerate(jobs):
         po, so = O.Stream(P).process_scan(m, pts, 0.0, guess, n_threads=8)
         assert np.array_equal(poses[k].view(np.uint32), np.asarray(po, np.float32).view(np.uint32)), (k, poses[k], po)
+        assert_pose_close(pd[k], po)
+    # the index-order centroids differ in their last bits, so the default poses are not all PCL's
+    assert not np.array_equal(pd.view(np.uint32), poses.view(np.uint32))
 
 
 def test_exact_voxel_grid_is_bit_identical_to_oracle():
-    """fbr_voxel_grid with FBR_VG_EXACT=1 (child process) returns PCL's centroids bit for bit on
+    """fbr_voxel_grid on an exact_voxel_order = 1 context returns PCL's centroids bit for bit on
     every kernel path: in-LDS, global scratch and device-wide clouds."""
-    import subprocess
-    import sys
     rng = np.random.default_rng(23)
     clouds = {}
     for n in (3000, 18432, 18433, 40000):
@@ -714,17 +765,9 @@ def test_exact_voxel_grid_is_bit_identical_to_oracle():
         pts["z"] = rng.normal(0, 0.4, n) + (rng.random(n) < 0.3) * rng.uniform(0, 6, n)
         pts["intensity"] = rng.uniform(0, 255, n)
         clouds[n] = pts
-    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_vg_exact_in.npz")
-    np.savez(path, **{str(n): p for n, p in clouds.items()})
-    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api; "
-            "from feature_base_pointcloud_registration_amd.fbr_types import default_params; "
-            "c = api.Context(default_params(16, 900)); d = np.load(%r); "
-            "sys.stdout.buffer.write(b''.join(c.voxel_grid(d[k], 0.4).tobytes() for k in %r))"
-            % (REPO, path, [str(n) for n in clouds]))
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, FBR_VG_EXACT="1"),
-                       timeout=120)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert r.stdout == b"".join(O.voxel_grid(p, 0.4).tobytes() for p in clouds.values())
+    with api.Context(default_params(16, 900, exact_voxel_order=1)) as c:
+        got = b"".join(c.voxel_grid(p, 0.4).tobytes() for p in clouds.values())
+    assert got == b"".join(O.voxel_grid(p, 0.4).tobytes() for p in clouds.values())
 
 
 def _adversarial_ring_scan(H, W, seed):
@@ -756,43 +799,25 @@ def _adversarial_ring_scan(H, W, seed):
     return np.concatenate(pts)
 
 
-@pytest.mark.parametrize("mode", ["2", "1"], ids=["four-waves", "one-wave"])
-def test_wave_ring_filter_is_bit_identical_to_workgroup_kernel(mode):
+def test_wave_ring_filter_is_bit_identical_to_workgroup_kernel():
     """The per-ring surf VoxelGrid kernels: the four-waves-per-ring kernel (k_voxel_ring_q, register
-    bitonic / counting-rank run sorts; FBR_VR_WAVE=2, the batch default) and the one-wave kernel
-    (FBR_VR_WAVE=1), each in a child process, against the 512-thread kernel (the default for single
-    scans, in process): identical surf clouds, labels and corners on C1 / C2 / C3 scans and on
-    adversarial rings (every candidate its own voxel), and within SURF_ULPS of the oracle."""
-    import subprocess
-    import sys
+    bitonic / counting-rank run sorts; the default above 256 rings, i.e. batches) forced on a
+    single-scan context (fbr_diag_ring_filter) against the 512-thread kernel (the single-scan
+    default): identical surf clouds, labels and corners on C1 / C2 / C3 scans and on adversarial
+    rings (every candidate its own voxel), and within SURF_ULPS of the oracle."""
     cases = [("C1", synth.scan(synth.job(1)[0], 16, 1800, seed=1)),
              ("C2", synth.make_jobs("C2", 1, base_seed=77)[0][0]),
              ("C3", synth.make_jobs("C3", 1, base_seed=78)[0][0]),
              ("C1", _adversarial_ring_scan(16, 1800, 5))]
-    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_vr_wave_in.npz")
-    np.savez(path, *[c[1] for c in cases])
-    code = ("import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api, synth; "
-            "d = np.load(%r); out = []\n"
-            "for k, cfg in enumerate(%r):\n"
-            "    c = api.Context(synth.config_params(cfg)); f = c.features(d['arr_%%d' %% k]); c.close()\n"
-            "    out += [f['label'].tobytes(), f['corner'].tobytes(), f['surf'].tobytes()]\n"
-            "sys.stdout.buffer.write(b''.join(len(x).to_bytes(8, 'little') + x for x in out))"
-            % (REPO, path, [c[0] for c in cases]))
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, FBR_VR_WAVE=mode),
-                       timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
-    blob, ref = r.stdout, []
-    while blob:
-        n = int.from_bytes(blob[:8], "little")
-        ref.append(blob[8:8 + n])
-        blob = blob[8 + n:]
     for k, (cfg, pts) in enumerate(cases):
         P = synth.config_params(cfg)
-        with api.Context(P) as ctx:
+        with api.Context(P) as ctx, api.Context(P) as cq:
+            cq.diag_ring_filter(2)
             fg = ctx.features(pts)
-        assert fg["label"].tobytes() == ref[3 * k], (k, cfg)
-        assert fg["corner"].tobytes() == ref[3 * k + 1], (k, cfg)
-        assert fg["surf"].tobytes() == ref[3 * k + 2], (k, cfg, len(fg["surf"]), len(ref[3 * k + 2]) // 16)
+            fq = cq.features(pts)
+        assert fg["label"].tobytes() == fq["label"].tobytes(), (k, cfg)
+        assert fg["corner"].tobytes() == fq["corner"].tobytes(), (k, cfg)
+        assert fg["surf"].tobytes() == fq["surf"].tobytes(), (k, cfg, len(fg["surf"]), len(fq["surf"]))
         fo = O.Stream(P).features(pts)
         assert_features_equal(fo, fg)
 

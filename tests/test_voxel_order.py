@@ -157,12 +157,15 @@ def _morton(x, y, z):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant,cap,nw", [(0, 4096, 8), (1, 4096, 4), (2, 40000, 16), (3, 18432, 16), (4, 18432, 16)],
-                         ids=["ring-lds-512", "segment-lds-256", "global-1024", "inplace-atomic", "inplace-leader"])
+@pytest.mark.parametrize("variant,cap,nw", [(0, 4096, 8), (1, 4096, 4), (2, 40000, 16), (3, 18432, 16), (4, 18432, 16),
+                                            (5, 18432, 16)],
+                         ids=["ring-lds-512", "segment-lds-256", "global-1024", "inplace-atomic", "inplace-leader",
+                              "inplace-leader-r03"])
 def test_voxel_radix_sorts_are_stable_sorts(variant, cap, nw):
     """Every wave-chunk radix sort configuration of k_voxel.hip (fbr_selftest_radix_sort) against a
     host stable sort, on every chunk fill including full ones and on long equal-digit runs.  Variant
-    4 is round 3's ballot-leader digit count in the in-place sort."""
+    4 is round 3's ballot-leader digit count in the in-place sort, 5 the exact form round 3 reverted
+    (the leader count plus a wave-uniform early exit in both loops)."""
     from feature_base_pointcloud_registration_amd import api
     for n, nbits, keys in _radix_cases(cap, nw):
         keys = np.asarray(keys, np.uint64).astype(np.uint32) & np.uint32((1 << nbits) - 1 if nbits < 32 else 0xFFFFFFFF)
