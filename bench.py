@@ -105,6 +105,10 @@ def parse():
                     help="strong scaling: N jobs per step split into contiguous per-rank blocks (C4: 1024)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend of the pose-record gather (gloo: host records, tests)")
+    ap.add_argument("--gather", default="torch", choices=["torch", "native"],
+                    help="pose-record all-gather for N > 1: torch.distributed (--backend), or the library's own "
+                         "RCCL communicator (fbr_comm_create / fbr_batch_allgather; the process group, gloo, "
+                         "then only carries the RCCL id, barriers and the timing)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on device 0 (world-size > 1 rehearsal on a one-GPU box)")
     ap.add_argument("--records-out", default=None, help="rank 0 writes the gathered records (.npy)")
@@ -265,6 +269,8 @@ def main():
         import torch  # noqa: F401  (load torch's HIP runtime first; the library shares it)
         import torch.distributed as dist
         torch.cuda.set_device(dev)
+        if args.gather == "native":
+            args.backend = "gloo"  # torch carries no records: the C-ABI's RCCL communicator does
         dist.init_process_group(backend=args.backend, init_method="env://")
 
     from feature_base_pointcloud_registration_amd import api, shard, synth
@@ -303,6 +309,21 @@ def main():
         if args.backend == "nccl":
             gather_buf = torch.zeros(Bpad * shard.RECORD_FLOATS, dtype=torch.float32, device=f"cuda:{dev}")
     gathered = [None]
+    native = dist is not None and args.gather == "native"
+    launches, native_done = [0], [-1]
+    if native:
+        obj = [api.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm = api.Comm(ctx, obj[0], world, rank, Bpad)
+        recv = torch.zeros(world * Bpad * shard.RECORD_FLOATS, dtype=torch.float32, device=f"cuda:{dev}")
+
+    def native_gather(upto):
+        """fbr_batch_allgather of every launch <= upto not yet gathered (the same ids on every rank;
+        consecutive gathers are ordered on the device by the library)."""
+        while native_done[0] < upto:
+            native_done[0] += 1
+            comm.allgather(native_done[0], recv.data_ptr())
+            gathered[0] = recv
 
     def gather_ready():
         """All-gather the records of the latest launch the library has fully enqueued (launches are
@@ -319,15 +340,21 @@ def main():
         return True
 
     def gather_rest():  # after the last launch: every launch not yet gathered, in order
+        if native:
+            native_gather(launches[0] - 1)
+            return
         ctx.batch_flush()
         while gather_ready():
             pass
 
     def step():
         ctx.batch_launch()
+        launches[0] += 1
         if dist is None:
             return
-        if args.backend == "nccl":
+        if native:  # launch n returns once n - 2 is fully enqueued: gather it without a host wait
+            native_gather(launches[0] - 3)
+        elif args.backend == "nccl":
             gather_ready()
         else:  # gloo: host records
             poses_h, stats_h = ctx.batch_results()
@@ -337,7 +364,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    if dist is not None and args.backend == "nccl":
+    if dist is not None and (native or args.backend == "nccl"):
         gather_rest()
     ctx.batch_wait()
     kernels = ["gn_knn", "gn_residual", "gn_solve", "project", "extract", "features", "voxel_ring", "concat",
@@ -345,7 +372,7 @@ def main():
     # one untimed profiled step: per-kernel device times (HIP events) and the dominant kernel
     ctx.set_profiling(True)
     step()
-    if dist is not None and args.backend == "nccl":
+    if dist is not None and (native or args.backend == "nccl"):
         gather_rest()
     ctx.batch_wait()
     ctx.set_profiling(False)
@@ -365,7 +392,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    if dist is not None and args.backend == "nccl":  # the last launches' records
+    if dist is not None and (native or args.backend == "nccl"):  # the last launches' records
         gather_rest()
     ctx.batch_wait()
     if dist is not None:
@@ -398,6 +425,8 @@ def main():
     if args.profile == "all":  # the roofline kernel: largest total kernel time inside the timed region
         dom = max(modelled, key=lambda k: timed[k][0])
 
+    if native:
+        comm.close()
     if rank != 0:
         ctx.close()
         if dist is not None:
@@ -498,8 +527,10 @@ def main():
             "mean_local_map_points": round(tot["M"] / B, 1),
             "mean_queries_per_scan": round(tot["Q"] / B, 1),
             "mean_gn_iterations": round(float(stats["iterations"].mean()), 3),
-            "parallelism": (f"scan-shard x{world}, {'RCCL' if args.backend == 'nccl' else 'gloo'} pose all-gather"
-                            if world > 1 else "single GPU"),
+            "parallelism": (f"scan-shard x{world}, " + ("RCCL pose all-gather through the C-ABI (fbr_batch_allgather)"
+                                                         if native else f"{'RCCL' if args.backend == 'nccl' else 'gloo'} "
+                                                                        "pose all-gather (torch.distributed)")
+                            if dist is not None else "single GPU"),
             "imu_deskew": bool(args.deskew),
         },
         "roofline": {

@@ -144,7 +144,7 @@ struct fbr_ctx {
   int nsub_pref = 3;                  // sub-batches per batch launch (FBR_NSUB overrides): 3 unpipelined (at
                                       // B = 128: 2 -> 76.1k, 3 -> 78.5k, 4 -> 46.7k scans/s), 1 pipelined
   int H = 0, W = 0, Bcap = 0;
-  // Batch launches rotate over nslot work slots (FBR_PIPE, default 3; 1 when max_batch = 1): the
+  // Batch launches rotate over nslot work slots (fbr_params.pipeline_depth, default 3; 1 when max_batch = 1): the
   // next launch's projection / features overlap the previous ones' Gauss-Newton tails.  Work arrays
   // hold Bwork = nslot * Bcap jobs; inputs hold Bcap.
   static constexpr int kMaxSlots = 3;
@@ -1872,6 +1872,8 @@ struct fbr_comm {
   ncclComm_t nc = nullptr;
   int dev = 0, nranks = 0, rank = 0, max_jobs = 0;
   float* send = nullptr;  // [max_jobs][8] this rank's padded records
+  hipEvent_t done = nullptr;  // after the latest all-gather: the next one (on another launch's
+  bool used = false;          // stream) reuses `send` and the caller's recv buffer
 };
 
 extern "C" {
@@ -1899,13 +1901,16 @@ int fbr_comm_create(fbr_comm** out, fbr_ctx* c, const uint8_t id[FBR_COMM_ID_BYT
   m->max_jobs = max_jobs_per_rank;
   ncclUniqueId uid;
   std::memcpy(uid.internal, id, FBR_COMM_ID_BYTES);
-  if (hipMalloc((void**)&m->send, sizeof(float) * 8 * (size_t)max_jobs_per_rank) != hipSuccess) {
+  if (hipMalloc((void**)&m->send, sizeof(float) * 8 * (size_t)max_jobs_per_rank) != hipSuccess ||
+      hipEventCreateWithFlags(&m->done, hipEventDisableTiming) != hipSuccess) {
+    (void)hipFree(m->send);
     delete m;
     return FBR_ERR_HIP;
   }
   // blocks until every rank has joined (bootstrap over the id's socket)
   if (rccl().comm_init_rank(&m->nc, nranks, uid, rank) != ncclSuccess) {
     (void)hipFree(m->send);
+    (void)hipEventDestroy(m->done);
     delete m;
     return FBR_ERR_HIP;
   }
@@ -1919,6 +1924,7 @@ int fbr_comm_destroy(fbr_comm* m) {
   int rc = FBR_OK;
   if (m->nc && rccl().comm_destroy(m->nc) != ncclSuccess) rc = FBR_ERR_HIP;
   (void)hipFree(m->send);
+  if (m->done) (void)hipEventDestroy(m->done);
   delete m;
   return rc;
 }
@@ -1941,12 +1947,15 @@ int fbr_batch_allgather(fbr_ctx* c, fbr_comm* m, int64_t launch_id, void* recv, 
   const GnRun& r = c->run[s];
   hipStream_t st = r.subs[0].st;
   for (int k = 1; k < r.nsub; ++k) CK(hipStreamWaitEvent(st, c->xev[r.subs[k].k], 0));
+  if (m->used) CK(hipStreamWaitEvent(st, m->done, 0));  // the previous gather (maybe another stream)
   const int64_t w0 = (int64_t)s * c->Bcap;
   if (c->staged_B < m->max_jobs)  // padding records: zeros
     CK(hipMemsetAsync(m->send + 8 * (int64_t)c->staged_B, 0, sizeof(float) * 8 * (m->max_jobs - c->staged_B), st));
   launch_export_records(st, c->staged_B, c->d_pose_out + w0 * 6, c->d_stats + w0, c->d_err + w0, c->d_guess, m->send);
   CK(hipGetLastError());
   if (rccl().all_gather(m->send, recv, (size_t)8 * m->max_jobs, ncclFloat32, m->nc, st) != ncclSuccess) return FBR_ERR_HIP;
+  CK(hipEventRecord(m->done, st));
+  m->used = true;
   if (done_stream) *done_stream = (void*)st;
   else {
     CK(hipEventRecord(c->ev_ext, st));

@@ -62,14 +62,15 @@ constexpr int kProjThreads = 256, kProjPPT = 8, kProjChunk = kProjThreads * kPro
 __global__ void __launch_bounds__(kProjThreads)
 k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ nin, int64_t nmax, int H, int W,
           int tile_log2, int32_t* __restrict__ owner, int32_t* __restrict__ err, int64_t n_single) {
-  extern __shared__ int32_t tile[];  // [H][1 << tile_log2]
+  extern __shared__ int32_t tile[];  // [H][(1 << tile_log2) + 1]: the pad puts the consecutive rings of one
+                                     // column (consecutive points in firing order) in distinct banks
   __shared__ int32_t cellk[kProjChunk];
   __shared__ int red[2][kProjThreads / 64];
   const int job = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // the job's feature-capacity flags start clear (k_features ORs into them; this saves the
   // single-scan path a 6 us fill dispatch on its critical path)
   if (err && blockIdx.x == 0 && tid == 0) err[job] = 0;
-  const int tcols = 1 << tile_log2, tcells = H << tile_log2;
+  const int tcols = 1 << tile_log2, tcells = H << tile_log2, tpitch = tcols + 1;
   const int64_t n = n_single >= 0 ? n_single : nin[job];  // single scans: the count as an argument
   const fbr_point_xyzirt* P = pts + (int64_t)job * nmax;
   int32_t* O = owner + (int64_t)job * H * W;
@@ -102,16 +103,16 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
       cmax = max(cmax, red[1][w]);
     }
     if (cmax >= 0 && cmax - cmin < tcols) {
-      for (int e = tid; e < tcells; e += kProjThreads) tile[e] = kEmptyOwner;
+      for (int e = tid; e < H * tpitch; e += kProjThreads) tile[e] = kEmptyOwner;
       __syncthreads();
       for (int k = 0; k < kProjPPT; ++k) {
         const int v = cellk[k * kProjThreads + tid];
         if (v >= 0)
-          atomicMin(&tile[((v >> 16) << tile_log2) + ((v & 0xFFFF) - cmin)], (int32_t)(base + k * kProjThreads + tid));
+          atomicMin(&tile[(v >> 16) * tpitch + ((v & 0xFFFF) - cmin)], (int32_t)(base + k * kProjThreads + tid));
       }
       __syncthreads();
       for (int e = tid; e < tcells; e += kProjThreads) {
-        const int32_t v = tile[e];
+        const int32_t v = tile[(e >> tile_log2) * tpitch + (e & (tcols - 1))];
         if (v != kEmptyOwner) atomicMin(&O[(e >> tile_log2) * W + cmin + (e & (tcols - 1))], v);
       }
     } else {
@@ -196,10 +197,14 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, int32_t* __res
           float4* __restrict__ cloud, int32_t* __restrict__ col, float* __restrict__ range,
           int32_t* __restrict__ start_ring, int32_t* __restrict__ end_ring, int32_t* __restrict__ nvalid,
           DeskArgs desk) {
+  // [HB][CG + 1] arrays: the column-by-column gather has consecutive lanes on consecutive rows, and
+  // the pad puts those in distinct banks (a CG-word pitch put a whole wave on one bank group:
+  // 13.8 conflict cycles per LDS instruction, profiles/r05a_sq_decomp.txt)
   extern __shared__ float4 lds_c[];
-  float4* pxyz = lds_c;                                    // [HB][CG] gathered xyzi
-  int32_t* own = reinterpret_cast<int32_t*>(pxyz + HB * CG);  // [HB][CG] owners of the tile
-  float* prng = reinterpret_cast<float*>(own + HB * CG);   // [HB][CG] range (deskew only)
+  const int PC = CG + 1;
+  float4* pxyz = lds_c;                                    // [HB][PC] gathered xyzi
+  int32_t* own = reinterpret_cast<int32_t*>(pxyz + HB * PC);  // [HB][PC] owners of the tile
+  float* prng = reinterpret_cast<float*>(own + HB * PC);   // [HB][PC] range (deskew only)
   __shared__ int32_t rowoff[64];    // output offset of each tile row before this chunk
   __shared__ int32_t scan[256];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -254,7 +259,7 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, int32_t* __res
       o = *a;
       if (o != kEmptyOwner) *a = kEmptyOwner;
     }
-    own[i] = o;
+    own[r * PC + c] = o;
   }
   __syncthreads();
   // deskew: transStartInverse from the scan's first deskewed point (the minimum owner)
@@ -273,7 +278,7 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, int32_t* __res
   }
   // gather, column by column (consecutive threads = consecutive rings of one column)
   for (int i = tid; i < HB * CG; i += 256) {
-    const int c = i / HB, r = i % HB, k = r * CG + c;
+    const int c = i / HB, r = i % HB, k = r * PC + c;
     const int32_t o = own[k];
     if (o != kEmptyOwner) {
       const fbr_point_xyzirt q = P[o];
@@ -296,7 +301,7 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, int32_t* __res
     const int r = p * rpp + tid / CG;
     int rank = 0;
     const int c = tid % CG;
-    const int k = r * CG + c;
+    const int k = r * PC + c;
     const bool v = r < nr && own[k] != kEmptyOwner;
     // prefix over the CG cells of the row: ballots over the wave's 64 lanes (CG = 32: two rows per
     // wave; CG >= 64: a row spans CG / 64 waves, combined through LDS)
@@ -411,7 +416,7 @@ void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* n
   if (blocks < 1) blocks = 1;
   int tile_log2 = 6;  // 64 columns, shrunk so the tile stays <= 32 KB
   while (tile_log2 > 3 && ((int64_t)H << tile_log2) > 8192) --tile_log2;
-  const size_t lds = sizeof(int32_t) * ((size_t)H << tile_log2);
+  const size_t lds = sizeof(int32_t) * (size_t)H * ((1 << tile_log2) + 1);
   fbr_launch(k_project, dim3(blocks, B), dim3(kProjThreads), lds, s, pts, nin, nmax, H, W, tile_log2, owner, err,
              n_single);
 }
@@ -435,7 +440,7 @@ void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, in
   const int tiles = ((H + T.hb - 1) / T.hb) * compact_nchunk(T.cg, W);
   const int groups = (B + 7) / 8;
   const dim3 grid((unsigned)(groups * 8 * tiles));
-  const size_t cells = (size_t)T.hb * T.cg;
+  const size_t cells = (size_t)T.hb * (T.cg + 1);  // padded pitch (k_compact)
   if (desk.mode)
     fbr_launch(k_compact<true>, grid, dim3(256), (uint32_t)(cells * 24), s, pts, nmax, owner, rowcnt, choff, B, H, W,
                T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk);

@@ -8,7 +8,7 @@
 // voxels emitted in ascending key order, centroid = float sum of x,y,z,intensity / count.
 // PCL sorts (key, index) with the unstable std::sort, so the order of points inside one voxel —
 // and hence the last bits of the centroid sum — is introsort-specific.  The kernels reproduce it
-// (fbr_introsort.h) when FBR_VG_EXACT=1: std::sort's partition phase on (PCL key, index), then
+// (fbr_introsort.h) when fbr_params.exact_voxel_order = 1: std::sort's partition phase on (PCL key, index), then
 // their stable radix sort of that sequence, which is std::sort's result; centroids are bit-exact.
 // By default the partition phase is skipped (points summed in index order, centroids to float
 // rounding, at about twice the exact mode's throughput).

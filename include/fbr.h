@@ -361,7 +361,7 @@ int fbr_debug_counters(long long* launches, long long* host_syncs, long long* fl
  * computes the per-job CropBox map statistics, which depend only on the guesses); launch enqueues
  * the whole path for the staged batch (asynchronous, inputs are not modified so it may be
  * re-launched); wait blocks; results copies the latest launch's poses/stats out.
- * Launches are pipelined three deep (FBR_PIPE = 1..3, default 3; 1 when max_batch = 1):
+ * Launches are pipelined fbr_params.pipeline_depth deep (1..3, default 3; 1 when max_batch = 1):
  * consecutive launches rotate over the work buffers and streams of the launch slots, and
  * fbr_batch_launch returns once the launch two before it is fully enqueued, leaving the tail of its own Gauss-Newton loop (whose length the device decides)
  * to the next launch / flush / wait call.  So launch n's projection and features run beside launch
@@ -384,7 +384,7 @@ int fbr_batch_results(fbr_ctx* ctx, float* poses_out /* [n_jobs][6] */,
  * memory of the ctx's device, [n_jobs][8] x 4 B) — the payload of the cross-GPU pose all-gather. */
 int fbr_batch_export(fbr_ctx* ctx, void* device_dst);
 /* Pipelined form: export the records of the oldest launch not yet exported, if it is fully
- * enqueued (after fbr_batch_launch n: at least launch n - (FBR_PIPE - 1); after fbr_batch_flush:
+ * enqueued (after fbr_batch_launch n: at least launch n - (pipeline_depth - 1); after fbr_batch_flush:
  * every launch), without waiting for the launches in flight; launches are exported in launch
  * order, each once.  The copy runs on that launch's stream after it, and after the
  * work queued so far on `wait_stream` (a HIP stream of the caller still reading device_dst, or
@@ -414,8 +414,10 @@ int fbr_comm_destroy(fbr_comm* comm);
  * fbr_batch_results (a job over the feature capacity: its guess, FBR_REG_FEATURE_CAPACITY).  The
  * launch is first enqueued to its end (the host follows its GN flags); the export and the
  * all-gather then run on that launch's stream, returned in *done_stream (wait on it before reading
- * recv), or, with done_stream NULL, joined into the ctx stream.  The launch must still own its work
- * slot (one of the last FBR_PIPE launches of the staged batch): FBR_ERR_STATE otherwise. */
+ * recv), or, with done_stream NULL, joined into the ctx stream.  Consecutive calls are ordered on
+ * the device (each after the previous one's all-gather), so one recv buffer may serve them all.
+ * The launch must still own its work slot (one of the last pipeline_depth launches of the staged
+ * batch): FBR_ERR_STATE otherwise. */
 int fbr_batch_allgather(fbr_ctx* ctx, fbr_comm* comm, int64_t launch_id, void* recv, void** done_stream);
 
 /* Sum of the per-scan algorithmic byte counts of the last completed batch (roofline input). */

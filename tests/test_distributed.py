@@ -134,6 +134,18 @@ def test_bench_rccl_path_one_rank(tmp_path):
     assert res["records_check"] == {"jobs": 16, "mismatched_words": 0}
 
 
+@pytest.mark.gpu
+def test_bench_native_gather_one_rank_matches_torch_path(tmp_path):
+    """bench.py --gather native: the pose records go through the library's own RCCL communicator
+    (fbr_comm_create / fbr_batch_allgather, two launches behind the newest), torch only broadcasts
+    the RCCL id; world 1 on the box's GPU.  The gathered records equal the torch-RCCL path's."""
+    rn, recn = _run_bench(1, ["--total-jobs", "16", "--gather", "native"], tmp_path, "native")
+    rt, rect = _run_bench(1, ["--total-jobs", "16"], tmp_path, "torch")
+    assert rn["records_check"] == {"jobs": 16, "mismatched_words": 0}
+    assert "fbr_batch_allgather" in rn["config"]["parallelism"]
+    assert np.array_equal(recn.view(np.int32), rect.view(np.int32))
+
+
 # ------------------------------------------------------------------ native RCCL path (no torch)
 def _write_shard_input(path, H, W, cmap, smap, jobs):
     import struct
