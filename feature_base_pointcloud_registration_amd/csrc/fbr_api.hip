@@ -446,6 +446,16 @@ int stage_project(fbr_ctx* c, const Sub& sb) {
   return FBR_OK;
 }
 
+// Batch jobs resolve the surf walk only within reach of each segment's end (FeatArgs::surf_full;
+// FBR_FEAT_SURF_WINDOW=0: the whole walk, for A/B).
+bool feat_surf_window() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_FEAT_SURF_WINDOW");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 // err_clear: stage_project has just cleared the jobs' feature-capacity flags (k_project).
 int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode, bool err_clear = false) {
   const int64_t j0 = sb.j0, HW = c->HW, H = c->H;
@@ -473,6 +483,7 @@ int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode, bool err_clear =
   a.corner_slot = c->d_corner_slot + j0 * H * kCornerPerRing;
   a.corner_cnt = c->d_corner_cnt + j0 * H;
   a.err = c->d_err + j0;
+  a.surf_full = stream_mode || !feat_surf_window() ? 1 : 0;  // batch jobs export no labels
   feat_caps(c->W, a);
   a.gscratch = c->d_feat_scratch + j0 * H * a.gslot_bytes;
   a.stamps = c->d_feat_stamps ? c->d_feat_stamps + j0 * H * 12 : nullptr;

@@ -44,6 +44,16 @@ __device__ __forceinline__ void knn_insert(Knn5& r, unsigned long long x) {
   r.k[0] = lt[0] ? x : r.k[0];
 }
 
+// pcl::CropBox's inclusive test (p outside [bmin, bmax] on some axis) as one compare: for finite
+// floats b - x > 0 exactly when x < b (the difference of distinct floats is never rounded to 0,
+// denormals are kept), so "outside" is the largest of the six excesses being positive; 6 subtractions
+// and 2 three-way maxima instead of 6 compares whose masks the compiler combined in 16-bit registers.
+__device__ __forceinline__ bool crop_out(const float4& p, float bx0, float by0, float bz0, float bx1, float by1,
+                                         float bz1) {
+  const float ex = fmaxf(fmaxf(bx0 - p.x, p.x - bx1), fmaxf(by0 - p.y, p.y - by1));
+  return fmaxf(ex, fmaxf(bz0 - p.z, p.z - bz1)) > 0.0f;
+}
+
 // Lower bound of |q - p| along one axis for a point p in the cell at offset o from q's cell
 // (cells are [k*c, (k+1)*c) with c a power of two, so every edge is exact).  Rounding is
 // monotone, so fl(edge - q) <= |fl(q - p)| and the bound composed in the distance's own
@@ -205,7 +215,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         const float4 p = m.pts[i];
         // pcl::CropBox (inclusive) as one mask: a point outside gets d2 = +inf (never inserted)
         bool out = false;  // rows inside the box skip the test
-        if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
+        if (!inside) out = crop_out(p, bx0, by0, bz0, bx1, by1, bz1);
         float dist = 0.0f, diff;
         diff = qx - p.x; dist += diff * diff;                            // flann::L2_Simple
         diff = qy - p.y; dist += diff * diff;
@@ -234,7 +244,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       }
       const float4 p = m.pts[i++];
       bool out = false;
-      if (!inside) out = (p.x < bx0) | (p.y < by0) | (p.z < bz0) | (p.x > bx1) | (p.y > by1) | (p.z > bz1);
+      if (!inside) out = crop_out(p, bx0, by0, bz0, bx1, by1, bz1);
       float dist = 0.0f, diff;
       diff = qx - p.x; dist += diff * diff;  // flann::L2_Simple
       diff = qy - p.y; dist += diff * diff;

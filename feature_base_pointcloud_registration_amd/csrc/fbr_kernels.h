@@ -104,6 +104,11 @@ struct FeatArgs {
   unsigned char* gscratch;  // [B*H][gslot_bytes] sorted-path buffers (stale-slot segment, ties)
   int64_t gslot_bytes;
   unsigned long long* stamps;  // diagnostic builds only: [B*H][12] phase cycle sums
+  // 0 (independent batch jobs): the surf walk is resolved only as far as it reaches the next
+  // segment (its picks' suppression past ep), since nothing else of it is observable there: the
+  // per-ring VoxelGrid takes label <= 0 (picked surf -1 and 0 alike, featureExtraction.h:279-284)
+  // and no label leaves a batch.  1 (single scans: cloudLabel is an output): the whole walk.
+  int surf_full = 1;
 };
 size_t features_lds_bytes(const FeatArgs& a, int nwv);  // nwv: waves per ring
 size_t features_gslot_bytes(const FeatArgs& a);

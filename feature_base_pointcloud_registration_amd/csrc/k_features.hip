@@ -51,6 +51,7 @@ __device__ __forceinline__ void wsync() {
 
 namespace {
 constexpr uint64_t kPadKey = ~0ull;
+constexpr int kSurfWindow = 64;  // batch surf walk: members resolved left of ep (FeatArgs::surf_full)
 constexpr int kWin = 256 + 16;  // phase-2 window: 4 chunks + 8 on each side
 constexpr int kWinBytes = kWin * (sizeof(float) + sizeof(int16_t));  // 1632 B per wave (16-B multiple)
 }  // namespace
@@ -182,20 +183,24 @@ __device__ __forceinline__ uint32_t win10(uint64_t a, uint64_t b, uint64_t c, in
 
 // Greedy rounds.  cmbits(u) = 10-bit mask of the higher-priority conflicting members of u.
 // und: candidate members on entry; on exit tak = the members the sequential walk takes.
+// frz (optional): frozen members -- candidates outside the resolved window, kept undecided: they
+// block the members they outrank and are never decided themselves; the rounds then stop when a
+// round decides nothing (members whose outcome depends on a frozen one stay in und).
 template <int WMAX, typename CmF>
 __device__ __forceinline__ void greedy_rounds(int m, int lane, uint64_t (&und)[WMAX], uint64_t (&tak)[WMAX], CmF cmbits,
-                              const FeatArgs& a, int job) {
+                              const FeatArgs& a, int job, const uint64_t* frz = nullptr) {
   const int nwm = (m >> 6) + 1;
   uint32_t cmr[WMAX];
 #pragma unroll
   for (int w = 0; w < WMAX; ++w) cmr[w] = (w < nwm && 64 * w + lane <= m) ? cmbits(64 * w + lane) : 0u;
   for (int round = 0;; ++round) {
-    bool any = false;
+    bool any = false, progress = false;
 #pragma unroll
     for (int w = 0; w < WMAX; ++w) {
-      if (w < nwm && und[w] != 0ull) {  // words whose candidates are all decided are skipped
+      const uint64_t live = frz ? und[w] & ~frz[w] : und[w];
+      if (w < nwm && live != 0ull) {  // words whose candidates are all decided are skipped
         bool nt = false, tk = false;
-        const bool mine = (und[w] >> lane) & 1ull;
+        const bool mine = (live >> lane) & 1ull;
         if (mine) {
           const uint32_t wt = win10(w > 0 ? tak[w - 1] : 0ull, tak[w], w + 1 < WMAX ? tak[w + 1] : 0ull, lane);
           const uint32_t wu = win10(w > 0 ? und[w - 1] : 0ull, und[w], w + 1 < WMAX ? und[w + 1] : 0ull, lane);
@@ -212,10 +217,11 @@ __device__ __forceinline__ void greedy_rounds(int m, int lane, uint64_t (&und)[W
         }
         const uint64_t bn = __ballot(nt);
         und[w] &= ~(bt | bn);
-        any |= und[w] != 0ull;
+        progress |= (bt | bn) != 0ull;
+        any |= (frz ? und[w] & ~frz[w] : und[w]) != 0ull;
       }
     }
-    if (!any) break;
+    if (!any || (frz && !progress)) break;
     if (round > 4 * (m + 2)) {  // unreachable: each round decides the best-ranked undecided
       if (lane == 0) atomicOr(&a.err[job], 8);
       break;
@@ -676,6 +682,9 @@ k_features(FeatArgs a) {
       return;
     }
   };
+  int lastj = -1;  // the ring's last non-empty segment
+  for (int j = 0; j < 6; j++)
+    if ((s * (6 - j) + e * j) / 6 < (s * (5 - j) + e * (j + 1)) / 6 - 1) lastj = j;
   for (int j = 0; j < 6; j++) {
     const int sp = (s * (6 - j) + e * j) / 6;
     const int ep = (s * (5 - j) + e * (j + 1)) / 6 - 1;
@@ -959,23 +968,60 @@ k_features(FeatArgs a) {
       FBR_STAMP(5);
       if constexpr (NWV == 1) prefetch_curv(j + 1);  // scurv is not read again in this segment
       // -- surf walk: ascending, ep last -> higher priority = not higher corner priority --
+      // Batch jobs (a.surf_full == 0) need only the walk's picks within reach of ep (they suppress
+      // the next segment's first members); the last segment of a ring needs none.  The members of
+      // the window [ulo, m] are resolved with the candidates just left of it frozen (undecided);
+      // if a member within reach of ep stays undecided (its chain of higher-priority conflicts
+      // leaves the window), the whole walk runs.
+      const bool bnd = !a.surf_full;
+      const int ulo = bnd ? max(0, m - (kSurfWindow - 1)) : 0;
+      auto surf_cand = [&](bool window) __attribute__((always_inline)) {
 #pragma unroll
-      for (int w = 0; w < WMAX; ++w) {
-        const int u = 64 * w + lane;
-        bool cand = false;
-        if (u <= m) {
-          const int li = sp + u - S.wlo;
-          cand = !S.picked.get(li) && S.surfc.get(li);
+        for (int w = 0; w < WMAX; ++w) {
+          const int u = 64 * w + lane;
+          bool cand = false;
+          if (u <= m && (!window || u >= ulo - 5)) {
+            const int li = sp + u - S.wlo;
+            cand = !S.picked.get(li) && S.surfc.get(li);
+          }
+          und[w] = __ballot(cand);
+          tak[w] = 0ull;
         }
-        und[w] = __ballot(cand);
-        tak[w] = 0ull;
-      }
-#ifndef FBR_FEAT_SKIP_SURF
-      greedy_rounds(m, lane, und, tak, [&](int u) {
+      };
+      auto surf_cm = [&](int u) {
         const uint32_t c = S.cm[u];
         return ((c >> 10) & 1023u) & ~(c & 1023u);
-      }, a, job);
+      };
+      if (bnd && j == lastj) {  // the ring's last segment: no surf pick of it is observable
+#pragma unroll
+        for (int w = 0; w < WMAX; ++w) tak[w] = 0ull;
+      } else {
+        surf_cand(bnd && ulo > 0);
+#ifndef FBR_FEAT_SKIP_SURF
+        if (bnd && ulo > 0) {
+          uint64_t frz[WMAX];
+#pragma unroll
+          for (int w = 0; w < WMAX; ++w) {
+            const int u = 64 * w + lane;
+            frz[w] = und[w] & __ballot(u < ulo);
+          }
+          greedy_rounds(m, lane, und, tak, surf_cm, a, job, frz);
+          // every candidate within reach of ep decided?
+          bool open = false;
+#pragma unroll
+          for (int w = 0; w < WMAX; ++w) {
+            const int u = 64 * w + lane;
+            open |= u >= m - 4 && u <= m && ((und[w] >> lane) & 1ull) && !((frz[w] >> lane) & 1ull);
+          }
+          if (__any(open)) {
+            surf_cand(false);
+            greedy_rounds(m, lane, und, tak, surf_cm, a, job);
+          }
+        } else {
+          greedy_rounds(m, lane, und, tak, surf_cm, a, job);
+        }
 #endif
+      }
       FBR_STAMP(6);
 #pragma unroll
       for (int w = 0; w < WMAX; ++w) {

@@ -721,6 +721,31 @@ def test_sparse_grid_registration_is_bit_identical_to_dense(c2_map):
     assert _c2_batch_in_child(jobs, {"FBR_GRID_SPARSE": "1"}, True) == _c2_batch_here(c2_map, jobs)
 
 
+def test_batch_surf_walk_window_is_unobservable(c2_map):
+    """Batch jobs resolve the surf walk only within reach of each segment's end (FeatArgs::surf_full
+    = 0): the picked surf labels (-1) are no output of a batch and the per-ring VoxelGrid takes every
+    label <= 0 alike, so only the picks' suppression into the next segment matters.  Against the
+    whole walk (FBR_FEAT_SURF_WINDOW=0, child process) on C2 jobs, C3 jobs and adversarial rings
+    (long monotone curvature runs that push the window's fallback): poses and stats bit-equal."""
+    jobs = synth.make_jobs("C2", 12, base_seed=640)
+    assert _c2_batch_in_child(jobs, {"FBR_FEAT_SURF_WINDOW": "0"}, False) == _c2_batch_here(c2_map, jobs)
+    c3 = synth.make_jobs("C3", 2, base_seed=641)
+    scans, guesses = [j[0] for j in c3], np.stack([j[1] for j in c3])
+    pw, sw = _cfg_batch_in_child("C3", scans, guesses, {"FBR_FEAT_SURF_WINDOW": "0"})
+    with api.Context(synth.config_params("C3", max_batch=2)) as ctx:
+        ctx.set_map(*synth.config_map("C3"))
+        ph, sh = ctx.process_batch(scans, guesses)
+    assert np.array_equal(pw.view(np.int32), ph.view(np.int32)) and sw.tobytes() == sh.tobytes()
+    # adversarial rings (C1 shape): smooth walls, random ranges, alternating rings
+    adv = [_adversarial_ring_scan(16, 1800, 70 + k) for k in range(4)]
+    g = np.zeros((4, 6), np.float32)
+    pa, sa = _cfg_batch_in_child("C1", adv, g, {"FBR_FEAT_SURF_WINDOW": "0"})
+    with api.Context(synth.config_params("C1", max_batch=4)) as ctx:
+        ctx.set_map(*synth.config_map("C1"))
+        pb, sb = ctx.process_batch(adv, g)
+    assert np.array_equal(pa.view(np.int32), pb.view(np.int32)) and sa.tobytes() == sb.tobytes()
+
+
 def test_exact_voxel_order_gives_bit_identical_poses(c2_map):
     """exact_voxel_order = 1: every VoxelGrid sums a voxel's points in std::sort's order
     (csrc/fbr_introsort.h), so the per-ring, mapping-DS and start-up map centroids are PCL's bit for
