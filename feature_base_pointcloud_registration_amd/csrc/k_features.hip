@@ -805,6 +805,35 @@ k_features(FeatArgs a) {
     float* tlv = (float*)S.rb;                         // direct path: taken corners (value, member)
     uint16_t* tlu = (uint16_t*)(tlv + segcap);
     uint16_t* vis = tlu + segcap;                      // taken corners in visit order
+    // Conflict masks of member u from curvature comparisons (the direct path): returns whether a
+    // conflicting neighbour has the same curvature (its order would be introsort's).
+    auto cm_member = [&](int u) __attribute__((always_inline)) -> bool {
+      const int li = sp - S.wlo + u;
+      const int f = reach_fwd(S, li), b = reach_bwd(S, li);
+      float cv[11];
+#pragma unroll
+      for (int d = 0; d < 11; ++d) cv[d] = S.scurv[max(li + d - 5, 0) - S.sbase];
+      const float vu = cv[5];
+      // neighbour bits (bit 4+d forward, 5-d backward) as ranges: forward d <= min(f, m-u),
+      // backward d <= min(b, u); ep (member m) outranks every neighbour
+      const int lf = min(f, m - u), lb = min(b, u);
+      const uint32_t nbf = ((1u << lf) - 1u) << 5, nbb = ((1u << lb) - 1u) << (5 - lb);
+      const uint32_t epb = (m - u >= 1 && m - u <= 5) ? 1u << (4 + m - u) : 0u;
+      uint32_t gt = 0, eq = 0;
+#pragma unroll
+      for (int d = 1; d <= 5; ++d) {
+        gt |= (cv[5 + d] > vu ? 1u : 0u) << (4 + d);
+        eq |= (!(cv[5 + d] < vu || cv[5 + d] > vu) ? 1u : 0u) << (4 + d);  // equal or NaN
+        gt |= (cv[5 - d] > vu ? 1u : 0u) << (5 - d);
+        eq |= (!(cv[5 - d] < vu || cv[5 - d] > vu) ? 1u : 0u) << (5 - d);
+      }
+      const uint32_t notep = u != m ? ~0u : 0u;
+      const uint32_t nb = nbf | nbb;
+      const uint32_t hc = ((gt | epb) & nbf) | (gt & nbb & notep);
+      S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
+      return ((eq & ~epb & nbf) | (eq & nbb & notep)) != 0u;
+    };
+    const bool cm_sparse = !a.surf_full && !has_stale;
     bool direct = !has_stale;
 #ifdef FBR_FEAT_SKIP_CM
     if (direct) {
@@ -816,41 +845,40 @@ k_features(FeatArgs a) {
     if (direct) {
 #endif
       bool tf = false;
-      for (int k0 = 64 * wv; k0 <= m; k0 += NT) {
-        const int u = k0 + lane;
-        const int li0 = sp - S.wlo + k0, W0 = li0 >> 6;  // li0 >= 0
-        const uint64_t gm1 = W0 >= 1 ? S.gap.w[W0 - 1] : ~0ull;  // wave-uniform words
-        const uint64_t g0 = W0 < S.nw ? S.gap.w[W0] : 0ull;
-        const uint64_t g1 = W0 + 1 < S.nw ? S.gap.w[W0 + 1] : 0ull;
-        const uint64_t g2 = W0 + 2 < S.nw ? S.gap.w[W0 + 2] : 0ull;
-        const int off = (li0 & 63) + lane;
-        const uint64_t fw = win64(g0, g1, g2, off);   // bit d = gap at li+d
-        const uint64_t bw = win64(gm1, g0, g1, off);  // bit 63-d = gap at li-1-d
-        if (u <= m) {
-          const int li = li0 + lane;
-          const int f = __builtin_ctzll(fw | 0x20ull), b = __builtin_clzll(bw | (1ull << 58));
-          float cv[11];
-#pragma unroll
-          for (int d = 0; d < 11; ++d) cv[d] = S.scurv[max(li + d - 5, 0) - S.sbase];
-          const float vu = cv[5];
-          // neighbour bits (bit 4+d forward, 5-d backward) as ranges: forward d <= min(f, m-u),
-          // backward d <= min(b, u); ep (member m) outranks every neighbour
-          const int lf = min(f, m - u), lb = min(b, u);
-          const uint32_t nbf = ((1u << lf) - 1u) << 5, nbb = ((1u << lb) - 1u) << (5 - lb);
-          const uint32_t epb = (m - u >= 1 && m - u <= 5) ? 1u << (4 + m - u) : 0u;
-          uint32_t gt = 0, eq = 0;
-#pragma unroll
-          for (int d = 1; d <= 5; ++d) {
-            gt |= (cv[5 + d] > vu ? 1u : 0u) << (4 + d);
-            eq |= (!(cv[5 + d] < vu || cv[5 + d] > vu) ? 1u : 0u) << (4 + d);  // equal or NaN
-            gt |= (cv[5 - d] > vu ? 1u : 0u) << (5 - d);
-            eq |= (!(cv[5 - d] < vu || cv[5 - d] > vu) ? 1u : 0u) << (5 - d);
+      // Batch jobs need cm only for the corner candidates and the surf window [m - 63, m] (none
+      // for the surf walk of the ring's last segment): the members are listed in region B (free
+      // until the corner walk) and only those are computed; the rest follow in the rare case the
+      // surf window falls back to the whole walk (cm_rest below).
+      int nlist = m + 1;
+      if (cm_sparse) {
+        uint16_t* list = (uint16_t*)S.rb;
+        if (wv == 0) {
+          int cnt = 0;
+          const int wlo_u = j == lastj ? m + 1 : max(0, m - (kSurfWindow - 1));
+          for (int k0 = 0; k0 <= m; k0 += 64) {
+            const int u = k0 + lane;
+            bool need = false;
+            if (u <= m) {
+              const int li = sp + u - S.wlo;
+              need = u >= wlo_u || (!S.picked.get(li) && S.edgec.get(li));
+            }
+            const uint64_t bm = __ballot(need);
+            if (need) list[cnt + __popcll(bm & ((1ull << lane) - 1ull))] = (uint16_t)u;
+            cnt += __popcll(bm);
           }
-          const uint32_t notep = u != m ? ~0u : 0u;
-          const uint32_t nb = nbf | nbb;
-          const uint32_t hc = ((gt | epb) & nbf) | (gt & nbb & notep);
-          tf |= ((eq & ~epb & nbf) | (eq & nbb & notep)) != 0u;
-          S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
+          if (lane == 0) S.tmask[15] = (uint64_t)cnt;
+        }
+        if constexpr (NWV == 1) wsync();
+        else __syncthreads();
+        nlist = (int)S.tmask[15];
+      }
+      for (int k0 = 64 * wv; k0 < nlist; k0 += NT) {
+        if (cm_sparse) {
+          const int k = k0 + lane;
+          if (k < nlist) tf |= cm_member(((const uint16_t*)S.rb)[k]);
+        } else {
+          const int u = k0 + lane;
+          if (u <= m) tf |= cm_member(u);
         }
       }
       if constexpr (NWV == 1) {
@@ -1014,6 +1042,12 @@ k_features(FeatArgs a) {
             open |= u >= m - 4 && u <= m && ((und[w] >> lane) & 1ull) && !((frz[w] >> lane) & 1ull);
           }
           if (__any(open)) {
+            if (direct) {  // cm was computed for the listed members only: all of them now
+              bool tf2 = false;
+              for (int u = lane; u <= m; u += 64) tf2 |= cm_member(u);
+              wsync();
+              if (__any(tf2)) sorted_order();  // a relevant tie: introsort's order for the whole walk
+            }
             surf_cand(false);
             greedy_rounds(m, lane, und, tak, surf_cm, a, job);
           }

@@ -148,17 +148,29 @@ __global__ void k_rowcount(const int32_t* __restrict__ owner, int H, int W, int 
   const int nch = compact_nchunk(cg, W);
   int32_t* CH = choff + ((int64_t)job * H + row) * nch;
   int run = 0, mn = kEmptyOwner;
-  for (int c0 = 0; c0 < W; c0 += 64) {
-    const int c = c0 + lane;
-    const int32_t o = c < W ? O[c] : kEmptyOwner;
-    mn = min(mn, o);
-    const uint64_t m = __ballot(o != kEmptyOwner);
-    // chunk starts inside this 64-column step (cg is a multiple of 32)
-    if (lane == 0) {
-      if (c0 % cg == 0) CH[c0 / cg] = run;
-      if ((c0 + 32) % cg == 0 && c0 + 32 < W) CH[(c0 + 32) / cg] = run + __popcll(m & 0xFFFFFFFFull);
+  // four 64-column steps per round, their loads issued together (the row is one dependent chain
+  // of ballots; a single scan's 64 row waves otherwise wait ~29 L2 round trips each)
+  for (int c00 = 0; c00 < W; c00 += 256) {
+    int32_t o4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c00 + 64 * q + lane;
+      o4[q] = c < W ? O[c] : kEmptyOwner;
     }
-    run += __popcll(m);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c0 = c00 + 64 * q;
+      if (c0 >= W) break;  // wave-uniform
+      const int32_t o = o4[q];
+      mn = min(mn, o);
+      const uint64_t m = __ballot(o != kEmptyOwner);
+      // chunk starts inside this 64-column step (cg is a multiple of 32)
+      if (lane == 0) {
+        if (c0 % cg == 0) CH[c0 / cg] = run;
+        if ((c0 + 32) % cg == 0 && c0 + 32 < W) CH[(c0 + 32) / cg] = run + __popcll(m & 0xFFFFFFFFull);
+      }
+      run += __popcll(m);
+    }
   }
   if (rowmin)
     for (int off = 32; off > 0; off >>= 1) mn = min(mn, __shfl_xor(mn, off));
