@@ -240,7 +240,7 @@ def stream_copy_bandwidth(device=0, nbytes=2 << 30, iters=20):
 
 def valu_peak(device=0, waves_per_simd=4, kind=0, iters=4096, reps=5):
     """(wave-level VALU G instr/s, ms per launch) of the fbr_valu_peak probe: kind 0 v_fma_f32,
-    1 v_add_u32, 2 v_pk_fma_f32, waves_per_simd waves on every SIMD."""
+    1 v_add_u32, 2 v_pk_fma_f32, 3 v_cmp_lt_u64, 4 v_cmp_lt_u32, waves_per_simd waves on every SIMD."""
     g, ms = ctypes.c_double(), ctypes.c_double()
     _check(lib().fbr_valu_peak(device, waves_per_simd, kind, iters, reps, ctypes.byref(g), ctypes.byref(ms)),
            "fbr_valu_peak")

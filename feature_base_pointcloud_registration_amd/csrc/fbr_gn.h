@@ -105,7 +105,9 @@ __device__ __forceinline__ bool row_range(const MapGrid& m, int y, int z, int x0
 // Diagnostic builds only (tools/knn_stats.py): [queries, rows considered, rows scanned, points
 // scanned, points inserted, accepted queries, corner queries, wave iterations of the point loop,
 // warm-started queries, queries whose neighbours equal the previous iteration's], accumulated into
-// GnArgs::knn_stats (one device buffer for every kNN translation unit)
+// GnArgs::knn_stats (one device buffer for every kNN translation unit); then, for the flat walk,
+// [flat queries, points within the static cut], a histogram of that count per flat query (bins
+// 0..31, 32..63, >= 64) at [12, 46), [points scanned, wave trips] at [46, 48)
 #define FBR_KS(i, v) ks[i] += (v)
 #else
 #define FBR_KS(i, v) \
@@ -251,8 +253,12 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       diff = qz - p.z; dist += diff * diff;
       const unsigned hi = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
       FBR_KS(4, __int_as_float((int)hi) < knn_d(r.k[4]) ? 1 : 0);
+      FBR_KS(10, __int_as_float((int)hi) <= fminf(bound, kBelowOne) ? 1 : 0);  // within the static cut
 #ifdef FBR_KNN_STATS
-      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ks[7] += 1;  // one per wave iteration
+      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+        ks[7] += 1;  // one per wave iteration
+        ks[11] += 1;
+      }
 #endif
       knn_insert(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
     }
@@ -572,7 +578,7 @@ __device__ __forceinline__ void gn_knn_block(const GnArgs& a, int v, int use_pre
       bound = mx;
     }
     Knn5 nn;
-    unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned ks[12] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     knn5_grid<R, RX, kFlat, kSparse, LPQ>(mg, x0, y0, z0, g.crop_min, g.crop_max, bound, nn, ks, rows, sub);
     if constexpr (LPQ > 1) knn5_merge<LPQ>(nn);
     const bool ok = nn.k[4] < kKnnEmpty;
@@ -596,6 +602,13 @@ __device__ __forceinline__ void gn_knn_block(const GnArgs& a, int v, int use_pre
     ks[8] = have_prev;
     ks[9] = same;
     for (int k = 0; k < 10; ++k) atomicAdd(&a.knn_stats[k], (unsigned long long)ks[k]);
+    if (kFlat && use_prev) {
+      atomicAdd(&a.knn_stats[10], 1ull);
+      atomicAdd(&a.knn_stats[11], (unsigned long long)ks[10]);
+      atomicAdd(&a.knn_stats[12 + (ks[10] < 32 ? ks[10] : ks[10] < 64 ? 32 : 33)], 1ull);
+      atomicAdd(&a.knn_stats[46], (unsigned long long)ks[3]);
+      atomicAdd(&a.knn_stats[47], (unsigned long long)ks[11]);
+    }
 #endif
     if (kFused && ok)
       rok = res_row(g, mg.by_id, ids, 1, corner, p, x0, y0, z0, row, b, a.fitc + (int64_t)it * 6 * kResThreads + tid,

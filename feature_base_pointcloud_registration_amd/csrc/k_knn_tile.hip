@@ -363,7 +363,7 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tile(GnArgs a, int iter, un
             knn_insert(nn, ((unsigned long long)hb << 32) | (unsigned)__float_as_int(p.w));
           }
         } else {  // the tile did not fit: the grid search
-          unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+          unsigned ks[12] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
           knn5_grid<R, RX, false, false, 1>(mg, q.x0, q.y0, q.z0, g.crop_min, g.crop_max, q.bound, nn, ks);
           (void)ks;
         }
@@ -389,7 +389,7 @@ __global__ void __launch_bounds__(256) k_gn_knn_list(GnArgs a, int iter) {
     BinQuery q;
     bin_query(a, it, tid, item, g, q);
     Knn5 nn;
-    unsigned ks[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned ks[12] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     knn5_grid<R, RX, false, false, 1>(item.y == 0 ? a.mc : a.ms, q.x0, q.y0, q.z0, g.crop_min, g.crop_max, q.bound,
                                       nn, ks);
     (void)ks;

@@ -285,8 +285,8 @@ namespace fbr {
 unsigned long long* knn_stats_buffer() {
   static unsigned long long* p = [] {
     unsigned long long* q = nullptr;
-    if (hipMalloc(&q, sizeof(unsigned long long) * 10) != hipSuccess) return (unsigned long long*)nullptr;
-    hipMemset(q, 0, sizeof(unsigned long long) * 10);
+    if (hipMalloc(&q, sizeof(unsigned long long) * 48) != hipSuccess) return (unsigned long long*)nullptr;
+    hipMemset(q, 0, sizeof(unsigned long long) * 48);
     return q;
   }();
   return p;
@@ -295,8 +295,8 @@ unsigned long long* knn_stats_buffer() {
 extern "C" int fbr_diag_knn_stats(unsigned long long* out, int reset) {
   unsigned long long* p = fbr::knn_stats_buffer();
   if (!p) return FBR_ERR_HIP;
-  if (out && hipMemcpy(out, p, sizeof(unsigned long long) * 10, hipMemcpyDeviceToHost) != hipSuccess) return FBR_ERR_HIP;
-  if (reset && hipMemset(p, 0, sizeof(unsigned long long) * 10) != hipSuccess) return FBR_ERR_HIP;
+  if (out && hipMemcpy(out, p, sizeof(unsigned long long) * 48, hipMemcpyDeviceToHost) != hipSuccess) return FBR_ERR_HIP;
+  if (reset && hipMemset(p, 0, sizeof(unsigned long long) * 48) != hipSuccess) return FBR_ERR_HIP;
   return FBR_OK;
 }
 #endif

@@ -264,7 +264,8 @@ extern "C" int fbr_stream_copy_bandwidth(int hip_device, int64_t bytes, int iter
 // VALU issue-rate probe (measurement helper for the VALU roofline, bench.py / tools/valu_calib.py):
 // every lane runs 8 independent dependency chains of one VALU instruction for `iters` rounds, written
 // as inline asm so the compiler can neither pack (SLP) nor drop them.  kind 0: v_fma_f32, 1:
-// v_add_u32, 2: v_pk_fma_f32 (2 lanes of f32 per slot).  The grid is n_cu * waves_per_simd
+// v_add_u32, 2: v_pk_fma_f32 (2 lanes of f32 per slot), 3: v_cmp_lt_u64, 4: v_cmp_lt_u32 (both
+// into SGPR pairs: the compares of the kNN list insertion).  The grid is n_cu * waves_per_simd
 // workgroups of 256 threads (4 waves: one per SIMD), so every SIMD holds waves_per_simd waves.
 namespace fbr {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -300,6 +301,24 @@ __global__ void __launch_bounds__(256) k_valu_peak(float* out, int iters, float 
 #pragma unroll
     for (int u = 0; u < 8; ++u) s += x[u];
     out[t] = (float)s;
+  } else if constexpr (KIND == 3 || KIND == 4) {  // 64-bit / 32-bit unsigned compares into SGPR pairs
+    uint64_t x[8], m[8];
+    const uint64_t y = (uint64_t)__float_as_uint(a) << 20;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = (uint64_t)(t + u) << 16;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if constexpr (KIND == 3) asm volatile("v_cmp_lt_u64_e64 %0, %1, %2" : "=s"(m[u]) : "v"(x[u]), "v"(y));
+          else asm volatile("v_cmp_lt_u32_e64 %0, %1, %2" : "=s"(m[u]) : "v"((uint32_t)x[u]), "v"((uint32_t)y));
+        }
+    }
+    uint64_t s = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s ^= m[u];
+    out[t] = (float)(s & 0xffff);
   } else {
     f32x2 x[8];
     f32x2 va = {a, a}, vb = {b, b};
@@ -323,7 +342,7 @@ __global__ void __launch_bounds__(256) k_valu_peak(float* out, int iters, float 
 // events over `reps` launches after one warm-up launch).
 extern "C" int fbr_valu_peak(int hip_device, int waves_per_simd, int kind, int iters, int reps, double* ginst_per_s,
                              double* ms_per_launch) {
-  if (waves_per_simd < 1 || waves_per_simd > 8 || kind < 0 || kind > 2 || iters <= 0 || reps <= 0 || !ginst_per_s)
+  if (waves_per_simd < 1 || waves_per_simd > 8 || kind < 0 || kind > 4 || iters <= 0 || reps <= 0 || !ginst_per_s)
     return FBR_ERR_INVALID_ARG;
   if (hipSetDevice(hip_device) != hipSuccess) return FBR_ERR_NO_DEVICE;
   hipDeviceProp_t prop;
@@ -339,7 +358,9 @@ extern "C" int fbr_valu_peak(int hip_device, int waves_per_simd, int kind, int i
     auto launch = [&]() {
       if (kind == 0) hipLaunchKernelGGL(fbr::k_valu_peak<0>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0000001f, 0.5f);
       else if (kind == 1) hipLaunchKernelGGL(fbr::k_valu_peak<1>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0000001f, 0.5f);
-      else hipLaunchKernelGGL(fbr::k_valu_peak<2>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0000001f, 0.5f);
+      else if (kind == 2) hipLaunchKernelGGL(fbr::k_valu_peak<2>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0000001f, 0.5f);
+      else if (kind == 3) hipLaunchKernelGGL(fbr::k_valu_peak<3>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0000001f, 0.5f);
+      else hipLaunchKernelGGL(fbr::k_valu_peak<4>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0000001f, 0.5f);
     };
     launch();
     (void)hipEventRecord(e0, 0);

@@ -27,8 +27,9 @@ L.fbr_diag_feature_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 L.fbr_diag_feature_stamps(ctx._h, None)  # allocate the stamp buffer
 ctx.batch_stage([j[0] for j in jobs], np.stack([j[1] for j in jobs]))
 ctx.batch_launch(); ctx.batch_wait()
-out = np.zeros((B * H, 12), np.uint64)
+out = np.zeros((8 * B * H, 12), np.uint64)  # the buffer spans every launch slot (<= 8)
 L.fbr_diag_feature_stamps(ctx._h, out.ctypes.data)
+out = out[:B * H]  # slot 0: the first launch
 names = ["load", "flags+picked", "seg: sort", "seg: members/cm", "seg: corner rounds", "seg: cap+apply",
          "seg: surf rounds", "seg: apply surf", "seg: candidates", "outputs", "seg: direct cm", "seg: direct rank"]
 tot = out.astype(np.float64).mean(0)

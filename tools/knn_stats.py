@@ -24,7 +24,8 @@ jobs = synth.make_jobs(CFG, B)
 L = api.lib()
 L.fbr_diag_knn_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
 for cell in (sys.argv[2:] or ["0.5"]):  # "YZ" or "YZ/X" cell sizes in m
-    os.environ["FBR_KNN_CELL"] = cell.split("/")[0]
+    if cell != "default":
+        os.environ["FBR_KNN_CELL"] = cell.split("/")[0]
     if "/" in cell:
         os.environ["FBR_KNN_CELL_X"] = cell.split("/")[1]
     ctx = api.Context(P)
@@ -34,7 +35,7 @@ for cell in (sys.argv[2:] or ["0.5"]):  # "YZ" or "YZ/X" cell sizes in m
     L.fbr_diag_knn_stats(None, 1)
     ctx.set_profiling(True)
     ctx.batch_launch(); ctx.batch_wait()
-    st = np.zeros(10, np.uint64)
+    st = np.zeros(48, np.uint64)
     L.fbr_diag_knn_stats(st.ctypes.data, 0)
     q = float(st[0])
     print(f"cell {cell}: queries {int(q)} (corner {int(st[6])}) accepted {st[5] / q:.3f} | per query: rows considered "
@@ -43,4 +44,11 @@ for cell in (sys.argv[2:] or ["0.5"]):  # "YZ" or "YZ/X" cell sizes in m
           f"{float(st[3]) / (64.0 * float(st[7])):.3f} (points scanned / (64 x wave iterations)) | "
           f"neighbours unchanged from the previous iteration: {float(st[9]) / max(float(st[8]), 1.0):.3f} "
           f"of {int(st[8])} warm-started queries")
+    if st[10]:
+        h = st[12:46].astype(np.float64) / float(st[10])
+        cum = np.cumsum(h)
+        print(f"  flat queries {int(st[10])}: points within the static cut {st[11] / float(st[10]):.2f} per query; "
+              f"share with more than 8 / 12 / 16 / 24 / 31: {1 - cum[8]:.4f} / {1 - cum[12]:.4f} / {1 - cum[16]:.4f} / "
+              f"{1 - cum[24]:.4f} / {1 - cum[31]:.4f}; >= 64: {h[33]:.5f}; flat walk: {st[46] / float(st[10]):.2f} points "
+              f"per query, lane efficiency {float(st[46]) / (64.0 * float(max(st[47], 1))):.3f}")
     ctx.close()
