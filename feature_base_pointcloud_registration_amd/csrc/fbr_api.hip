@@ -457,7 +457,9 @@ bool feat_surf_window() {
 }
 
 // err_clear: stage_project has just cleared the jobs' feature-capacity flags (k_project).
-int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode, bool err_clear = false) {
+// labels_out: cloudLabel is an output of the call (fbr_extract_features), so every surf walk runs
+// whole; otherwise only the picks that reach something observable are resolved (FeatArgs).
+int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode, bool err_clear = false, bool labels_out = false) {
   const int64_t j0 = sb.j0, HW = c->HW, H = c->H;
   FeatArgs a{};
   a.B = sb.B;
@@ -476,14 +478,15 @@ int stage_features(fbr_ctx* c, const Sub& sb, bool stream_mode, bool err_clear =
     a.label = c->d_label_stream;
   } else {
     CK(hipMemsetAsync(c->d_sstate + j0, 0, sizeof(StreamState) * sb.B, sb.st));
-    CK(hipMemsetAsync(c->d_label + j0 * HW, 0, (size_t)sb.B * HW, sb.st));
     a.stream = c->d_sstate + j0;
     a.label = c->d_label + j0 * HW;
   }
   a.corner_slot = c->d_corner_slot + j0 * H * kCornerPerRing;
   a.corner_cnt = c->d_corner_cnt + j0 * H;
   a.err = c->d_err + j0;
-  a.surf_full = stream_mode || !feat_surf_window() ? 1 : 0;  // batch jobs export no labels
+  a.surf_full = labels_out || !feat_surf_window() ? 1 : 0;
+  a.carry = stream_mode ? 1 : 0;
+  a.fresh = stream_mode ? 0 : 1;
   feat_caps(c->W, a);
   a.gscratch = c->d_feat_scratch + j0 * H * a.gslot_bytes;
   a.stamps = c->d_feat_stamps ? c->d_feat_stamps + j0 * H * 12 : nullptr;
@@ -650,10 +653,12 @@ int register_prepare(fbr_ctx* c, const Sub& sb, bool trace) {
 }
 
 // Workgroups of the per-iteration GN kernels (each loops over the work items; FBR_GN_GRID overrides).
+// 16384 covers the ~11k items of a C2 launch of 341 jobs with one workgroup each (8192 left a second
+// round of items to half the workgroups: flat gn_knn -4 % per step, r05q).
 int gn_grid_cap() {
   static const int v = [] {
     const char* e = std::getenv("FBR_GN_GRID");
-    return e ? std::max(1, std::atoi(e)) : 8192;
+    return e ? std::max(1, std::atoi(e)) : 16384;
   }();
   return v;
 }
@@ -1545,7 +1550,7 @@ int fbr_extract_features(fbr_ctx* c, int8_t* label, fbr_point_xyzi* corner, int6
   if (!c) return FBR_ERR_INVALID_ARG;
   if (!c->have_projection) return FBR_ERR_STATE;
   CK(hipSetDevice(c->dev));
-  int rc = stage_features(c, single_sub(c), true);
+  int rc = stage_features(c, single_sub(c), true, false, true);
   if (rc) return rc;
   rc = check_err(c, 1);
   if (rc) return rc;

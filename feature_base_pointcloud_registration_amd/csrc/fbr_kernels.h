@@ -109,6 +109,13 @@ struct FeatArgs {
   // per-ring VoxelGrid takes label <= 0 (picked surf -1 and 0 alike, featureExtraction.h:279-284)
   // and no label leaves a batch.  1 (single scans: cloudLabel is an output): the whole walk.
   int surf_full = 1;
+  // Stream mode (single scans): cloudLabel[0..4] and cloudNeighborPicked[0..4] carry to the next
+  // scan, so with surf_full = 0 the segments starting at index <= 9 (whose members reach them) still
+  // run the whole walk.
+  int carry = 0;
+  // Batch jobs start from a fresh node: labels at indices < 5 are written even when 0 (no stale
+  // value to keep), so the label buffer needs no clearing between launches.
+  int fresh = 0;
 };
 size_t features_lds_bytes(const FeatArgs& a, int nwv);  // nwv: waves per ring
 size_t features_gslot_bytes(const FeatArgs& a);

@@ -833,7 +833,8 @@ k_features(FeatArgs a) {
       S.cm[u] = hc | (nb << 10) | ((uint32_t)f << 20) | ((uint32_t)b << 24);
       return ((eq & ~epb & nbf) | (eq & nbb & notep)) != 0u;
     };
-    const bool cm_sparse = !a.surf_full && !has_stale;
+    const bool seg_full = a.surf_full || (a.carry && sp <= 9);  // the whole surf walk is observable
+    const bool cm_sparse = !seg_full && !has_stale;
     bool direct = !has_stale;
 #ifdef FBR_FEAT_SKIP_CM
     if (direct) {
@@ -1001,7 +1002,7 @@ k_features(FeatArgs a) {
       // the window [ulo, m] are resolved with the candidates just left of it frozen (undecided);
       // if a member within reach of ep stays undecided (its chain of higher-priority conflicts
       // leaves the window), the whole walk runs.
-      const bool bnd = !a.surf_full;
+      const bool bnd = !seg_full;
       const int ulo = bnd ? max(0, m - (kSurfWindow - 1)) : 0;
       auto surf_cand = [&](bool window) __attribute__((always_inline)) {
 #pragma unroll
@@ -1089,7 +1090,7 @@ k_features(FeatArgs a) {
     const int li = k - S.wlo;
     const int8_t lab = S.labpos.get(li) ? 1 : (S.labneg.get(li) ? -1 : 0);
     if (k >= 5 && k < n - 5) LB[k] = lab;      // cloudLabel reset range (:126)
-    else if (k < 5 && lab != 0) LB[k] = lab;   // stale slots keep earlier values
+    else if (k < 5 && (lab != 0 || a.fresh)) LB[k] = lab;  // stale slots keep earlier values
   }
   if (cb <= 0 && tid < 5 && tid < S.L) st->picked04[tid] = S.picked.get(tid) ? 1 : 0;
   if (tid == 0) a.corner_cnt[slot] = corner_cnt;

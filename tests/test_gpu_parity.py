@@ -746,6 +746,47 @@ def test_batch_surf_walk_window_is_unobservable(c2_map):
     assert np.array_equal(pa.view(np.int32), pb.view(np.int32)) and sa.tobytes() == sb.tobytes()
 
 
+def _stream_sequence_bytes(c2_map, scans):
+    """Every fbr_process_scan result of a C2 stream sequence (0.2 s apart: each scan registers), then
+    fbr_extract_features on the last projection, which starts from the carried scratch state."""
+    H, W = synth.CONFIGS["C2"][:2]
+    out = b""
+    with api.Context(default_params(H, W)) as ctx:
+        ctx.set_map(*c2_map)
+        pose = np.zeros(6, np.float32)
+        for k, pts in enumerate(scans):
+            pose, st = ctx.process_scan(pts, 0.2 * k, pose)
+            out += pose.tobytes() + np.array([st[f] for f in sorted(st)], np.float64).tobytes()
+        f = ctx.extract_features(len(ctx.project(scans[-1])["col_ind"]))
+        out += f["label"].tobytes() + f["corner"].tobytes() + f["surf"].tobytes()
+    return out
+
+
+def test_stream_surf_walk_window_is_unobservable(c2_map):
+    """fbr_process_scan resolves the surf walk only where it is observable too (FeatArgs::carry):
+    cloudLabel is no output of the call, but cloudLabel[0..4] and cloudNeighborPicked[0..4] carry to
+    the next scan, so the segments starting at index <= 9 run the whole walk.  A stream of C2 scans
+    and adversarial rings, then fbr_extract_features from the carried state: byte-equal to the whole
+    walk (FBR_FEAT_SURF_WINDOW=0, child process)."""
+    import subprocess
+    import sys
+    jobs = synth.make_jobs("C2", 4, base_seed=660)
+    scans = []
+    for k, (pts, _, _) in enumerate(jobs):
+        scans += [pts, _adversarial_ring_scan(64, 1800, 90 + k)]
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_child_stream_seq.npz")
+    np.savez(path, *scans, cmap=c2_map[0], smap=c2_map[1])
+    code = ("import sys, numpy as np; sys.path[:0] = [%r, %r, %r]; "
+            "import test_gpu_parity as T; d = np.load(%r); "
+            "sc = [d['arr_%%d' %% k] for k in range(%d)]; "
+            "sys.stdout.buffer.write(T._stream_sequence_bytes((d['cmap'], d['smap']), sc))"
+            % (REPO, os.path.join(REPO, "oracle"), os.path.dirname(os.path.abspath(__file__)), path, len(scans)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=300,
+                       env=dict(os.environ, FBR_FEAT_SURF_WINDOW="0"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout == _stream_sequence_bytes(c2_map, scans)
+
+
 def test_exact_voxel_order_gives_bit_identical_poses(c2_map):
     """exact_voxel_order = 1: every VoxelGrid sums a voxel's points in std::sort's order
     (csrc/fbr_introsort.h), so the per-ring, mapping-DS and start-up map centroids are PCL's bit for
