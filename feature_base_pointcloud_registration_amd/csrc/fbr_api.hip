@@ -230,6 +230,11 @@ struct fbr_ctx {
   bool profiling = false;
   std::map<std::string, KernelTimer> timers;
   std::vector<int32_t> last_iters, last_q, last_n, last_m;
+  // Work items of the previous single scan: the next one's Gauss-Newton grids are sized from it
+  // (2x, at least 16 workgroups) instead of from the capacity bound.  The kernels loop over the
+  // items whatever the grid, so the hint only moves time: the C2 bound of ~900 items launched
+  // ~870 workgroups (x 8 in the wide kNN mode) that found no item.
+  int items_hint = 0;
   unsigned long long* d_feat_stamps = nullptr;  // diagnostic builds (FBR_FEAT_STAMPS) only
   // IMU deskew (fbr_set_deskew)
   fbr_deskew_table* d_desk = nullptr;  // [Bcap] tables (allocated on first use)
@@ -763,7 +768,8 @@ int gn_run_pass(fbr_ctx* c, GnRun& r, bool block, bool* progress) {
     }
     all_done = false;
     const bool tail = gn_tail_div() > 0 && (int64_t)r.active[k] * gn_tail_div() <= sb.B;
-    const int grid = std::max(1, std::min(r.a[k].max_items, tail ? std::min(gn_grid_cap(), 1024) : gn_grid_cap()));
+    int grid = std::max(1, std::min(r.a[k].max_items, tail ? std::min(gn_grid_cap(), 1024) : gn_grid_cap()));
+    if (sb.stream_mode && c->items_hint > 0) grid = std::min(grid, std::max(16, 2 * c->items_hint));
     if (gn_fused() || tail) {
       TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, r.a[k], grid, it, true));
     } else {
@@ -1666,6 +1672,7 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
     c->time_last = stamp;
     for (int k = 0; k < 6; ++k) pose_inout[k] = pose[k];
     c->stream_degenerate = st.degenerate;
+    c->items_hint = (st.n_corner_ds + 255) / 256 + (st.n_surf_ds + 255) / 256;  // 256-query items (k_gn_init)
   }
   if (stats) *stats = st;
   return FBR_OK;

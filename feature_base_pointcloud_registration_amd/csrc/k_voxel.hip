@@ -1509,7 +1509,7 @@ constexpr int kVgSplitMaxDevices = 64;
 int vg_split() {
   static const int v = [] {
     const char* e = std::getenv("FBR_VG_SPLIT");
-    const int p = e ? std::atoi(e) : 4;
+    const int p = e ? std::atoi(e) : 8;
     return p < 2 ? 1 : std::min(p, 8);
   }();
   return v;
@@ -1522,7 +1522,8 @@ void launch_voxel_grid(hipStream_t s, const VgArgs& a) {
   for (int k = 0; k < 2; ++k)
     if (a.s[k].nseg > 0) cap = std::max<int64_t>(cap, a.s[k].cap);
   const bool exact = a.s[0].exact || a.s[1].exact;  // both sets share the context's mode
-  // few segments (single-scan calls): P workgroups per segment (FBR_VG_SPLIT = P, default 4; 1 off)
+  // few segments (single-scan calls): P workgroups per segment (FBR_VG_SPLIT = P, default 8: C2 latency
+  // -10 us against 4, profiles/r05w_latency_knob_sweep.txt; 1 off)
   const int P = vg_split();
   if (!exact && P > 1 && cap > kVgLdsCap && vg_inplace() && nseg * P <= kVgSplitSlots) {
     // look-back flags of the current device (agent-scope atomics must stay on the device that runs
