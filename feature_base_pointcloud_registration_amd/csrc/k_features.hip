@@ -74,12 +74,12 @@ struct FeatLds {
   uint32_t* cm;       // [segcap] conflict masks
   unsigned char* rb;  // region B: phase-2 range/col windows, then the taken-corner lists
   uint64_t* tmask;    // [WMAX] taken mask copy for the cap scan
-  // sorted path (stale-slot segment, relevant ties): per-ring global scratch slot
+  // sorted path (stale-slot segment, relevant ties): per-ring global scratch slot (but sorder / rankc)
   uint64_t* keys;     // [kseg]
   SmoothEntry* seg;   // [segcap] serial-path entries
   SmoothEntry* tmp;   // [segcap] materialisation scratch
-  uint16_t* sorder;   // [segcap] member index at each sorted position
-  uint16_t* rankc;    // [segcap] corner visit rank of each member
+  uint16_t* sorder;   // [segcap] member index at each sorted position (LDS region B)
+  uint16_t* rankc;    // [segcap] corner visit rank of each member (LDS region B)
   SortFrame* sstack;  // [kSortStack] introsort emulation stack (tie segments, lane 0)
 };
 
@@ -237,13 +237,14 @@ __device__ __forceinline__ void greedy_rounds(int m, int lane, uint64_t (&und)[W
 // left of the latter, and returns min(g_K, r_{K-1}) for the first k = K where that fails
 // (swapped elements stop the scans).  Checked against std::sort on tie-heavy arrays
 // (tests/test_oracle_pinning.py).  Depth exhaustion falls back to the serial heap sort.
-__device__ int wave_partition(SmoothEntry* a, int lo, int hi, float p, int* posL, int* posR, int lane) {
+__device__ __forceinline__ int wave_partition(SmoothEntry* a, int lo, int hi, float p, uint16_t* posL, uint16_t* posR,
+                                              int lane) {
   int cntL = 0;
   for (int b = lo; b < hi; b += 64) {
     const int i = b + lane;
     const bool isL = i < hi && !(a[i].v < p);
     const uint64_t bl = __ballot(isL);
-    if (isL) posL[cntL + __popcll(bl & ((1ull << lane) - 1ull))] = i;
+    if (isL) posL[cntL + __popcll(bl & ((1ull << lane) - 1ull))] = (uint16_t)i;
     cntL += __popcll(bl);
   }
   int cntR = 0;
@@ -251,7 +252,7 @@ __device__ int wave_partition(SmoothEntry* a, int lo, int hi, float p, int* posL
     const int i = t - lane;
     const bool isR = i >= lo && !(p < a[i].v);
     const uint64_t br = __ballot(isR);
-    if (isR) posR[cntR + __popcll(br & ((1ull << lane) - 1ull))] = i;
+    if (isR) posR[cntR + __popcll(br & ((1ull << lane) - 1ull))] = (uint16_t)i;
     cntR += __popcll(br);
   }
   wsync();
@@ -275,8 +276,8 @@ __device__ int wave_partition(SmoothEntry* a, int lo, int hi, float p, int* posL
   return min(cut, hi);
 }
 
-__device__ void wave_introsort_partitions(SmoothEntry* a, int n, SortFrame* stack, int* posL, int* posR,
-                                          int lane) {
+__device__ __forceinline__ void wave_introsort_partitions(SmoothEntry* a, int n, SortFrame* stack, uint16_t* posL,
+                                                          uint16_t* posR, int lane) {
   int sp = 0;
   stack[sp++] = SortFrame{0, n, 2 * sm_lg(n)};  // every lane writes / reads the same frames
   while (sp > 0) {
@@ -413,14 +414,17 @@ __device__ __forceinline__ bool stale_walks_fast(const FeatLds& S, int slen, con
     if (lane == w1) mm &= (hi & 63) == 63 ? ~0ull : ((1ull << ((hi & 63) + 1)) - 1ull);
     pv |= mm;
   };
-  // corners: k = ep .. sp (:208-242)
+  // corners: k = ep .. sp (:208-242); the walks visit only the entries that pass the curvature
+  // test (a ballot per 64 entries: the others are no-ops in the reference loops)
   int taken = 0;
   bool stop = false;
   for (int c0 = (m >> 6) << 6; c0 >= 0 && !stop; c0 -= 64) {
     const uint32_t vv = c0 + lane <= m ? info[c0 + lane] : 0u;
-    for (int l = min(63, m - c0); l >= 0; --l) {
+    uint64_t cand = __ballot((vv >> 22) & 1u);
+    while (cand) {
+      const int l = 63 - __builtin_clzll(cand);  // descending entries
+      cand &= ~(1ull << l);
       const uint32_t v = __builtin_amdgcn_readlane(vv, l);
-      if (!((v >> 22) & 1u)) continue;
       const int li = (int)(v & 0xFFFFu);
       if (is_picked(li)) continue;
       if (++taken > kCornerPerSeg) {
@@ -435,18 +439,22 @@ __device__ __forceinline__ bool stale_walks_fast(const FeatLds& S, int slen, con
     }
   }
   const int nc = min(taken, kCornerPerSeg);
-  // surf: k = sp .. ep (:245-276)
+  // surf: k = sp .. ep (:245-276); the picked-surf labels collect in the lanes' window words
+  uint64_t lv = 0ull;
   for (int c0 = 0; c0 <= m; c0 += 64) {
     const uint32_t vv = c0 + lane <= m ? info[c0 + lane] : 0u;
-    for (int l = 0; l <= min(63, m - c0); ++l) {
+    uint64_t cand = __ballot((vv >> 23) & 1u);
+    while (cand) {
+      const int l = __builtin_ctzll(cand);  // ascending entries
+      cand &= cand - 1ull;
       const uint32_t v = __builtin_amdgcn_readlane(vv, l);
-      if (!((v >> 23) & 1u)) continue;
       const int li = (int)(v & 0xFFFFu);
       if (is_picked(li)) continue;
-      if (lane == 0) atomicOr((unsigned long long*)&S.labneg.w[li >> 6], 1ull << (li & 63));
+      lv |= lane == (li >> 6) - w_lo ? 1ull << (li & 63) : 0ull;
       mark(li - (int)((v >> 19) & 7u), li + (int)((v >> 16) & 7u));
     }
   }
+  if (lv) atomicOr((unsigned long long*)&S.labneg.w[myw], (unsigned long long)lv);
   if (myw < S.nw) S.picked.w[myw] = pv;
   wsync();
   for (int t = lane; t < nc; t += 64) corner_out[corner_cnt + t] = CL[tlist[t]];
@@ -534,11 +542,14 @@ k_features(FeatArgs a) {
     S.keys = (uint64_t*)g;           g += sizeof(uint64_t) * kseg;
     S.seg = (SmoothEntry*)g;         g += sizeof(SmoothEntry) * segcap;
     S.tmp = (SmoothEntry*)g;         g += sizeof(SmoothEntry) * segcap;
-    S.sorder = (uint16_t*)g;         g += sizeof(uint16_t) * segcap;
-    S.rankc = (uint16_t*)g;          g += sizeof(uint16_t) * segcap;
+    g += 2 * sizeof(uint16_t) * segcap;  // (sorder / rankc: in region B below)
     unsigned char* g0 = a.gscratch + (int64_t)slot * a.gslot_bytes;
     S.gcurv = (float*)(g0 + (((g - g0) + 15) & ~(int64_t)15));
   }
+  // the sorted path's member order and ranks in LDS region B (free from the tie sort's end to the
+  // corner cap scan, the only readers; the cm loop reads ~10 ranks per member)
+  S.sorder = (uint16_t*)S.rb;
+  S.rankc = S.sorder + segcap;
   S.sbase = 0;
 
   const float* R = a.range + job * HW;
@@ -736,24 +747,24 @@ k_features(FeatArgs a) {
       FBR_STAMP(2);
       if (tie) {
         // equal curvatures: their order is introsort's; materialise std::sort's result in S.seg
+        // (the partition phase on an LDS copy in region B, 8 B x segcap, whose lists are dead here,
+        // with the partition positions as u16 in cm: no global round trip per partition step)
+        SmoothEntry* A = nan ? S.seg : (SmoothEntry*)S.rb;
         for (int t = lane; t < m; t += 64) {
           const int pos = sp + t;
-          S.seg[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.scurv[pos - S.wlo - S.sbase], pos};
+          A[t] = (pos == 4) ? SmoothEntry{st->smooth4_value, st->smooth4_ind} : SmoothEntry{S.scurv[pos - S.wlo - S.sbase], pos};
         }
         wsync();
         if (nan) {
           if (lane == 0) std_sort_emul(S.seg, m, S.sstack);
           wsync();
         } else {
-          wave_introsort_partitions(S.seg, m, S.sstack, (int*)S.cm, (int*)S.sorder, lane);
+          wave_introsort_partitions(A, m, S.sstack, (uint16_t*)S.cm, (uint16_t*)S.cm + segcap, lane);
           for (int t = lane; t < kpow; t += 64)
-            S.keys[t] = t < m ? (((uint64_t)__float_as_uint(S.seg[t].v) << 16) | (uint64_t)t) : kPadKey;
+            S.keys[t] = t < m ? (((uint64_t)__float_as_uint(A[t].v) << 16) | (uint64_t)t) : kPadKey;
           wsync();
           bitonic_sort_keys<QP>(S.keys, kpow, lane);  // stable sort of the partitioned array
-          SmoothEntry* tmp = (SmoothEntry*)S.cm;       // cm + sorder + rankc = 8 B per entry
-          for (int k = lane; k < m; k += 64) tmp[k] = S.seg[S.keys[k] & 0xFFFFu];
-          wsync();
-          for (int k = lane; k < m; k += 64) S.seg[k] = tmp[k];
+          for (int k = lane; k < m; k += 64) S.seg[k] = A[S.keys[k] & 0xFFFFu];
           wsync();
         }
       } else if (has_stale) {

@@ -42,5 +42,10 @@ print(f"per-ring totals: ring 0 mean {tot_r[:, 0].mean():.0f}, rings 1.. mean {t
       f"max {tot_r.max():.0f} (ring {int(tot_r.argmax() % H)}), median {np.median(tot_r):.0f}")
 r0 = per_ring[:, 0, :].mean(0)
 print("ring 0 breakdown:", ", ".join(f"{n} {v:.0f}" for n, v in zip(names, r0) if v > 0))
+flat = per_ring.reshape(B * H, 12)
+tot_f = flat.sum(1)
+for i in np.argsort(-tot_f)[:6]:  # the slowest rings (a single scan waits for its slowest ring)
+    print(f"ring {i % H} of job {i // H}: {tot_f[i]:.0f}:", ", ".join(f"{n} {v:.0f}" for n, v in zip(names, flat[i]) if v > 0))
+print(f"rings above 1.5x the median: {int((tot_f > 1.5 * np.median(tot_f)).sum())} of {len(tot_f)}")
 ctx.set_profiling(True); ctx.batch_launch(); ctx.batch_wait()
 print("features kernel ms:", ctx.kernel_time("features"))
