@@ -63,29 +63,36 @@ VALU_PEAK_GINST, VALU_PEAK_SOURCE = valu_peak_ginst()
 def kernel_bytes(name, tot):
     n_in, HW, n, C = tot["n_in"], tot["HW"], tot["n"], tot["C"]
     S, F, Q, IQ = tot["S"], tot["F"], tot["Q"], tot["IQ"]
+    IQc = tot.get("IQc", 0.0)  # corner query-iterations (the rest are surf)
     return {
         "project": 24.0 * n_in + 4.0 * n,        # raw point (24 B AoS) read + first-wins owner claim
         "extract": 4.0 * HW + 4.0 * n + 24.0 * n + 24.0 * n,  # owner image read + claimed cells reset, owning
                                                              # raw point gather, xyzi+col+range write
-        "features": 9.0 * n + 32.0 * C,          # range + col read, label written; corner points read + written
+        "features": 17.0 * n + 32.0 * C,         # range + col read, label written, the ring's curvature staged
+                                                 # through its scratch slot (4 B written, 4 B read back per
+                                                 # segment); corner points read + written
         "voxel_ring": 17.0 * n + 16.0 * S,       # label + candidate point read, per-ring DS write
         "concat": 32.0 * F,                      # per-ring corner / surf outputs read + job clouds written
         "voxel_scan": 16.0 * F + 16.0 * Q,       # corner + surf clouds read, DS queries written
-        "gn_knn": 36.0 * IQ,                     # query 16 B read + 5 map indices 20 B written (the map's
-                                                 # neighbour rows are cache hits: C2's map is 1.5 MB)
-        "gn_residual": 36.0 * IQ,                # query 16 B + 5 map indices 20 B read (neighbour gathers: cache)
+        "gn_knn": 37.0 * IQ + 20.0 * (IQ - Q),   # query 16 B read, 5 map indices 20 B + same-flag 1 B written;
+                                                 # from iteration 1 the previous 5 indices (warm start) read;
+                                                 # the map's rows are cache hits (C2's map is 1.5 MB)
+        "gn_residual": 38.0 * IQ + 8.0 * IQc + 16.0 * IQ,  # query 16 B + 5 indices 20 B + same / fit state
+                                                 # 2 B; the fit cache (line 24 B / plane 16 B: read when the
+                                                 # neighbours are unchanged, written when refitted); neighbour
+                                                 # gathers are cache hits
     }.get(name, 0.0)
 
 
 BYTE_MODEL = {
     "project": "24 B per raw point + 4 B owner claim per valid point",
     "extract": "4 B per range-image cell + 4 B owner reset + 24 B raw-point gather + 24 B written per valid point",
-    "features": "9 B per valid point (range + col read, label written) + 32 B per corner pick",
+    "features": "17 B per valid point (range + col read, label written, curvature staged through the ring's scratch slot 8 B) + 32 B per corner pick",
     "voxel_ring": "17 B per valid point + 16 B per per-ring DS point",
     "concat": "32 B per feature point",
     "voxel_scan": "16 B per feature point + 16 B per DS query",
-    "gn_knn": "36 B per query-iteration (query 16 B + 5 indices 20 B; neighbour rows of the map are L2/MALL hits)",
-    "gn_residual": "36 B per query-iteration (query 16 B + 5 indices 20 B; neighbour gathers are L2/MALL hits)",
+    "gn_knn": "37 B per query-iteration (query 16 B, 5 indices 20 B + same flag 1 B written) + 20 B per warm-started one (previous indices); map rows are L2/MALL hits",
+    "gn_residual": "54 B per query-iteration (query 16 B, 5 indices 20 B, 2 B state, 16 B plane fit cache) + 8 B per corner one (24 B line fit); neighbour gathers are L2/MALL hits",
 }
 
 # rocprofv3 kernel symbols behind each launcher name (tools/roofline_check.py maps a profile's rows)
@@ -379,7 +386,7 @@ def main():
     ctx.batch_wait()
     ctx.set_profiling(False)
     prof = {k: ctx.kernel_time(k) for k in kernels}
-    modelled = [k for k in kernels if kernel_bytes(k, dict.fromkeys(["n_in", "HW", "n", "C", "S", "F", "Q", "IQ"], 1.0)) > 0]
+    modelled = [k for k in kernels if kernel_bytes(k, dict.fromkeys(["n_in", "HW", "n", "C", "S", "F", "Q", "IQ", "IQc"], 1.0)) > 0]
     dom = max(modelled, key=lambda k: prof[k][0])  # provisional (the profiled step); final pick below
     if dist is not None:
         import torch
@@ -444,6 +451,7 @@ def main():
                F=float((stats["n_corner"] + stats["n_surf"]).sum()),
                Q=float((stats["n_corner_ds"] + stats["n_surf_ds"]).sum()),
                IQ=float(((stats["n_corner_ds"] + stats["n_surf_ds"]) * stats["iterations"]).sum()),
+               IQc=float((stats["n_corner_ds"] * stats["iterations"]).sum()),
                M=float((stats["n_corner_map"] + stats["n_surf_map"]).sum()))
 
     # per-launch VALU instructions (rocprofv3 SQ pass of the same config and batch, tools/valu_pmc.py)
