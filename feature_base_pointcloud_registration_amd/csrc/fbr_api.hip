@@ -265,9 +265,41 @@ struct fbr_ctx {
   uint8_t* h_msg = nullptr;               // pinned staging of raw PointCloud2 bytes (grown on demand)
   uint64_t h_msg_cap = 0;
   Ingest ing;                 // fbr_process_batch host ingest (allocated on first use)
+  // fbr_process_scan's direct result (GnArgs::direct): the ending k_gn_solve packs the job's
+  // result into h_direct (host-mapped); the host spins on its generation word instead of
+  // enqueueing finalize + pack + copy and synchronising.  The no-op iterations the host had
+  // enqueued ahead of the last flag may still be queued when the call returns (tail_pending):
+  // the next single-scan call is ordered after them on the stream, every other entry point
+  // synchronises the stream first (enter).
+  JobResult* h_direct = nullptr;
+  JobResult* d_direct = nullptr;
+  int32_t* d_direct_done = nullptr;
+  int32_t direct_gen = 0;     // generation of the current single-scan run (0: direct off)
+  int32_t direct_gen_seq = 0;
+  bool tail_pending = false;
 };
 
 namespace {
+
+// Single scans take their result from the ending solve (FBR_DIRECT=0: finalize + pack + copy).
+bool direct_results() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_DIRECT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+// Every public entry point: the context's device, and no single-scan tail left on the stream
+// unless the call is a single scan itself (keep_tail: its work is ordered after the tail).
+hipError_t enter(fbr_ctx* c, bool keep_tail = false) {
+  hipError_t e = hipSetDevice(c->dev);
+  if (e == hipSuccess && c->tail_pending && !keep_tail) {
+    e = fbr_sync(c->stream);
+    c->tail_pending = false;
+  }
+  return e;
+}
 
 void timer_begin(fbr_ctx* c, hipStream_t st, const char* name, hipEvent_t* ev_end) {
   *ev_end = nullptr;
@@ -586,6 +618,16 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   a.desk = c->desk_any ? c->d_desk + sb.in0 : nullptr;
   a.nocrop = c->map_nocrop ? 1 : 0;
   a.deg_carry = sb.stream_mode ? c->stream_degenerate : 0;
+  if (c->direct_gen && sb.stream_mode && sb.B == 1 && c->d_direct) {
+    a.direct = c->d_direct;
+    a.direct_done = c->d_direct_done;
+    a.direct_gen = c->direct_gen;
+    a.nvalid = c->d_nvalid + j0;
+    a.ncorner = c->d_ncorner + j0;
+    a.nsurf = c->d_nsurf + j0;
+    a.ferr = c->d_err + j0;
+    a.cropcnt = c->d_cropcnt + (int64_t)sb.in0 * 2;
+  }
   return a;
 }
 
@@ -760,7 +802,7 @@ int gn_run_pass(fbr_ctx* c, GnRun& r, bool block, bool* progress) {
       if (r.watch[k] && r.active[k] == 0) r.live[k] = false;
     }
     if (!r.live[k] || it >= c->P.max_iterations) {
-      TIMED_ON(c, sb.st, "gn_finalize", launch_gn_finalize(sb.st, r.a[k]));
+      if (!r.a[k].direct) TIMED_ON(c, sb.st, "gn_finalize", launch_gn_finalize(sb.st, r.a[k]));
       CK(hipEventRecord(c->xev[sb.k], sb.st));  // the sub-batch's last work (batch_quiesce joins it)
       r.done[k] = true;
       *progress = true;
@@ -854,14 +896,44 @@ int stage_register(fbr_ctx* c, const Sub& sb, bool trace) {
 // Per-job results of the last B jobs, packed on the device and returned by one copy (then one
 // host synchronisation): poses (when poses_out), stats, and the features' capacity errors
 // (FBR_ERR_UNSUPPORTED if any job has one).  with_reg = false: the registration was gated off.
+// A single scan's direct result (GnArgs::direct): spin on its generation word; false when the
+// stream drained without it (then the caller takes the enqueued path).
+int wait_direct(fbr_ctx* c, bool* got) {
+  volatile int32_t* gen = &c->h_direct->pad;
+  *got = false;
+  for (int64_t polls = 1;; ++polls) {
+    if (*gen == c->direct_gen) break;
+    if ((polls & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(c->stream);
+      if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
+      if (q == hipSuccess && *gen != c->direct_gen) return FBR_OK;
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  std::memcpy(c->h_result, (const void*)c->h_direct, sizeof(JobResult));
+  *got = true;
+  return FBR_OK;
+}
+
 int copy_results(fbr_ctx* c, int B, fbr_reg_stats* stats, float* poses_out, bool with_reg = true, int64_t w0 = 0,
                  bool per_job = false) {
-  launch_pack_results(c->stream, B, with_reg ? 1 : 0, c->d_pose_out + w0 * 6, c->d_stats + w0, c->d_nvalid + w0,
-                      c->d_ncorner + w0, c->d_nsurf + w0, c->d_cropcnt, c->d_err + w0, per_job ? c->d_guess : nullptr,
-                      c->d_result);
-  CK(hipMemcpyAsync(c->h_result, c->d_result, sizeof(JobResult) * B, hipMemcpyDeviceToHost, c->stream));
   const auto tw = std::chrono::steady_clock::now();
-  CK(fbr_sync(c->stream));
+  bool direct = false;
+  if (c->direct_gen && with_reg && B == 1 && w0 == 0 && !per_job) {
+    const int rc = wait_direct(c, &direct);
+    if (rc) return rc;
+    // the stream may still run the no-op iterations enqueued ahead of the last flag (tail_pending)
+    if (direct) c->tail_pending = true;
+    else TIMED(c, "gn_finalize", launch_gn_finalize(c->stream, gn_args(c, single_sub(c), false)));
+  }
+  if (!direct) {
+    launch_pack_results(c->stream, B, with_reg ? 1 : 0, c->d_pose_out + w0 * 6, c->d_stats + w0, c->d_nvalid + w0,
+                        c->d_ncorner + w0, c->d_nsurf + w0, c->d_cropcnt, c->d_err + w0, per_job ? c->d_guess : nullptr,
+                        c->d_result);
+    CK(hipMemcpyAsync(c->h_result, c->d_result, sizeof(JobResult) * B, hipMemcpyDeviceToHost, c->stream));
+    CK(fbr_sync(c->stream));
+  }
   if (c->crop_join) {  // the single-scan CropBox statistics: their own copy on the side stream (no
     c->crop_join = false;  // cross-stream dependency on the device; that stream finished long ago)
     CK(fbr_sync(c->xstream[1]));
@@ -1058,7 +1130,11 @@ hipError_t queue_guess(fbr_ctx* c, const float* guess) {
 int upload_scan(fbr_ctx* c, int job, const fbr_point_xyzirt* pts, int64_t n, const float* guess = nullptr) {
   if (n < 0 || n > c->NMAX) return FBR_ERR_CAPACITY;
   c->no_time_call = false;
-  CK(fbr_sync(c->stream));  // staging free (a no-op after the previous call's result copy)
+  // staging free: a no-op after the previous call's result copy; after a direct result the stream
+  // may still hold that call's no-op iterations, which read no staging buffer (the scan's DMA ran
+  // before its projection), and this call's work is ordered after them
+  if (c->tail_pending) c->tail_pending = false;
+  else CK(fbr_sync(c->stream));
   CK(queue_guess(c, guess));
   if (n && pinned_upload()) {
     CK(pinned_upload_async(c->dev, c->d_pts + job * c->NMAX, c->h_scan, pts, sizeof(fbr_point_xyzirt) * n, c->stream));
@@ -1077,7 +1153,8 @@ int upload_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* msg_flags, const
   int rc = resolve_msg(msg, &L);
   if (rc) return rc;
   if (L.n > c->NMAX) return FBR_ERR_CAPACITY;
-  CK(fbr_sync(c->stream));  // staging free (a no-op after the previous call's result copy)
+  if (c->tail_pending) c->tail_pending = false;  // as upload_scan
+  else CK(fbr_sync(c->stream));
   CK(queue_guess(c, guess));
   if (L.bytes > c->msg_cap) {
     if (c->d_msg) CK(hipFree(c->d_msg));
@@ -1372,12 +1449,16 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
                             hipHostMallocDefault) != hipSuccess ||
               hipHostMalloc((void**)&c->h_nin, sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
               hipHostMalloc((void**)&c->h_crop, sizeof(int32_t) * 2, hipHostMallocDefault) != hipSuccess ||
-              hipHostMalloc((void**)&c->h_guess, sizeof(float) * 6, hipHostMallocDefault) != hipSuccess;
+              hipHostMalloc((void**)&c->h_guess, sizeof(float) * 6, hipHostMallocDefault) != hipSuccess ||
+              hipHostMalloc((void**)&c->h_direct, sizeof(JobResult), hipHostMallocMapped) != hipSuccess ||
+              hipHostGetDevicePointer((void**)&c->d_direct, c->h_direct, 0) != hipSuccess ||
+              dalloc(&c->d_direct_done, 1);
   if (fail) {
     fbr_destroy(c);
     return FBR_ERR_HIP;
   }
   std::memset(c->h_iter_flags, 0, sizeof(unsigned long long) * kMaxSub * std::max(1, p->max_iterations));
+  std::memset(c->h_direct, 0, sizeof(JobResult));
   if (hipMemset(c->d_sstream, 0, sizeof(StreamState)) != hipSuccess ||
       hipMemset(c->d_label_stream, 0, HW) != hipSuccess || hipMemset(c->d_col, 0, sizeof(int32_t) * Bw * HW) != hipSuccess ||
       hipMemset(c->d_range, 0, sizeof(float) * Bw * HW) != hipSuccess ||
@@ -1403,14 +1484,15 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_fitc, c->d_fits, c->d_nsame, c->d_fb_list, c->d_bin, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
                   c->d_desk, c->d_desk_mode, c->d_rowmin, c->d_choff,
-                  c->d_kf_c, c->d_kf_s, c->d_kraw_c, c->d_kraw_s, c->d_kds_c, c->d_kds_s, c->d_kf_segs, c->d_bounds};
+                  c->d_kf_c, c->d_kf_s, c->d_kraw_c, c->d_kraw_s, c->d_kds_c, c->d_kds_s, c->d_kf_segs, c->d_bounds, c->d_direct_done};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);
   free_grid(c->grid_c);
   free_grid(c->grid_s);
   arena_free(c->arena);
-  for (void* h : {(void*)c->h_result, (void*)c->h_scan, (void*)c->h_nin, (void*)c->h_msg, (void*)c->h_crop, (void*)c->h_guess})
+  for (void* h : {(void*)c->h_result, (void*)c->h_scan, (void*)c->h_nin, (void*)c->h_msg, (void*)c->h_crop, (void*)c->h_guess,
+                  (void*)c->h_direct})
     if (h) (void)hipHostFree(h);
   if (c->d_result) (void)hipFree(c->d_result);
   if (c->ing.cstream) (void)fbr_sync(c->ing.cstream);
@@ -1449,7 +1531,7 @@ int fbr_destroy(fbr_ctx* c) {
 int fbr_set_map(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corner, const fbr_point_xyzi* surf,
                 int64_t n_surf) {
   if (!c || n_corner < 0 || n_surf < 0 || (n_corner && !corner) || (n_surf && !surf)) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   c->crop_cached = false;
   c->map_nocrop = false;
   int rc = voxel_grid_once(c, corner, n_corner, c->P.mapping_corner_leaf_size, c->map_c_host);
@@ -1488,7 +1570,7 @@ int fbr_get_map(fbr_ctx* c, int64_t* n_corner, int64_t* n_surf, fbr_point_xyzi* 
   if (!c) return FBR_ERR_INVALID_ARG;
   if (!c->has_map) return FBR_ERR_NO_MAP;
   if (c->map_nocrop) {  // keyframe local map (device-resident)
-    CK(hipSetDevice(c->dev));
+    CK(enter(c));
     if (n_corner) *n_corner = c->kds_c_n;
     if (n_surf) *n_surf = c->kds_s_n;
     if (corner && c->kds_c_n) CK(fbr_memcpy_sync(corner, c->d_kds_c, sizeof(float4) * c->kds_c_n, hipMemcpyDeviceToHost));
@@ -1513,7 +1595,7 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
 int fbr_project(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, int32_t* start_ring, int32_t* end_ring,
                 int32_t* col_ind, float* range, fbr_point_xyzi* cloud, int64_t* n_out) {
   if (!c || (n_in && !points)) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   int rc = drop_staged_batch(c);
   if (rc) return rc;
   rc = upload_scan(c, 0, points, n_in);
@@ -1524,7 +1606,7 @@ int fbr_project(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, int32_
 int fbr_project_msg(fbr_ctx* c, const fbr_pointcloud2* msg, int32_t* start_ring, int32_t* end_ring, int32_t* col_ind,
                     float* range, fbr_point_xyzi* cloud, int64_t* n_out, int32_t* msg_flags) {
   if (!c || !msg) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   int rc = drop_staged_batch(c);
   if (rc) return rc;
   rc = upload_msg(c, msg, msg_flags);
@@ -1555,7 +1637,7 @@ int fbr_extract_features(fbr_ctx* c, int8_t* label, fbr_point_xyzi* corner, int6
                          int64_t* n_surf) {
   if (!c) return FBR_ERR_INVALID_ARG;
   if (!c->have_projection) return FBR_ERR_STATE;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   int rc = stage_features(c, single_sub(c), true, false, true);
   if (rc) return rc;
   rc = check_err(c, 1);
@@ -1576,7 +1658,7 @@ int fbr_register_trace(fbr_ctx* c, const fbr_point_xyzi* corner, int64_t n_corne
                        int64_t n_surf, float pose_inout[6], fbr_reg_stats* stats, float* trace) {
   if (!c || !pose_inout) return FBR_ERR_INVALID_ARG;
   if (!c->has_map) return FBR_ERR_NO_MAP;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   int rc = drop_staged_batch(c);
   if (!rc) rc = upload_cloud(c, c->d_corner_all, c->d_ncorner, corner, n_corner);
   if (!rc) rc = upload_cloud(c, c->d_surf_all, c->d_nsurf, surf, n_surf);
@@ -1609,7 +1691,7 @@ int fbr_process_scan(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, d
                      fbr_reg_stats* stats) {
   if (!c || !pose_inout || (n_in && !points)) return FBR_ERR_INVALID_ARG;
   const auto t0 = std::chrono::steady_clock::now();
-  CK(hipSetDevice(c->dev));
+  CK(enter(c, true));
   int rc = drop_staged_batch(c);
   if (rc) return rc;
   rc = upload_scan(c, 0, points, n_in, will_register(c, stamp) ? pose_inout : nullptr);
@@ -1623,7 +1705,7 @@ int fbr_process_scan(fbr_ctx* c, const fbr_point_xyzirt* points, int64_t n_in, d
 int fbr_process_msg(fbr_ctx* c, const fbr_pointcloud2* msg, double stamp, float pose_inout[6], fbr_reg_stats* stats,
                     int32_t* msg_flags) {
   if (!c || !msg || !pose_inout) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c, true));
   int rc = drop_staged_batch(c);
   if (rc) return rc;
   rc = upload_msg(c, msg, msg_flags, will_register(c, stamp) ? pose_inout : nullptr);
@@ -1661,12 +1743,17 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
   float pose[6];
   if (run) {
     c->crop_cached = true;
+    c->direct_gen = direct_results() ? (c->direct_gen_seq = c->direct_gen_seq % 0x7fffffff + 1) : 0;
     rc = stage_register(c, single_sub(c), false);
     c->crop_cached = false;
-    if (rc) return rc;
+    if (rc) {
+      c->direct_gen = 0;
+      return rc;
+    }
   }
   host_time(1, t0);
   rc = copy_results(c, 1, &st, pose, run);
+  c->direct_gen = 0;
   if (rc) return rc;  // capacity error: the pose stays the guess, the time gate is not consumed
   if (run) {
     c->time_last = stamp;
@@ -1681,7 +1768,7 @@ int process_uploaded(fbr_ctx* c, double stamp, float pose_inout[6], fbr_reg_stat
 
 int fbr_reset_stream(fbr_ctx* c) {
   if (!c) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   CK(hipMemsetAsync(c->d_sstream, 0, sizeof(StreamState), c->stream));
   CK(hipMemsetAsync(c->d_label_stream, 0, c->HW, c->stream));
   CK(hipMemsetAsync(c->d_col, 0, sizeof(int32_t) * c->HW, c->stream));
@@ -1703,7 +1790,7 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
     if (n_in[j] < 0 || n_in[j] > c->NMAX) return FBR_ERR_CAPACITY;
     if (n_in[j] && !scans[j]) return FBR_ERR_INVALID_ARG;
   }
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   int rc = drop_staged_batch(c);  // launches in flight read the inputs: they are enqueued first
   if (rc) return rc;
   c->no_time_call = false;
@@ -1730,7 +1817,7 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
 int fbr_set_deskew(fbr_ctx* c, const fbr_deskew_table* tables, int n_tables) {
   if (!c || n_tables < 0 || (n_tables > 0 && !tables)) return FBR_ERR_INVALID_ARG;
   if (n_tables > c->Bcap) return FBR_ERR_CAPACITY;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   std::vector<int32_t> mode(c->Bcap, 0);
   bool any = false;
   for (int j = 0; j < n_tables; ++j) {
@@ -1752,7 +1839,7 @@ int fbr_batch_launch(fbr_ctx* c) {
   if (!c) return FBR_ERR_INVALID_ARG;
   if (c->staged_B <= 0) return FBR_ERR_STATE;
   if (!c->has_map) return FBR_ERR_NO_MAP;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   const auto t0 = std::chrono::steady_clock::now();
   // Sub-batches on separate streams: one sub-batch's low-occupancy phases (the features' ring-0
   // waves, the last Gauss-Newton iterations) overlap the others' work.  Consecutive launches take
@@ -1792,13 +1879,13 @@ int fbr_batch_launch(fbr_ctx* c) {
 
 int fbr_batch_flush(fbr_ctx* c) {
   if (!c) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   return advance_runs(c, -1);
 }
 
 int fbr_batch_wait(fbr_ctx* c) {
   if (!c) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   const int rc = batch_quiesce(c);
   if (rc) return rc;
   CK(fbr_sync(c->stream));
@@ -1808,7 +1895,7 @@ int fbr_batch_wait(fbr_ctx* c) {
 int fbr_batch_results(fbr_ctx* c, float* poses_out, fbr_reg_stats* stats) {
   if (!c) return FBR_ERR_INVALID_ARG;
   if (c->staged_B <= 0 || c->last_slot < 0) return FBR_ERR_STATE;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   const int rc = batch_quiesce(c);
   if (rc) return rc;
   return copy_results(c, c->staged_B, stats, poses_out, true, (int64_t)c->last_slot * c->Bcap, true);
@@ -1817,7 +1904,7 @@ int fbr_batch_results(fbr_ctx* c, float* poses_out, fbr_reg_stats* stats) {
 int fbr_batch_export(fbr_ctx* c, void* device_dst) {
   if (!c || !device_dst) return FBR_ERR_INVALID_ARG;
   if (c->staged_B <= 0 || c->last_slot < 0) return FBR_ERR_STATE;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   const int rc = batch_quiesce(c);
   if (rc) return rc;
   const int64_t w0 = (int64_t)c->last_slot * c->Bcap;
@@ -1833,7 +1920,7 @@ int fbr_batch_export_ready(fbr_ctx* c, void* device_dst, void* wait_stream, void
   *export_stream = nullptr;
   *launch_id = -1;
   if (c->staged_B <= 0) return FBR_ERR_STATE;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   // the oldest launch not yet exported, if it is fully enqueued: launches are exported in order
   // (one call per fbr_batch_launch never falls behind: launch n returns with n-1 enqueued)
   int s = -1;
@@ -1916,7 +2003,7 @@ int fbr_comm_create(fbr_comm** out, fbr_ctx* c, const uint8_t id[FBR_COMM_ID_BYT
   if (!out || !c || !id || nranks < 1 || rank < 0 || rank >= nranks || max_jobs_per_rank < 1) return FBR_ERR_INVALID_ARG;
   *out = nullptr;
   if (!rccl().ok) return FBR_ERR_UNSUPPORTED;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   fbr_comm* m = new fbr_comm();
   m->dev = c->dev;
   m->nranks = nranks;
@@ -1964,7 +2051,7 @@ int fbr_batch_allgather(fbr_ctx* c, fbr_comm* m, int64_t launch_id, void* recv, 
   for (int q = 0; q < c->nslot; ++q)
     if (c->slot_launch[q] == launch_id) s = q;
   if (s < 0) return FBR_ERR_STATE;  // its slot has been reused by a later launch
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   int rc = advance_runs(c, s);  // the launch fully enqueued (the host follows its GN flags)
   if (rc) return rc;
   const GnRun& r = c->run[s];
@@ -2038,7 +2125,7 @@ bool ingest_compact_enabled() {
 // one H2D copy per scan on the copy stream, then record up_ev[slot].  Runs on a worker thread
 // while the previous device batch computes.
 int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, const int64_t* n_in, int B) {
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   Ingest& g = c->ing;
   fbr_point_xyzirt* dst = g.d_pts_slot[slot];
   // compact records unless a deskew table may read the per-point time (deskewPoint, :545-580)
@@ -2152,7 +2239,7 @@ int fbr_process_batch(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const in
   }
   if (n_jobs == 0) return FBR_OK;
   if (!c->has_map) return FBR_ERR_NO_MAP;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   int rc = ingest_init(c);
   if (rc) return rc;
   c->ing.h2d_bytes = 0.0;
@@ -2240,7 +2327,7 @@ int fbr_ingest_bytes(fbr_ctx* c, double* h2d_bytes) {
 
 int fbr_voxel_grid(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf, fbr_point_xyzi* out, int64_t* n_out) {
   if (!c || n < 0 || (n && !in) || !(leaf > 0)) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   std::vector<fbr_point_xyzi> o;
   int rc = voxel_grid_once(c, in, n, leaf, o);
   if (rc) return rc;
@@ -2252,7 +2339,7 @@ int fbr_voxel_grid(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf, 
 // Diagnostic: per-ring phase cycle sums of k_features (only filled by a -DFBR_FEAT_STAMPS build).
 extern "C" int fbr_diag_feature_stamps(fbr_ctx* c, unsigned long long* out /* [max_batch*n_scan][12] */) {
   if (!c) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   const size_t n = (size_t)c->Bwork * c->H * 12;  // both launch slots (the first launch uses slot 0)
   if (!c->d_feat_stamps) {
     CK(hipMalloc(&c->d_feat_stamps, sizeof(unsigned long long) * n));
@@ -2288,7 +2375,7 @@ int fbr_set_profiling_kernels(fbr_ctx* c, const char* names) {
 
 int fbr_kernel_time(fbr_ctx* c, const char* kernel, double* total_ms, int64_t* launches) {
   if (!c || !kernel) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   auto itr = c->timers.find(kernel);
   if (itr == c->timers.end()) {
     if (total_ms) *total_ms = 0.0;
@@ -2348,7 +2435,7 @@ void fbr_keyframe_params_default(fbr_keyframe_params* p) {
 int fbr_keyframes_add(fbr_ctx* c, const fbr_keypose* pose, const fbr_point_xyzi* corner, int64_t n_corner,
                       const fbr_point_xyzi* surf, int64_t n_surf) {
   if (!c || !pose || n_corner < 0 || n_surf < 0 || (n_corner && !corner) || (n_surf && !surf)) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   int rc = grow(&c->d_kf_c, &c->kf_c_cap, c->kf_c_used + n_corner, c->kf_c_used, c->stream);
   if (!rc) rc = grow(&c->d_kf_s, &c->kf_s_cap, c->kf_s_used + n_surf, c->kf_s_used, c->stream);
   if (rc) return rc;
@@ -2400,7 +2487,7 @@ int fbr_keyframes_reset(fbr_ctx* c) {
 int fbr_extract_surrounding_keyframes(fbr_ctx* c, double stamp, const fbr_keyframe_params* kp, int64_t* n_corner_map,
                                       int64_t* n_surf_map, int32_t* n_frames) {
   if (!c || !kp || !(kp->search_radius >= 0) || !(kp->pose_density > 0)) return FBR_ERR_INVALID_ARG;
-  CK(hipSetDevice(c->dev));
+  CK(enter(c));
   if (n_frames) *n_frames = 0;
   const int64_t N = (int64_t)c->kf_poses.size();
   if (N == 0) {  // extractSurroundingKeyFrames (:967-968): nothing to extract, map unchanged

@@ -136,24 +136,6 @@ __device__ __forceinline__ bool row_range(const MapGrid& m, int y, int z, int x0
 // absolute map index = sub (mod LPQ) (knn5_merge combines the lists).  A lane prunes with its own
 // 5th distance, which is never below the merged one (its list holds the 5 nearest of a subset),
 // so every point of the merged 5 nearest is still scanned by its lane.
-// The (ky, kz) visit ranks of the K x K rows in the order the row loop visits them (by rank sum,
-// then ky): the flat queue's row order.
-template <int K>
-struct RowOrder {
-  int ky[K * K], kz[K * K];
-  constexpr RowOrder() : ky(), kz() {
-    int t = 0;
-    for (int s = 0; s <= 2 * (K - 1); ++s)
-      for (int y = 0; y < K; ++y) {
-        const int z = s - y;
-        if (z < 0 || z >= K) continue;
-        ky[t] = y;
-        kz[t] = z;
-        ++t;
-      }
-  }
-};
-
 template <int R, int RX, bool kFlat = false, bool kSparse = false, int LPQ = 1>
 __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const float* bmin, const float* bmax,
                           float bound, Knn5& r, unsigned* ks, int2* rows = nullptr, int sub = 0) {
@@ -191,70 +173,8 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
   const bool xin = xlo >= bx0 && xhi <= bx1;
   int nrow = 0;  // kFlat: rows queued
   int total = 0;  // kFlat: points queued
-#ifdef FBR_KNN_ROWS2
-  constexpr bool kRows2 = kFlat && !kSparse;
-#else
-  constexpr bool kRows2 = false;
-#endif
-  if constexpr (kRows2) {
-    // Flat queue, dense grid: every row's cell range in one round of loads.  The rows' bounds and
-    // x extents are computed first (branch-free: a pruned row reads cell_start[0] twice, an empty
-    // range), then the 2 * K * K cell_start loads are issued together and the non-empty rows are
-    // queued in the same order as the per-row form, so the queue and the walk are unchanged.
-    constexpr int NR = K * K;
-    constexpr RowOrder<K> ord{};
-    const float cut = fminf(bound, kBelowOne);  // r is still empty (kKnnEmpty: d = 1.0)
-#ifndef FBR_KNN_ROWS2_NB
-#define FBR_KNN_ROWS2_NB 32
-#endif
-    constexpr int NB = FBR_KNN_ROWS2_NB < NR ? FBR_KNN_ROWS2_NB : NR;
 #pragma unroll
-    for (int u0 = 0; u0 < NR; u0 += NB) {
-      int bb[NB], ee[NB];
-      bool rin[NB];
-#pragma unroll
-      for (int u = 0; u < NB; ++u) {
-        if (u0 + u >= NR) continue;
-        const int ky = ord.ky[u0 + u], kz = ord.kz[u0 + u];
-        const int y = cy + oyk[ky], z = cz + ozk[kz];
-        float lb = 0.0f;
-        lb += ly2[ky];
-        lb += lz2[kz];
-        int xa = 0, xb = 0;  // the per-row form's x extent
-        bool go_a = true, go_b = true;
-#pragma unroll
-        for (int o = 1; o <= RX; ++o) {
-          float ta = 0.0f, tb = 0.0f;
-          ta += lxm2[o]; ta += ly2[ky]; ta += lz2[kz];
-          tb += lxp2[o]; tb += ly2[ky]; tb += lz2[kz];
-          go_a = go_a && !(ta > cut);
-          go_b = go_b && !(tb > cut);
-          if (go_a) xa = -o;
-          if (go_b) xb = o;
-        }
-        const int x0 = max(cx + xa, 0), x1 = min(cx + xb, X - 1);
-        const bool ok = y >= 0 && y < Y && z >= 0 && z < Z && !(lb > cut) && x0 <= x1;
-        const int rowbase = (z * Y + y) * X;
-        bb[u] = m.cell_start[ok ? rowbase + x0 : 0];
-        ee[u] = m.cell_start[ok ? rowbase + x1 + 1 : 0];
-        const float ylo = (fy + (float)oyk[ky]) * c, zlo = (fz + (float)ozk[kz]) * c;
-        rin[u] = xin & (ylo >= by0) & (ylo + c <= by1) & (zlo >= bz0) & (zlo + c <= bz1);
-      }
-#pragma unroll
-      for (int u = 0; u < NB; ++u) {
-        if (u0 + u >= NR) continue;
-        FBR_KS(1, 1);
-        FBR_KS(2, ee[u] > bb[u] ? 1 : 0);
-        FBR_KS(3, ee[u] - bb[u]);
-        if (ee[u] > bb[u]) {
-          rows[nrow++ * kResThreads] = make_int2(bb[u], rin[u] ? (int)((unsigned)ee[u] | 0x80000000u) : ee[u]);
-          total += ee[u] - bb[u];
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int ksum = 0; ksum <= 2 * (K - 1) && !kRows2; ++ksum) {
+  for (int ksum = 0; ksum <= 2 * (K - 1); ++ksum) {
 #pragma unroll
     for (int ky = 0; ky < K; ++ky) {
       const int kz = ksum - ky;

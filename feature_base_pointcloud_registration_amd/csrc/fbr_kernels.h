@@ -254,6 +254,7 @@ void free_grid(DevGrid& d);
 int grid_build_device(hipStream_t s, DevArena& ar, const float4* pts, int64_t n, float invx, float inv,
                       bool force_sparse, DevGrid& out);
 
+struct JobResult;
 struct GnArgs {
   int B, max_iter;
   const float4* cornerDS;
@@ -297,6 +298,18 @@ struct GnArgs {
   int deg_carry;             // isDegenerate before the first LMOptimization (the member carried
                              // across registration() calls, mapOptmization.h:137); 0 for batch jobs
   unsigned long long* knn_stats;  // diagnostic builds (FBR_KNN_STATS): the kNN counters, else null
+  // Single scans (fbr_process_scan): the k_gn_solve that ends the run (no job active, or the last
+  // iteration) also runs transformUpdate and packs each job's JobResult into host-mapped memory
+  // (`direct`, pad = direct_gen), so the host reads the result without a finalize launch, a pack
+  // launch and a copy.  null: the host enqueues k_gn_finalize and k_pack_results.
+  JobResult* direct;
+  int32_t* direct_done;      // [1] the ending solve's claim (zeroed by k_gn_init)
+  int32_t direct_gen;
+  const int32_t* nvalid;     // the pack's inputs: [B] valid points, corner / surf features, the
+  const int32_t* ncorner;    // features' capacity flags, CropBox counts [B][2]
+  const int32_t* nsurf;
+  const int32_t* ferr;
+  const int32_t* cropcnt;
 };
 #ifdef FBR_KNN_STATS
 unsigned long long* knn_stats_buffer();

@@ -42,6 +42,7 @@ __global__ void k_gn_init(GnArgs a) {
   __shared__ int32_t scan[1024];
   const int tid = threadIdx.x;
   for (int i = tid; i < 4 * max(1, a.max_iter); i += 1024) a.iter_cnt[i] = 0;  // k_gn_solve's + block-tile counters
+  if (a.direct_done && tid == 0) *a.direct_done = 0;
   int base = 0;
   for (int j0 = 0; j0 < a.B; j0 += 1024) {
     const int job = j0 + tid;
@@ -105,36 +106,9 @@ k_gn_residual(GnArgs a) {
 }
 
 
-// Two waves per job: wave 0's lanes 0..27 sum the job's item partials (each entry in item order,
-// as before); then wave 0's lane 0 solves the normal equations while, at iteration 0, wave 1's
-// lane 0 computes the degeneracy projection (the two are independent; on one wave they would run
-// back to back); lane 0 then runs the rest of the LMOptimization step.  The number of jobs still
-// iterating is accumulated with agent-scope atomics; the last workgroup to finish publishes it to
-// host-mapped memory as (generation << 32 | count) so the host stops enqueueing iterations once
-// the batch converged.
-__global__ void __launch_bounds__(kSolveThreads) k_gn_solve(GnArgs a, int iter_idx, unsigned long long gen) {
-  __shared__ SolveLds sl;
-  const int job = blockIdx.x, tid = threadIdx.x;
-  gn_solve_block(a, job, sl);
+// transformUpdate of one job (:1444-1479) into pose_out / stats.
+__device__ void gn_finalize_job(const GnArgs& a, int job) {
   const GnState& g = a.gn[job];
-  if (tid == 0) {
-    atomicAdd(&a.iter_cnt[2 * iter_idx], g.active);
-    __threadfence();
-    const int done = atomicAdd(&a.iter_cnt[2 * iter_idx + 1], 1);
-    if (done == a.B - 1) {
-      __threadfence();
-      const int cnt = atomicAdd(&a.iter_cnt[2 * iter_idx], 0);
-      if (a.iter_flags)
-        __hip_atomic_store(&a.iter_flags[iter_idx], (gen << 32) | (unsigned long long)cnt, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-
-__global__ void k_gn_finalize(GnArgs a) {
-  const int job = blockIdx.x * blockDim.x + threadIdx.x;
-  if (job >= a.B) return;
-  GnState& g = a.gn[job];
   float p[6];
   for (int k = 0; k < 6; ++k) p[k] = g.pose[k];
   if (g.status == FBR_REG_OK) {  // transformUpdate (:1444-1479)
@@ -158,6 +132,83 @@ __global__ void k_gn_finalize(GnArgs a) {
   s.n_sel = g.n_sel;
   s.n_corner_ds = a.ncds[job];
   s.n_surf_ds = a.nsds[job];
+}
+
+// One job's packed result (k_pack_results; the solve's direct path with pad = the run's generation).
+__device__ JobResult pack_job(int j, int with_reg, const float* pose_out, const fbr_reg_stats* stats,
+                              const int32_t* nvalid, const int32_t* ncorner, const int32_t* nsurf,
+                              const int32_t* cropcnt, const int32_t* err, const float* guess, int32_t pad) {
+  JobResult r;
+  if (with_reg && guess && err[j]) {  // batch job over the feature capacity: the guess, flagged
+    for (int k = 0; k < 6; ++k) r.pose[k] = guess[6 * j + k];
+    r.st = fbr_reg_stats{};
+    r.st.status = FBR_REG_FEATURE_CAPACITY;
+    r.st.n_corner_map = cropcnt[2 * j];
+    r.st.n_surf_map = cropcnt[2 * j + 1];
+  } else if (with_reg) {
+    for (int k = 0; k < 6; ++k) r.pose[k] = pose_out[6 * j + k];
+    r.st = stats[j];
+    r.st.n_corner_map = cropcnt[2 * j];
+    r.st.n_surf_map = cropcnt[2 * j + 1];
+  } else {
+    for (int k = 0; k < 6; ++k) r.pose[k] = 0.0f;
+    r.st = fbr_reg_stats{};
+    r.st.status = FBR_REG_SKIPPED_INTERVAL;
+  }
+  r.st.n_points = nvalid[j];
+  r.st.n_corner = ncorner[j];
+  r.st.n_surf = nsurf[j];
+  r.err = err[j];
+  r.pad = pad;
+  return r;
+}
+
+// Two waves per job: wave 0's lanes 0..27 sum the job's item partials (each entry in item order,
+// as before); then wave 0's lane 0 solves the normal equations while, at iteration 0, wave 1's
+// lane 0 computes the degeneracy projection (the two are independent; on one wave they would run
+// back to back); lane 0 then runs the rest of the LMOptimization step.  The number of jobs still
+// iterating is accumulated with agent-scope atomics; the last workgroup to finish publishes it to
+// host-mapped memory as (generation << 32 | count) so the host stops enqueueing iterations once
+// the batch converged.
+__global__ void __launch_bounds__(kSolveThreads) k_gn_solve(GnArgs a, int iter_idx, unsigned long long gen) {
+  __shared__ SolveLds sl;
+  const int job = blockIdx.x, tid = threadIdx.x;
+  gn_solve_block(a, job, sl);
+  const GnState& g = a.gn[job];
+  if (tid == 0) {
+    atomicAdd(&a.iter_cnt[2 * iter_idx], g.active);
+    __threadfence();
+    const int done = atomicAdd(&a.iter_cnt[2 * iter_idx + 1], 1);
+    if (done == a.B - 1) {
+      __threadfence();
+      const int cnt = atomicAdd(&a.iter_cnt[2 * iter_idx], 0);
+      // the run ends here (the host enqueues nothing after a zero count, and no iteration after the
+      // last): transformUpdate and the packed results straight into host memory, once per run
+      // (the host enables it for one-job runs, where this thread's own solve wrote the job's state)
+      if (a.direct && (cnt == 0 || iter_idx == a.max_iter - 1) && atomicExch(a.direct_done, 1) == 0) {
+        constexpr int NW = (int)(sizeof(JobResult) / 4);  // the last word is pad: the generation
+        for (int j = 0; j < a.B; ++j) {
+          gn_finalize_job(a, j);
+          const JobResult r = pack_job(j, 1, a.pose_out, a.stats, a.nvalid, a.ncorner, a.nsurf, a.cropcnt, a.ferr,
+                                       nullptr, a.direct_gen);
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(&r);
+          uint32_t* d = reinterpret_cast<uint32_t*>(a.direct + j);
+          for (int q = 0; q < NW - 1; ++q) __hip_atomic_store(d + q, w[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __threadfence_system();  // the record before its generation word
+          __hip_atomic_store(d + NW - 1, w[NW - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __threadfence_system();
+      }
+      if (a.iter_flags)
+        __hip_atomic_store(&a.iter_flags[iter_idx], (gen << 32) | (unsigned long long)cnt, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+__global__ void k_gn_finalize(GnArgs a) {
+  const int job = blockIdx.x * blockDim.x + threadIdx.x;
+  if (job < a.B) gn_finalize_job(a, job);
 }
 
 // CropBox counts of the global map for every job's box (laserCloud{Corner,Surf}FromMapDSNum,
@@ -200,30 +251,7 @@ __global__ void k_pack_results(int B, int with_reg, const float* pose_out, const
                                const int32_t* nvalid, const int32_t* ncorner, const int32_t* nsurf,
                                const int32_t* cropcnt, const int32_t* err, const float* guess, JobResult* out) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= B) return;
-  JobResult r;
-  if (with_reg && guess && err[j]) {  // batch job over the feature capacity: the guess, flagged
-    for (int k = 0; k < 6; ++k) r.pose[k] = guess[6 * j + k];
-    r.st = fbr_reg_stats{};
-    r.st.status = FBR_REG_FEATURE_CAPACITY;
-    r.st.n_corner_map = cropcnt[2 * j];
-    r.st.n_surf_map = cropcnt[2 * j + 1];
-  } else if (with_reg) {
-    for (int k = 0; k < 6; ++k) r.pose[k] = pose_out[6 * j + k];
-    r.st = stats[j];
-    r.st.n_corner_map = cropcnt[2 * j];
-    r.st.n_surf_map = cropcnt[2 * j + 1];
-  } else {
-    for (int k = 0; k < 6; ++k) r.pose[k] = 0.0f;
-    r.st = fbr_reg_stats{};
-    r.st.status = FBR_REG_SKIPPED_INTERVAL;
-  }
-  r.st.n_points = nvalid[j];
-  r.st.n_corner = ncorner[j];
-  r.st.n_surf = nsurf[j];
-  r.err = err[j];
-  r.pad = 0;
-  out[j] = r;
+  if (j < B) out[j] = pack_job(j, with_reg, pose_out, stats, nvalid, ncorner, nsurf, cropcnt, err, guess, 0);
 }
 
 void launch_pack_results(hipStream_t s, int B, int with_reg, const float* pose_out, const fbr_reg_stats* stats,
