@@ -133,7 +133,13 @@ struct GnRun {
   int active[kMaxSub] = {};  // jobs still iterating `lag` iterations ago (an upper bound now)
   int it[kMaxSub] = {};      // next iteration to enqueue
   long polls[kMaxSub] = {};  // unanswered flag reads of the current wait
+  std::chrono::steady_clock::time_point wait0[kMaxSub];  // start of the current wait
 };
+
+// A flag wait asks the runtime whether the stream drained (flags not visible although the work
+// is done) only after this long: hipStreamQuery puts a marker into the stream, and a marker between
+// two iterations' kernels cost ~5.7 us on the device (every launch enqueued after a wait had one).
+constexpr int64_t kStreamQueryAfterNs = 2000000;
 
 struct fbr_ctx {
   fbr_params P;
@@ -776,8 +782,11 @@ int gn_run_pass(fbr_ctx* c, GnRun& r, bool block, bool* progress) {
       volatile unsigned long long* f = c->h_iter_flags + (int64_t)sb.k * mi + (it - r.lag);
       unsigned long long v = *f;
       const auto tspin = std::chrono::steady_clock::now();
+      if (r.polls[k] == 0) r.wait0[k] = tspin;
       while ((v >> 32) != g32) {
-        if ((++r.polls[k] & 1023) == 1023) {
+        if ((++r.polls[k] & 1023) == 1023 &&
+            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - r.wait0[k]).count() >
+                kStreamQueryAfterNs) {
           const hipError_t q = hipStreamQuery(sb.st);
           if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
           if (q == hipSuccess && ((v = *f) >> 32) != g32) {
@@ -901,9 +910,11 @@ int stage_register(fbr_ctx* c, const Sub& sb, bool trace) {
 int wait_direct(fbr_ctx* c, bool* got) {
   volatile int32_t* gen = &c->h_direct->pad;
   *got = false;
+  const auto t0 = std::chrono::steady_clock::now();
   for (int64_t polls = 1;; ++polls) {
     if (*gen == c->direct_gen) break;
-    if ((polls & 1023) == 0) {
+    if ((polls & 1023) == 0 && std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                   std::chrono::steady_clock::now() - t0).count() > kStreamQueryAfterNs) {
       const hipError_t q = hipStreamQuery(c->stream);
       if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
       if (q == hipSuccess && *gen != c->direct_gen) return FBR_OK;
