@@ -1208,8 +1208,18 @@ __device__ int vr_sort_runs(const uint32_t* kb, int R, uint16_t* sid, uint16_t* 
 // ring holds ~1.5k candidates in ~230 runs of equal keys (C2).  (Round 4 also measured one wave
 // per ring: 2.3x fewer VALU instructions than the 512-thread kernel but ~14 dependent round trips
 // per ring, slower overall; removed in round 5.)
+// Occupancy (round 5): the ring's waves mostly wait on their few dependent memory round trips, so
+// more rings per CU pay.  Pass A keeps only x, y, z of its points (80 -> 72 VGPRs: still 6-7 waves
+// per SIMD, no change), and KQ = 8 is held to 64 VGPRs (8 waves per SIMD) at the cost of 44 B of
+// spills: voxel_ring 1.37 -> 1.22 ms per B = 1024 step, 106.4k -> 109.3k scans/s interleaved
+// (profiles/r05af_voxel_ring_occupancy_ab.txt).  KQ = 16 (rings of 2049-4096 points) keeps its own
+// allocation (the compiler's choice for this attribute pair: 118 VGPRs, 28 B of spills).  The
+// allocation is sensitive to the attribute's spelling: (8) on both instances or (8, 8) here gives
+// 64 VGPRs; a separate kernel per KQ or (8, 8) with another maximum for KQ = 16 missed the target
+// (69 VGPRs, 7 waves) on this compiler.
 template <int KQ>  // steps of 64 points per wave: 4 * 64 * KQ >= the ring capacity
-__global__ void __launch_bounds__(256) k_voxel_ring_q(VgRing A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KQ <= 8 ? 8 : 1, KQ <= 8 ? 8 : 10)))
+k_voxel_ring_q(VgRing A) {
   constexpr int NW = 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ float mmx[NW][6];
@@ -1316,8 +1326,8 @@ __global__ void __launch_bounds__(256) k_voxel_ring_q(VgRing A) {
     const uint64_t b = __ballot(cd[u]);
     const int pos = base + __popcll(b & lt);
     if (cd[u]) {
-      if (G.overflow) {
-        out[pos] = pt[u];  // PCL: "Leaf size is too small" -> output = input, in index order
+      if (G.overflow) {  // PCL: "Leaf size is too small" -> output = input, in index order
+        out[pos] = CL[q0 + 64 * u + lane];  // re-read: only x, y, z stay live from pass A
       } else {
         kb[pos] = G.key(pt[u]);
         off[pos] = (uint16_t)(q0 + 64 * u + lane);
