@@ -39,7 +39,7 @@ cp $OUT/sq_decomp.json profiles/sq_decomp.json
 cat $OUT/hbm_traffic.txt $OUT/valu_pmc.txt $OUT/sq_decomp.txt $OUT/mem_pmc.txt
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- python3 $CMD > $OUT/bench_trace.log 2>&1 || exit 22
 echo trace done
-python3 tools/roofline_check.py $(find $OUT/trace -name "*kernel_stats.csv" | head -1) $OUT/bench_trace.log > $OUT/roofline_check.txt 2>&1 || exit 23
+python3 tools/roofline_check.py $(find $OUT/trace -name "*kernel_stats.csv" | head -1) $OUT/bench_trace.log --trace $(find $OUT/trace -name "*kernel_trace.csv" | head -1) > $OUT/roofline_check.txt 2>&1 || exit 23
 python3 tools/concurrency.py $(find $OUT/trace -name "*kernel_trace.csv" | head -1) 6 > $OUT/concurrency.txt 2>&1 || exit 24
 cat $OUT/roofline_check.txt $OUT/concurrency.txt
 C5="bench.py --config C5 --batch 16 --steps 3 --warmup 1 --latency 0 --ingest 0 --exact-line 0 --no-cpu-baseline"

@@ -9,7 +9,13 @@ bench's algorithmic bytes per launch (bench.py kernel_bytes / DESIGN.md §4), an
 carries them, the VALU-issue fraction each gives for the bench's VALU instructions per launch
 (rocprofv3 SQ pass, tools/valu_pmc.py) against the measured issue peak (profiles/valu_calib.json).
 
-usage: roofline_check.py KERNEL_STATS.csv BENCH.json [--peak 8000]
+With --trace KERNEL_TRACE.csv (the same run's rocprofv3 kernel trace) the rocprofv3 column covers
+the timed region only: per launcher, the dispatches after the untimed launches' share (bench.py runs
+`warmup` launches, then one profiled launch alone, then the `steps` timed ones; k_project dispatches
+count the launches).  The stats summary averages the untimed launches too, which run with fewer
+launches beside them, so their kernels are shorter than the overlapped ones the bench times.
+
+usage: roofline_check.py KERNEL_STATS.csv BENCH.json [--trace KERNEL_TRACE.csv] [--peak 8000]
 """
 import argparse
 import csv
@@ -31,17 +37,35 @@ def rocprof_avg_us(rows, symbols):
     return (total_ns / calls / 1e3, calls) if calls else (None, 0)
 
 
+def trace_avg_us(trace_rows, symbols, skip_frac):
+    """Mean launcher-call duration from per-dispatch rows, dropping the first skip_frac of each
+    symbol's dispatches (in start order)."""
+    total_ns, calls = 0.0, 0
+    for sym in symbols:
+        d = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in trace_rows if sym in r["Kernel_Name"])
+        d = d[int(round(skip_frac * len(d))):]
+        total_ns += sum(e - b for b, e in d)
+        calls = max(calls, len(d))
+    return (total_ns / calls / 1e3, calls) if calls else (None, 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("stats_csv")
     ap.add_argument("bench_json")
     ap.add_argument("--peak", type=float, default=8000.0, help="GB/s (MI355X HBM3E spec)")
+    ap.add_argument("--trace", default=None, help="the same run's kernel_trace.csv: timed region only")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.stats_csv)))
     with open(a.bench_json) as f:
         line = [l for l in f.read().splitlines() if l.strip().startswith("{")][-1]
     res = json.loads(line)
     roof = res["roofline"]
+    trace_rows, skip = None, 0.0
+    if a.trace:
+        trace_rows = list(csv.DictReader(open(a.trace)))
+        nlaunch = sum(1 for r in trace_rows if "k_project" in r["Kernel_Name"])
+        skip = (nlaunch - res["steps"]) / nlaunch if nlaunch else 0.0  # warmup + the profiled launch
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -51,7 +75,10 @@ def main():
           f"{'bench frac':>10s} {'rocprof frac':>12s} {'bench valu':>10s} {'rocprof valu':>12s}")
     nan = float("nan")
     for k, r in roof["kernels"].items():
-        avg, calls = rocprof_avg_us(rows, symbols.get(k, [k]))
+        if trace_rows is not None:
+            avg, calls = trace_avg_us(trace_rows, symbols.get(k, [k]), skip)
+        else:
+            avg, calls = rocprof_avg_us(rows, symbols.get(k, [k]))
         bpl = r["bytes_per_launch"]
         rf = bpl / (avg * 1e-6) / 1e9 / a.peak if avg else nan
         vb = r.get("valu_frac", nan)
