@@ -32,16 +32,54 @@ struct Knn5 {
 __device__ __forceinline__ float knn_d(unsigned long long k) { return __int_as_float((int)(k >> 32)); }
 __device__ __forceinline__ int knn_id(unsigned long long k) { return (int)(unsigned)k; }
 
-// Branch-free sorted insertion: the "less than slot t" flags are monotone over t, so every slot
-// takes its own key, its left neighbour's, or the new one (5 compares + 20 selects, no SALU mask
-// arithmetic and no serial compare-swap chain).
-__device__ __forceinline__ void knn_insert(Knn5& r, unsigned long long x) {
+// The sorted insertion of a key into the 5-NN list as v_min_f64 / v_max_f64 over the keys read as
+// doubles: a key's high word is the
+// bits of a float d2 >= +0 (at most +inf = 0x7f800000 for a point outside the crop box), so every
+// key is a non-negative finite double (a subnormal when d2 = 0; the kernels keep f64 denormals,
+// amdhsa_float_denorm_mode_16_64 3) and double order is the key's unsigned order.  9 v_min_f64 /
+// v_max_f64 instead of 5 64-bit compares, 20 selects and the wait states between them.  Written as
+// inline asm: the compiler's fmin / fmax quiet-NaN canonicalisation of the loop-carried keys would
+// add a v_max_f64 per slot.
+// The slots do not chain: with k sorted, the new k[t] is min(k[t], max(k[t-1], x)) (x below k[t-1]
+// shifts k[t-1] up, else x or k[t] stays), so every slot is two operations deep, visited from the top
+// so each max reads the old k[t-1].
+__device__ __forceinline__ void knn_insert_f64(Knn5& r, unsigned long long xk) {
+  const double x = __longlong_as_double((long long)xk);
+  double k[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) k[t] = __longlong_as_double((long long)r.k[t]);
+#pragma unroll
+  for (int t = 4; t > 0; --t) {
+    double m;
+    asm("v_max_f64 %0, %1, %2" : "=v"(m) : "v"(k[t - 1]), "v"(x));
+    asm("v_min_f64 %0, %0, %1" : "+v"(k[t]) : "v"(m));
+  }
+  asm("v_min_f64 %0, %0, %1" : "+v"(k[0]) : "v"(x));
+#pragma unroll
+  for (int t = 0; t < 5; ++t) r.k[t] = (unsigned long long)__double_as_longlong(k[t]);
+}
+// Branch-free sorted insertion with selects: the "less than slot t" flags are monotone over t, so
+// every slot takes its own key, its left neighbour's, or the new one (5 compares + 20 selects).
+__device__ __forceinline__ void knn_insert_sel(Knn5& r, unsigned long long x) {
   bool lt[5];
 #pragma unroll
   for (int t = 0; t < 5; ++t) lt[t] = x < r.k[t];
 #pragma unroll
   for (int t = 4; t > 0; --t) r.k[t] = lt[t - 1] ? r.k[t - 1] : (lt[t] ? x : r.k[t]);  // lt[t-1] implies lt[t]
   r.k[0] = lt[0] ? x : r.k[0];
+}
+// Which form a kernel uses (round 5, profiles/r05aj_*, r05ak_knn_f64_insert_ab.txt): the f64 form
+// for the 1 m (C2) and 0.25 m cells, where it took gn_knn 2.29 -> 2.00 ms per B = 1024 step
+// (flat dispatch VALU 1.745e8 -> 1.342e8) and C2 109.5k -> 112-113k scans/s; the selects for the
+// 0.5 m cells (C3, C5), whose per-row kernel at 85 -> 90 VGPRs lost 2.5 % on C3 with the f64 form
+// (C5 gained 1.5 %).  FBR_KNN_F64_R2=1 builds the f64 form there too.
+#ifndef FBR_KNN_F64_R2
+#define FBR_KNN_F64_R2 0
+#endif
+template <int R>
+__device__ __forceinline__ void knn_insert(Knn5& r, unsigned long long x) {
+  if constexpr (R != 2 || FBR_KNN_F64_R2) knn_insert_f64(r, x);
+  else knn_insert_sel(r, x);
 }
 
 // pcl::CropBox's inclusive test (p outside [bmin, bmax] on some axis) as one compare: for finite
@@ -227,7 +265,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
 #ifdef FBR_KNN_STATS
         if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ks[7] += 1;  // one per wave iteration
 #endif
-        knn_insert(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
+        knn_insert<R>(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
       }
     }
   }
@@ -260,7 +298,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         ks[11] += 1;
       }
 #endif
-      knn_insert(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
+      knn_insert<R>(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
     }
   }
 }
@@ -279,7 +317,7 @@ __device__ __forceinline__ void knn5_merge(Knn5& r) {
       o[t] = ((unsigned long long)hi << 32) | lo;
     }
 #pragma unroll
-    for (int t = 0; t < 5; ++t) knn_insert(r, o[t]);
+    for (int t = 0; t < 5; ++t) knn_insert_f64(r, o[t]);
   }
 }
 

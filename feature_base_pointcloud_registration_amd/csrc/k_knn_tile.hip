@@ -360,7 +360,7 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tile(GnArgs a, int iter, un
             diff = q.y0 - p.y; dist += diff * diff;
             diff = q.z0 - p.z; dist += diff * diff;
             const unsigned hb = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
-            knn_insert(nn, ((unsigned long long)hb << 32) | (unsigned)__float_as_int(p.w));
+            knn_insert<R>(nn, ((unsigned long long)hb << 32) | (unsigned)__float_as_int(p.w));
           }
         } else {  // the tile did not fit: the grid search
           unsigned ks[12] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};

@@ -787,6 +787,54 @@ def test_stream_surf_walk_window_is_unobservable(c2_map):
     assert r.stdout == _stream_sequence_bytes(c2_map, scans)
 
 
+def _mixed_sequence_bytes(c2_map, scans, guesses):
+    """Single scans (pose chain; one inside the mapping_process_interval gate), a batch staged and
+    launched right after a single scan (its no-op GN tail may still be queued), more single scans,
+    then fbr_project + fbr_extract_features: every result's bytes."""
+    H, W = synth.CONFIGS["C2"][:2]
+    out = b""
+    with api.Context(default_params(H, W, max_batch=2)) as ctx:
+        ctx.set_map(*c2_map)
+        pose = guesses[0].copy()
+        for k, stamp in enumerate([0.0, 0.2, 0.25, 0.5]):  # 0.25: inside the 0.15 s gate -> skipped
+            pose, st = ctx.process_scan(scans[k], stamp, pose)
+            out += pose.tobytes() + np.array([st[f] for f in sorted(st)], np.float64).tobytes()
+        ctx.batch_stage(scans[4:6], guesses[4:6])
+        ctx.batch_launch()
+        pb, sb = ctx.batch_results()
+        out += pb.tobytes() + sb.tobytes()
+        for k, stamp in enumerate([1.0, 1.2]):
+            pose, st = ctx.process_scan(scans[6 + k], stamp, pose)
+            out += pose.tobytes() + np.array([st[f] for f in sorted(st)], np.float64).tobytes()
+        f = ctx.extract_features(len(ctx.project(scans[0])["col_ind"]))
+        out += f["label"].tobytes() + f["corner"].tobytes() + f["surf"].tobytes()
+    return out
+
+
+def test_single_scan_direct_results_match_enqueued_path(c2_map):
+    """fbr_process_scan takes its pose and statistics from the GN solve that ends the run (host-mapped
+    record, no finalize / pack launch or copy, the no-op iterations enqueued ahead may still be
+    queued when it returns).  A mixed sequence of single scans (one gated off), a batch launched right
+    after a single scan, and a projection + feature call is byte-equal to the enqueued path
+    (FBR_DIRECT=0, child process)."""
+    import subprocess
+    import sys
+    jobs = synth.make_jobs("C2", 8, base_seed=680)
+    scans, guesses = [j[0] for j in jobs], np.stack([j[1] for j in jobs])
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_child_mixed_seq.npz")
+    np.savez(path, *scans, guesses=guesses, cmap=c2_map[0], smap=c2_map[1])
+    code = ("import sys, numpy as np; sys.path[:0] = [%r, %r, %r]; "
+            "import test_gpu_parity as T; d = np.load(%r); "
+            "sc = [d['arr_%%d' %% k] for k in range(%d)]; "
+            "sys.stdout.buffer.write(T._mixed_sequence_bytes((d['cmap'], d['smap']), sc, d['guesses']))"
+            % (REPO, os.path.join(REPO, "oracle"), os.path.dirname(os.path.abspath(__file__)), path, len(scans)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=300,
+                       env=dict(os.environ, FBR_DIRECT="0"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    here = _mixed_sequence_bytes(c2_map, scans, guesses)
+    assert len(here) > 0 and r.stdout == here
+
+
 def test_exact_voxel_order_gives_bit_identical_poses(c2_map):
     """exact_voxel_order = 1: every VoxelGrid sums a voxel's points in std::sort's order
     (csrc/fbr_introsort.h), so the per-ring, mapping-DS and start-up map centroids are PCL's bit for
