@@ -253,14 +253,14 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       }
       for (int i = LPQ == 1 ? b : b + ((sub - b) & (LPQ - 1)); i < e; i += LPQ) {
         const float4 p = m.pts[i];
-        // pcl::CropBox (inclusive) as one mask: a point outside gets d2 = +inf (never inserted)
-        bool out = false;  // rows inside the box skip the test
-        if (!inside) out = crop_out(p, bx0, by0, bz0, bx1, by1, bz1);
         float dist = 0.0f, diff;
         diff = qx - p.x; dist += diff * diff;                            // flann::L2_Simple
         diff = qy - p.y; dist += diff * diff;
         diff = qz - p.z; dist += diff * diff;
-        const unsigned hi = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
+        // pcl::CropBox (inclusive) as one mask: a point outside gets d2 = +inf (never inserted);
+        // rows inside the box skip the test
+        unsigned hi = (unsigned)__float_as_int(dist);
+        if (!inside && crop_out(p, bx0, by0, bz0, bx1, by1, bz1)) hi = 0x7f800000u;
         FBR_KS(4, __int_as_float((int)hi) < knn_d(r.k[4]) ? 1 : 0);
 #ifdef FBR_KNN_STATS
         if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ks[7] += 1;  // one per wave iteration
@@ -283,13 +283,14 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         inside = q.y < 0;
       }
       const float4 p = m.pts[i++];
-      bool out = false;
-      if (!inside) out = crop_out(p, bx0, by0, bz0, bx1, by1, bz1);
       float dist = 0.0f, diff;
       diff = qx - p.x; dist += diff * diff;  // flann::L2_Simple
       diff = qy - p.y; dist += diff * diff;
       diff = qz - p.z; dist += diff * diff;
-      const unsigned hi = out ? 0x7f800000u : (unsigned)__float_as_int(dist);
+      // the distance unconditionally, the box test only on rows that straddle the box: the
+      // compiler otherwise sinks the distance under a branch on the test's result
+      unsigned hi = (unsigned)__float_as_int(dist);
+      if (!inside && crop_out(p, bx0, by0, bz0, bx1, by1, bz1)) hi = 0x7f800000u;
       FBR_KS(4, __int_as_float((int)hi) < knn_d(r.k[4]) ? 1 : 0);
       FBR_KS(10, __int_as_float((int)hi) <= fminf(bound, kBelowOne) ? 1 : 0);  // within the static cut
 #ifdef FBR_KNN_STATS
