@@ -37,6 +37,23 @@ constexpr float kGridCell = 1.0f;         // kNN search grid cell (>= sqrt of th
 // and rounding it to float is innocuous for sqrt (53 >= 2*24+2 bits).
 __host__ __device__ inline float sqrt_rn(float x) { return (float)sqrt((double)x); }
 
+// 64-bit unsigned order through the f64 unit: a u64 below 0x7FF0000000000000 read as a double is a
+// non-negative, non-NaN double (a subnormal below 2^52; the kernels keep f64 denormals), and the
+// order of those doubles is the integers' order, so v_min_f64 / v_max_f64 pick the smaller / larger
+// key in one instruction each, where a 64-bit compare and two selects take three.  Inline asm: the
+// compiler's fmin / fmax would first canonicalise each operand (sNaN quieting in IEEE mode).
+constexpr unsigned long long kF64KeyMax = 0x7FEFFFFFFFFFFFFFull;  // largest such key (finite double)
+__device__ __forceinline__ unsigned long long key_min(unsigned long long a, unsigned long long b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(__longlong_as_double((long long)a)), "v"(__longlong_as_double((long long)b)));
+  return (unsigned long long)__double_as_longlong(r);
+}
+__device__ __forceinline__ unsigned long long key_max(unsigned long long a, unsigned long long b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(__longlong_as_double((long long)a)), "v"(__longlong_as_double((long long)b)));
+  return (unsigned long long)__double_as_longlong(r);
+}
+
 // x86-64 cvttsd2si: NaN / out-of-range -> INT_MIN (imageProjection.cpp:611 conversion).
 __host__ __device__ inline int x86_cvt(double v) {
   if (!(v > -2147483649.0 && v < 2147483648.0)) return (int)0x80000000;
