@@ -50,7 +50,7 @@ __device__ __forceinline__ void wsync() {
 }
 
 namespace {
-constexpr uint64_t kPadKey = ~0ull;
+constexpr uint64_t kPadKey = kF64KeyMax;  // above every (curvature bits << 16 | position) key
 constexpr int kSurfWindow = 64;  // batch surf walk: members resolved left of ep (FeatArgs::surf_full)
 constexpr int kWin = 256 + 16;  // phase-2 window: 4 chunks + 8 on each side
 constexpr int kWinBytes = kWin * (sizeof(float) + sizeof(int16_t));  // 1632 B per wave (16-B multiple)
@@ -304,7 +304,8 @@ __device__ __forceinline__ void wave_introsort_partitions(SmoothEntry* a, int n,
 // Bitonic sort of kpow (power of two, <= 128 * QP) 64-bit keys held in registers: element
 // e = 64 * r + lane sits in register r of its lane, so a compare-exchange at distance j2 < 64 is a
 // lane shuffle and one at j2 >= 64 is between two registers of the same lane.  keys[] is read
-// once and written once (it was a global-scratch network with a wave sync per stage).
+// once and written once (it was a global-scratch network with a wave sync per stage).  The keys
+// are below 2^48, so the exchanges run on the f64 unit (key_min / key_max, fbr_common.h).
 template <int QP>
 __device__ __forceinline__ void bitonic_sort_keys(uint64_t* keys, int kpow, int lane) {
   constexpr int KPL = 2 * QP;
@@ -323,9 +324,9 @@ __device__ __forceinline__ void bitonic_sort_keys(uint64_t* keys, int kpow, int 
                 const int e = 64 * r + lane;
                 const bool up = (e & k2) == 0;
                 const uint64_t x = k[r], y = k[(r + jr) % KPL];
-                const bool sw = (x > y) == up;
-                k[r] = sw ? y : x;
-                k[(r + jr) % KPL] = sw ? x : y;
+                const uint64_t mn = key_min(x, y), mx = key_max(x, y);
+                k[r] = up ? mn : mx;
+                k[(r + jr) % KPL] = up ? mx : mn;
               }
             }
           }
@@ -346,7 +347,7 @@ __device__ __forceinline__ void bitonic_sort_keys(uint64_t* keys, int kpow, int 
           const uint64_t x = k[r];
           const uint32_t ylo = __shfl_xor((uint32_t)x, j2), yhi = __shfl_xor((uint32_t)(x >> 32), j2);
           const uint64_t y = ((uint64_t)yhi << 32) | ylo;
-          const uint64_t mn = x < y ? x : y, mx = x < y ? y : x;
+          const uint64_t mn = key_min(x, y), mx = key_max(x, y);
           k[r] = (lower == up) ? mn : mx;
         }
       }
