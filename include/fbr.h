@@ -334,7 +334,11 @@ int fbr_register_trace(fbr_ctx* ctx, const fbr_point_xyzi* corner, int64_t n_cor
 
 /* One scan through the whole path in stream mode (cloudHandler after the cache queue,
  * imageProjection.cpp:197-225): the FeatureExtraction scratch state carries over between calls
- * as in the reference; `stamp` feeds the mappingProcessInterval gate (mapOptmization.h:279). */
+ * as in the reference; `stamp` feeds the mappingProcessInterval gate (mapOptmization.h:279).
+ * Returns as soon as the pose is known (the Gauss-Newton solve that ends the run writes it to
+ * host-mapped memory); Gauss-Newton iterations enqueued ahead of that point may still be draining
+ * on the context's stream, and every other entry point waits for them first.  The caller's buffer
+ * may be reused once the call returns. */
 int fbr_process_scan(fbr_ctx* ctx, const fbr_point_xyzirt* points, int64_t n_in, double stamp,
                      float pose_inout[6], fbr_reg_stats* stats);
 /* Forget the carried FeatureExtraction / time-gate state (as a freshly constructed node). */
