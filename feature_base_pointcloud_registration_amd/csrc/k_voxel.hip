@@ -1122,9 +1122,6 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
 // compare-exchanges inside a lane for distances below E, xor lane exchanges above.  The values are
 // below kF64KeyMax (a run key < 2^32 shifted by 16, or the padding kF64KeyMax), so the exchanges
 // take their minima / maxima on the f64 unit (key_min / key_max, fbr_common.h).
-#ifndef FBR_VR_F64_SORT
-#define FBR_VR_F64_SORT 1
-#endif
 template <int E>
 __device__ __forceinline__ void wave_bitonic_u64(uint64_t (&v)[E], int lane) {
   constexpr int N = 64 * E;
@@ -1140,11 +1137,7 @@ __device__ __forceinline__ void wave_bitonic_u64(uint64_t (&v)[E], int lane) {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           const uint64_t o = shfl_xor_u64(v[e], m);
-#if FBR_VR_F64_SORT
           v[e] = take_min ? key_min(o, v[e]) : key_max(o, v[e]);
-#else
-          v[e] = (take_min ? (o < v[e]) : (v[e] < o)) ? o : v[e];
-#endif
         }
       } else {
 #pragma unroll
@@ -1152,15 +1145,9 @@ __device__ __forceinline__ void wave_bitonic_u64(uint64_t (&v)[E], int lane) {
           if (e & j) continue;
           const bool asc = ((lane * E + e) & k) == 0;
           const uint64_t a = v[e], b = v[e | j];
-#if FBR_VR_F64_SORT
           const uint64_t lo = key_min(a, b), hi = key_max(a, b);
           v[e] = asc ? lo : hi;
           v[e | j] = asc ? hi : lo;
-#else
-          const bool sw = asc ? (b < a) : (a < b);
-          v[e] = sw ? b : a;
-          v[e | j] = sw ? a : b;
-#endif
         }
       }
     }
