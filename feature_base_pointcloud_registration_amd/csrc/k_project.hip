@@ -433,11 +433,14 @@ void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* n
              n_single);
 }
 
-// Compaction tile size in cells (FBR_COMPACT_CELLS: 512, 1024 or 2048).
+// Compaction tile size in cells (FBR_COMPACT_CELLS: 512, 1024 or 2048).  512 since round 5: 10 KB of
+// LDS per workgroup, twice the tiles in flight per CU; once the other kernels had shrunk, C2 B = 1024
+// 114.5-114.9k -> 115.7-115.8k and C3 +0.9 % interleaved (profiles/r05ar_compact_cells_ab.txt; it was
+// even with 1024 in round 4).
 int compact_cells() {
   static const int v = [] {
     const char* e = std::getenv("FBR_COMPACT_CELLS");
-    const int c = e ? std::atoi(e) : 1024;
+    const int c = e ? std::atoi(e) : 512;
     return c >= 2048 ? 2048 : c >= 1024 ? 1024 : 512;
   }();
   return v;
