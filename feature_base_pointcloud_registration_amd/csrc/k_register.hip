@@ -71,16 +71,23 @@ __global__ void k_gn_init(GnArgs a) {
         g.active = 0;
       }
     }
-    scan[tid] = nc_items + ns_items;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-      const int v = tid >= off ? scan[tid - off] : 0;
-      __syncthreads();
-      scan[tid] += v;
-      __syncthreads();
+    // exclusive prefix of the jobs' item counts: wave scans, then the 16 wave totals (two barriers
+    // per 1024 jobs; the Hillis-Steele form took 20, ~5 us of a single scan's critical path)
+    const int v = nc_items + ns_items, lane = tid & 63, w = tid >> 6;
+    int inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(inc, off);
+      if (lane >= off) inc += y;
     }
-    const int incl = scan[tid];
-    const int excl = base + incl - (nc_items + ns_items);
+    if (lane == 63) scan[w] = inc;
+    __syncthreads();
+    int pre = 0, tot = 0;
+    for (int k = 0; k < 16; ++k) {
+      pre += k < w ? scan[k] : 0;
+      tot += scan[k];
+    }
+    const int excl = base + pre + inc - v;
     if (job < a.B) {
       a.item_range[2 * job] = excl;
       a.item_range[2 * job + 1] = excl + nc_items + ns_items;
@@ -91,8 +98,8 @@ __global__ void k_gn_init(GnArgs a) {
       for (int t = 0; t < ns_items; ++t, ++it)
         if (it < a.max_items) a.items[it] = make_int4(job, 1, t * kResThreads, min(kResThreads, ns - t * kResThreads));
     }
-    base += scan[1023];
-    __syncthreads();
+    base += tot;
+    __syncthreads();  // every wave read scan[] before the next chunk's totals overwrite it
   }
   if (tid == 0) a.nitems[0] = min(base, a.max_items);
 }

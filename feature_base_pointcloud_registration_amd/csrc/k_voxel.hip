@@ -763,7 +763,20 @@ __global__ void __launch_bounds__(T) k_voxel_grid_split(VgArgs A, int P, unsigne
   const int hb = min(10, G.nbits), sh = G.nbits - hb, nbin = 1 << hb;
   for (int b = tid; b < nbin; b += T) hist[b] = 0u;
   __syncthreads();
-  for (int i = tid; i < n; i += T) atomicAdd(&hist[G.key(in[i]) >> sh], 1u);
+  // wave w owns the contiguous chunk [c0, c1) of the cloud (at most KPL steps of 64: n <= LCAP)
+  // and keeps its keys in registers for the compaction below (one read of the cloud)
+  const int per = (((n + NW - 1) / NW) + 63) & ~63;
+  const int c0 = min(n, w * per), c1 = min(n, c0 + per);
+  uint32_t kv[KPL];
+#pragma unroll
+  for (int k = 0; k < KPL; ++k) {
+    const int i = c0 + 64 * k + lane;
+    kv[k] = 0u;
+    if (i < c1) {
+      kv[k] = G.key(in[i]);
+      atomicAdd(&hist[kv[k] >> sh], 1u);
+    }
+  }
   __syncthreads();
   // this part's bin range [b0, b1): the first bins whose inclusive prefix exceeds n * part / P
   // and n * (part + 1) / P (inclusive scan over the bins, one bin per thread, T >= 1024)
@@ -794,36 +807,41 @@ __global__ void __launch_bounds__(T) k_voxel_grid_split(VgArgs A, int P, unsigne
     __syncthreads();
   }
   const int b0 = misc[0], b1 = misc[1];  // empty range: b0 = nbin, b1 = -1
-  // ---- this part's points in index order (block-wide ordered compaction) ----
+  // ---- this part's points in index order: every wave counts its chunk's points, one prefix over
+  // the waves, then each wave writes its chunk in order (chunks are in index order): two barriers
+  // (a block-wide pass per 1024 points took two per pass) ----
   unsigned char* q = smem + ((((unsigned char*)(misc + 4) - smem) + 15) & ~15);
   FBR_LDS_AS uint32_t* keys = (FBR_LDS_AS uint32_t*)q;
   FBR_LDS_AS uint16_t* vals = (FBR_LDS_AS uint16_t*)((FBR_LDS_AS uint32_t*)q + LCAP);
-  int nk = 0;
-  for (int i0 = 0; i0 < n; i0 += T) {
-    const int i = i0 + tid;
-    uint32_t key = 0;
-    bool keep = false;
-    if (i < n) {
-      key = G.key(in[i]);
-      const int b = (int)(key >> sh);
-      keep = b >= b0 && b <= b1;
-    }
+  const uint64_t lt = (1ull << lane) - 1ull;
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < KPL; ++k) {
+    const int i = c0 + 64 * k + lane;
+    const int b = (int)(kv[k] >> sh);
+    cnt += __popcll(__ballot(i < c1 && b >= b0 && b <= b1));
+  }
+  if (lane == 0) wsum[w] = (uint32_t)cnt;
+  __syncthreads();
+  int pre = 0, nk = 0;
+  for (int k = 0; k < NW; ++k) {
+    if (k < w) pre += (int)wsum[k];
+    nk += (int)wsum[k];
+  }
+#pragma unroll
+  for (int k = 0; k < KPL; ++k) {
+    const int i = c0 + 64 * k + lane;
+    const int b = (int)(kv[k] >> sh);
+    const bool keep = i < c1 && b >= b0 && b <= b1;
     const uint64_t m = __ballot(keep);
-    if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
-    __syncthreads();
-    int pre = nk, tot = 0;
-    for (int k = 0; k < NW; ++k) {
-      if (k < w) pre += (int)wsum[k];
-      tot += (int)wsum[k];
-    }
     if (keep) {
-      const int pos = pre + __popcll(m & ((1ull << lane) - 1ull));
-      keys[pos] = key;
+      const int pos = pre + __popcll(m & lt);
+      keys[pos] = kv[k];
       vals[pos] = (uint16_t)i;
     }
-    nk += tot;
-    __syncthreads();
+    pre += __popcll(m);
   }
+  __syncthreads();
   if (nk > 0) vg_radix_sort_inplace<T, KPL>(keys, vals, nk, G.nbits, hist, wsum);
   // ---- voxel count, publish, look back ----
   int heads = 0;
