@@ -252,7 +252,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         continue;
       }
       for (int i = LPQ == 1 ? b : b + ((sub - b) & (LPQ - 1)); i < e; i += LPQ) {
-        const float4 p = m.pts[i];
+        const float4 p = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(m.pts) + (uint32_t)i * 16u);
         float dist = 0.0f, diff;
         diff = qx - p.x; dist += diff * diff;                            // flann::L2_Simple
         diff = qy - p.y; dist += diff * diff;
@@ -282,7 +282,10 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         e = q.y & 0x7fffffff;
         inside = q.y < 0;
       }
-      const float4 p = m.pts[i++];
+      // a 32-bit byte offset (maps below 2^28 points) lets the load take the SGPR base + VGPR offset
+      // form: one shift instead of a 64-bit address per point
+      const float4 p = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(m.pts) + (uint32_t)i * 16u);
+      ++i;
       float dist = 0.0f, diff;
       diff = qx - p.x; dist += diff * diff;  // flann::L2_Simple
       diff = qy - p.y; dist += diff * diff;

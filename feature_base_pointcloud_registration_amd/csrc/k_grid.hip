@@ -161,7 +161,8 @@ bool force_sparse_env() {
 int grid_build_device(hipStream_t s, DevArena& ar, const float4* src, int64_t n, float invx, float inv,
                       bool force_sparse, DevGrid& out) {
   free_grid(out);
-  if (n > (int64_t)INT32_MAX / 2) return FBR_ERR_CAPACITY;
+  // the kNN walks address map points with a 32-bit byte offset (fbr_gn.h): below 2^28 points
+  if (n >= ((int64_t)1 << 28)) return FBR_ERR_CAPACITY;
   int rc = FBR_OK;
   auto ok = [&](hipError_t e) {
     if (e != hipSuccess && !rc) rc = FBR_ERR_HIP;
