@@ -193,8 +193,10 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
   int oyk[K], ozk[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    oyk[k] = rank_offset(k, sgy);
-    ozk[k] = rank_offset(k, sgz);
+    // flat queue: rows in one fixed order for every lane (the queued set does not depend on it), so
+    // lanes of a wave that share rows walk them in step
+    oyk[k] = kFlat ? k - R : rank_offset(k, sgy);
+    ozk[k] = kFlat ? k - R : rank_offset(k, sgz);
     const float ly = axis_lb(qy, fy, oyk[k], c), lz = axis_lb(qz, fz, ozk[k], c);
     ly2[k] = ly * ly;
     lz2[k] = lz * lz;
