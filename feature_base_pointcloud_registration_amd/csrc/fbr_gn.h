@@ -273,21 +273,28 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
   }
   if constexpr (kFlat) {
     // counted walk: one trip per queued point (the lane's total), the row advance a short branch
-    // (a while loop that tests for the next row first: +16 % per dispatch, r04ae)
+    // (a while loop that tests for the next row first: +16 % per dispatch, r04ae).  The row offset
+    // is a 32-bit byte offset (maps below 2^28 points): the load takes the SGPR base + VGPR offset
+    // form, one shift instead of a 64-bit address per point.
     int2 q = rows[0];  // unread when nothing is queued
     int j = 0, i = q.x, e = q.y & 0x7fffffff;
     bool inside = q.y < 0;
+    // one point load in flight: trip t + 1's point is requested before trip t's is tested (the
+    // last trip re-requests its own point, so no index runs past a row)
+    auto ld = [&](int k) __attribute__((always_inline)) {
+      return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(m.pts) + (uint32_t)k * 16u);
+    };
+    float4 p = ld(total > 0 ? i : 0);
     for (int t = 0; t < total; ++t) {
-      if (i == e) {  // next queued row (every queued row is non-empty)
+      const bool in_cur = inside;
+      const int cur = i;
+      if (++i == e && t + 1 < total) {  // next queued row (every queued row is non-empty)
         q = rows[++j * kResThreads];
         i = q.x;
         e = q.y & 0x7fffffff;
         inside = q.y < 0;
       }
-      // a 32-bit byte offset (maps below 2^28 points) lets the load take the SGPR base + VGPR offset
-      // form: one shift instead of a 64-bit address per point
-      const float4 p = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(m.pts) + (uint32_t)i * 16u);
-      ++i;
+      const float4 pn = ld(t + 1 < total ? i : cur);
       float dist = 0.0f, diff;
       diff = qx - p.x; dist += diff * diff;  // flann::L2_Simple
       diff = qy - p.y; dist += diff * diff;
@@ -295,7 +302,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       // the distance unconditionally, the box test only on rows that straddle the box: the
       // compiler otherwise sinks the distance under a branch on the test's result
       unsigned hi = (unsigned)__float_as_int(dist);
-      if (!inside && crop_out(p, bx0, by0, bz0, bx1, by1, bz1)) hi = 0x7f800000u;
+      if (!in_cur && crop_out(p, bx0, by0, bz0, bx1, by1, bz1)) hi = 0x7f800000u;
       FBR_KS(4, __int_as_float((int)hi) < knn_d(r.k[4]) ? 1 : 0);
       FBR_KS(10, __int_as_float((int)hi) <= fminf(bound, kBelowOne) ? 1 : 0);  // within the static cut
 #ifdef FBR_KNN_STATS
@@ -305,6 +312,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
       }
 #endif
       knn_insert<R>(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
+      p = pn;
     }
   }
 }
