@@ -253,8 +253,12 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         total += e - b;
         continue;
       }
-      for (int i = LPQ == 1 ? b : b + ((sub - b) & (LPQ - 1)); i < e; i += LPQ) {
-        const float4 p = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(m.pts) + (uint32_t)i * 16u);
+      // one point load in flight within the row (the row's last point re-requests itself)
+      const int i0 = LPQ == 1 ? b : b + ((sub - b) & (LPQ - 1));
+      float4 p = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(m.pts) + (uint32_t)(i0 < e ? i0 : b) * 16u);
+      for (int i = i0; i < e; i += LPQ) {
+        const int nx = i + LPQ < e ? i + LPQ : i;
+        const float4 pn = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(m.pts) + (uint32_t)nx * 16u);
         float dist = 0.0f, diff;
         diff = qx - p.x; dist += diff * diff;                            // flann::L2_Simple
         diff = qy - p.y; dist += diff * diff;
@@ -268,6 +272,7 @@ __device__ void knn5_grid(const MapGrid& m, float qx, float qy, float qz, const 
         if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) ks[7] += 1;  // one per wave iteration
 #endif
         knn_insert<R>(r, ((unsigned long long)hi << 32) | (unsigned)__float_as_int(p.w));
+        p = pn;
       }
     }
   }
