@@ -135,6 +135,8 @@ def parse():
     ap.add_argument("--exact-line", type=int, default=1,
                     help="rank 0 at N=1: a second context with exact_voxel_order = 1 (PCL's point order inside voxels, "
                          "bit-identical poses) reports its throughput and parity block; 0 disables")
+    ap.add_argument("--exact-voxel-order", type=int, default=0,
+                    help="fbr_params.exact_voxel_order of the main line (1: std::sort's in-voxel point order)")
     ap.add_argument("--deskew", action="store_true",
                     help="enable the IMU deskew path (SURVEY 8f row 3): one imuDeskewInfo table per job")
     ap.add_argument("--dist", action="store_true",
@@ -295,7 +297,8 @@ def main():
         counts = [args.batch] * world
     B = j1 - j0
     Bpad = max(counts)   # all-gather blocks are padded to the largest rank's
-    P = synth.config_params(cfg, max_batch=B, pipeline_depth=args.pipeline_depth)
+    P = synth.config_params(cfg, max_batch=B, pipeline_depth=args.pipeline_depth,
+                            exact_voxel_order=args.exact_voxel_order)
     corner_map, surf_map = synth.config_map(cfg)
     jobs = synth.make_jobs(cfg, B, base_seed=1000 + j0)  # job j uses seed 1000 + j
     scans = [j[0] for j in jobs]
@@ -331,7 +334,8 @@ def main():
         consecutive gathers are ordered on the device by the library)."""
         while native_done[0] < upto:
             native_done[0] += 1
-            comm.allgather(native_done[0], recv.data_ptr())
+            # recv is read on torch's stream: the next gather waits for those reads
+            comm.allgather(native_done[0], recv.data_ptr(), torch.cuda.current_stream().cuda_stream)
             gathered[0] = recv
 
     def gather_ready():

@@ -121,7 +121,7 @@ def lib():
             "fbr_comm_unique_id": (ctypes.c_int, [_VP]),
             "fbr_comm_create": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
             "fbr_comm_destroy": (ctypes.c_int, [_VP]),
-            "fbr_batch_allgather": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP]),
+            "fbr_batch_allgather": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -611,8 +611,10 @@ def comm_unique_id():
 
 class Comm:
     """The pose-record communicator of one rank (fbr_comm_create): RCCL over the context's device.
-    allgather(launch_id, recv_ptr) all-gathers that launch's 32-B records of every rank into the
-    device buffer recv_ptr ([nranks][max_jobs][8] f32) and returns the HIP stream to wait on."""
+    allgather(launch_id, recv_ptr, wait_stream) all-gathers that launch's 32-B records of every rank
+    into the device buffer recv_ptr ([nranks][max_jobs][8] f32), after the work queued on
+    wait_stream (the caller's stream still reading recv, or None), and returns the HIP stream to
+    wait on before reading recv."""
 
     def __init__(self, ctx, uid, nranks, rank, max_jobs):
         self._h = _VP()
@@ -622,10 +624,10 @@ class Comm:
         self._ctx = ctx
         self.nranks, self.rank, self.max_jobs = int(nranks), int(rank), int(max_jobs)
 
-    def allgather(self, launch_id, recv_ptr):
+    def allgather(self, launch_id, recv_ptr, wait_stream=None):
         st = _VP()
         _check(lib().fbr_batch_allgather(self._ctx._h, self._h, int(launch_id), ctypes.c_void_p(recv_ptr),
-                                         ctypes.byref(st)), "fbr_batch_allgather")
+                                         ctypes.c_void_p(wait_stream or None), ctypes.byref(st)), "fbr_batch_allgather")
         return st.value or 0
 
     def close(self):

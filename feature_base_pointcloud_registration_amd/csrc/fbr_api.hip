@@ -413,7 +413,9 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
   uint32_t* d_sc = nullptr;
   int rc = FBR_OK;
   const bool large = n >= vg_large_min();
-  if (dalloc(&d_in, n) || dalloc(&d_out, n) || dalloc(&d_cnt, 2) || (!large && dalloc(&d_sc, kVgScratch * n))) {
+  // d_cnt: {input count, output count, look-back error word (k_voxel_grid_split: a part that gave
+  // up its look-back flags it, whichever part writes the count)}
+  if (dalloc(&d_in, n) || dalloc(&d_out, n) || dalloc(&d_cnt, 3) || (!large && dalloc(&d_sc, kVgScratch * n))) {
     rc = FBR_ERR_HIP;
   } else {
     int32_t nn = (int32_t)n;
@@ -444,12 +446,15 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
       a.s[0].leaf = leaf;
       a.s[0].nseg = 1;
       a.s[0].exact = c->P.exact_voxel_order ? 1 : 0;
-      launch_voxel_grid(c->stream, a);
-      int32_t nout = 0;
-      if (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-          fbr_sync(c->stream) != hipSuccess || nout < 0) {
+      a.err = d_cnt + 2;
+      int32_t ce[2] = {0, 0};  // output count, error word
+      if (hipMemsetAsync(d_cnt + 2, 0, sizeof(int32_t), c->stream) != hipSuccess) rc = FBR_ERR_HIP;
+      if (!rc) launch_voxel_grid(c->stream, a);
+      if (rc || hipMemcpyAsync(ce, d_cnt + 1, sizeof(ce), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+          fbr_sync(c->stream) != hipSuccess || ce[0] < 0 || ce[1] != 0) {
         rc = FBR_ERR_HIP;
       } else {
+        const int32_t nout = ce[0];
         out.resize(nout);
         if (nout && fbr_memcpy_sync(out.data(), d_out, sizeof(float4) * nout, hipMemcpyDeviceToHost) != hipSuccess)
           rc = FBR_ERR_HIP;
@@ -1258,10 +1263,10 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
     (void)hipFree(d_cnt);
     return rc;
   }
-  if (dalloc(&d_cnt, 2) || dalloc(&d_sc, kVgScratch * n)) {
+  if (dalloc(&d_cnt, 3) || dalloc(&d_sc, kVgScratch * n)) {  // input count, output count, error word
     rc = FBR_ERR_HIP;
   } else {
-    int32_t nn = (int32_t)n, nout = 0;
+    int32_t nn = (int32_t)n, ce[2] = {0, 0};
     VgArgs a{};
     a.s[0].in = d_in;
     a.s[0].stride_in = n;
@@ -1274,14 +1279,16 @@ int voxel_grid_dev(fbr_ctx* c, const float4* d_in, int64_t n, float leaf, float4
     a.s[0].leaf = leaf;
     a.s[0].nseg = 1;
     a.s[0].exact = c->P.exact_voxel_order ? 1 : 0;
-    if (hipMemcpyAsync(d_cnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+    a.err = d_cnt + 2;  // a lost look-back part flags it, whichever part writes the count
+    if (hipMemcpyAsync(d_cnt, &nn, sizeof(int32_t), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemsetAsync(d_cnt + 2, 0, sizeof(int32_t), c->stream) != hipSuccess) {
       rc = FBR_ERR_HIP;
     } else {
       launch_voxel_grid(c->stream, a);
-      if (hipMemcpyAsync(&nout, d_cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-          fbr_sync(c->stream) != hipSuccess || nout < 0)
+      if (hipMemcpyAsync(ce, d_cnt + 1, sizeof(ce), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+          fbr_sync(c->stream) != hipSuccess || ce[0] < 0 || ce[1] != 0)
         rc = FBR_ERR_HIP;
-      *n_out = rc ? 0 : nout;
+      *n_out = rc ? 0 : ce[0];
     }
   }
   (void)hipFree(d_cnt);
@@ -1969,6 +1976,7 @@ struct RcclApi {
   ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
 };
 const RcclApi& rccl() {
@@ -1981,8 +1989,9 @@ const RcclApi& rccl() {
     a.get_unique_id = (decltype(a.get_unique_id))dlsym(h, "ncclGetUniqueId");
     a.comm_init_rank = (decltype(a.comm_init_rank))dlsym(h, "ncclCommInitRank");
     a.comm_destroy = (decltype(a.comm_destroy))dlsym(h, "ncclCommDestroy");
+    a.comm_abort = (decltype(a.comm_abort))dlsym(h, "ncclCommAbort");
     a.all_gather = (decltype(a.all_gather))dlsym(h, "ncclAllGather");
-    a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.all_gather;
+    a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.comm_abort && a.all_gather;
     return a;
   }();
   return api;
@@ -1995,6 +2004,8 @@ struct fbr_comm {
   float* send = nullptr;  // [max_jobs][8] this rank's padded records
   hipEvent_t done = nullptr;  // after the latest all-gather: the next one (on another launch's
   bool used = false;          // stream) reuses `send` and the caller's recv buffer
+  hipEvent_t ev_wait = nullptr;  // the caller's reader of recv (fbr_batch_allgather's wait_stream)
+  bool failed = false;        // a call returned an error: peers may be blocked, destroy aborts
 };
 
 extern "C" {
@@ -2013,6 +2024,8 @@ int fbr_comm_create(fbr_comm** out, fbr_ctx* c, const uint8_t id[FBR_COMM_ID_BYT
                     int max_jobs_per_rank) {
   if (!out || !c || !id || nranks < 1 || rank < 0 || rank >= nranks || max_jobs_per_rank < 1) return FBR_ERR_INVALID_ARG;
   *out = nullptr;
+  // every batch this ctx can stage fits the rank's block: the collective never fails on capacity
+  if (max_jobs_per_rank < c->Bcap) return FBR_ERR_CAPACITY;
   if (!rccl().ok) return FBR_ERR_UNSUPPORTED;
   CK(enter(c));
   fbr_comm* m = new fbr_comm();
@@ -2023,8 +2036,10 @@ int fbr_comm_create(fbr_comm** out, fbr_ctx* c, const uint8_t id[FBR_COMM_ID_BYT
   ncclUniqueId uid;
   std::memcpy(uid.internal, id, FBR_COMM_ID_BYTES);
   if (hipMalloc((void**)&m->send, sizeof(float) * 8 * (size_t)max_jobs_per_rank) != hipSuccess ||
-      hipEventCreateWithFlags(&m->done, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&m->done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&m->ev_wait, hipEventDisableTiming) != hipSuccess) {
     (void)hipFree(m->send);
+    if (m->done) (void)hipEventDestroy(m->done);
     delete m;
     return FBR_ERR_HIP;
   }
@@ -2032,6 +2047,7 @@ int fbr_comm_create(fbr_comm** out, fbr_ctx* c, const uint8_t id[FBR_COMM_ID_BYT
   if (rccl().comm_init_rank(&m->nc, nranks, uid, rank) != ncclSuccess) {
     (void)hipFree(m->send);
     (void)hipEventDestroy(m->done);
+    (void)hipEventDestroy(m->ev_wait);
     delete m;
     return FBR_ERR_HIP;
   }
@@ -2043,19 +2059,21 @@ int fbr_comm_destroy(fbr_comm* m) {
   if (!m) return FBR_ERR_INVALID_ARG;
   (void)hipSetDevice(m->dev);
   int rc = FBR_OK;
-  if (m->nc && rccl().comm_destroy(m->nc) != ncclSuccess) rc = FBR_ERR_HIP;
+  // after a failed collective the peers may be inside an all-gather this rank never joined:
+  // abort (tear down without the collective handshake) instead of destroying
+  if (m->nc && (m->failed ? rccl().comm_abort(m->nc) : rccl().comm_destroy(m->nc)) != ncclSuccess) rc = FBR_ERR_HIP;
   (void)hipFree(m->send);
   if (m->done) (void)hipEventDestroy(m->done);
+  if (m->ev_wait) (void)hipEventDestroy(m->ev_wait);
   delete m;
   return rc;
 }
 
-int fbr_batch_allgather(fbr_ctx* c, fbr_comm* m, int64_t launch_id, void* recv, void** done_stream) {
-  if (!c || !m || !recv) return FBR_ERR_INVALID_ARG;
-  if (done_stream) *done_stream = nullptr;
+namespace {
+int batch_allgather(fbr_ctx* c, fbr_comm* m, int64_t launch_id, void* recv, void* wait_stream, void** done_stream) {
   if (m->dev != c->dev) return FBR_ERR_INVALID_ARG;
   if (c->staged_B <= 0 || c->launch_seq == 0) return FBR_ERR_STATE;
-  if (c->staged_B > m->max_jobs) return FBR_ERR_CAPACITY;
+  if (c->staged_B > m->max_jobs) return FBR_ERR_CAPACITY;  // unreachable: fbr_comm_create checks max_batch
   if (launch_id < 0) launch_id = c->launch_seq - 1;
   if (launch_id < c->first_valid || launch_id >= c->launch_seq) return FBR_ERR_STATE;
   int s = -1;
@@ -2069,6 +2087,10 @@ int fbr_batch_allgather(fbr_ctx* c, fbr_comm* m, int64_t launch_id, void* recv, 
   hipStream_t st = r.subs[0].st;
   for (int k = 1; k < r.nsub; ++k) CK(hipStreamWaitEvent(st, c->xev[r.subs[k].k], 0));
   if (m->used) CK(hipStreamWaitEvent(st, m->done, 0));  // the previous gather (maybe another stream)
+  if (wait_stream) {  // the caller's reads of the previous result out of recv
+    CK(hipEventRecord(m->ev_wait, (hipStream_t)wait_stream));
+    CK(hipStreamWaitEvent(st, m->ev_wait, 0));
+  }
   const int64_t w0 = (int64_t)s * c->Bcap;
   if (c->staged_B < m->max_jobs)  // padding records: zeros
     CK(hipMemsetAsync(m->send + 8 * (int64_t)c->staged_B, 0, sizeof(float) * 8 * (m->max_jobs - c->staged_B), st));
@@ -2083,6 +2105,15 @@ int fbr_batch_allgather(fbr_ctx* c, fbr_comm* m, int64_t launch_id, void* recv, 
     CK(hipStreamWaitEvent(c->stream, c->ev_ext, 0));
   }
   return FBR_OK;
+}
+}  // namespace
+
+int fbr_batch_allgather(fbr_ctx* c, fbr_comm* m, int64_t launch_id, void* recv, void* wait_stream, void** done_stream) {
+  if (!c || !m || !recv) return FBR_ERR_INVALID_ARG;
+  if (done_stream) *done_stream = nullptr;
+  const int rc = batch_allgather(c, m, launch_id, recv, wait_stream, done_stream);
+  if (rc) m->failed = true;
+  return rc;
 }
 
 int fbr_batch_bytes(fbr_ctx* c, double* bytes_total, double* bytes_gn) {

@@ -100,6 +100,10 @@ struct GridDesc {        // 3D grid over a map (cell indices, not metres, in ori
 // occupied chunk stores kChunkX + 1 point offsets and is found through an open-addressing hash of
 // its (z, y, x / kChunkX) key.  A kNN row range spans at most 2 chunks (<= 2 * 8 + 1 cells).
 constexpr int kChunkX = 16;
+// A map point that can be a kNN candidate (KdTreeFLANN drops non-finite points).
+__host__ __device__ inline bool map_point_finite(const float4& p) {
+  return fabsf(p.x) <= 3.402823466e38f && fabsf(p.y) <= 3.402823466e38f && fabsf(p.z) <= 3.402823466e38f;
+}
 constexpr unsigned long long kChunkEmpty = ~0ull;
 __host__ __device__ inline unsigned long long chunk_key(int z, int y, int xc) {
   return ((unsigned long long)(unsigned)z << 48) | ((unsigned long long)(unsigned)y << 24) | (unsigned long long)(unsigned)xc;

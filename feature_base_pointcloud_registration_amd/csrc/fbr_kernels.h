@@ -147,9 +147,11 @@ struct VgSet {               // nseg segments of one cloud family, one leaf size
 constexpr int64_t kVgScratch = 5;
 struct VgArgs {
   VgSet s[2];                // segments of set 0, then of set 1 (set 1 may be empty)
-  // per-segment error words (segment j of either set = job j; may be null): k_voxel_grid_split ORs
-  // kVgErrLookback into them when its bounded look-back gives up (the segment's count is then 0;
-  // with err null it is -1, which the single-cloud callers report as FBR_ERR_HIP)
+  // per-segment error words (segment j of either set = job j): k_voxel_grid_split ORs
+  // kVgErrLookback into them when the bounded look-back of any part gives up.  A middle part that
+  // gives up skips its emit while the last part may still see every flag and write a full count,
+  // so callers must check the error word, not only the count (the batch jobs' error words, the
+  // single-cloud callers' own word).  With err null a lost last part writes -1.
   int32_t* err = nullptr;
 };
 constexpr int32_t kVgErrLookback = 16;

@@ -17,6 +17,10 @@
 //           range per row exactly as on the dense grid.
 // Both give the kNN the same candidate sets.  HBM-bound builds: 16 B read + 16 B written per
 // point plus the sort.
+// Non-finite map points are never candidates (KdTreeFLANN skips them): they stay out of the cell
+// bounds, the dense layout parks them in a phantom cell past the last real one (cell_start[n_cells]
+// ends the real cells' points), and the sparse layout sorts them behind every chunk.  They keep
+// their map index in by_id, which no neighbour list can name.
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
@@ -31,8 +35,13 @@ namespace fbr {
 __global__ void __launch_bounds__(256)
 k_grid_bounds(const float4* __restrict__ pts, int64_t n, float invx, float inv, int* bounds) {
   int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
+  int bad = 0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float4 p = pts[i];
+    if (!map_point_finite(p)) {
+      ++bad;
+      continue;
+    }
     const int c[3] = {(int)floorf(p.x * invx), (int)floorf(p.y * inv), (int)floorf(p.z * inv)};
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
@@ -51,6 +60,8 @@ k_grid_bounds(const float4* __restrict__ pts, int64_t n, float invx, float inv, 
       atomicMax(&bounds[3 + d], hi[d]);
     }
   }
+  for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o);
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(&bounds[6], bad);
 }
 
 __device__ __forceinline__ void grid_cell3(const float4& p, const GridDesc& g, int& cx, int& cy, int& cz) {
@@ -59,22 +70,25 @@ __device__ __forceinline__ void grid_cell3(const float4& p, const GridDesc& g, i
   cz = (int)floorf(p.z * g.inv_cell) - (int)g.origin[2];
 }
 
+// Dense cell of a map point; the phantom cell n_cells for a non-finite one.
+__device__ __forceinline__ int64_t grid_cell_dense(const float4& p, const GridDesc& g) {
+  if (!map_point_finite(p)) return g.n_cells;
+  int cx, cy, cz;
+  grid_cell3(p, g, cx, cy, cz);
+  return ((int64_t)cz * g.dims[1] + cy) * g.dims[0] + cx;
+}
+
 // ---- dense ----
 __global__ void __launch_bounds__(256) k_grid_count(const float4* __restrict__ pts, int64_t n, GridDesc g, int32_t* cnt) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    int cx, cy, cz;
-    grid_cell3(pts[i], g, cx, cy, cz);
-    atomicAdd(&cnt[(cz * g.dims[1] + cy) * g.dims[0] + cx], 1);
-  }
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    atomicAdd(&cnt[grid_cell_dense(pts[i], g)], 1);
 }
 
 __global__ void __launch_bounds__(256)
 k_grid_scatter(const float4* __restrict__ pts, int64_t n, GridDesc g, int32_t* fill, float4* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float4 p = pts[i];
-    int cx, cy, cz;
-    grid_cell3(p, g, cx, cy, cz);
-    const int slot = atomicAdd(&fill[(cz * g.dims[1] + cy) * g.dims[0] + cx], 1);
+    const int slot = atomicAdd(&fill[grid_cell_dense(p, g)], 1);
     out[slot] = make_float4(p.x, p.y, p.z, __int_as_float((int)i));  // w = map index (kNN tie-break)
   }
 }
@@ -83,10 +97,14 @@ k_grid_scatter(const float4* __restrict__ pts, int64_t n, GridDesc g, int32_t* f
 __global__ void __launch_bounds__(256)
 k_chunk_keys(const float4* __restrict__ pts, int64_t n, GridDesc g, unsigned long long* keys, uint32_t* vals) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float4 p = pts[i];
     int cx, cy, cz;
-    grid_cell3(pts[i], g, cx, cy, cz);
-    // (z, y, x) cell order; key >> log2(kChunkX) is the chunk key (chunk_key)
-    keys[i] = ((unsigned long long)(unsigned)cz << 52) | ((unsigned long long)(unsigned)cy << 28) | (unsigned)cx;
+    grid_cell3(p, g, cx, cy, cz);
+    // (z, y, x) cell order; key >> log2(kChunkX) is the chunk key (chunk_key); non-finite points
+    // sort behind every real key (z < 2^12) and are cut off before the chunk pass
+    keys[i] = map_point_finite(p) ? ((unsigned long long)(unsigned)cz << 52) | ((unsigned long long)(unsigned)cy << 28) |
+                                        (unsigned)cx
+                                  : ~0ull;
     vals[i] = (uint32_t)i;
   }
 }
@@ -170,18 +188,20 @@ int grid_build_device(hipStream_t s, DevArena& ar, const float4* src, int64_t n,
   };
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 2048));
   // cell bounds (min x, y, z, max x, y, z), read back once
-  int b[6] = {0, 0, 0, 0, 0, 0};
+  int b[7] = {0, 0, 0, 0, 0, 0, 0};  // cell min x, y, z, max x, y, z; non-finite points
   if (!ok(arena_reserve(ar, arena_bytes(sizeof(b)), s))) return rc;
   int* d_bounds = arena_take<int>(ar, sizeof(b));
   if (!d_bounds) return FBR_ERR_HIP;
   if (!ok(hipMemsetD32Async((hipDeviceptr_t)d_bounds, (unsigned)INT_MAX, 3, s)) ||
-      !ok(hipMemsetD32Async((hipDeviceptr_t)(d_bounds + 3), (unsigned)INT_MIN, 3, s)))
+      !ok(hipMemsetD32Async((hipDeviceptr_t)(d_bounds + 3), (unsigned)INT_MIN, 3, s)) ||
+      !ok(hipMemsetD32Async((hipDeviceptr_t)(d_bounds + 6), 0u, 1, s)))
     return rc;
   if (n > 0) fbr_launch(k_grid_bounds, dim3(grid), dim3(256), 0, s, src, n, invx, inv, d_bounds);
   ok(hipMemcpyAsync(b, d_bounds, sizeof(b), hipMemcpyDeviceToHost, s));
   ok(hipStreamSynchronize(s));
   if (rc) return rc;
-  if (n == 0)
+  const int64_t nf = n - b[6];  // finite points: the only candidates
+  if (nf == 0)
     for (int d = 0; d < 6; ++d) b[d] = 0;
   int64_t dims[3];
   for (int d = 0; d < 3; ++d) dims[d] = (int64_t)b[3 + d] - b[d] + 1;
@@ -218,7 +238,7 @@ int grid_build_device(hipStream_t s, DevArena& ar, const float4* src, int64_t n,
         if (n > 0) fbr_launch(k_grid_count, dim3(grid), dim3(256), 0, s, src, n, g, cnt);
         // cell_start = exclusive scan of the counts (ncell + 1 entries: the last is n)
         if (ok(rocprim::exclusive_scan(tmp, tb, cnt, out.cs, 0, (size_t)(ncell + 1), rocprim::plus<int32_t>(), s)) &&
-            ok(hipMemcpyAsync(cnt, out.cs, sizeof(int32_t) * ncell, hipMemcpyDeviceToDevice, s)) && n > 0)
+            ok(hipMemcpyAsync(cnt, out.cs, sizeof(int32_t) * (ncell + 1), hipMemcpyDeviceToDevice, s)) && n > 0)
           fbr_launch(k_grid_scatter, dim3(grid), dim3(256), 0, s, src, n, g, cnt, out.pts);
       }
     }
@@ -245,14 +265,14 @@ int grid_build_device(hipStream_t s, DevArena& ar, const float4* src, int64_t n,
   void* tmp = arena_take<void>(ar, std::max(tb_sort, tb_scan));
   if (!k0 || !k1 || !ckey || !v0 || !v1 || !head || !cid || !tmp) return FBR_ERR_HIP;
   uint32_t nchunks = 0;
-  if (n > 0) {
+  if (nf > 0) {  // the non-finite points sort last and stay out of the chunks
     fbr_launch(k_chunk_keys, dim3(grid), dim3(256), 0, s, src, n, g, k0, v0);
     if (ok(rocprim::radix_sort_pairs(tmp, tb_sort, k0, k1, v0, v1, (size_t)n, 0, 64, s))) {
-      fbr_launch(k_chunk_scatter, dim3(grid), dim3(256), 0, s, src, n, k1, v1, out.pts, head);
+      fbr_launch(k_chunk_scatter, dim3(grid), dim3(256), 0, s, src, nf, k1, v1, out.pts, head);
       uint32_t last[2] = {0, 0};
-      if (ok(rocprim::exclusive_scan(tmp, tb_scan, head, cid, 0u, (size_t)n, rocprim::plus<uint32_t>(), s)) &&
-          ok(hipMemcpyAsync(&last[0], cid + n - 1, 4, hipMemcpyDeviceToHost, s)) &&
-          ok(hipMemcpyAsync(&last[1], head + n - 1, 4, hipMemcpyDeviceToHost, s)) && ok(hipStreamSynchronize(s)))
+      if (ok(rocprim::exclusive_scan(tmp, tb_scan, head, cid, 0u, (size_t)nf, rocprim::plus<uint32_t>(), s)) &&
+          ok(hipMemcpyAsync(&last[0], cid + nf - 1, 4, hipMemcpyDeviceToHost, s)) &&
+          ok(hipMemcpyAsync(&last[1], head + nf - 1, 4, hipMemcpyDeviceToHost, s)) && ok(hipStreamSynchronize(s)))
         nchunks = last[0] + last[1];
     }
   }
@@ -265,7 +285,7 @@ int grid_build_device(hipStream_t s, DevArena& ar, const float4* src, int64_t n,
       ok(hipMalloc((void**)&out.hvals, sizeof(int32_t) * hsize)) &&
       ok(hipMemsetAsync(out.cs, 0xFF, sizeof(int32_t) * (kChunkX + 1) * std::max<uint32_t>(nchunks, 1), s)) &&
       ok(hipMemsetAsync(out.hkeys, 0xFF, sizeof(unsigned long long) * hsize, s)) && nchunks > 0) {
-    fbr_launch(k_chunk_cells, dim3(grid), dim3(256), 0, s, n, k1, cid, head, out.cs, ckey);
+    fbr_launch(k_chunk_cells, dim3(grid), dim3(256), 0, s, nf, k1, cid, head, out.cs, ckey);
     const int cg = (int)std::max<int64_t>(1, std::min<int64_t>((nchunks + 255) / 256, 2048));
     fbr_launch(k_chunk_finish, dim3(cg), dim3(256), 0, s, (int64_t)nchunks, out.cs, ckey, out.hkeys, out.hvals,
                g.hmask);

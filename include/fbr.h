@@ -27,7 +27,8 @@
 extern "C" {
 #endif
 
-#define FBR_ABI_VERSION 3  /* 3: fbr_params.exact_voxel_order / pipeline_depth (were reserved_[0..1]);
+#define FBR_ABI_VERSION 4  /* 4: fbr_batch_allgather takes wait_stream (the caller's reader of recv);
+                              3: fbr_params.exact_voxel_order / pipeline_depth (were reserved_[0..1]);
                               2: fbr_selftest_math writes 6 floats per element (was 4) */
 
 /* ---- status codes ------------------------------------------------------------------------- */
@@ -405,7 +406,9 @@ int fbr_batch_export_ready(fbr_ctx* ctx, void* device_dst, void* wait_stream, vo
  *   rank 0:     fbr_comm_unique_id(id), then hands id to the other ranks (any out-of-band channel);
  *   every rank: fbr_comm_create(&comm, ctx, id, nranks, rank, max_jobs_per_rank)  (blocks until
  *               all ranks joined), then per launch fbr_batch_allgather(ctx, comm, launch_id, recv,
- *               &stream) with the same launch_id on every rank. */
+ *               wait_stream, &stream) with the same launch_id on every rank.
+ * max_jobs_per_rank must be at least the ctx's fbr_params.max_batch (FBR_ERR_CAPACITY otherwise), so
+ * no staged batch can exceed the communicator's blocks once it exists. */
 #define FBR_COMM_ID_BYTES 128
 typedef struct fbr_comm fbr_comm;
 int fbr_comm_unique_id(uint8_t id_out[FBR_COMM_ID_BYTES]);
@@ -419,10 +422,17 @@ int fbr_comm_destroy(fbr_comm* comm);
  * launch is first enqueued to its end (the host follows its GN flags); the export and the
  * all-gather then run on that launch's stream, returned in *done_stream (wait on it before reading
  * recv), or, with done_stream NULL, joined into the ctx stream.  Consecutive calls are ordered on
- * the device (each after the previous one's all-gather), so one recv buffer may serve them all.
+ * the device (each after the previous one's all-gather).  recv is written only after the work
+ * queued so far on `wait_stream` (a HIP stream of the caller still reading the previous result out
+ * of recv, or NULL when recv is read only on *done_stream / the ctx stream), so one recv buffer may
+ * serve every call.
  * The launch must still own its work slot (one of the last pipeline_depth launches of the staged
- * batch): FBR_ERR_STATE otherwise. */
-int fbr_batch_allgather(fbr_ctx* ctx, fbr_comm* comm, int64_t launch_id, void* recv, void** done_stream);
+ * batch): FBR_ERR_STATE otherwise.  Every argument and state check runs before anything is
+ * enqueued, but the call is a collective: a rank that returns an error has not joined the
+ * all-gather, its peers stay blocked in it, and the caller must tear the group down (every rank:
+ * fbr_comm_destroy, which aborts the RCCL communicator after a failed call). */
+int fbr_batch_allgather(fbr_ctx* ctx, fbr_comm* comm, int64_t launch_id, void* recv, void* wait_stream,
+                        void** done_stream);
 
 /* Sum of the per-scan algorithmic byte counts of the last completed batch (roofline input). */
 int fbr_batch_bytes(fbr_ctx* ctx, double* bytes_total, double* bytes_gn);

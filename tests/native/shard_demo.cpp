@@ -146,11 +146,11 @@ int run_rank(const Input& in, const std::string& out, int rank, int world, int l
     st = fbr_batch_launch(ctx);
     if (st) return fail(rank, "fbr_batch_launch", st);
     if (k > 0) {
-      st = fbr_batch_allgather(ctx, comm, k - 1, recv, &gst);
+      st = fbr_batch_allgather(ctx, comm, k - 1, recv, nullptr, &gst);
       if (st) return fail(rank, "fbr_batch_allgather", st);
     }
   }
-  st = fbr_batch_allgather(ctx, comm, launches - 1, recv, &gst);
+  st = fbr_batch_allgather(ctx, comm, launches - 1, recv, nullptr, &gst);
   if (st) return fail(rank, "fbr_batch_allgather", st);
   if (hipStreamSynchronize((hipStream_t)gst) != hipSuccess) return fail(rank, "hipStreamSynchronize", FBR_ERR_HIP);
   std::vector<float> rec(8 * (size_t)max_block * world);

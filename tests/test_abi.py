@@ -46,7 +46,7 @@ def test_params_default_match_params_yaml():
 
 
 def test_strerror_and_abi_version():
-    assert api.lib().fbr_abi_version() == 3
+    assert api.lib().fbr_abi_version() == 4
     for code in range(-7, 1):
         assert api.strerror(code) and api.strerror(code) != "unknown status"
     assert api.strerror(-99) == "unknown status"
