@@ -57,42 +57,58 @@ def valu_peak_ginst():
 VALU_PEAK_GINST, VALU_PEAK_SOURCE = valu_peak_ginst()
 
 # Algorithmic bytes per unit for each kernel family: the minimal HBM traffic the kernel's job needs
-# (DESIGN.md §4 holds the same table; every model is <= the FETCH/WRITE counter bytes).  Units per
-# step: n_in raw points, HW range-image cells, n valid points, C corner picks, S per-ring surf DS
-# points, F = C + S feature points, Q DS queries, IQ query-iterations, MG the map grid's points.
+# (DESIGN.md §4 holds the same table; SURVEY §8(d)'s per-unit figures).  Units per step: n_in raw
+# points, HW range-image cells, n valid points, C corner picks, S per-ring surf DS points, F = C + S
+# feature points, Q DS queries, IQ query-iterations (IQc of them corner ones).  The traffic the
+# design itself adds on top (scratch it stages, caches it keeps) is design_bytes below: reported
+# beside the algorithmic figure, never folded into the roofline fraction.
 def kernel_bytes(name, tot):
     n_in, HW, n, C = tot["n_in"], tot["HW"], tot["n"], tot["C"]
     S, F, Q, IQ = tot["S"], tot["F"], tot["Q"], tot["IQ"]
-    IQc = tot.get("IQc", 0.0)  # corner query-iterations (the rest are surf)
     return {
         "project": 24.0 * n_in + 4.0 * n,        # raw point (24 B AoS) read + first-wins owner claim
         "extract": 4.0 * HW + 4.0 * n + 24.0 * n + 24.0 * n,  # owner image read + claimed cells reset, owning
                                                              # raw point gather, xyzi+col+range write
-        "features": 17.0 * n + 32.0 * C,         # range + col read, label written, the ring's curvature staged
-                                                 # through its scratch slot (4 B written, 4 B read back per
-                                                 # segment); corner points read + written
+        "features": 9.0 * n + 32.0 * C,          # range + col read, label written; corner points read + written
         "voxel_ring": 17.0 * n + 16.0 * S,       # label + candidate point read, per-ring DS write
         "concat": 32.0 * F,                      # per-ring corner / surf outputs read + job clouds written
         "voxel_scan": 16.0 * F + 16.0 * Q,       # corner + surf clouds read, DS queries written
-        "gn_knn": 37.0 * IQ + 20.0 * (IQ - Q),   # query 16 B read, 5 map indices 20 B + same-flag 1 B written;
-                                                 # from iteration 1 the previous 5 indices (warm start) read;
-                                                 # the map's rows are cache hits (C2's map is 1.5 MB)
-        "gn_residual": 38.0 * IQ + 8.0 * IQc + 16.0 * IQ,  # query 16 B + 5 indices 20 B + same / fit state
-                                                 # 2 B; the fit cache (line 24 B / plane 16 B: read when the
-                                                 # neighbours are unchanged, written when refitted); neighbour
-                                                 # gathers are cache hits
+        "gn_knn": 36.0 * IQ,                     # query 16 B read, 5 map indices 20 B written; the map rows
+                                                 # are cache hits (C2's map is 1.5 MB)
+        "gn_residual": 36.0 * IQ,                # query 16 B + 5 indices 20 B read; neighbour gathers are
+                                                 # cache hits (SURVEY §8(d)'s 96 B per query-iteration is
+                                                 # these two kernels with the gathers counted)
+    }.get(name, 0.0)
+
+
+def design_bytes(name, tot):
+    """HBM traffic the design adds to a kernel's algorithmic bytes (design choices, not the job):
+    features stages each ring's curvature through its scratch slot (4 B written, 4 B read back per
+    point); gn_knn writes a 1-B same-neighbours flag and reads the previous iteration's 5 indices as
+    its warm start; gn_residual reads the flag and fit state (2 B) and the fit cache (plane 16 B,
+    line 24 B: read when the neighbours are unchanged, written when refitted)."""
+    n, Q, IQ, IQc = tot["n"], tot["Q"], tot["IQ"], tot.get("IQc", 0.0)
+    return {
+        "features": 8.0 * n,
+        "gn_knn": 1.0 * IQ + 20.0 * (IQ - Q),
+        "gn_residual": 2.0 * IQ + 16.0 * IQ + 8.0 * IQc,
     }.get(name, 0.0)
 
 
 BYTE_MODEL = {
     "project": "24 B per raw point + 4 B owner claim per valid point",
     "extract": "4 B per range-image cell + 4 B owner reset + 24 B raw-point gather + 24 B written per valid point",
-    "features": "17 B per valid point (range + col read, label written, curvature staged through the ring's scratch slot 8 B) + 32 B per corner pick",
+    "features": "9 B per valid point (range + col read, label written) + 32 B per corner pick",
     "voxel_ring": "17 B per valid point + 16 B per per-ring DS point",
     "concat": "32 B per feature point",
     "voxel_scan": "16 B per feature point + 16 B per DS query",
-    "gn_knn": "37 B per query-iteration (query 16 B, 5 indices 20 B + same flag 1 B written) + 20 B per warm-started one (previous indices); map rows are L2/MALL hits",
-    "gn_residual": "54 B per query-iteration (query 16 B, 5 indices 20 B, 2 B state, 16 B plane fit cache) + 8 B per corner one (24 B line fit); neighbour gathers are L2/MALL hits",
+    "gn_knn": "36 B per query-iteration (query 16 B read, 5 indices 20 B written); map rows are L2/MALL hits",
+    "gn_residual": "36 B per query-iteration (query 16 B, 5 indices 20 B read); neighbour gathers are L2/MALL hits",
+}
+DESIGN_MODEL = {
+    "features": "8 B per valid point: the ring's curvature staged through its scratch slot",
+    "gn_knn": "1 B same-neighbours flag per query-iteration + 20 B warm start (previous 5 indices) per warm-started one",
+    "gn_residual": "2 B flag / fit state + 16 B plane fit cache per query-iteration, + 8 B per corner one (24 B line)",
 }
 
 # rocprofv3 kernel symbols behind each launcher name (tools/roofline_check.py maps a profile's rows)
@@ -200,6 +216,7 @@ def latency_line(cfg, corner_map, surf_map, n, cpu_scans=0):
         warm_pose = pose.copy()
         api.debug_counters(reset=True)
         api.host_times(reset=True)
+        api.wait_stats(reset=True)
         for k in range(3, n + 3):
             t = time.perf_counter()
             pose, st = c.process_scan(scans[k], 0.2 * k, pose)
@@ -207,9 +224,15 @@ def latency_line(cfg, corner_map, surf_map, n, cpu_scans=0):
             poses.append(pose.copy())
         launches, syncs, polls = api.debug_counters()
         ht = api.host_times()
+        fallbacks, long_waits, wait_max_s, queries = api.wait_stats()
     ms = np.array(ms)
     out = {"scans": n, "ms_per_scan_mean": round(float(ms.mean()), 4), "ms_per_scan_p50": round(float(np.median(ms)), 4),
            "ms_per_scan_p99": round(float(np.percentile(ms, 99)), 4),
+           "ms_per_scan_max": round(float(ms.max()), 4),
+           # host waits on device results (GN iteration flags, the direct result): fallbacks (not
+           # visible although the stream drained), waits > 1 ms, the longest, stream queries
+           "result_waits": {"fallbacks": fallbacks, "over_1ms": long_waits, "max_ms": round(1e3 * wait_max_s, 4),
+                            "stream_queries": queries},
            "launches_per_scan": round(launches / n, 2), "host_syncs_per_scan": round(syncs / n, 2),
            "gn_flag_polls_per_scan": round(polls / n, 2),
            # host wall time inside fbr_process_scan per scan: scan upload (staging copy + enqueue),
@@ -476,11 +499,16 @@ def main():
             ms, launches, steps_measured, live = prof[k][0], prof[k][1], 1, False
         lps = launches / max(steps_measured, 1)
         bpl = kernel_bytes(k, tot) / max(lps, 1e-9)
+        dpl = design_bytes(k, tot) / max(lps, 1e-9)
         avg_s = ms / 1000.0 / max(launches, 1)
         ach = bpl / avg_s / 1e9 if avg_s > 0 else 0.0
         r = dict(bytes_per_launch=bpl, avg_launch_us=round(avg_s * 1e6, 3), launches_per_step=lps,
                  achieved_GBps=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
                  ms_per_step=round(ms / max(steps_measured, 1), 4), live=live)
+        if dpl > 0:  # the design's own traffic, beside (not inside) the algorithmic fraction
+            r["design_bytes_per_launch"] = dpl
+            r["design_model"] = DESIGN_MODEL[k]
+            r["frac_with_design_bytes"] = round((bpl + dpl) / avg_s / 1e9 / HBM_PEAK_GBS, 5) if avg_s > 0 else 0.0
         if k in valu and avg_s > 0:  # the launch's wave-level VALU instructions over its live duration
             ipl = valu[k]["insts_valu_per_launch"]
             r["valu_insts_per_launch"] = ipl
@@ -511,8 +539,15 @@ def main():
         try:
             with open(args.pmc_json) as f:
                 pm = json.load(f)
-            if pm.get("config") == cfg and pm.get("batch") == B and dom in pm.get("kernels", {}):
-                traffic = pm["kernels"][dom]["hbm_bytes_per_launch"]
+            if pm.get("config") == cfg and pm.get("batch") == B:
+                # every kernel's counter bytes per launch (FETCH_SIZE + WRITE_SIZE, one launch alone)
+                # against its algorithmic bytes: the wasted-traffic ratio
+                for k, e in pm.get("kernels", {}).items():
+                    if k in kroof and kroof[k]["bytes_per_launch"] > 0:
+                        kroof[k]["traffic"] = e["hbm_bytes_per_launch"]
+                        kroof[k]["traffic_over_algorithmic"] = round(e["hbm_bytes_per_launch"] / kroof[k]["bytes_per_launch"], 3)
+                if dom in pm.get("kernels", {}):
+                    traffic = pm["kernels"][dom]["hbm_bytes_per_launch"]
         except Exception:
             traffic = None
 
@@ -546,6 +581,11 @@ def main():
                                                                         "pose all-gather (torch.distributed)")
                             if dist is not None else "single GPU"),
             "imu_deskew": bool(args.deskew),
+            "exact_voxel_order": int(args.exact_voxel_order),
+            "timed_region": ("fbr_batch_launch of a staged batch, every stage on the device: projection, features, "
+                             "per-ring and mapping VoxelGrids, CropBox statistics, Gauss-Newton registration, "
+                             "results; excludes the host-to-device copy of the raw scans and guesses "
+                             "(fbr_batch_stage: inputs resident in HBM), reported separately as the ingest line"),
         },
         "roofline": {
             "bound": "valu" if valu_bound else "hbm",
@@ -571,6 +611,8 @@ def main():
                        if live else "kernel dispatch start/end timestamps, profiled untimed step"),
             "rocprof_symbols": KERNEL_SYMBOLS[dom],
             "byte_model": BYTE_MODEL[dom],
+            "design_bytes_per_launch": kroof[dom].get("design_bytes_per_launch", 0.0),
+            "design_model": DESIGN_MODEL.get(dom),
             "kernels": {k: {kk: v for kk, v in r.items() if kk != "live"} for k, r in kroof.items()},
         },
         "kernel_ms_per_step": {k: round(v[0], 4) for k, v in prof.items()},  # profiled untimed step

@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = [
     "fbr_imu_convert", "fbr_imu_deskew_info", "fbr_set_deskew", "fbr_stream_copy_bandwidth", "fbr_valu_peak",
     "fbr_keyframe_params_default", "fbr_keyframes_add", "fbr_keyframes_set_pose", "fbr_keyframes_count",
     "fbr_keyframes_reset", "fbr_extract_surrounding_keyframes",
-    "fbr_comm_unique_id", "fbr_comm_create", "fbr_comm_destroy", "fbr_batch_allgather",
+    "fbr_comm_unique_id", "fbr_comm_create", "fbr_comm_create_local", "fbr_comm_destroy", "fbr_batch_allgather",
 ]
 
 
@@ -120,6 +120,7 @@ def lib():
             "fbr_extract_surrounding_keyframes": (ctypes.c_int, [_VP, ctypes.c_double, _VP, _VP, _VP, _VP]),
             "fbr_comm_unique_id": (ctypes.c_int, [_VP]),
             "fbr_comm_create": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+            "fbr_comm_create_local": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int]),
             "fbr_comm_destroy": (ctypes.c_int, [_VP]),
             "fbr_batch_allgather": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP]),
         }
@@ -161,6 +162,17 @@ def host_times(reset=False):
     v = (ctypes.c_longlong * 4)()
     _check(f(v, int(reset)), "fbr_diag_host_times")
     return tuple(x * 1e-9 for x in v)
+
+
+def wait_stats(reset=False):
+    """Host waits on device results since the last reset -- diagnostic (fbr_diag_wait_stats):
+    (fallbacks: a flag or direct result not visible although its stream drained, waits longer than
+    1 ms, the longest wait in s, stream queries)."""
+    f = lib().fbr_diag_wait_stats
+    f.restype, f.argtypes = ctypes.c_int, [_VP, ctypes.c_int]
+    v = (ctypes.c_longlong * 4)()
+    _check(f(v, int(reset)), "fbr_diag_wait_stats")
+    return int(v[0]), int(v[1]), v[2] * 1e-9, int(v[3])
 
 
 def batch_times(reset=False):

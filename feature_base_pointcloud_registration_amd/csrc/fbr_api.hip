@@ -134,12 +134,33 @@ struct GnRun {
   int it[kMaxSub] = {};      // next iteration to enqueue
   long polls[kMaxSub] = {};  // unanswered flag reads of the current wait
   std::chrono::steady_clock::time_point wait0[kMaxSub];  // start of the current wait
+  int64_t next_query[kMaxSub] = {};  // ns into the current wait of the next stream query
 };
 
 // A flag wait asks the runtime whether the stream drained (flags not visible although the work
-// is done) only after this long: hipStreamQuery puts a marker into the stream, and a marker between
-// two iterations' kernels cost ~5.7 us on the device (every launch enqueued after a wait had one).
-constexpr int64_t kStreamQueryAfterNs = 2000000;
+// is done) only once it has lasted several times longer than the waits of its kind usually do:
+// hipStreamQuery puts a marker into the stream, and a marker between two iterations' kernels cost
+// ~5.7 us on the device (every launch enqueued after a wait had one).  The bound is 4x the
+// smoothed duration of the completed waits of that kind (GN flags of batch runs, of single-scan
+// runs, single-scan direct results), within [kQueryMinNs, kQueryMaxNs]; queries repeat at most
+// every half bound.  (Round 5 used a fixed 2 ms, which a late-visible flag turned into a 2 ms scan.)
+constexpr int64_t kQueryMinNs = 150000, kQueryMaxNs = 2000000;
+struct WaitBound {
+  double ema_ns = 0.0;
+  int64_t after() const {
+    return ema_ns <= 0.0 ? kQueryMaxNs : std::min<int64_t>(kQueryMaxNs, std::max<int64_t>(kQueryMinNs, (int64_t)(4.0 * ema_ns)));
+  }
+  void done(int64_t ns) { ema_ns = ema_ns <= 0.0 ? (double)ns : 0.875 * ema_ns + 0.125 * (double)ns; }
+};
+enum { kWaitBatchFlag = 0, kWaitScanFlag = 1, kWaitDirect = 2 };
+// Every completed wait into the process-wide wait statistics (fbr_diag_wait_stats).
+void wait_stat(int64_t ns) {
+  DebugCounters& d = debug_counters();
+  if (ns > 1000000) d.waits_over_1ms.fetch_add(1, std::memory_order_relaxed);
+  long long m = d.wait_max_ns.load(std::memory_order_relaxed);
+  while (ns > m && !d.wait_max_ns.compare_exchange_weak(m, ns, std::memory_order_relaxed)) {
+  }
+}
 
 struct fbr_ctx {
   fbr_params P;
@@ -147,6 +168,7 @@ struct fbr_ctx {
   hipStream_t stream = nullptr;   // primary stream (single-scan calls, batch sub-batch 0, export)
   hipStream_t xstream[kMaxSub] = {};  // extra streams of batch sub-batches 1.. (index 0 unused)
   hipEvent_t xev[kMaxSub] = {};       // fork / join events
+  WaitBound wait_bound[3];            // kWaitBatchFlag / kWaitScanFlag / kWaitDirect
   int nsub_pref = 3;                  // sub-batches per batch launch (FBR_NSUB overrides): 3 unpipelined (at
                                       // B = 128: 2 -> 76.1k, 3 -> 78.5k, 4 -> 46.7k scans/s), 1 pipelined
   int H = 0, W = 0, Bcap = 0;
@@ -199,6 +221,7 @@ struct fbr_ctx {
   GnState* d_gn = nullptr;
   int4* d_items = nullptr;
   int32_t *d_nitems = nullptr, *d_item_range = nullptr, *d_cropcnt = nullptr;
+  int32_t* d_cropwork = nullptr;  // [Bwork][2]: a launch's CropBox counts while they accumulate
   double* d_partial = nullptr;
   int32_t* d_nbr = nullptr;
   float* d_fitc = nullptr;     // [max_items][6][256] per-query fit cache (k_gn_residual)
@@ -609,11 +632,6 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
     return e ? std::atoi(e) : 1;
   }();
   a.fit_cache = fit_cache;
-  static const int res_mfma = [] {  // opt-in: -3 % gn_residual, headline within noise
-    const char* e = std::getenv("FBR_RES_MFMA");
-    return e ? std::atoi(e) : 0;
-  }();
-  a.res_mfma = res_mfma;
   a.iter_flags = c->d_iter_flags + (int64_t)sb.k * mi;
   a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 4 * mi;  // [2 * mi] solve, [mi] queued, [mi] blocks
   if (c->d_bin) {
@@ -671,9 +689,8 @@ int crop_stats(fbr_ctx* c, const Sub& sb) {
     CK(fbr_sync(sb.st));
     return FBR_OK;
   }
-  CK(hipMemsetAsync(cnt, 0, sizeof(int32_t) * 2 * sb.B, sb.st));
-  TIMED_ON(c, sb.st, "crop", launch_crop_count(sb.st, a, c->grid_c.pts, c->grid_c.g.n_points, 0, cnt));
-  TIMED_ON(c, sb.st, "crop", launch_crop_count(sb.st, a, c->grid_s.pts, c->grid_s.g.n_points, 1, cnt));
+  TIMED_ON(c, sb.st, "crop", launch_crop_count(sb.st, a, c->grid_c.pts, c->grid_c.g.n_points, c->grid_s.pts,
+                                                c->grid_s.g.n_points, c->d_cropwork + (int64_t)sb.j0 * 2, cnt));
   return FBR_OK;
 }
 
@@ -702,7 +719,8 @@ int register_prepare(fbr_ctx* c, const Sub& sb, bool trace) {
   GnArgs a = gn_args(c, sb, trace);
   if (trace) CK(hipMemsetAsync(a.trace, 0, sizeof(float) * sb.B * c->P.max_iterations * 6, sb.st));
   TIMED_ON(c, sb.st, "gn_init", launch_gn_init(sb.st, a));  // also zeroes a.iter_cnt
-  // map-in-box statistics depend only on the guesses: computed once per staged batch
+  // map-in-box statistics (from the kNN grid, every launch; the single-scan path runs them on a side
+  // stream beside its front end, the keyframe map's are host constants set at staging)
   if (!c->crop_cached) {
     const int rc = crop_stats(c, sb);
     if (rc) return rc;
@@ -721,14 +739,6 @@ int gn_grid_cap() {
   return v;
 }
 
-// kNN and residual in one launch (FBR_GN_FUSED=0/1 overrides the default).
-bool gn_fused() {
-  static const bool v = [] {
-    const char* e = std::getenv("FBR_GN_FUSED");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
-}
 
 // Tail mode: once at most 1/FBR_GN_TAIL of a sub-batch's jobs are still iterating (default 8),
 // its iterations run fused (kNN + residual in one launch) on a smaller grid: the few remaining
@@ -787,20 +797,42 @@ int gn_run_pass(fbr_ctx* c, GnRun& r, bool block, bool* progress) {
       volatile unsigned long long* f = c->h_iter_flags + (int64_t)sb.k * mi + (it - r.lag);
       unsigned long long v = *f;
       const auto tspin = std::chrono::steady_clock::now();
-      if (r.polls[k] == 0) r.wait0[k] = tspin;
+      if (r.polls[k] == 0) {
+        r.wait0[k] = tspin;
+        r.next_query[k] = c->wait_bound[sb.stream_mode ? kWaitScanFlag : kWaitBatchFlag].after();
+      }
       while ((v >> 32) != g32) {
-        if ((++r.polls[k] & 1023) == 1023 &&
-            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - r.wait0[k]).count() >
-                kStreamQueryAfterNs) {
-          const hipError_t q = hipStreamQuery(sb.st);
-          if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
-          if (q == hipSuccess && ((v = *f) >> 32) != g32) {
-            r.watch[k] = false;  // flag not visible although the stream drained: enqueue the rest
-            break;
+        if ((++r.polls[k] & 1023) == 1023) {
+          const int64_t waited =
+              std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - r.wait0[k]).count();
+          if (waited > r.next_query[k]) {
+            r.next_query[k] = waited + std::max<int64_t>(kQueryMinNs, r.next_query[k] / 2);
+            debug_counters().stream_queries.fetch_add(1, std::memory_order_relaxed);
+            const hipError_t q = hipStreamQuery(sb.st);
+            if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
+            if (q == hipSuccess && ((v = *f) >> 32) != g32) {
+              // the stream drained but the host-mapped flag is not visible: the solve's count is in
+              // device memory (iter_cnt[2 i]), final once the stream is idle; read it and go on
+              // watching (round 5 enqueued every remaining iteration here)
+              int32_t cnt = 0;
+              if (hipMemcpyAsync(&cnt, r.a[k].iter_cnt + 2 * (it - r.lag), sizeof(cnt), hipMemcpyDeviceToHost, sb.st) !=
+                      hipSuccess ||
+                  fbr_sync(sb.st) != hipSuccess)
+                return FBR_ERR_HIP;
+              v = (g32 << 32) | (unsigned long long)(uint32_t)cnt;
+              debug_counters().flag_fallbacks.fetch_add(1, std::memory_order_relaxed);
+              break;
+            }
           }
         }
         if (!block) break;
         v = *f;
+      }
+      if ((v >> 32) == g32) {  // the wait's duration (from its first poll) into the bound and the stats
+        const int64_t waited =
+            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - r.wait0[k]).count();
+        c->wait_bound[sb.stream_mode ? kWaitScanFlag : kWaitBatchFlag].done(waited);
+        wait_stat(waited);
       }
       if (block || (v >> 32) == g32 || !r.watch[k])
         debug_counters().batch_ns[1].fetch_add(
@@ -826,7 +858,7 @@ int gn_run_pass(fbr_ctx* c, GnRun& r, bool block, bool* progress) {
     const bool tail = gn_tail_div() > 0 && (int64_t)r.active[k] * gn_tail_div() <= sb.B;
     int grid = std::max(1, std::min(r.a[k].max_items, tail ? std::min(gn_grid_cap(), 1024) : gn_grid_cap()));
     if (sb.stream_mode && c->items_hint > 0) grid = std::min(grid, std::max(16, 2 * c->items_hint));
-    if (gn_fused() || tail) {
+    if (tail) {  // kNN and residual in one launch (whole runs fused: 4 % slower at round 6, r06b)
       TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, r.a[k], grid, it, true));
     } else {
       TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, r.a[k], grid, it, false));
@@ -916,15 +948,31 @@ int wait_direct(fbr_ctx* c, bool* got) {
   volatile int32_t* gen = &c->h_direct->pad;
   *got = false;
   const auto t0 = std::chrono::steady_clock::now();
+  int64_t next_query = c->wait_bound[kWaitDirect].after();
   for (int64_t polls = 1;; ++polls) {
     if (*gen == c->direct_gen) break;
-    if ((polls & 1023) == 0 && std::chrono::duration_cast<std::chrono::nanoseconds>(
-                                   std::chrono::steady_clock::now() - t0).count() > kStreamQueryAfterNs) {
-      const hipError_t q = hipStreamQuery(c->stream);
-      if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
-      if (q == hipSuccess && *gen != c->direct_gen) return FBR_OK;
+    if ((polls & 1023) == 0) {
+      const int64_t waited =
+          std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+      if (waited > next_query) {
+        next_query = waited + std::max<int64_t>(kQueryMinNs, next_query / 2);
+        debug_counters().stream_queries.fetch_add(1, std::memory_order_relaxed);
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q != hipSuccess && q != hipErrorNotReady) return FBR_ERR_HIP;
+        if (q == hipSuccess && *gen != c->direct_gen) {  // the caller copies the enqueued results
+          debug_counters().flag_fallbacks.fetch_add(1, std::memory_order_relaxed);
+          wait_stat(waited);
+          return FBR_OK;
+        }
+      }
     }
     __builtin_ia32_pause();
+  }
+  {
+    const int64_t waited =
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    c->wait_bound[kWaitDirect].done(waited);
+    wait_stat(waited);
   }
   std::atomic_thread_fence(std::memory_order_acquire);
   std::memcpy(c->h_result, (const void*)c->h_direct, sizeof(JobResult));
@@ -1449,7 +1497,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_ncorner, Bw) || dalloc(&c->d_nsurf, Bw) || dalloc(&c->d_ncds, Bw) || dalloc(&c->d_nsds, Bw) ||
               dalloc(&c->d_vg_scratch, c->vg_scratch_elems) ||
               dalloc(&c->d_gn, Bw) || dalloc(&c->d_items, c->max_items) || dalloc(&c->d_nitems, kMaxSub) ||
-              dalloc(&c->d_item_range, 2 * Bw) || dalloc(&c->d_cropcnt, 2 * B) ||
+              dalloc(&c->d_item_range, 2 * Bw) || dalloc(&c->d_cropcnt, 2 * B) || dalloc(&c->d_cropwork, 2 * Bw) ||
               dalloc(&c->d_partial, (int64_t)c->max_items * 32) ||
               dalloc(&c->d_nbr, (int64_t)c->max_items * 5 * 256) ||
               dalloc(&c->d_fitc, (int64_t)c->max_items * 6 * 256) || dalloc(&c->d_fits, (int64_t)c->max_items * 256) ||
@@ -1500,7 +1548,7 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_corner_slot, c->d_corner_cnt, c->d_surf_ring, c->d_surf_ring_cnt, c->d_ring_box,
                   c->d_err, c->d_corner_all, c->d_surf_all, c->d_cornerDS, c->d_surfDS, c->d_ncorner, c->d_nsurf,
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
-                  c->d_item_range, c->d_cropcnt, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_fitc, c->d_fits, c->d_nsame, c->d_fb_list, c->d_bin, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
+                  c->d_item_range, c->d_cropcnt, c->d_cropwork, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_fitc, c->d_fits, c->d_nsame, c->d_fb_list, c->d_bin, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
                   c->d_desk, c->d_desk_mode, c->d_rowmin, c->d_choff,
                   c->d_kf_c, c->d_kf_s, c->d_kraw_c, c->d_kraw_s, c->d_kds_c, c->d_kds_s, c->d_kf_segs, c->d_bounds, c->d_direct_done};
   for (void* p : ptrs)
@@ -1821,12 +1869,12 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
                        c->stream));
   if (!rc) q(hipMemcpyAsync(c->d_nin, n_in, sizeof(int64_t) * n_jobs, hipMemcpyHostToDevice, c->stream));
   if (!rc) q(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * n_jobs, hipMemcpyHostToDevice, c->stream));
-  if (!rc && c->has_map) rc = crop_stats(c, Sub{0, n_jobs, 0, c->stream});
+  if (!rc && c->has_map && c->map_nocrop) rc = crop_stats(c, Sub{0, n_jobs, 0, c->stream});
   if (!rc) q(hipEventRecord(c->ev_staged, c->stream));  // every launch's streams start after it
   // the caller's host buffers may be reused once this returns: drain the queued copies on every path
   q(fbr_sync(c->stream));
   if (rc) return rc;
-  c->crop_cached = c->has_map;
+  c->crop_cached = c->has_map && c->map_nocrop;
   c->staged_B = n_jobs;
   c->staged_nin.assign(n_in, n_in + n_jobs);
   return FBR_OK;
@@ -1978,6 +2026,8 @@ struct RcclApi {
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
   ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
 };
 const RcclApi& rccl() {
   static const RcclApi api = [] {
@@ -1991,7 +2041,10 @@ const RcclApi& rccl() {
     a.comm_destroy = (decltype(a.comm_destroy))dlsym(h, "ncclCommDestroy");
     a.comm_abort = (decltype(a.comm_abort))dlsym(h, "ncclCommAbort");
     a.all_gather = (decltype(a.all_gather))dlsym(h, "ncclAllGather");
-    a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.comm_abort && a.all_gather;
+    a.group_start = (decltype(a.group_start))dlsym(h, "ncclGroupStart");
+    a.group_end = (decltype(a.group_end))dlsym(h, "ncclGroupEnd");
+    a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.comm_abort && a.all_gather && a.group_start &&
+           a.group_end;
     return a;
   }();
   return api;
@@ -2052,6 +2105,62 @@ int fbr_comm_create(fbr_comm** out, fbr_ctx* c, const uint8_t id[FBR_COMM_ID_BYT
     return FBR_ERR_HIP;
   }
   *out = m;
+  return FBR_OK;
+}
+
+int fbr_comm_create_local(fbr_comm** out, fbr_ctx* const* ctxs, int n, int max_jobs_per_rank) {
+  if (!out || !ctxs || n < 1 || max_jobs_per_rank < 1) return FBR_ERR_INVALID_ARG;
+  for (int i = 0; i < n; ++i) out[i] = nullptr;
+  for (int i = 0; i < n; ++i) {
+    if (!ctxs[i]) return FBR_ERR_INVALID_ARG;
+    for (int j = 0; j < i; ++j)
+      if (ctxs[j]->dev == ctxs[i]->dev) return FBR_ERR_INVALID_ARG;  // one rank per device
+    if (max_jobs_per_rank < ctxs[i]->Bcap) return FBR_ERR_CAPACITY;
+  }
+  if (!rccl().ok) return FBR_ERR_UNSUPPORTED;
+  ncclUniqueId uid;
+  if (rccl().get_unique_id(&uid) != ncclSuccess) return FBR_ERR_HIP;
+  std::vector<fbr_comm*> m(n, nullptr);
+  auto cleanup = [&] {
+    for (fbr_comm* q : m) {
+      if (!q) continue;
+      (void)hipSetDevice(q->dev);
+      if (q->nc) (void)rccl().comm_abort(q->nc);
+      (void)hipFree(q->send);
+      if (q->done) (void)hipEventDestroy(q->done);
+      if (q->ev_wait) (void)hipEventDestroy(q->ev_wait);
+      delete q;
+    }
+  };
+  for (int i = 0; i < n; ++i) {
+    if (enter(ctxs[i]) != hipSuccess) {
+      cleanup();
+      return FBR_ERR_HIP;
+    }
+    m[i] = new fbr_comm();
+    m[i]->dev = ctxs[i]->dev;
+    m[i]->nranks = n;
+    m[i]->rank = i;
+    m[i]->max_jobs = max_jobs_per_rank;
+    if (hipMalloc((void**)&m[i]->send, sizeof(float) * 8 * (size_t)max_jobs_per_rank) != hipSuccess ||
+        hipEventCreateWithFlags(&m[i]->done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m[i]->ev_wait, hipEventDisableTiming) != hipSuccess) {
+      cleanup();
+      return FBR_ERR_HIP;
+    }
+  }
+  // every device's rank from this thread: the inits form one group (RCCL would otherwise wait in
+  // the first init for ranks this thread has not started yet)
+  bool ok = rccl().group_start() == ncclSuccess;
+  for (int i = 0; ok && i < n; ++i) {
+    ok = hipSetDevice(m[i]->dev) == hipSuccess && rccl().comm_init_rank(&m[i]->nc, n, uid, i) == ncclSuccess;
+  }
+  ok = (rccl().group_end() == ncclSuccess) && ok;
+  if (!ok) {
+    cleanup();
+    return FBR_ERR_HIP;
+  }
+  for (int i = 0; i < n; ++i) out[i] = m[i];
   return FBR_OK;
 }
 
@@ -2256,13 +2365,13 @@ int ingest_stage(fbr_ctx* c, int slot, const int64_t* n_in, int B, const float* 
   CK(hipMemcpyAsync(c->d_nin, n_in, sizeof(int64_t) * B, hipMemcpyHostToDevice, c->stream));
   CK(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * B, hipMemcpyHostToDevice, c->stream));
   CK(hipStreamWaitEvent(c->stream, c->ing.up_ev[slot], 0));
-  if (c->has_map) {
+  if (c->has_map && c->map_nocrop) {
     const int rc = crop_stats(c, Sub{0, B, 0, c->stream});
     if (rc) return rc;
   }
   CK(hipEventRecord(c->ev_staged, c->stream));
   CK(fbr_sync(c->stream));  // n_in / poses_in are the caller's
-  c->crop_cached = c->has_map;
+  c->crop_cached = c->has_map && c->map_nocrop;
   c->staged_B = B;
   c->staged_nin.assign(n_in, n_in + B);
   return FBR_OK;
@@ -2327,6 +2436,20 @@ extern "C" int fbr_diag_host_times(long long* out4, int reset) {
   for (int k = 0; k < 4; ++k) {
     if (out4) out4[k] = d.host_ns[k].load();
     if (reset) d.host_ns[k] = 0;
+  }
+  return FBR_OK;
+}
+
+// Diagnostic: host waits on device results since the last reset: [0] fallbacks (a flag or a direct
+// result not visible although its stream drained: the value is then read from device memory / the
+// enqueued copy), [1] completed waits longer than 1 ms, [2] the longest wait (ns), [3] stream
+// queries made by the waits.
+extern "C" int fbr_diag_wait_stats(long long* out4, int reset) {
+  DebugCounters& d = debug_counters();
+  std::atomic<long long>* v[4] = {&d.flag_fallbacks, &d.waits_over_1ms, &d.wait_max_ns, &d.stream_queries};
+  for (int k = 0; k < 4; ++k) {
+    if (out4) out4[k] = v[k]->load();
+    if (reset) *v[k] = 0;
   }
   return FBR_OK;
 }

@@ -442,6 +442,31 @@ __device__ __forceinline__ void res_halve(double* v, int lane) {
   }
 }
 
+// The residual of query (x0, y0, z0) against its fitted line / plane (corner_apply / surf_apply)
+// and its LMOptimization row (:1286-1332); false when the correspondence is rejected.
+__device__ __forceinline__ bool res_apply_row(const GnState& g, bool corner, const float* fit, const float4& p, float x0,
+                                              float y0, float z0, float* row, float& b) {
+  float4 c;
+  const bool ok = corner ? corner_apply(fit, x0, y0, z0, c) : surf_apply(fit, x0, y0, z0, c);
+  if (ok) {
+    // camera-frame swap
+    const float srx = g.trig[0], crx = g.trig[1], sry = g.trig[2], cry = g.trig[3], srz = g.trig[4], crz = g.trig[5];
+    const float pox = p.y, poy = p.z, poz = p.x;
+    const float cox = c.y, coy = c.z, coz = c.x;
+    const float arx = (crx * sry * srz * pox + crx * crz * sry * poy - srx * sry * poz) * cox +
+                      (-srx * srz * pox - crz * srx * poy - crx * poz) * coy +
+                      (crx * cry * srz * pox + crx * cry * crz * poy - cry * srx * poz) * coz;
+    const float ary = ((cry * srx * srz - crz * sry) * pox + (sry * srz + cry * crz * srx) * poy + crx * cry * poz) * cox +
+                      ((-cry * crz - srx * sry * srz) * pox + (cry * srz - crz * srx * sry) * poy - crx * sry * poz) * coz;
+    const float arz = ((crz * srx * sry - cry * srz) * pox + (-cry * crz - srx * sry * srz) * poy) * cox +
+                      (crx * crz * pox - crx * srz * poy) * coy +
+                      ((sry * srz + cry * crz * srx) * pox + (crz * sry - cry * srx * srz) * poy) * coz;
+    row[0] = arz; row[1] = arx; row[2] = ary; row[3] = coz; row[4] = cox; row[5] = coy;
+    b = -c.w;
+  }
+  return ok;
+}
+
 // cornerOptimization / surfOptimization + the LMOptimization row (:1286-1332) of one query whose 5
 // neighbours are the map points nb[0..4] (map indices); false when the correspondence is rejected.
 // fc / fs: the query's fit cache (fit floats at stride kResThreads, state 0 none / 1 fitted /
@@ -474,32 +499,16 @@ __device__ __forceinline__ bool res_row(const GnState& g, const float4* by_id, c
     }
   }
   if (!fit_ok) return false;
-  float4 c;
-  const bool ok = corner ? corner_apply(fit, x0, y0, z0, c) : surf_apply(fit, x0, y0, z0, c);
-  if (ok) {
-    // camera-frame swap
-    const float srx = g.trig[0], crx = g.trig[1], sry = g.trig[2], cry = g.trig[3], srz = g.trig[4], crz = g.trig[5];
-    const float pox = p.y, poy = p.z, poz = p.x;
-    const float cox = c.y, coy = c.z, coz = c.x;
-    const float arx = (crx * sry * srz * pox + crx * crz * sry * poy - srx * sry * poz) * cox +
-                      (-srx * srz * pox - crz * srx * poy - crx * poz) * coy +
-                      (crx * cry * srz * pox + crx * cry * crz * poy - cry * srx * poz) * coz;
-    const float ary = ((cry * srx * srz - crz * sry) * pox + (sry * srz + cry * crz * srx) * poy + crx * cry * poz) * cox +
-                      ((-cry * crz - srx * sry * srz) * pox + (cry * srz - crz * srx * sry) * poy - crx * sry * poz) * coz;
-    const float arz = ((crz * srx * sry - cry * srz) * pox + (-cry * crz - srx * sry * srz) * poy) * cox +
-                      (crx * crz * pox - crx * srz * poy) * coy +
-                      ((sry * srz + cry * crz * srx) * pox + (crz * sry - cry * srx * srz) * poy) * coz;
-    row[0] = arz; row[1] = arx; row[2] = ary; row[3] = coz; row[4] = cox; row[5] = coy;
-    b = -c.w;
-  }
-  return ok;
+  return res_apply_row(g, corner, fit, p, x0, y0, z0, row, b);
 }
 
 // The item's fp64 normal-equation partial (21 upper AtA entries, 6 AtB, count; 4 zero pads):
 // every lane of the workgroup calls this with its row (zeros when it has none).  The wave sum is a
 // transposed butterfly: at each halving step a lane keeps half of its values and trades the other
 // half with its partner, so 32 values cost 32 shuffles instead of 6 per value.  Lane l (bit 0
-// clear) ends with the wave sum of value res_index(l); the 4 wave sums are added in LDS.
+// clear) ends with the wave sum of value ridx(l) (its bits 5..1 reversed); the 4 wave sums are
+// added in LDS.  (A matrix-core form of this partial, v_mfma_f64_16x16x4 over the rows staged in
+// LDS, bought 3 % of the kernel in round 4: the kernel is bound by its gathers and fits.)
 __device__ __forceinline__ void res_reduce(double (*red)[28], int tid, const float* row, float b, bool ok,
                                            double* out) {
   const int lane = tid & 63, wave = tid >> 6;
@@ -527,64 +536,6 @@ __device__ __forceinline__ void res_reduce(double (*red)[28], int tid, const flo
   __syncthreads();
 }
 
-// The same partial on the matrix cores.  A wave's 64 rows form an 8-column matrix
-// M = [row | b | ok] (a rejected query's row is zero) and the 28 values are the upper triangle of
-// M^T M (columns 0-5 with 0-5, 0-5 with b, ok with ok).  The rows are staged in LDS (`stage`: 512
-// floats per wave) and fed to 8 v_mfma_f64_16x16x4_f64, one per block of 8 rows: lane l gives
-// element l & 7 of row 8 kb + (l >> 3) as A[i = l & 15][k = l >> 4] and as B[k][j = l & 15], so
-// rows 8 kb + 2k and 8 kb + 2k + 1 share k and the tile's two diagonal 8 x 8 blocks accumulate
-// M^T M of the even and odd rows (the off-diagonal blocks are never read).  Every product is a
-// float product, exact in fp64; the sums are fp64 in the MFMA's order instead of the butterfly's.
-// The VALU is left with the staging and 8 conversions per lane: the transposed butterfly costs
-// ~250 VALU instructions per lane, on a path whose other kernels are VALU-bound too.
-typedef double fbr_f64x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ int res_index(int i, int j) {  // (row i, column j) of M^T M -> partial slot
-  if (i > j) return -1;
-  if (j < 6) return i * 6 - i * (i - 1) / 2 + (j - i);
-  if (j == 6) return i < 6 ? 21 + i : -1;
-  return i == 7 ? 27 : -1;
-}
-__device__ __forceinline__ void res_reduce_mfma(double (*red)[28], float* stage, int tid, const float* row, float b,
-                                                bool ok, double* out) {
-  const int lane = tid & 63, wave = tid >> 6;
-  float* st = stage + wave * 512;
-  const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  reinterpret_cast<float4*>(st)[2 * lane] = ok ? make_float4(row[0], row[1], row[2], row[3]) : z;
-  reinterpret_cast<float4*>(st)[2 * lane + 1] = ok ? make_float4(row[4], row[5], b, 1.0f) : z;
-  wave_lds_sync();
-  fbr_f64x4 c = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int kb = 0; kb < 8; ++kb) {
-    const double x = (double)st[kb * 64 + lane];
-    c = __builtin_amdgcn_mfma_f64_16x16x4f64(x, x, c, 0, 0, 0);
-  }
-  // C[i][j] is register i >> 2 of lane j + 16 (i & 3); the even- and odd-row blocks are summed
-  // by the lanes j < 8 of each 16-lane group: D[g][j] and D[g + 4][j], g = lane >> 4
-  const bool up = (lane & 8) != 0;
-  const double x0 = up ? c[2] : c[0], x1 = up ? c[3] : c[1];
-  const double d0 = x0 + __shfl_xor(x0, 8), d1 = x1 + __shfl_xor(x1, 8);
-  if (!up) {
-    const int j = lane & 7, g = lane >> 4;
-    const int i0 = res_index(g, j), i1 = res_index(g + 4, j);
-    if (i0 >= 0) red[wave][i0] = d0;
-    if (i1 >= 0) red[wave][i1] = d1;
-  }
-  __syncthreads();
-  if (tid < 28) {
-    double s = 0.0;
-    for (int w = 0; w < kResThreads / 64; ++w) s += red[w][tid];
-    out[tid] = s;
-  }
-  __syncthreads();
-}
-
-// Normal-equation partial of the item (res_mfma: matrix cores, FBR_RES_MFMA; else the butterfly).
-__device__ __forceinline__ void res_partial(double (*red)[28], float* stage, int res_mfma, int tid, const float* row,
-                                            float b, bool ok, double* out) {
-  if (res_mfma) res_reduce_mfma(red, stage, tid, row, b, ok, out);
-  else res_reduce(red, tid, row, b, ok, out);
-}
-
 // kNN pass: one lane per query, writes the 5 neighbour map indices (slot 0 = -1: no correspondence).
 // R = grid cells per side covering radius 1 (both map grids share one cell size).  kFused: the
 // same lane goes on to its residual row and the workgroup reduces the item's normal-equation
@@ -594,8 +545,7 @@ __device__ __forceinline__ void res_partial(double (*red)[28], float* stage, int
 // chain is LPQ times shorter; lane `sub` == 0 of each query writes the results.
 // One virtual workgroup v (item v / LPQ, query group v % LPQ) of the kNN pass (k_gn_knn's body).
 template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ>
-__device__ __forceinline__ void gn_knn_block(const GnArgs& a, int v, int use_prev, double (*red)[28], float* stage,
-                                             int2* rows) {
+__device__ __forceinline__ void gn_knn_block(const GnArgs& a, int v, int use_prev, double (*red)[28], int2* rows) {
   constexpr int QPB = kResThreads / LPQ;  // queries per workgroup
   const int sub = (int)threadIdx.x % LPQ;
   const int it = v / LPQ;
@@ -671,7 +621,7 @@ __device__ __forceinline__ void gn_knn_block(const GnArgs& a, int v, int use_pre
       rok = res_row(g, mg.by_id, ids, 1, corner, p, x0, y0, z0, row, b, a.fitc + (int64_t)it * 6 * kResThreads + tid,
                     a.fits + q, same);
   }
-  if (kFused) res_partial(red, stage, a.res_mfma, tid, row, b, rok, a.partial + (int64_t)it * kPartial);
+  if (kFused) res_reduce(red, tid, row, b, rok, a.partial + (int64_t)it * kPartial);
 }
 
 template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ = 1>
@@ -679,11 +629,10 @@ __global__ void __launch_bounds__(kResThreads)
 k_gn_knn(GnArgs a, int use_prev) {
   static_assert(LPQ == 1 || (!kFused && !kFlat), "wide mode is the plain kNN pass");
   __shared__ double red[kFused ? kResThreads / 64 : 1][28];
-  __shared__ __attribute__((aligned(16))) float stage[kFused ? kResThreads * 8 : 4];
   __shared__ int2 rows[kFlat ? (2 * R + 1) * (2 * R + 1) : 1][kResThreads];
   const int nitems = a.nitems[0];
   for (int v = blockIdx.x; v < nitems * LPQ; v += gridDim.x)
-    gn_knn_block<R, RX, kFused, kFlat, kSparse, LPQ>(a, v, use_prev, red, stage, &rows[0][threadIdx.x]);
+    gn_knn_block<R, RX, kFused, kFlat, kSparse, LPQ>(a, v, use_prev, red, &rows[0][threadIdx.x]);
 }
 
 // pcl::getTransformation (x,y,z,roll,pitch,yaw) in float with glibc's sinf / cosf
@@ -701,7 +650,10 @@ __device__ void pose_to_T(const float* tr, float* T, float* trig) {
 }
 
 // The residual rows of work item `it` and its normal-equation partial (k_gn_residual's body).
-__device__ __forceinline__ void gn_residual_item(const GnArgs& a, int it, double (*red)[28], float* stage) {
+// (Round 6 measured packing an item's refits into the first waves -- list them in LDS, fit, barrier,
+// apply: -15 % VALU instructions per dispatch but +6 % duration alone, the two extra barriers
+// exposing the gathers' latency; profiles/r06b_residual_refit_compaction_ab.txt.)
+__device__ __forceinline__ void gn_residual_item(const GnArgs& a, int it, double (*red)[28]) {
   const int tid = threadIdx.x;
   const int4 item = a.items[it];
   const int job = item.x;
@@ -721,7 +673,7 @@ __device__ __forceinline__ void gn_residual_item(const GnArgs& a, int it, double
     ok = res_row(g, corner ? a.mc.by_id : a.ms.by_id, nb, kResThreads, corner, p, x0, y0, z0, row, b,
                  a.fitc + (int64_t)it * 6 * kResThreads + tid, a.fits + q, a.nsame[q] != 0);
   }
-  res_partial(red, stage, a.res_mfma, tid, row, b, ok, a.partial + (int64_t)it * kPartial);
+  res_reduce(red, tid, row, b, ok, a.partial + (int64_t)it * kPartial);
 }
 
 // The normal equations of one job in float, as LMOptimization forms them (matAtA / matAtB).

@@ -35,6 +35,9 @@ struct DebugCounters {
   std::atomic<long long> host_ns[4] = {0, 0, 0, 0};
   // batch calls: [0] fbr_batch_launch wall time, [1] of it spent waiting for GN iteration flags
   std::atomic<long long> batch_ns[2] = {0, 0};
+  // host waits on device results (fbr_diag_wait_stats): fallbacks, waits > 1 ms, longest wait (ns),
+  // stream queries
+  std::atomic<long long> flag_fallbacks{0}, waits_over_1ms{0}, wait_max_ns{0}, stream_queries{0};
 };
 inline DebugCounters& debug_counters() {
   static DebugCounters c;
@@ -284,7 +287,6 @@ struct GnArgs {
   int8_t* fits;              // [max_items][256] fit cache state (0 none, 1 fitted, 2 rejected)
   int8_t* nsame;             // [max_items][256] 1: this iteration's neighbours equal the previous ones
   int fit_cache;             // reuse cached fits (FBR_FIT_CACHE, default 1)
-  int res_mfma;              // item partials on the matrix cores (FBR_RES_MFMA=1; default: the butterfly)
   unsigned long long* iter_flags;  // host-mapped [max_iter]: (generation << 32) | jobs still active
   int32_t* iter_cnt;         // [max_iter][2] active-job count / finished workgroups, then [max_iter]
                              // queued-query and [max_iter] non-empty-block counts of the block
@@ -342,8 +344,10 @@ void launch_pack_results(hipStream_t s, int B, int with_reg, const float* pose_o
 // laserCloud{Corner,Surf}FromMapDSNum: CropBox counts of the global map per job.
 void launch_export_records(hipStream_t s, int B, const float* pose_out, const fbr_reg_stats* stats, const int32_t* err,
                            const float* guess, float* dst);
-void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* map_pts, int64_t n, int which,
-                       int32_t* counts /* [B][2] */);
+// (accumulated in `work` [B][2], this launch's work slot, then copied to `counts` [B][2]: a
+// recomputation never exposes a partial count to a reader of the same staged batch's counts)
+void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* corner_pts, int64_t n_corner,
+                       const float4* surf_pts, int64_t n_surf, int32_t* work, int32_t* counts);
 
 // ---- keyframe local map (k_keyframe.hip) ----
 struct KfSeg {               // one selected keyframe cloud: pool[src .. src+count) -> out[dst ..]

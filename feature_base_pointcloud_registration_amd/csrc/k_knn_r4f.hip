@@ -1,4 +1,4 @@
-// k_knn_r4f.hip — kNN kernels for 0.25 m y/z grid cells (R = 4 cells per side), fused kNN + residual row + item partial (GN tail mode, FBR_GN_FUSED).
+// k_knn_r4f.hip — kNN kernels for 0.25 m y/z grid cells (R = 4 cells per side), fused kNN + residual row + item partial (the GN tail mode).
 // One translation unit per (R, fused) so the instantiations compile in parallel (fbr_gn.h).
 #include "fbr_gn.h"
 

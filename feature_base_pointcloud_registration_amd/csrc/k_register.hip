@@ -107,9 +107,8 @@ __global__ void k_gn_init(GnArgs a) {
 __global__ void __launch_bounds__(kResThreads)
 k_gn_residual(GnArgs a) {
   __shared__ double red[kResThreads / 64][28];
-  __shared__ __attribute__((aligned(16))) float stage[kResThreads * 8];
   const int nitems = a.nitems[0];
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x) gn_residual_item(a, it, red, stage);
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) gn_residual_item(a, it, red);
 }
 
 
@@ -221,24 +220,36 @@ __global__ void k_gn_finalize(GnArgs a) {
 // CropBox counts of the global map for every job's box (laserCloud{Corner,Surf}FromMapDSNum,
 // statistics only: the registration applies the box per kNN candidate).  The box is the guess's
 // translation +- crop_half (registration :289-304), identical to the one k_gn_init stores.
-__global__ void k_crop_count(GnArgs a, const float4* pts, int64_t n, int which, int32_t* counts) {
-  extern __shared__ int32_t c[];
-  for (int j = threadIdx.x; j < a.B; j += blockDim.x) c[j] = 0;
+// One wave per (tile of 512 map points, 64 jobs): the tile is staged in LDS and every lane tests
+// all of it against its job's box (LDS broadcast reads), then adds its count once.  The counts of a
+// launch accumulate in a per-work-slot buffer (zeroed first) and are then copied to the inputs'
+// statistics slots, so a launch recomputing them never exposes a partial count to an earlier
+// launch of the same staged batch that reads them.  Integer counts: exact in any order.
+constexpr int kCropTile = 512;
+__global__ void __launch_bounds__(64) k_crop_count(GnArgs a, const float4* __restrict__ pc, int64_t nc,
+                                                   const float4* __restrict__ ps, int64_t ns, int64_t tiles_c,
+                                                   int32_t* counts) {
+  __shared__ float4 tile[kCropTile];
+  const int lane = threadIdx.x;
+  const int64_t t = blockIdx.x;
+  const int which = t < tiles_c ? 0 : 1;
+  const float4* pts = which ? ps : pc;
+  const int64_t n = which ? ns : nc;
+  const int64_t i0 = (which ? t - tiles_c : t) * kCropTile;
+  const int m = (int)min<int64_t>(kCropTile, n - i0);
+  for (int i = lane; i < m; i += 64) tile[i] = pts[i0 + i];
   __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float4 p = pts[i];
-    for (int j = 0; j < a.B; ++j) {
-      const float* gp = a.guess + 6 * j;
-      const float mn0 = -a.crop_half[0] + gp[3], mn1 = -a.crop_half[1] + gp[4], mn2 = -a.crop_half[2] + gp[5];
-      const float mx0 = a.crop_half[0] + gp[3], mx1 = a.crop_half[1] + gp[4], mx2 = a.crop_half[2] + gp[5];
-      if (p.x < mn0 || p.y < mn1 || p.z < mn2) continue;
-      if (p.x > mx0 || p.y > mx1 || p.z > mx2) continue;
-      atomicAdd(&c[j], 1);
-    }
+  const int j = blockIdx.y * 64 + lane;
+  if (j >= a.B) return;
+  const float* gp = a.guess + 6 * j;  // registration :289-292 (k_gn_init's box)
+  const float mn0 = -a.crop_half[0] + gp[3], mn1 = -a.crop_half[1] + gp[4], mn2 = -a.crop_half[2] + gp[5];
+  const float mx0 = a.crop_half[0] + gp[3], mx1 = a.crop_half[1] + gp[4], mx2 = a.crop_half[2] + gp[5];
+  int cnt = 0;
+  for (int i = 0; i < m; ++i) {
+    const float4 p = tile[i];
+    cnt += (int)(!(p.x < mn0 || p.y < mn1 || p.z < mn2) && !(p.x > mx0 || p.y > mx1 || p.z > mx2));
   }
-  __syncthreads();
-  for (int j = threadIdx.x; j < a.B; j += blockDim.x)
-    if (c[j]) atomicAdd(&counts[2 * j + which], c[j]);
+  if (cnt) atomicAdd(&counts[2 * j + which], cnt);
 }
 
 // 32-byte pose record per job {pose[6], iterations, status} for the cross-GPU gather.  A job over the
@@ -305,12 +316,16 @@ void launch_gn_solve(hipStream_t s, const GnArgs& a, int iter_idx, unsigned long
 void launch_gn_finalize(hipStream_t s, const GnArgs& a) {
   fbr_launch(k_gn_finalize, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
 }
-void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* pts, int64_t n, int which, int32_t* counts) {
-  if (n <= 0) return;
-  int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
-  fbr_launch(k_crop_count, dim3(grid), dim3(256), sizeof(int32_t) * a.B, s, a, pts, n, which, counts);
+void launch_crop_count(hipStream_t s, const GnArgs& a, const float4* pc, int64_t nc, const float4* ps, int64_t ns,
+                       int32_t* work, int32_t* counts) {
+  if (a.B <= 0) return;
+  (void)hipMemsetAsync(work, 0, sizeof(int32_t) * 2 * a.B, s);
+  const int64_t tc = (nc + kCropTile - 1) / kCropTile, ts = (ns + kCropTile - 1) / kCropTile;
+  if (tc + ts > 0)
+    fbr_launch(k_crop_count, dim3((unsigned)(tc + ts), (unsigned)((a.B + 63) / 64)), dim3(64), 0, s, a, pc, nc, ps, ns, tc,
+               work);
+  (void)hipMemcpyAsync(counts, work, sizeof(int32_t) * 2 * a.B, hipMemcpyDeviceToDevice, s);
 }
-
 }  // namespace fbr
 
 #ifdef FBR_KNN_STATS

@@ -294,13 +294,8 @@ __device__ int vg_radix_sort(uint32_t* (&kb)[2], V* (&vb)[2], int n, int nbits, 
 // of each digit's ballot peer group instead of LDS atomics; 2 = that, plus round 3's wave-uniform
 // early exit (`if (c0 + 64 * k >= c1) break;`) in the count and scatter loops: the exact form that
 // mis-sorted in round 3.
-#ifdef FBR_VG_IP_NOINLINE  // diagnostic build: round 3's outlined call (with a call frame), for the replay
-#define FBR_VG_IP_INLINE __attribute__((noinline))
-#else
-#define FBR_VG_IP_INLINE __attribute__((always_inline))
-#endif
 template <int T, int KPL, int kLeader = 0>
-__device__ FBR_VG_IP_INLINE void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint16_t* vals, int n, int nbits,
+__device__ __attribute__((always_inline)) void vg_radix_sort_inplace(FBR_LDS_AS uint32_t* keys, FBR_LDS_AS uint16_t* vals, int n, int nbits,
                                       uint32_t* hist, uint32_t* wsum) {
   constexpr int NW = T / 64, NB = 256, PER = NB * NW / T;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -672,11 +667,7 @@ __global__ void __launch_bounds__(T) k_voxel_grid_ip(VgArgs A) {
       }
     }
     FBR_VG_STAMP(2);
-#ifdef FBR_VG_IP_LEADER  // diagnostic build: round 3's ballot-leader digit counts (1), or its exact form (2)
-    vg_radix_sort_inplace<T, KPL, FBR_VG_IP_LEADER>(keys, vals, n, G.nbits, hist, wsum);
-#else
     vg_radix_sort_inplace<T, KPL>(keys, vals, n, G.nbits, hist, wsum);
-#endif
     FBR_VG_STAMP(3);
     total = vg_emit<T, true>(keys, vals, n, hist, wsum, in, out);  // hist: (NW + 1) * 2 KB
     FBR_VG_STAMP(4);

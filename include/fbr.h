@@ -414,6 +414,12 @@ typedef struct fbr_comm fbr_comm;
 int fbr_comm_unique_id(uint8_t id_out[FBR_COMM_ID_BYTES]);
 int fbr_comm_create(fbr_comm** out, fbr_ctx* ctx, const uint8_t id[FBR_COMM_ID_BYTES], int nranks, int rank,
                     int max_jobs_per_rank);
+/* One process driving several devices (one host thread, one ctx and one rank per device, SURVEY §7
+ * step 7): the communicators of all n contexts at once, rank i = ctxs[i] (distinct devices), made
+ * with one RCCL unique id inside an ncclGroupStart / ncclGroupEnd.  Each thread then calls
+ * fbr_batch_allgather with its own ctx and out[i], the same launch ids on every thread; each
+ * communicator is destroyed with fbr_comm_destroy. */
+int fbr_comm_create_local(fbr_comm** out /* [n] */, fbr_ctx* const* ctxs, int n, int max_jobs_per_rank);
 int fbr_comm_destroy(fbr_comm* comm);
 /* Collective (every rank, same launch_id; -1 = the latest launch): the records of that launch of
  * every rank into recv = [nranks][max_jobs_per_rank][8] x 4 B (device memory of the ctx's device;

@@ -9,10 +9,12 @@
 //         per job { float guess[6]; int64 n; n x 24 B fbr_point_xyzirt }
 // output: (rank 0) the gathered records of the last launch, rank order, padding removed:
 //         n_jobs x {float pose[6]; int32 iterations; int32 status}
-// usage : shard_demo IN OUT [--ranks N] [--launches L] [--same-device]
+// usage : shard_demo IN OUT [--ranks N] [--launches L] [--same-device] [--threads]
 //         The parent forks N rank processes before anything touches the GPU; rank 0 writes the
 //         RCCL unique id to OUT.id, the others read it (the out-of-band channel a real deployment
 //         takes from its launcher).  Rank r uses device r (--same-device: device 0).
+//         --threads: one process, one host thread + ctx + rank per device (devices 0..N-1), the
+//         communicators made together by fbr_comm_create_local.
 // exit  : 0 ok, 2 bad input, 3 library error (prints the status), 4 records differ from the
 //         rank's own fbr_batch_results
 #include <hip/hip_runtime_api.h>
@@ -79,11 +81,16 @@ int fail(int rank, const char* what, int st) {
   return 3;
 }
 
-int run_rank(const Input& in, const std::string& out, int rank, int world, int launches, bool same_device) {
+int max_block_of(int world, int n_jobs) {
+  int m = 0;
+  for (int r = 0; r < world; ++r) m = std::max(m, block_begin(r + 1, world, n_jobs) - block_begin(r, world, n_jobs));
+  return m;
+}
+
+// One rank's context: created on its device, map set, its block of the jobs staged.
+int setup_rank(const Input& in, int rank, int world, int dev, fbr_ctx** out_ctx) {
+  *out_ctx = nullptr;
   const int j0 = block_begin(rank, world, in.n_jobs), j1 = block_begin(rank + 1, world, in.n_jobs);
-  int max_block = 0;
-  for (int r = 0; r < world; ++r)
-    max_block = std::max(max_block, block_begin(r + 1, world, in.n_jobs) - block_begin(r, world, in.n_jobs));
   const int B = j1 - j0;
   fbr_params P;
   fbr_params_default(&P);
@@ -94,8 +101,9 @@ int run_rank(const Input& in, const std::string& out, int rank, int world, int l
   for (int j = j0; j < j1; ++j) nmax = std::max<int64_t>(nmax, (int64_t)in.jobs[j].pts.size());
   P.max_points_per_scan = (int32_t)nmax;
   fbr_ctx* ctx = nullptr;
-  int st = fbr_create(&ctx, &P, same_device ? 0 : rank);
+  int st = fbr_create(&ctx, &P, dev);
   if (st) return fail(rank, "fbr_create", st);
+  *out_ctx = ctx;
   st = fbr_set_map(ctx, in.corner.data(), (int64_t)in.corner.size(), in.surf.data(), (int64_t)in.surf.size());
   if (st) return fail(rank, "fbr_set_map", st);
   std::vector<const fbr_point_xyzirt*> scans;
@@ -108,40 +116,21 @@ int run_rank(const Input& in, const std::string& out, int rank, int world, int l
   }
   st = fbr_batch_stage(ctx, scans.data(), nin.data(), B, guesses.data());
   if (st) return fail(rank, "fbr_batch_stage", st);
+  return 0;
+}
 
-  // the communicator: rank 0 makes the id, the others take it from OUT.id
-  uint8_t id[FBR_COMM_ID_BYTES];
-  const std::string idf = out + ".id";
-  if (rank == 0) {
-    st = fbr_comm_unique_id(id);
-    if (st) return fail(rank, "fbr_comm_unique_id", st);
-    const std::string tmp = idf + ".tmp";
-    FILE* f = fopen(tmp.c_str(), "wb");
-    if (!f || fwrite(id, 1, sizeof(id), f) != sizeof(id)) return fail(rank, "write id", FBR_ERR_INVALID_ARG);
-    fclose(f);
-    rename(tmp.c_str(), idf.c_str());
-  } else {
-    bool got = false;
-    for (int t = 0; t < 6000 && !got; ++t) {  // up to 60 s
-      FILE* f = fopen(idf.c_str(), "rb");
-      if (f) {
-        got = fread(id, 1, sizeof(id), f) == sizeof(id);
-        fclose(f);
-      }
-      if (!got) std::this_thread::sleep_for(std::chrono::milliseconds(10));
-    }
-    if (!got) return fail(rank, "read id", FBR_ERR_STATE);
-  }
-  fbr_comm* comm = nullptr;
-  st = fbr_comm_create(&comm, ctx, id, world, rank, max_block);
-  if (st) return fail(rank, "fbr_comm_create", st);
-
-  // pipelined launches: after launch n, gather launch n - 1 (already fully enqueued or nearly so),
-  // the same launch id on every rank; the last one after the loop
+// Pipelined launches, each launch's records all-gathered (after launch n, launch n - 1, the same
+// launch id on every rank; the last one after the loop), then this rank's own results against its
+// block of the gathered records; rank 0 writes the records (rank order, padding removed).
+int run_launches(const Input& in, const std::string& out, int rank, int world, int launches, fbr_ctx* ctx,
+                 fbr_comm* comm) {
+  const int max_block = max_block_of(world, in.n_jobs);
+  const int B = block_begin(rank + 1, world, in.n_jobs) - block_begin(rank, world, in.n_jobs);
   void* recv = nullptr;
   const size_t rbytes = sizeof(float) * 8 * (size_t)max_block * world;
   if (hipMalloc(&recv, rbytes) != hipSuccess) return fail(rank, "hipMalloc", FBR_ERR_HIP);
   void* gst = nullptr;
+  int st = 0;
   for (int k = 0; k < launches; ++k) {
     st = fbr_batch_launch(ctx);
     if (st) return fail(rank, "fbr_batch_launch", st);
@@ -155,8 +144,6 @@ int run_rank(const Input& in, const std::string& out, int rank, int world, int l
   if (hipStreamSynchronize((hipStream_t)gst) != hipSuccess) return fail(rank, "hipStreamSynchronize", FBR_ERR_HIP);
   std::vector<float> rec(8 * (size_t)max_block * world);
   if (hipMemcpy(rec.data(), recv, rbytes, hipMemcpyDeviceToHost) != hipSuccess) return fail(rank, "hipMemcpy", FBR_ERR_HIP);
-
-  // this rank's own results against its block of the gathered records
   std::vector<float> poses(6 * (size_t)B);
   std::vector<fbr_reg_stats> stats(B);
   st = fbr_batch_results(ctx, poses.data(), stats.data());
@@ -178,31 +165,106 @@ int run_rank(const Input& in, const std::string& out, int rank, int world, int l
     if (f) fclose(f);
   }
   (void)hipFree(recv);
-  fbr_comm_destroy(comm);
-  fbr_destroy(ctx);
   if (bad) {
     fprintf(stderr, "rank %d: %d records differ from fbr_batch_results\n", rank, bad);
     return 4;
   }
   return 0;
 }
+
+// Process mode: this process is rank `rank`; the RCCL id travels through OUT.id.
+int run_rank(const Input& in, const std::string& out, int rank, int world, int launches, bool same_device) {
+  fbr_ctx* ctx = nullptr;
+  int rc = setup_rank(in, rank, world, same_device ? 0 : rank, &ctx);
+  if (rc) {
+    if (ctx) fbr_destroy(ctx);
+    return rc;
+  }
+  // the communicator: rank 0 makes the id, the others take it from OUT.id
+  uint8_t id[FBR_COMM_ID_BYTES];
+  const std::string idf = out + ".id";
+  int st = 0;
+  if (rank == 0) {
+    st = fbr_comm_unique_id(id);
+    if (st) return fail(rank, "fbr_comm_unique_id", st);
+    const std::string tmp = idf + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f || fwrite(id, 1, sizeof(id), f) != sizeof(id)) return fail(rank, "write id", FBR_ERR_INVALID_ARG);
+    fclose(f);
+    rename(tmp.c_str(), idf.c_str());
+  } else {
+    bool got = false;
+    for (int t = 0; t < 6000 && !got; ++t) {  // up to 60 s
+      FILE* f = fopen(idf.c_str(), "rb");
+      if (f) {
+        got = fread(id, 1, sizeof(id), f) == sizeof(id);
+        fclose(f);
+      }
+      if (!got) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+    if (!got) return fail(rank, "read id", FBR_ERR_STATE);
+  }
+  fbr_comm* comm = nullptr;
+  st = fbr_comm_create(&comm, ctx, id, world, rank, max_block_of(world, in.n_jobs));
+  if (st) return fail(rank, "fbr_comm_create", st);
+  rc = run_launches(in, out, rank, world, launches, ctx, comm);
+  fbr_comm_destroy(comm);
+  fbr_destroy(ctx);
+  return rc;
+}
+
+// Thread mode: one process, one host thread, one ctx and one rank per device.
+// The contexts are set up by their threads, the communicators of all of them at once by this
+// thread (fbr_comm_create_local: one RCCL group), then every thread runs its launches and gathers.
+int run_threads(const Input& in, const std::string& out, int world, int launches) {
+  std::vector<fbr_ctx*> ctx(world, nullptr);
+  std::vector<int> rc(world, 0);
+  {
+    std::vector<std::thread> th;
+    for (int r = 0; r < world; ++r) th.emplace_back([&, r] { rc[r] = setup_rank(in, r, world, r, &ctx[r]); });
+    for (auto& t : th) t.join();
+  }
+  int first = 0;
+  for (int r = 0; r < world; ++r)
+    if (rc[r] && !first) first = rc[r];
+  std::vector<fbr_comm*> comm(world, nullptr);
+  if (!first) {
+    const int st = fbr_comm_create_local(comm.data(), ctx.data(), world, max_block_of(world, in.n_jobs));
+    if (st) first = fail(0, "fbr_comm_create_local", st);
+  }
+  if (!first) {
+    std::vector<std::thread> th;
+    for (int r = 0; r < world; ++r)
+      th.emplace_back([&, r] { rc[r] = run_launches(in, out, r, world, launches, ctx[r], comm[r]); });
+    for (auto& t : th) t.join();
+    for (int r = 0; r < world; ++r)
+      if (rc[r] && !first) first = rc[r];
+  }
+  for (int r = 0; r < world; ++r) {
+    if (comm[r]) fbr_comm_destroy(comm[r]);
+    if (ctx[r]) fbr_destroy(ctx[r]);
+  }
+  return first;
+}
 }  // namespace
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: %s IN OUT [--ranks N] [--launches L] [--same-device]\n", argv[0]);
+    fprintf(stderr, "usage: %s IN OUT [--ranks N] [--launches L] [--same-device] [--threads]\n", argv[0]);
     return 2;
   }
   int ranks = 1, launches = 3;
-  bool same_device = false;
+  bool same_device = false, threads = false;
   for (int i = 3; i < argc; ++i) {
     if (!strcmp(argv[i], "--ranks") && i + 1 < argc) ranks = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--launches") && i + 1 < argc) launches = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--same-device")) same_device = true;
+    else if (!strcmp(argv[i], "--threads")) threads = true;
   }
   Input in;
   if (!read_input(argv[1], in) || ranks < 1 || ranks > in.n_jobs || launches < 1) return 2;
   const std::string out = argv[2];
+  if (threads) return run_threads(in, out, ranks, launches);  // rank r on device r
   (void)remove((out + ".id").c_str());
   // one process per rank, forked before any HIP call (the parent never touches the GPU)
   std::vector<pid_t> kids;

@@ -178,6 +178,68 @@ def test_native_shard_demo_builds_and_reports_no_device(tmp_path):
     assert "fbr_create" in r.stderr
 
 
+def test_native_shard_demo_thread_mode_reports_no_device(tmp_path):
+    """CPU: the one-process multi-device host (shard_demo --threads: one host thread, ctx and RCCL
+    rank per device, the communicators made together by fbr_comm_create_local) fails cleanly
+    without a GPU: fbr_create fails in the rank threads and the demo exits 3 before any collective."""
+    import subprocess
+    from conftest import build_shard_demo, has_gpu
+    from feature_base_pointcloud_registration_amd import synth
+    if has_gpu():
+        pytest.skip("a GPU is visible")
+    exe = build_shard_demo()
+    inp = tmp_path / "in.bin"
+    _write_shard_input(inp, 16, 1800, *synth.config_map("C1"), synth.make_jobs("C1", 2, base_seed=91))
+    r = subprocess.run([exe, str(inp), str(tmp_path / "out.bin"), "--ranks", "2", "--threads"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 3, (r.returncode, r.stderr)
+    assert "fbr_create" in r.stderr
+
+
+def test_comm_create_local_rejects_bad_arguments():
+    """CPU: fbr_comm_create_local validates before touching RCCL or a device: null outputs / contexts,
+    no ranks, no jobs -> FBR_ERR_INVALID_ARG."""
+    import ctypes
+    from feature_base_pointcloud_registration_amd import api
+    L = api.lib()
+    out = (ctypes.c_void_p * 2)()
+    ctxs = (ctypes.c_void_p * 2)()  # null contexts
+    assert L.fbr_comm_create_local(None, ctxs, 2, 8) == -1
+    assert L.fbr_comm_create_local(out, None, 2, 8) == -1
+    assert L.fbr_comm_create_local(out, ctxs, 0, 8) == -1
+    assert L.fbr_comm_create_local(out, ctxs, 2, 0) == -1
+    assert L.fbr_comm_create_local(out, ctxs, 2, 8) == -1  # null ctx entries
+    assert out[0] is None and out[1] is None
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_native_rccl_thread_mode_world1_matches_batch_results(tmp_path):
+    """GPU, one process with one host thread per device (the box has one device, so world 1): the
+    communicator comes from fbr_comm_create_local (ncclGroupStart / ncclCommInitRank per device /
+    ncclGroupEnd), the thread stages a C2 batch, runs three pipelined launches and all-gathers each;
+    the records equal the rank's fbr_batch_results (inside the demo) and the process-mode run of
+    the same jobs, bit for bit."""
+    import subprocess
+    from conftest import build_shard_demo
+    from feature_base_pointcloud_registration_amd import synth
+    exe = build_shard_demo()
+    H, W = synth.CONFIGS["C2"][:2]
+    cmap, smap = synth.config_map("C2")
+    jobs = synth.make_jobs("C2", 8, base_seed=4300)
+    inp = tmp_path / "in.bin"
+    _write_shard_input(inp, H, W, cmap, smap, jobs)
+    recs = []
+    for mode in (["--threads"], []):
+        out = tmp_path / f"out{len(mode)}.bin"
+        r = subprocess.run([exe, str(inp), str(out), "--ranks", "1", "--launches", "3", *mode], capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, (mode, r.returncode, r.stderr[-2000:])
+        recs.append(np.fromfile(out, np.float32))
+    assert recs[0].shape == recs[1].shape == (8 * 8,)
+    assert np.array_equal(recs[0].view(np.int32), recs[1].view(np.int32))
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
 def test_native_rccl_allgather_world1_matches_batch_results(tmp_path):

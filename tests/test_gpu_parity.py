@@ -940,7 +940,7 @@ def test_wave_ring_filter_is_bit_identical_to_workgroup_kernel():
     ({"FBR_KNN_CELL": "0.5"}, False),                          # R = 2 rows, the C3 / C5 cells
     ({"FBR_KNN_CELL": "0.5", "FBR_GRID_SPARSE": "1"}, True),   # the same over hashed chunks
     ({"FBR_KNN_LPQ": "8"}, False),                             # wide mode for every launch
-    ({"FBR_GN_FUSED": "1"}, False),                            # fused kNN + residual
+    ({"FBR_GN_TAIL": "1"}, False),                             # fused kNN + residual (tail mode throughout)
     ({"FBR_KNN_FLAT": "0"}, False),                            # per-row loop from iteration 1
 ], ids=["cells-0.5", "cells-0.5-sparse", "wide", "fused", "no-flat"])
 def test_knn_variants_are_bit_identical(c2_map, env, sparse):
