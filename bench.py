@@ -217,11 +217,13 @@ def latency_line(cfg, corner_map, surf_map, n, cpu_scans=0):
         api.debug_counters(reset=True)
         api.host_times(reset=True)
         api.wait_stats(reset=True)
+        iters = []
         for k in range(3, n + 3):
             t = time.perf_counter()
             pose, st = c.process_scan(scans[k], 0.2 * k, pose)
             ms.append(1e3 * (time.perf_counter() - t))
             poses.append(pose.copy())
+            iters.append(int(st["iterations"]))
         launches, syncs, polls = api.debug_counters()
         ht = api.host_times()
         fallbacks, long_waits, wait_max_s, queries = api.wait_stats()
@@ -229,6 +231,9 @@ def latency_line(cfg, corner_map, surf_map, n, cpu_scans=0):
     out = {"scans": n, "ms_per_scan_mean": round(float(ms.mean()), 4), "ms_per_scan_p50": round(float(np.median(ms)), 4),
            "ms_per_scan_p99": round(float(np.percentile(ms, 99)), 4),
            "ms_per_scan_max": round(float(ms.max()), 4),
+           # the slowest scans of the chain: (index in the chain, ms, GN iterations)
+           "slowest": [(int(i), round(float(ms[i]), 4), iters[i]) for i in np.argsort(ms)[::-1][:3]],
+           "gn_iterations_mean": round(float(np.mean(iters)), 3),
            # host waits on device results (GN iteration flags, the direct result): fallbacks (not
            # visible although the stream drained), waits > 1 ms, the longest, stream queries
            "result_waits": {"fallbacks": fallbacks, "over_1ms": long_waits, "max_ms": round(1e3 * wait_max_s, 4),
