@@ -124,7 +124,10 @@ def lib():
             "fbr_comm_destroy": (ctypes.c_int, [_VP]),
             "fbr_batch_allgather": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP]),
         }
+        diag = bool(os.environ.get("FBR_LIB"))  # an A/B build of another round may lack newer entry points
         for name, (res, args) in sig.items():
+            if diag and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
@@ -168,6 +171,8 @@ def wait_stats(reset=False):
     """Host waits on device results since the last reset -- diagnostic (fbr_diag_wait_stats):
     (fallbacks: a flag or direct result not visible although its stream drained, waits longer than
     1 ms, the longest wait in s, stream queries)."""
+    if not hasattr(lib(), "fbr_diag_wait_stats"):  # an A/B build of an earlier round (FBR_LIB)
+        return -1, -1, -1.0, -1
     f = lib().fbr_diag_wait_stats
     f.restype, f.argtypes = ctypes.c_int, [_VP, ctypes.c_int]
     v = (ctypes.c_longlong * 4)()

@@ -144,7 +144,9 @@ struct GnRun {
 // smoothed duration of the completed waits of that kind (GN flags of batch runs, of single-scan
 // runs, single-scan direct results), within [kQueryMinNs, kQueryMaxNs]; queries repeat at most
 // every half bound.  (Round 5 used a fixed 2 ms, which a late-visible flag turned into a 2 ms scan.)
-constexpr int64_t kQueryMinNs = 150000, kQueryMaxNs = 2000000;
+// The floor stays above the longest normal single-scan wait (0.44 ms measured, r06c): at 150 us
+// about one wait per scan queried its stream, and each query is a marker before the next kernel.
+constexpr int64_t kQueryMinNs = 500000, kQueryMaxNs = 2000000;
 struct WaitBound {
   double ema_ns = 0.0;
   int64_t after() const {
@@ -430,6 +432,16 @@ int64_t vg_large_min() {
 int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf, std::vector<fbr_point_xyzi>& out) {
   out.clear();
   if (n <= 0) return FBR_OK;
+  // a host cloud with a non-finite point is not dense: PCL's VoxelGrid (and getMinMax3D) skip such
+  // points (voxel_grid.cpp, is_dense false), which is the filter over the finite points alone
+  for (int64_t i = 0; i < n; ++i)
+    if (!(std::isfinite(in[i].x) && std::isfinite(in[i].y) && std::isfinite(in[i].z))) {
+      std::vector<fbr_point_xyzi> fin;
+      fin.reserve(n);
+      for (int64_t j = 0; j < n; ++j)
+        if (std::isfinite(in[j].x) && std::isfinite(in[j].y) && std::isfinite(in[j].z)) fin.push_back(in[j]);
+      return voxel_grid_once(c, fin.data(), (int64_t)fin.size(), leaf, out);
+    }
   if (n > INT32_MAX / 4) return FBR_ERR_CAPACITY;
   float4 *d_in = nullptr, *d_out = nullptr;
   int32_t* d_cnt = nullptr;

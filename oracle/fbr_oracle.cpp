@@ -290,6 +290,18 @@ struct cloud_point_index_idx {  // pcl/filters/voxel_grid.h
 static void voxel_grid(const P4* in, int64_t n, float leaf, std::vector<P4>& out) {
   out.clear();
   if (n <= 0) return;
+  // a cloud with a non-finite point is not dense: applyFilter and getMinMax3D then skip those points
+  // (voxel_grid.cpp, `if (!input_->is_dense) ... if (!pcl_isfinite(...)) continue;`), which is the
+  // dense path over the finite points (cloud_point_index renumbered, the same key sequence)
+  for (int64_t i = 0; i < n; ++i)
+    if (!(std::isfinite(in[i].x) && std::isfinite(in[i].y) && std::isfinite(in[i].z))) {
+      std::vector<P4> fin;
+      fin.reserve(n);
+      for (int64_t j = 0; j < n; ++j)
+        if (std::isfinite(in[j].x) && std::isfinite(in[j].y) && std::isfinite(in[j].z)) fin.push_back(in[j]);
+      voxel_grid(fin.data(), (int64_t)fin.size(), leaf, out);
+      return;
+    }
   const float inv = 1.0f / leaf;  // inverse_leaf_size_ = Ones / leaf_size_ (float)
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
   for (int64_t i = 0; i < n; ++i) {  // getMinMax3D (dense cloud)

@@ -249,6 +249,38 @@ def test_voxel_grid_golden_and_oracle():
         assert len(ctx.voxel_grid(d["pts"][:0], 0.4)) == 0
 
 
+def test_non_finite_map_points_are_skipped(c2_map):
+    """Non-finite points in host clouds (a PCD map with NaN returns): the device
+    VoxelGrid skips them as PCL's does for a non-dense cloud (equal bytes to the finite points'
+    filter), and a prior map with NaN / inf points injected gives the same DS map and the same
+    registrations as the clean map (the kNN grid never holds a non-finite candidate)."""
+    rng = np.random.default_rng(5)
+    cm, sm = c2_map
+
+    def poison(m, k):
+        b = np.concatenate([m, m[rng.choice(len(m), k, replace=False)]])
+        b["x"][len(m)::3] = np.nan
+        b["y"][len(m) + 1::3] = -np.inf
+        b["z"][len(m) + 2::3] = np.nan
+        return b[rng.permutation(len(b))]
+
+    bc, bs = poison(cm, 300), poison(sm, 900)
+    fin = lambda a: a[np.isfinite(a["x"]) & np.isfinite(a["y"]) & np.isfinite(a["z"])]  # noqa: E731
+    H, W = synth.CONFIGS["C2"][:2]
+    P = synth.config_params("C2")
+    jobs = synth.make_jobs("C2", 2, base_seed=4400)
+    out = []
+    for maps in ((fin(bc), fin(bs)), (bc, bs)):  # a fresh context (stream state) per map
+        with api.Context(P) as ctx:
+            if not out:
+                assert ctx.voxel_grid(bs, 0.4).tobytes() == ctx.voxel_grid(fin(bs), 0.4).tobytes()
+            ctx.set_map(*maps)
+            out.append((ctx.get_map(), [ctx.process_scan(p, float(k), g)[0] for k, (p, g, _) in enumerate(jobs)]))
+    (ref_map, ref), (got_map, got) = out
+    assert all(a.tobytes() == b.tobytes() for a, b in zip(ref_map, got_map))
+    assert all(a.tobytes() == b.tobytes() for a, b in zip(ref, got))
+
+
 # ------------------------------------------------------------------------------- registration
 def test_registration_golden_fixture():
     d = np.load(os.path.join(G, "reg_small.npz"))

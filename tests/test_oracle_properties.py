@@ -43,6 +43,24 @@ def test_projection_ring_major_order():
                        pr["range"], rtol=1e-6)
 
 
+def test_voxel_grid_skips_non_finite_points():
+    """A cloud with NaN / inf points is not dense, and PCL's VoxelGrid then skips them
+    (voxel_grid.cpp, getMinMax3D and applyFilter under !is_dense): the output equals the filter of
+    the finite points alone, byte for byte (the same key sequence for std::sort)."""
+    rng = np.random.default_rng(3)
+    pts = np.zeros(4000, POINT_XYZI)
+    for k in "xyz":
+        pts[k] = rng.uniform(-20, 20, 4000)
+    pts["intensity"] = rng.uniform(0, 100, 4000)
+    bad = pts.copy()
+    sel = rng.choice(4000, 40, replace=False)
+    bad["x"][sel[:20]] = np.nan
+    bad["z"][sel[20:30]] = np.inf
+    bad["y"][sel[30:]] = -np.nan
+    finite = np.isfinite(bad["x"]) & np.isfinite(bad["y"]) & np.isfinite(bad["z"])
+    assert O.voxel_grid(bad, 0.4).tobytes() == O.voxel_grid(bad[finite], 0.4).tobytes()
+
+
 def test_voxel_grid_properties():
     rng = np.random.default_rng(0)
     pts = np.zeros(5000, POINT_XYZI)

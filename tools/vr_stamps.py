@@ -16,8 +16,9 @@ from feature_base_pointcloud_registration_amd import api, synth  # noqa: E402
 from feature_base_pointcloud_registration_amd.fbr_types import default_params  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+EXACT = int(sys.argv[2]) if len(sys.argv) > 2 else 0  # 1: exact_voxel_order (std::sort's partition phase)
 H, W = 64, 1800
-P = default_params(H, W, max_batch=B)
+P = default_params(H, W, max_batch=B, exact_voxel_order=EXACT)
 cm, sm = synth.config_map("C2")
 jobs = synth.make_jobs("C2", B)
 ctx = api.Context(P)
@@ -33,7 +34,7 @@ t = out[:, :5].astype(np.int64)
 ok = t[:, 4] > 0
 t = t[ok]
 d = np.diff(t, axis=1).astype(np.float64)
-names = ["load+compact+minmax", "keys", "sort (3 passes)", "emit"]
+names = ["load+compact+minmax", "keys" + (" + partition phase" if EXACT else ""), "run sort", "emit"]
 print(f"rings stamped: {ok.sum()} of {len(out)}; mean ticks per ring {d.sum(1).mean():.0f} (s_memtime, 100 MHz)")
 for n, v in zip(names, d.mean(0)):
     print(f"  {n:22s} {v:10.1f}  {100 * v / d.sum(1).mean():5.1f}%")
