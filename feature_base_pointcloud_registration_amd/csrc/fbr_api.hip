@@ -97,8 +97,10 @@ struct Ingest {
   fbr_point_xyzirt* d_pts_slot[2] = {};  // slot 0 = the context's scan buffer, slot 1 allocated here
   int nthreads = 8;                  // packing threads per chunk
   double h2d_bytes = 0.0;            // bytes copied host -> device by the last fbr_process_batch
-  // Compact records (no deskew tables set: `time` is never read): per scan the rings (u16) and
-  // xyzi (f32 x 4), 18 B per point instead of 24, expanded on the device by k_expand_scans.
+  // Compact records (no deskew tables set: `time` is never read): per scan the x, y, z planes
+  // (f32) and the rings (u8 below 256 rings), 13 B per point instead of 24, expanded on the device
+  // by k_expand_scans (the batch returns poses and statistics, which no point's intensity or time
+  // reaches).
   uint8_t* d_stage = nullptr;        // [Bcap][ingest_region_bytes(NMAX)]
   int64_t* d_nin = nullptr;          // [2][Bcap] point counts of the staged scans (copy stream)
   int64_t* h_nin = nullptr;          // [2][Bcap] pinned
@@ -2298,7 +2300,7 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
   // ring bytes per point: u8 for sensors of < 256 rings, where every out-of-range ring (>= H, which
   // projectPointCloud drops, imageProjection.cpp:599) is stored as 255, still out of range
   const int rb = c->H < 256 ? 1 : 2;
-  auto host_bytes = [&](int64_t n) { return compact ? (16 + rb) * n : n * (int64_t)sizeof(fbr_point_xyzirt); };
+  auto host_bytes = [&](int64_t n) { return compact ? (12 + rb) * n : n * (int64_t)sizeof(fbr_point_xyzirt); };
   if (compact) {  // the counts for k_expand_scans, on the copy stream (slot's half of the pinned array)
     for (int jj = 0; jj < B; ++jj) g.h_nin[(int64_t)slot * c->Bcap + jj] = n_in[jj];
     CK(hipMemcpyAsync(g.d_nin + (int64_t)slot * c->Bcap, g.h_nin + (int64_t)slot * c->Bcap, sizeof(int64_t) * B,
@@ -2329,13 +2331,14 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
           continue;
         }
         const fbr_point_xyzirt* src = scans[jj];
-        float* xyzi = reinterpret_cast<float*>(base + off[jj - j]);
-        uint8_t* rr = base + off[jj - j] + 16 * n;
+        float* px = reinterpret_cast<float*>(base + off[jj - j]);
+        float* py = px + n;
+        float* pz = py + n;
+        uint8_t* rr = base + off[jj - j] + 12 * n;
         for (int64_t i = 0; i < n; ++i) {
-          xyzi[4 * i] = src[i].x;
-          xyzi[4 * i + 1] = src[i].y;
-          xyzi[4 * i + 2] = src[i].z;
-          xyzi[4 * i + 3] = src[i].intensity;
+          px[i] = src[i].x;
+          py[i] = src[i].y;
+          pz[i] = src[i].z;
         }
         if (rb == 1)
           for (int64_t i = 0; i < n; ++i) rr[i] = src[i].ring < c->H ? (uint8_t)src[i].ring : (uint8_t)255;

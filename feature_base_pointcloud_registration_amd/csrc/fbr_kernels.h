@@ -65,7 +65,7 @@ struct MsgDev {
 };
 void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_point_xyzirt* out);
 // Compact ingest records (fbr_process_batch without deskew tables): job j's staging region holds
-// its n points packed, [x, y, z, intensity f32 x n][ring x n], the rings as u8 when the sensor has
+// its n points packed, [x f32 x n][y f32 x n][z f32 x n][ring x n], the rings as u8 when the sensor has
 // at most 256 rings (rb = 1), else u16 (rb = 2); regions are ingest_region_bytes(nmax) apart.
 inline int64_t ingest_region_bytes(int64_t nmax) { return (18 * nmax + 15) & ~(int64_t)15; }
 void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, const int64_t* nin, int rb,

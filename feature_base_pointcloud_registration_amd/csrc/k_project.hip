@@ -388,11 +388,14 @@ void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_
     fbr_launch(k_unpack_msg<false>, grid, dim3(256), 0, s, data, L, out);
 }
 
-// K0' k_expand_scans: the compact ingest records of fbr_process_batch (no deskew: the reference
-// never reads `time` on this path, imageProjection.cpp:189-191) -> the 24-B scan buffer.  Job j's
-// staging region (ingest_region_bytes apart) holds its n points packed: xyzi (f32 x 4) x n, then
-// the rings x n (u8 when rb = 1, u16 when rb = 2); time = 0.  Slots past n are not written
-// (k_project reads n points).  HBM-bound: 16 + rb B read + 24 B written per point.
+// K0' k_expand_scans: the compact ingest records of fbr_process_batch -> the 24-B scan buffer.
+// No deskew: the reference never reads `time` on this path (imageProjection.cpp:189-191), and a
+// batch returns poses and statistics, which no point's intensity reaches (it rides along as the
+// clouds' w channel: never in a key, a distance, a residual or a count), so neither is shipped.
+// Job j's staging region (ingest_region_bytes apart) holds its n points as planes x[n], y[n],
+// z[n] (f32), then the rings x n (u8 when rb = 1, u16 when rb = 2); intensity = time = 0.  Slots
+// past n are not written (k_project reads n points).  HBM-bound: 12 + rb B read + 24 B written per
+// point.
 __global__ void __launch_bounds__(256)
 k_expand_scans(const uint8_t* __restrict__ stage, int64_t nmax, int64_t region, const int64_t* __restrict__ nin,
                int rb, fbr_point_xyzirt* __restrict__ out) {
@@ -401,13 +404,13 @@ k_expand_scans(const uint8_t* __restrict__ stage, int64_t nmax, int64_t region, 
   const int64_t n = min(nin[job], nmax);
   if (i >= n) return;
   const uint8_t* r = stage + job * region;
-  const float4 p = reinterpret_cast<const float4*>(r)[i];
-  const uint16_t ring = rb == 1 ? (uint16_t)r[16 * n + i] : reinterpret_cast<const uint16_t*>(r + 16 * n)[i];
+  const float* pl = reinterpret_cast<const float*>(r);
+  const uint16_t ring = rb == 1 ? (uint16_t)r[12 * n + i] : reinterpret_cast<const uint16_t*>(r + 12 * n)[i];
   fbr_point_xyzirt q;
-  q.x = p.x;
-  q.y = p.y;
-  q.z = p.z;
-  q.intensity = p.w;
+  q.x = pl[i];
+  q.y = pl[n + i];
+  q.z = pl[2 * n + i];
+  q.intensity = 0.0f;
   q.ring = ring;
   q.pad_ = 0;
   q.time = 0.0f;
