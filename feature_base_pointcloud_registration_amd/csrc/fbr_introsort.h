@@ -134,25 +134,74 @@ __device__ void is_heap_sort(KP k, VP v, int first, int last) {
   }
 }
 
+// The same partial_sort on a range of at most 64 elements held in one wave's registers (lane a + j
+// holds element j, key / val), by the whole wave in lockstep: every index of the heap walk is
+// wave-uniform, so an element is read with v_readlane (an SGPR) and written by the one lane that
+// holds it -- the identical sequence of comparisons and moves as is_heap_sort's single lane over
+// LDS, without an LDS round trip per step (round 6: depth-exhausted frames were ~40k cycles each).
+__device__ __forceinline__ void is_reg_heap_sort(uint32_t& key, uint32_t& val, int a, int len, int lane) {
+  auto K = [&](int i) { return (uint32_t)__builtin_amdgcn_readlane((int)key, a + i); };
+  auto V = [&](int i) { return (uint32_t)__builtin_amdgcn_readlane((int)val, a + i); };
+  auto set = [&](int i, uint32_t kk, uint32_t vv) {
+    if (lane == a + i) {
+      key = kk;
+      val = vv;
+    }
+  };
+  auto adjust = [&](int hole, int n, uint32_t vk, uint32_t vv) {
+    const int top = hole;
+    int second = hole;
+    while (second < (n - 1) / 2) {
+      second = 2 * (second + 1);
+      if (K(second) < K(second - 1)) second--;
+      set(hole, K(second), V(second));
+      hole = second;
+    }
+    if ((n & 1) == 0 && second == (n - 2) / 2) {
+      second = 2 * (second + 1);
+      set(hole, K(second - 1), V(second - 1));
+      hole = second - 1;
+    }
+    int parent = (hole - 1) / 2;  // __push_heap
+    while (hole > top && K(parent) < vk) {
+      set(hole, K(parent), V(parent));
+      hole = parent;
+      parent = (hole - 1) / 2;
+    }
+    set(hole, vk, vv);
+  };
+  if (len >= 2) {
+    int parent = (len - 2) / 2;
+    while (true) {
+      adjust(parent, len, K(parent), V(parent));
+      if (parent == 0) break;
+      parent--;
+    }
+  }
+  int last = len;
+  while (last > 1) {
+    --last;
+    const uint32_t vk = K(last), vv = V(last);  // __pop_heap(first, last, last)
+    set(last, K(0), V(0));
+    adjust(0, last, vk, vv);
+  }
+}
+
 // __unguarded_partition(lo, hi, pivot value p) by one wave; posL / posR: scratch indexed [lo, hi).
 // Returns the cut.  Ends with a wave sync.
 template <typename KP, typename VP, typename PP>
 __device__ int is_wave_partition(KP k, VP v, PP posL, PP posR, int lo, int hi, uint32_t p, int lane) {
   const uint64_t below = (1ull << lane) - 1ull;
-  int cL = 0;
-  for (int b = lo; b < hi; b += 64) {
-    const int i = b + lane;
+  // the left and right stopper scans in one loop (independent: their LDS reads overlap)
+  int cL = 0, cR = 0;
+  for (int o = 0; o < hi - lo; o += 64) {
+    const int i = lo + o + lane, t = hi - 1 - o - lane;
     const bool isL = i < hi && !(k[i] < p);
-    const uint64_t bl = __ballot(isL);
+    const bool isR = t >= lo && !(p < k[t]);
+    const uint64_t bl = __ballot(isL), br = __ballot(isR);
     if (isL) posL[lo + cL + __popcll(bl & below)] = i;
+    if (isR) posR[lo + cR + __popcll(br & below)] = t;
     cL += __popcll(bl);
-  }
-  int cR = 0;
-  for (int t = hi - 1; t >= lo; t -= 64) {
-    const int i = t - lane;
-    const bool isR = i >= lo && !(p < k[i]);
-    const uint64_t br = __ballot(isR);
-    if (isR) posR[lo + cR + __popcll(br & below)] = i;
     cR += __popcll(br);
   }
   is_wave_sync();
@@ -213,22 +262,25 @@ __device__ int is_block_partition(KP k, VP v, PP posL, PP posR, int lo, int hi, 
     if (!(x < p)) posL[lo + ol++] = i;
     if (!(p < x)) posR[lo + (cR - 1 - orr++)] = i;  // rank from the right
   }
+  if (tid == 0) sh[2 * NW] = 0;
   __syncthreads();
-  if (tid == 0) {  // K: first k < min(cL, cR) with g_k >= r_k (binary search over the prefix)
-    int a = 0, b = min(cL, cR);
-    while (a < b) {
-      const int c = (a + b) >> 1;
-      if ((int)posL[lo + c] < (int)posR[lo + c]) a = c + 1;
-      else b = c;
+  // K = #{k < min(cL, cR): g_k < r_k} (a prefix: g increases, r decreases), counted by every
+  // thread over a stride of k and summed (round 6; one lane's binary search was ~11 dependent LDS
+  // reads on the critical path of every large frame)
+  {
+    const int mn = min(cL, cR);
+    int cnt = 0;
+    for (int k0 = 0; k0 < mn; k0 += T) {
+      const int kk = k0 + tid;
+      cnt += __popcll(__ballot(kk < mn && (int)posL[lo + kk] < (int)posR[lo + kk]));
     }
-    const int K = a;
-    int cut = K < cL ? (int)posL[lo + K] : INT_MAX;
-    if (K > 0) cut = min(cut, (int)posR[lo + K - 1]);
-    sh[2 * NW] = K;
-    sh[2 * NW + 1] = min(cut, hi);
+    if (lane == 0 && cnt) atomicAdd(&sh[2 * NW], cnt);
   }
   __syncthreads();
-  const int K = sh[2 * NW], cut = sh[2 * NW + 1];
+  const int K = sh[2 * NW];
+  int cut = K < cL ? (int)posL[lo + K] : INT_MAX;
+  if (K > 0) cut = min(cut, (int)posR[lo + K - 1]);
+  cut = min(cut, hi);
   for (int kk = tid; kk < K; kk += T) is_swap(k, v, (int)posL[lo + kk], (int)posR[lo + kk]);
   __syncthreads();
   return cut;
@@ -256,16 +308,8 @@ __device__ void is_wave_small(KP k, VP v, PP posL, PP posR, int first, int last,
     const int a = __shfl(st_a, sp), b = __shfl(st_b, sp);
     int d = __shfl(st_d, sp);
     if (b - a <= 16) continue;
-    if (d == 0) {  // partial_sort(a, b, b): through memory, one lane
-      if (lane < m) {
-        k[first + lane] = key;
-        v[first + lane] = val;
-      }
-      is_wave_sync();
-      if (lane == 0) is_heap_sort(k, v, first + a, first + b);
-      is_wave_sync();
-      key = lane < m ? (uint32_t)k[first + lane] : 0xFFFFFFFFu;
-      val = lane < m ? (uint32_t)v[first + lane] : 0u;
+    if (d == 0) {  // partial_sort(a, b, b) on the registers
+      is_reg_heap_sort(key, val, a, b - a, lane);
       continue;
     }
     --d;
@@ -331,52 +375,78 @@ constexpr int kIsBig = 2048;  // default: frames larger than this are partitione
 
 // The partition phase of std::sort on (k, v)[0, n) by one workgroup of T threads.  posL / posR:
 // n-entry scratch; fa / fb: int frame lists {first, last, depth} of >= n / 17 + 2 entries each
-// (3 ints per frame); sh: LDS ints (>= 2 * T / 64 + 8).  Starts and ends with a barrier.  A stable sort by key of the result is std::sort's.
+// (3 ints per frame); sh: LDS ints (>= 2 * T / 64 + 8).  Starts and ends with a barrier.  A stable
+// sort by key of the result is std::sort's.
+// Each level's frames are pushed into the next list in two groups: the frames the whole workgroup
+// partitions (larger than BIG, depth left) from the front, every other frame from the back, so no
+// thread scans the whole list for the large ones (round 6: the per-ring key sequences are close to
+// median-of-3's bad case, ~16 levels of one or two large frames and many small ones,
+// tools/ring_partition_depth.py).  Depth-exhausted frames of at most 64 elements are heap-sorted in
+// one wave's registers.
 template <int T, typename KP, typename VP, typename PP, typename FP, int BIG = kIsBig>
 __device__ __attribute__((always_inline)) void is_partition_phase(KP k, VP v, PP posL, PP posR, int n, FP fa, FP fb, int* sh) {
   constexpr int NW = T / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int* ncur = sh + 2 * NW + 2;
-  int* nnext = sh + 2 * NW + 3;
+  int* cnt = sh + 2 * NW + 2;  // [0] large frames of the current list, [1] others, [2] / [3] the same for the next
+  const int capf = n / 17 + 2;  // frames per list; the others are stored from the back
+  auto large = [](int first, int last, int depth) { return last - first > BIG && depth > 0; };
   __syncthreads();
   if (tid == 0) {
-    *ncur = 0;
+    cnt[0] = cnt[1] = 0;
     if (n > 16) {
-      fa[0] = 0;
-      fa[1] = n;
-      fa[2] = 2 * is_lg(n);
-      *ncur = 1;
+      const int d = 2 * is_lg(n);
+      if (large(0, n, d)) {
+        is_push(fa, 0, 0, n, d);
+        cnt[0] = 1;
+      } else {
+        is_push(fa, capf - 1, 0, n, d);
+        cnt[1] = 1;
+      }
     }
   }
   __syncthreads();
+  // a child frame of more than 16 elements into the next list (one lane)
+  auto push = [&](FP f, int first, int last, int depth) {
+    if (last - first <= 16) return;
+    if (large(first, last, depth)) is_push(f, atomicAdd(&cnt[2], 1), first, last, depth);
+    else is_push(f, capf - 1 - atomicAdd(&cnt[3], 1), first, last, depth);
+  };
   while (true) {
-    const int nc = *ncur;
-    if (nc == 0) break;
+    const int nbig = cnt[0], nsmall = cnt[1];
+    if (nbig + nsmall == 0) break;
     __syncthreads();
-    if (tid == 0) *nnext = 0;
+    if (tid == 0) cnt[2] = cnt[3] = 0;
     __syncthreads();
-    // large frames: one at a time, every thread (their count is small)
-    for (int f = 0; f < nc; ++f) {
+    // large frames: one at a time, every thread
+    for (int f = 0; f < nbig; ++f) {
       const IsFrame F{fa[3 * f], fa[3 * f + 1], fa[3 * f + 2]};
-      if (F.last - F.first <= BIG || F.depth == 0) continue;  // uniform
       if (tid == 0) is_median_to_first(k, v, F.first, F.first + 1, F.first + (F.last - F.first) / 2, F.last - 1);
       __syncthreads();
       const uint32_t p = k[F.first];
       const int cut = is_block_partition<T>(k, v, posL, posR, F.first + 1, F.last, p, sh);
       if (tid == 0) {
-        if (cut - F.first > 16) is_push(fb, atomicAdd(nnext, 1), F.first, cut, F.depth - 1);
-        if (F.last - cut > 16) is_push(fb, atomicAdd(nnext, 1), cut, F.last, F.depth - 1);
+        push(fb, F.first, cut, F.depth - 1);
+        push(fb, cut, F.last, F.depth - 1);
       }
     }
-    // small frames (and depth-exhausted ones): one wave each, wave w takes frames w, w + NW, ...
-    // (every wave runs the same number of rounds: no wave leaves the loop early)
-    for (int base = 0; base < nc; base += NW) {
-      const int f = base + w;
-      if (f >= nc) continue;  // wave-uniform
+    // the others: one wave each, wave w takes frames w, w + NW, ... (every wave runs the same
+    // number of rounds: no wave leaves the loop early)
+    for (int base = 0; base < nsmall; base += NW) {
+      const int f = capf - 1 - (base + w);
+      if (base + w >= nsmall) continue;  // wave-uniform
       const IsFrame F{fa[3 * f], fa[3 * f + 1], fa[3 * f + 2]};
-      if (F.last - F.first > BIG && F.depth > 0) continue;  // done above
-      if (F.depth == 0) {
-        if (lane == 0) is_heap_sort(k, v, F.first, F.last);
+      if (F.depth == 0) {  // partial_sort(first, last, last)
+        const int m = F.last - F.first;
+        if (m <= 64) {
+          uint32_t key = lane < m ? (uint32_t)k[F.first + lane] : 0u, val = lane < m ? (uint32_t)v[F.first + lane] : 0u;
+          is_reg_heap_sort(key, val, 0, m, lane);
+          if (lane < m) {
+            k[F.first + lane] = key;
+            v[F.first + lane] = val;
+          }
+        } else if (lane == 0) {
+          is_heap_sort(k, v, F.first, F.last);
+        }
         is_wave_sync();
         continue;
       }
@@ -389,12 +459,15 @@ __device__ __attribute__((always_inline)) void is_partition_phase(KP k, VP v, PP
       const uint32_t p = k[F.first];
       const int cut = is_wave_partition(k, v, posL, posR, F.first + 1, F.last, p, lane);
       if (lane == 0) {
-        if (cut - F.first > 16) is_push(fb, atomicAdd(nnext, 1), F.first, cut, F.depth - 1);
-        if (F.last - cut > 16) is_push(fb, atomicAdd(nnext, 1), cut, F.last, F.depth - 1);
+        push(fb, F.first, cut, F.depth - 1);
+        push(fb, cut, F.last, F.depth - 1);
       }
     }
     __syncthreads();
-    if (tid == 0) *ncur = *nnext;
+    if (tid == 0) {
+      cnt[0] = cnt[2];
+      cnt[1] = cnt[3];
+    }
     FP t = fa;
     fa = fb;
     fb = t;

@@ -105,11 +105,33 @@ __global__ void __launch_bounds__(1024) k_selftest_isort2(uint32_t* k, uint32_t*
   }
 }
 
+// lds = 3: the per-ring filter's shape -- 512 threads, everything in LDS (n <= 4096, u16
+// positions) -- with the whole-workgroup partition from 128 elements up (the ring kernel uses 512)
+// so that the block partition and its parallel K count see many frames.
+constexpr int kIsortLdsCap3 = 4096;
+__global__ void __launch_bounds__(512) k_selftest_isort3(uint32_t* k, uint32_t* v, int n) {
+  __shared__ int sh[64];
+  __shared__ uint32_t lk[kIsortLdsCap3];
+  __shared__ uint16_t lv[kIsortLdsCap3], lpl[kIsortLdsCap3], lpr[kIsortLdsCap3];
+  __shared__ int lfa[3 * (kIsortLdsCap3 / 17 + 2)], lfb[3 * (kIsortLdsCap3 / 17 + 2)];
+  for (int i = threadIdx.x; i < n; i += 512) {
+    lk[i] = k[i];
+    lv[i] = (uint16_t)i;
+  }
+  is_partition_phase<512, FBR_IS_LDS uint32_t*, FBR_IS_LDS uint16_t*, FBR_IS_LDS uint16_t*, FBR_IS_LDS int*, 128>(
+      (FBR_IS_LDS uint32_t*)lk, (FBR_IS_LDS uint16_t*)lv, (FBR_IS_LDS uint16_t*)lpl, (FBR_IS_LDS uint16_t*)lpr, n,
+      (FBR_IS_LDS int*)lfa, (FBR_IS_LDS int*)lfb, sh);
+  for (int i = threadIdx.x; i < n; i += 512) {
+    k[i] = lk[i];
+    v[i] = lv[i];
+  }
+}
+
 }  // namespace fbr
 
 extern "C" int fbr_selftest_voxel_order(int64_t n, const uint32_t* keys, int lds, uint32_t* perm) {
   if (n < 0 || n > (int64_t)INT32_MAX / 4 || (n && (!keys || !perm)) || (lds == 1 && n > fbr::kIsortLdsCap) ||
-      (lds == 2 && n > fbr::kIsortLdsCap2))
+      (lds == 2 && n > fbr::kIsortLdsCap2) || (lds == 3 && n > fbr::kIsortLdsCap3) || lds < 0 || lds > 3)
     return FBR_ERR_INVALID_ARG;
   if (n == 0) return FBR_OK;
   std::vector<uint32_t> iv(n);
@@ -127,7 +149,8 @@ extern "C" int fbr_selftest_voxel_order(int64_t n, const uint32_t* keys, int lds
              hipMemcpy(dv, iv.data(), 4 * n, hipMemcpyHostToDevice) != hipSuccess) {
     rc = FBR_ERR_HIP;
   } else {
-    if (lds == 2) hipLaunchKernelGGL(fbr::k_selftest_isort2, dim3(1), dim3(1024), 0, 0, dk, dv, pl, pr, (int)n);
+    if (lds == 3) hipLaunchKernelGGL(fbr::k_selftest_isort3, dim3(1), dim3(512), 0, 0, dk, dv, (int)n);
+    else if (lds == 2) hipLaunchKernelGGL(fbr::k_selftest_isort2, dim3(1), dim3(1024), 0, 0, dk, dv, pl, pr, (int)n);
     else hipLaunchKernelGGL(fbr::k_selftest_isort, dim3(1), dim3(1024), 0, 0, dk, dv, pl, pr, fa, fb, (int)n, lds);
     if (hipMemcpy(perm, dv, 4 * n, hipMemcpyDeviceToHost) != hipSuccess) rc = FBR_ERR_HIP;
   }

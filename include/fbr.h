@@ -475,7 +475,8 @@ int fbr_selftest_eig_certified(int n, const float* a, float thr, int32_t* out);
  * emulation of std::sort's partition phase (libstdc++ introsort, fbr_introsort.h) leaves the
  * (keys[i], i) pairs in; a stable sort of that sequence by key is std::sort's result.  lds = 1
  * runs the LDS variant of the per-segment kernels (n <= 8192), 2 LDS keys with global-memory
- * positions (the mapping-DS kernel's, n <= 18432), 0 the global-memory one. */
+ * positions (the mapping-DS kernel's, n <= 18432), 3 the per-ring filter's shape (512 threads, all
+ * in LDS, n <= 4096, whole-workgroup partitions from 128 elements), 0 the global-memory one. */
 int fbr_selftest_voxel_order(int64_t n, const uint32_t* keys, int lds, uint32_t* perm);
 /* Diagnostic: the VoxelGrid kernels' stable LSD radix sorts on one array of n keys (the low
  * `nbits` significant), one workgroup: variant 0 = the per-ring filter's LDS sort (512 threads,

@@ -118,17 +118,48 @@ def test_partition_phase_then_stable_sort_is_std_sort():
     rng = np.random.default_rng(1)
     for keys in key_cases(rng, 48, 1500):
         assert np.array_equal(O.sort_voxel_pairs(keys), emulate(keys)), len(keys)
+    for keys in ring_key_cases(4):
+        assert np.array_equal(O.sort_voxel_pairs(keys), emulate(keys)), len(keys)
+
+
+def ring_key_cases(rings=12):
+    """The per-ring surf VoxelGrid's real key sequences (a C2 scan's rings: the candidates of the
+    non-empty segments, PCL keys at odometrySurfLeafSize): close to median-of-3's bad case, ~16
+    partition levels and depth-exhausted frames (tools/ring_partition_depth.py)."""
+    from feature_base_pointcloud_registration_amd import synth
+    P = synth.config_params("C2")
+    pts = synth.make_jobs("C2", 1, base_seed=1000)[0][0]
+    pr, f = O.project(P, pts), O.Stream(P).features(pts)
+    inv = np.float32(1.0) / np.float32(P.odometry_surf_leaf_size)
+    out = []
+    for r in range(0, 64, 64 // rings):
+        s, e = pr["start_ring"][r], pr["end_ring"][r]
+        idx = []
+        for j in range(6):
+            sp, ep = (s * (6 - j) + e * j) // 6, (s * (5 - j) + e * (j + 1)) // 6 - 1
+            if sp < ep:
+                idx += [k for k in range(sp, ep + 1) if f["label"][k] <= 0]
+        c = pr["cloud"][idx]
+        x = np.stack([c["x"], c["y"], c["z"]], 1).astype(np.float32)
+        mnb = np.floor(x.min(0) * inv).astype(np.int64)
+        dx = np.floor(x.max(0) * inv).astype(np.int64) - mnb + 1
+        ijk = np.floor(x * inv).astype(np.int64) - mnb
+        out.append((ijk[:, 0] + ijk[:, 1] * dx[0] + ijk[:, 2] * dx[0] * dx[1]).astype(np.uint32))
+    return out
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lds", [0, 1, 2])
+@pytest.mark.parametrize("lds", [0, 1, 2, 3])
 def test_device_voxel_order_is_std_sort(lds):
     rng = np.random.default_rng(2 + lds)
-    for keys in key_cases(rng, 120, {0: 60000, 1: 8000, 2: 18432}[lds]):
+    for keys in key_cases(rng, 120, {0: 60000, 1: 8000, 2: 18432, 3: 4096}[lds]):
         assert np.array_equal(api.selftest_voxel_order(keys, lds=lds), O.sort_voxel_pairs(keys)), len(keys)
-    for n in {0: (17, 2049, 18432, 18433), 1: (17, 2049, 8192), 2: (17, 2049, 8192, 18431, 18432)}[lds]:
+    for n in {0: (17, 2049, 18432, 18433), 1: (17, 2049, 8192), 2: (17, 2049, 8192, 18431, 18432),
+              3: (17, 129, 2049, 4096)}[lds]:
         keys = rng.integers(0, max(1, n // 6), n).astype(np.uint32)
         assert np.array_equal(api.selftest_voxel_order(keys, lds=lds), O.sort_voxel_pairs(keys)), n
+    for keys in ring_key_cases():
+        assert np.array_equal(api.selftest_voxel_order(keys, lds=lds), O.sort_voxel_pairs(keys)), len(keys)
 
 
 def _radix_cases(cap, nw):
