@@ -113,11 +113,7 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
       __syncthreads();
       for (int e = tid; e < tcells; e += kProjThreads) {
         const int32_t v = tile[(e >> tile_log2) * tpitch + (e & (tcols - 1))];
-#ifdef FBR_PROJ_PLAIN_STORE  // diagnostic timing build only: plain stores instead of the merge atomics (not first-wins-safe)
-        if (v != kEmptyOwner) O[(e >> tile_log2) * W + cmin + (e & (tcols - 1))] = v;
-#else
         if (v != kEmptyOwner) atomicMin(&O[(e >> tile_log2) * W + cmin + (e & (tcols - 1))], v);
-#endif
       }
     } else {
       for (int k = 0; k < kProjPPT; ++k) {
