@@ -138,9 +138,11 @@ def parse():
     ap.add_argument("--latency", type=int, default=50,
                     help="single-stream line: N pose-chained scans through fbr_process_scan (the reference's "
                          "operating mode, imageProjection.cpp:206-218), rank 0 at N=1; 0 disables")
-    ap.add_argument("--ingest", type=int, default=2,
+    ap.add_argument("--ingest", type=int, default=4,
                     help="ingest-inclusive line: REPS x B jobs from host memory through fbr_process_batch "
-                         "(pinned double-buffered staging), rank 0 at N=1; 0 disables")
+                         "(pinned double-buffered staging; the first batch's upload and the last batch's "
+                         "compute overlap nothing, so few REPS understate the streaming rate), rank 0 at "
+                         "N=1; 0 disables")
     ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C5"])
     ap.add_argument("--pipeline-depth", type=int, default=0,
                     help="fbr_params.pipeline_depth: batch launch slots (0 = the library default, 3)")

@@ -102,8 +102,9 @@ struct Ingest {
   // by k_expand_scans (the batch returns poses and statistics, which no point's intensity or time
   // reaches).
   uint8_t* d_stage = nullptr;        // [Bcap][ingest_region_bytes(NMAX)]
-  int64_t* d_nin = nullptr;          // [2][Bcap] point counts of the staged scans (copy stream)
-  int64_t* h_nin = nullptr;          // [2][Bcap] pinned
+  int64_t* d_nin = nullptr;          // [2][2][Bcap] per input slot: the staged scans' point counts,
+                                     // then their records' byte offsets in d_stage (copy stream)
+  int64_t* h_nin = nullptr;          // [2][2][Bcap] pinned
   bool compact_used = false;         // the last fbr_process_batch used compact records
 };
 
@@ -2263,6 +2264,7 @@ int ingest_init(fbr_ctx* c) {
   int64_t mb = 64;
   if (const char* e = std::getenv("FBR_STAGE_MB")) mb = std::max<int64_t>(1, std::atoll(e));
   g.chunk_bytes = std::max<int64_t>(mb << 20, c->NMAX * (int64_t)sizeof(fbr_point_xyzirt));
+  g.chunk_bytes = (g.chunk_bytes + 63) & ~(int64_t)63;  // 16-B aligned records for the streaming stores
   // 16 packing threads (the CPU share of a one-GPU box; 8 -> 16: ingest line +10-20 %, r06m/r06n)
   g.nthreads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   if (const char* e = std::getenv("FBR_STAGE_THREADS")) g.nthreads = std::max(1, std::atoi(e));
@@ -2273,9 +2275,62 @@ int ingest_init(fbr_ctx* c) {
   g.d_pts_slot[0] = c->d_pts;
   if (dalloc(&g.d_pts_slot[1], (int64_t)c->Bcap * c->NMAX)) return FBR_ERR_HIP;
   if (dalloc(&g.d_stage, (int64_t)c->Bcap * ingest_region_bytes(c->NMAX))) return FBR_ERR_HIP;
-  if (dalloc(&g.d_nin, 2 * (int64_t)c->Bcap)) return FBR_ERR_HIP;
-  CK(hipHostMalloc((void**)&g.h_nin, sizeof(int64_t) * 2 * c->Bcap, hipHostMallocDefault));
+  if (dalloc(&g.d_nin, 4 * (int64_t)c->Bcap)) return FBR_ERR_HIP;
+  CK(hipHostMalloc((void**)&g.h_nin, sizeof(int64_t) * 4 * c->Bcap, hipHostMallocDefault));
   return FBR_OK;
+}
+
+// FBR_INGEST_NT=0: the packers use plain stores instead of streaming ones.
+bool ingest_nt_stores() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_INGEST_NT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+// One scan's compact record (fbr_kernels.h: ingest_plane / ingest_region_bytes) at the 16-B aligned
+// `out`, in one pass over the caller's 24-B points.  Groups of 16 points go out as streaming stores
+// (no read-for-ownership of the pinned chunk, and the caller's points are read once); a ring at or
+// beyond H (projectPointCloud drops it, imageProjection.cpp:599) is stored as 255 when rb = 1.
+void pack_compact(const fbr_point_xyzirt* src, int64_t n, int H, int rb, uint8_t* out) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  const int64_t m = ingest_plane(n);
+  float* px = reinterpret_cast<float*>(out);
+  float* py = px + m;
+  float* pz = py + m;
+  uint8_t* rr = out + 12 * m;
+  auto ring8 = [&](const fbr_point_xyzirt& p) { return p.ring < H ? (uint8_t)p.ring : (uint8_t)255; };
+  int64_t i = 0;
+  if (ingest_nt_stores())
+    for (; i + 16 <= n; i += 16) {
+      const fbr_point_xyzirt* s = src + i;
+      for (int g = 0; g < 4; ++g) {
+        const fbr_point_xyzirt* q = s + 4 * g;
+        __builtin_nontemporal_store(f4{q[0].x, q[1].x, q[2].x, q[3].x}, reinterpret_cast<f4*>(px + i + 4 * g));
+        __builtin_nontemporal_store(f4{q[0].y, q[1].y, q[2].y, q[3].y}, reinterpret_cast<f4*>(py + i + 4 * g));
+        __builtin_nontemporal_store(f4{q[0].z, q[1].z, q[2].z, q[3].z}, reinterpret_cast<f4*>(pz + i + 4 * g));
+      }
+      if (rb == 1) {
+        u4 w;
+        for (int g = 0; g < 4; ++g)
+          w[g] = (unsigned)ring8(s[4 * g]) | (unsigned)ring8(s[4 * g + 1]) << 8 |
+                 (unsigned)ring8(s[4 * g + 2]) << 16 | (unsigned)ring8(s[4 * g + 3]) << 24;
+        __builtin_nontemporal_store(w, reinterpret_cast<u4*>(rr + i));  // 12 m and i are multiples of 16
+      } else {
+        for (int k = 0; k < 16; ++k) reinterpret_cast<uint16_t*>(rr)[i + k] = s[k].ring;
+      }
+    }
+  for (; i < n; ++i) {
+    px[i] = src[i].x;
+    py[i] = src[i].y;
+    pz[i] = src[i].z;
+    if (rb == 1)
+      rr[i] = ring8(src[i]);
+    else
+      reinterpret_cast<uint16_t*>(rr)[i] = src[i].ring;
+  }
 }
 
 // FBR_INGEST_COMPACT=0: always ship the 24-B records.
@@ -2288,7 +2343,8 @@ bool ingest_compact_enabled() {
 }
 
 // Upload B scans into input slot `slot`: pack them into free pinned chunks (host threads), queue
-// one H2D copy per scan on the copy stream, then record up_ev[slot].  Runs on a worker thread
+// one H2D copy per chunk (compact records) or per scan (24-B records) on the copy stream, expand the
+// compact records into the slot's scan buffer, then record up_ev[slot].  Runs on a worker thread
 // while the previous device batch computes.
 int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, const int64_t* n_in, int B) {
   CK(enter(c));
@@ -2297,16 +2353,16 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
   // compact records unless a deskew table may read the per-point time (deskewPoint, :545-580)
   const bool compact = ingest_compact_enabled() && !c->desk_any;
   g.compact_used = compact;
-  const int64_t region = ingest_region_bytes(c->NMAX);
   // ring bytes per point: u8 for sensors of < 256 rings, where every out-of-range ring (>= H, which
   // projectPointCloud drops, imageProjection.cpp:599) is stored as 255, still out of range
   const int rb = c->H < 256 ? 1 : 2;
-  auto host_bytes = [&](int64_t n) { return compact ? (12 + rb) * n : n * (int64_t)sizeof(fbr_point_xyzirt); };
-  if (compact) {  // the counts for k_expand_scans, on the copy stream (slot's half of the pinned array)
-    for (int jj = 0; jj < B; ++jj) g.h_nin[(int64_t)slot * c->Bcap + jj] = n_in[jj];
-    CK(hipMemcpyAsync(g.d_nin + (int64_t)slot * c->Bcap, g.h_nin + (int64_t)slot * c->Bcap, sizeof(int64_t) * B,
-                      hipMemcpyHostToDevice, g.cstream));
-  }
+  auto host_bytes = [&](int64_t n) {
+    return compact ? 12 * ingest_plane(n) + rb * n : n * (int64_t)sizeof(fbr_point_xyzirt);
+  };
+  // k_expand_scans' counts and record offsets (the slot's half of the pinned array)
+  int64_t* h_nin = g.h_nin + 2 * (int64_t)slot * c->Bcap;
+  int64_t* h_off = h_nin + c->Bcap;
+  int64_t dpos = 0;  // d_stage offset of the next chunk: the chunks land back to back
   std::vector<int64_t> off;
   for (int j = 0; j < B;) {
     const int k = g.next_chunk;
@@ -2322,6 +2378,11 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
       ++j1;
     }
     if (j1 == j) return FBR_ERR_CAPACITY;  // (chunk_bytes >= NMAX * 24: not reached)
+    const int64_t end = off.back() + host_bytes(n_in[j1 - 1]);  // the chunk's bytes
+    for (int jj = j; jj < j1; ++jj) {
+      h_nin[jj] = n_in[jj];
+      h_off[jj] = dpos + off[jj - j];
+    }
     const int nt = std::max(1, std::min(g.nthreads, j1 - j));
     auto pack = [&](int t) {
       for (int jj = j + t; jj < j1; jj += nt) {
@@ -2331,42 +2392,34 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
           std::memcpy(base + off[jj - j], scans[jj], n * sizeof(fbr_point_xyzirt));
           continue;
         }
-        const fbr_point_xyzirt* src = scans[jj];
-        float* px = reinterpret_cast<float*>(base + off[jj - j]);
-        float* py = px + n;
-        float* pz = py + n;
-        uint8_t* rr = base + off[jj - j] + 12 * n;
-        for (int64_t i = 0; i < n; ++i) {
-          px[i] = src[i].x;
-          py[i] = src[i].y;
-          pz[i] = src[i].z;
-        }
-        if (rb == 1)
-          for (int64_t i = 0; i < n; ++i) rr[i] = src[i].ring < c->H ? (uint8_t)src[i].ring : (uint8_t)255;
-        else
-          for (int64_t i = 0; i < n; ++i) reinterpret_cast<uint16_t*>(rr)[i] = src[i].ring;
+        pack_compact(scans[jj], n, c->H, rb, base + off[jj - j]);
       }
+      if (ingest_nt_stores()) __builtin_ia32_sfence();  // the streaming stores before the DMA reads them
     };
     std::vector<std::thread> th;
     for (int t = 1; t < nt; ++t) th.emplace_back(pack, t);
     pack(0);
     for (auto& x : th) x.join();
-    for (int jj = j; jj < j1; ++jj)
-      if (n_in[jj]) {
-        if (compact)
-          CK(hipMemcpyAsync(g.d_stage + (int64_t)jj * region, base + off[jj - j], host_bytes(n_in[jj]),
-                            hipMemcpyHostToDevice, g.cstream));
-        else
+    // compact records: the whole chunk in one copy (1.4 MB copies ran at 41 GB/s on the box, 64 MB
+    // ones at 57: tools/h2d_probe.py); 24-B records straight into their scan slots
+    if (compact)
+      CK(hipMemcpyAsync(g.d_stage + dpos, base, end, hipMemcpyHostToDevice, g.cstream));
+    else
+      for (int jj = j; jj < j1; ++jj)
+        if (n_in[jj])
           CK(hipMemcpyAsync(dst + (int64_t)jj * c->NMAX, base + off[jj - j], n_in[jj] * sizeof(fbr_point_xyzirt),
                             hipMemcpyHostToDevice, g.cstream));
-      }
     CK(hipEventRecord(g.chunk_ev[k], g.cstream));
+    dpos += (end + 15) & ~(int64_t)15;
     g.chunk_used[k] = true;
     for (int jj = j; jj < j1; ++jj) g.h2d_bytes += (double)(n_in[jj] ? host_bytes(n_in[jj]) : 0);
     j = j1;
   }
-  if (compact)  // stream order: after the copies
-    launch_expand_scans(g.cstream, g.d_stage, c->NMAX, B, g.d_nin + (int64_t)slot * c->Bcap, rb, dst);
+  if (compact) {  // stream order: after the copies
+    int64_t* d_nin = g.d_nin + 2 * (int64_t)slot * c->Bcap;
+    CK(hipMemcpyAsync(d_nin, h_nin, sizeof(int64_t) * 2 * c->Bcap, hipMemcpyHostToDevice, g.cstream));
+    launch_expand_scans(g.cstream, g.d_stage, c->NMAX, B, d_nin, d_nin + c->Bcap, rb, dst);
+  }
   CK(hipEventRecord(g.up_ev[slot], g.cstream));
   return FBR_OK;
 }

@@ -64,12 +64,15 @@ struct MsgDev {
   int32_t off[6];
 };
 void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_point_xyzirt* out);
-// Compact ingest records (fbr_process_batch without deskew tables): job j's staging region holds
-// its n points packed, [x f32 x n][y f32 x n][z f32 x n][ring x n], the rings as u8 when the sensor has
-// at most 256 rings (rb = 1), else u16 (rb = 2); regions are ingest_region_bytes(nmax) apart.
-inline int64_t ingest_region_bytes(int64_t nmax) { return (18 * nmax + 15) & ~(int64_t)15; }
-void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, const int64_t* nin, int rb,
-                         fbr_point_xyzirt* out);
+// Compact ingest records (fbr_process_batch without deskew tables): job j's record, at byte offset
+// off[j] of the stage (16-B aligned, back to back as the staging chunks lay them out), holds its n
+// points as planes [x f32 x m][y f32 x m][z f32 x m][ring x n], m = ingest_plane(n) (16-B aligned
+// planes, for the packers' streaming stores), the rings as u8 when the sensor has at most 256 rings
+// (rb = 1), else u16 (rb = 2).  ingest_region_bytes(nmax) bounds one record, padding included.
+__host__ __device__ inline int64_t ingest_plane(int64_t n) { return (n + 3) & ~(int64_t)3; }
+inline int64_t ingest_region_bytes(int64_t nmax) { return (14 * nmax + 48 + 15) & ~(int64_t)15; }
+void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, const int64_t* nin,
+                         const int64_t* off, int rb, fbr_point_xyzirt* out);
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
                     int W, int32_t* owner,
                     int32_t* err, int64_t n_single = -1);

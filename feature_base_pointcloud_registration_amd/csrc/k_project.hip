@@ -392,24 +392,26 @@ void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_
 // No deskew: the reference never reads `time` on this path (imageProjection.cpp:189-191), and a
 // batch returns poses and statistics, which no point's intensity reaches (it rides along as the
 // clouds' w channel: never in a key, a distance, a residual or a count), so neither is shipped.
-// Job j's staging region (ingest_region_bytes apart) holds its n points as planes x[n], y[n],
-// z[n] (f32), then the rings x n (u8 when rb = 1, u16 when rb = 2); intensity = time = 0.  Slots
+// Job j's record (at byte offset off[j] of the stage) holds its n points as planes x[m], y[m],
+// z[m] (f32, m = ingest_plane(n)), then the rings x n (u8 when rb = 1, u16 when rb = 2);
+// intensity = time = 0.  Slots
 // past n are not written (k_project reads n points).  HBM-bound: 12 + rb B read + 24 B written per
 // point.
 __global__ void __launch_bounds__(256)
-k_expand_scans(const uint8_t* __restrict__ stage, int64_t nmax, int64_t region, const int64_t* __restrict__ nin,
-               int rb, fbr_point_xyzirt* __restrict__ out) {
+k_expand_scans(const uint8_t* __restrict__ stage, int64_t nmax, const int64_t* __restrict__ nin,
+               const int64_t* __restrict__ off, int rb, fbr_point_xyzirt* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t job = blockIdx.y;
   const int64_t n = min(nin[job], nmax);
   if (i >= n) return;
-  const uint8_t* r = stage + job * region;
+  const uint8_t* r = stage + off[job];
   const float* pl = reinterpret_cast<const float*>(r);
-  const uint16_t ring = rb == 1 ? (uint16_t)r[12 * n + i] : reinterpret_cast<const uint16_t*>(r + 12 * n)[i];
+  const int64_t m = ingest_plane(n);
+  const uint16_t ring = rb == 1 ? (uint16_t)r[12 * m + i] : reinterpret_cast<const uint16_t*>(r + 12 * m)[i];
   fbr_point_xyzirt q;
   q.x = pl[i];
-  q.y = pl[n + i];
-  q.z = pl[2 * n + i];
+  q.y = pl[m + i];
+  q.z = pl[2 * m + i];
   q.intensity = 0.0f;
   q.ring = ring;
   q.pad_ = 0;
@@ -417,11 +419,11 @@ k_expand_scans(const uint8_t* __restrict__ stage, int64_t nmax, int64_t region, 
   out[job * nmax + i] = q;
 }
 
-void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, const int64_t* nin, int rb,
-                         fbr_point_xyzirt* out) {
+void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, const int64_t* nin,
+                         const int64_t* off, int rb, fbr_point_xyzirt* out) {
   if (B <= 0 || nmax <= 0) return;
-  fbr_launch(k_expand_scans, dim3((unsigned)((nmax + 255) / 256), B), dim3(256), 0, s, stage, nmax,
-             ingest_region_bytes(nmax), nin, rb, out);
+  fbr_launch(k_expand_scans, dim3((unsigned)((nmax + 255) / 256), B), dim3(256), 0, s, stage, nmax, nin, off, rb,
+             out);
 }
 
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,

@@ -420,6 +420,32 @@ def test_process_batch_drops_out_of_range_rings_like_staged_path(c2_map):
     assert (sb["n_points"] < np.array([len(s) for s in scans]) - 3000).all()  # the 4000 are gone
 
 
+@pytest.mark.parametrize("h_extra", [0, 200])
+def test_process_batch_ragged_scans_match_staged_path(c2_map, h_extra):
+    """The packers write 16-point groups with streaming stores and the rest one point at a time,
+    into 16-B aligned planes (fbr_api.hip pack_compact): scans of every length mod 16, a 5-point
+    scan and an empty one give fbr_batch_stage's results bit for bit.  h_extra = 200 declares 264
+    rings, so the rings ship as u16 (rb = 2)."""
+    H, W = synth.CONFIGS["C2"][:2]
+    lens_cut = [0, 1, 2, 3, 7, 9, 14, 15]
+    P = default_params(H + h_extra, W, max_batch=len(lens_cut) + 2)
+    jobs = synth.make_jobs("C2", len(lens_cut), base_seed=90)
+    scans = [pts[:len(pts) - cut].copy() for (pts, _, _), cut in zip(jobs, lens_cut)]
+    scans += [jobs[0][0][:5].copy(), jobs[1][0][:0].copy()]
+    assert len({len(s) % 16 for s in scans[:len(lens_cut)]}) >= 6
+    guesses = np.stack([j[1] for j in jobs] + [jobs[0][1], jobs[1][1]])
+    with api.Context(P) as ctx:
+        ctx.set_map(*c2_map)
+        pb, sb = ctx.process_batch(scans, guesses)
+        ctx.batch_stage(scans, guesses)
+        ctx.batch_launch()
+        ctx.batch_wait()
+        ps, ss = ctx.batch_results()
+    assert np.array_equal(pb.view(np.int32), ps.view(np.int32))
+    assert np.array_equal(sb, ss)
+    assert (sb["status"][:len(lens_cut)] == 0).all()
+
+
 def test_batch_tail_mode_matches_oracle(c2_map):
     """24 jobs = 3 sub-batches of 8: each sub-batch's last iterating job runs its final Gauss-Newton
     iterations in tail mode (fused kNN + residual launch, fbr_api.hip gn_tail_div); every pose and
