@@ -197,6 +197,32 @@ def ingest_line(ctx, scans, guesses, resident_poses, reps, B):
     }
 
 
+def mask_check(ctx, scans, poses, stats, P, S, O, launches=5):
+    """Whole feature masks of the headline batch (fbr_batch_set_full_masks / fbr_batch_labels): the
+    first S jobs' cloudLabel against the oracle's bit for bit, the full-mask launches' poses and
+    statistics against the timed ones (the default launches resolve only the observable surf
+    picks), and the rate of full-mask launches (untimed by the headline)."""
+    B = len(scans)
+    ctx.batch_set_full_masks(True)
+    t0 = time.perf_counter()
+    for _ in range(launches):
+        ctx.batch_launch()
+    ctx.batch_wait()
+    t_full = time.perf_counter() - t0
+    pf, sf = ctx.batch_results()
+    eq = 0
+    for j in range(S):
+        lab = ctx.batch_labels(j)
+        ref = O.Stream(P).features(scans[j])["label"]
+        eq += int(len(lab) == len(ref) and np.array_equal(lab, ref))
+    ctx.batch_set_full_masks(False)
+    return {"n": S, "mask_bit_equal": eq,
+            "poses_equal_timed": bool((pf.view(np.int32) == poses.view(np.int32)).all()),
+            "stats_equal_timed": bool(np.array_equal(sf, stats)),
+            "full_mask_scans_per_s": round(launches * B / t_full, 1),
+            "path": "fbr_batch_set_full_masks + fbr_batch_labels on the staged headline batch"}
+
+
 def latency_line(cfg, corner_map, surf_map, n, cpu_scans=0):
     """The reference's operating mode: one scan at a time, each registration starting from the
     previous result (imageProjection.cpp:206-218), host scan in, pose out.  Reports wall ms per
@@ -681,6 +707,7 @@ def main():
             "pose_bit_equal": int((poses[:S].view(np.int32) == ref.view(np.int32)).all(axis=1).sum()),
             "iterations_hist": {int(k): int(v) for k, v in zip(*np.unique(it_g, return_counts=True))},
         }
+        result["feature_masks"] = mask_check(ctx, scans, poses, stats, P, S, O)
         result["pose_rmse_vs_ref"] = {
             "trans_m": float(np.sqrt(np.mean(np.sum(dt.astype(np.float64) ** 2, axis=1)))),
             "rot_rad": float(np.sqrt(np.mean(np.sum(dr ** 2, axis=1)))),

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = [
     "fbr_destroy", "fbr_set_map", "fbr_get_map", "fbr_project", "fbr_extract_features",
     "fbr_register", "fbr_register_trace", "fbr_process_scan", "fbr_reset_stream",
     "fbr_process_batch", "fbr_ingest_bytes", "fbr_debug_counters", "fbr_map_grid_info", "fbr_batch_stage", "fbr_batch_launch", "fbr_batch_wait",
-    "fbr_batch_flush", "fbr_batch_export_ready", "fbr_batch_results", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
+    "fbr_batch_flush", "fbr_batch_export_ready", "fbr_batch_results", "fbr_batch_set_full_masks", "fbr_batch_labels", "fbr_batch_export", "fbr_batch_bytes", "fbr_set_profiling", "fbr_set_profiling_kernels", "fbr_kernel_time", "fbr_stream",
     "fbr_voxel_grid", "fbr_affine_from_pose", "fbr_pose_from_affine", "fbr_selftest_math", "fbr_selftest_eigen6", "fbr_selftest_eig_certified", "fbr_selftest_voxel_order", "fbr_selftest_radix_sort",
     "fbr_load_map", "fbr_pcd_read", "fbr_pcd_write_ascii", "fbr_pcd_write_binary",
     "fbr_msg_to_points", "fbr_points_to_msg_data", "fbr_project_msg", "fbr_process_msg",
@@ -84,6 +84,8 @@ def lib():
             "fbr_batch_wait": (ctypes.c_int, [_VP]),
             "fbr_batch_results": (ctypes.c_int, [_VP, _VP, _VP]),
             "fbr_batch_export": (ctypes.c_int, [_VP, _VP]),
+            "fbr_batch_set_full_masks": (ctypes.c_int, [_VP, ctypes.c_int]),
+            "fbr_batch_labels": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _I64, _VP]),
             "fbr_batch_flush": (ctypes.c_int, [_VP]),
             "fbr_batch_export_ready": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
             "fbr_batch_bytes": (ctypes.c_int, [_VP, _VP, _VP]),
@@ -561,6 +563,20 @@ class Context:
         stats = np.zeros(self._staged, REG_STATS)
         _check(lib().fbr_batch_results(self._h, ptr(poses), ptr(stats)), "fbr_batch_results")
         return poses, stats
+
+    def batch_set_full_masks(self, on=True):
+        """Later batch launches compute whole feature masks (fbr_batch_set_full_masks)."""
+        _check(lib().fbr_batch_set_full_masks(self._h, int(bool(on))), "fbr_batch_set_full_masks")
+
+    def batch_labels(self, job):
+        """cloudLabel of batch job `job` of the latest (full-mask) launch: int8 [n_points]."""
+        n = _I64()
+        rc = lib().fbr_batch_labels(self._h, int(job), None, 0, ctypes.byref(n))
+        if rc not in (0, -4):  # FBR_ERR_CAPACITY: the count is in n
+            _check(rc, "fbr_batch_labels")
+        out = np.zeros(max(n.value, 1), np.int8)
+        _check(lib().fbr_batch_labels(self._h, int(job), ptr(out), len(out), ctypes.byref(n)), "fbr_batch_labels")
+        return out[:n.value]
 
     def batch_export(self, device_ptr):
         """Enqueue the 32 B/job pose records into device memory at `device_ptr` (int address)."""

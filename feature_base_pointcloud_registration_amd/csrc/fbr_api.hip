@@ -187,6 +187,8 @@ struct fbr_ctx {
   int64_t launch_seq = 0;     // batch launches so far
   int last_slot = -1;         // slot of the latest launch (-1: none since the last stage)
   int64_t slot_launch[kMaxSlots] = {-1, -1, -1};  // launch number of each slot's latest launch
+  bool batch_full_masks = false;            // fbr_batch_set_full_masks: launches compute whole masks
+  bool slot_full_masks[kMaxSlots] = {};     // ... and which slots' latest launch did
   int64_t exported = -1;      // latest launch whose records fbr_batch_export_ready exported
   int64_t first_valid = 0;    // launches below this id belong to a dropped batch (fbr_batch_allgather)
   int diag_err_job = -1;      // diagnostic (fbr_diag_force_capacity_error): batch job flagged over capacity
@@ -1940,12 +1942,16 @@ int fbr_batch_launch(fbr_ctx* c) {
   }
   for (int k = 0; k < nsub && !rc; ++k) {
     rc = stage_project(c, subs[k]);
-    if (!rc) rc = stage_features(c, subs[k], false, true);
+    if (!rc && c->batch_full_masks)  // cloudLabel of a fresh FeatureExtraction: zeros outside the picks
+      rc = hipMemsetAsync(c->d_label + (int64_t)subs[k].j0 * c->HW, 0, (size_t)subs[k].B * c->HW, subs[k].st) ? FBR_ERR_HIP
+                                                                                                            : FBR_OK;
+    if (!rc) rc = stage_features(c, subs[k], false, true, c->batch_full_masks);
     if (!rc) rc = register_prepare(c, subs[k], false);
   }
   if (rc) return rc;
   gn_run_start(c, c->run[slot], subs, nsub, false);
   c->last_slot = slot;
+  c->slot_full_masks[slot] = c->batch_full_masks;
   c->slot_launch[slot] = c->launch_seq++;
   bool p = false;
   rc = gn_run_pass(c, c->run[slot], false, &p);  // the iterations that need no flag yet
@@ -1980,6 +1986,33 @@ int fbr_batch_results(fbr_ctx* c, float* poses_out, fbr_reg_stats* stats) {
   const int rc = batch_quiesce(c);
   if (rc) return rc;
   return copy_results(c, c->staged_B, stats, poses_out, true, (int64_t)c->last_slot * c->Bcap, true);
+}
+
+int fbr_batch_set_full_masks(fbr_ctx* c, int on) {
+  if (!c) return FBR_ERR_INVALID_ARG;
+  c->batch_full_masks = on != 0;
+  return FBR_OK;
+}
+
+int fbr_batch_labels(fbr_ctx* c, int job, int8_t* label, int64_t cap, int64_t* n_out) {
+  if (!c || !n_out || cap < 0 || (cap > 0 && !label)) return FBR_ERR_INVALID_ARG;
+  *n_out = 0;
+  if (c->staged_B <= 0 || c->last_slot < 0) return FBR_ERR_STATE;
+  if (job < 0 || job >= c->staged_B) return FBR_ERR_INVALID_ARG;
+  if (!c->slot_full_masks[c->last_slot]) return FBR_ERR_STATE;  // window masks are incomplete
+  CK(enter(c));
+  const int rc = batch_quiesce(c);
+  if (rc) return rc;
+  const int64_t w = (int64_t)c->last_slot * c->Bcap + job;
+  CK(fbr_sync(c->stream));
+  for (const GnRun& r : c->run)
+    for (int k = 0; k < r.nsub; ++k) CK(fbr_sync(r.subs[k].st));
+  int32_t nv = 0;
+  CK(hipMemcpy(&nv, c->d_nvalid + w, sizeof(int32_t), hipMemcpyDeviceToHost));
+  *n_out = nv;
+  if (nv > cap) return FBR_ERR_CAPACITY;
+  if (nv > 0) CK(hipMemcpy(label, c->d_label + w * c->HW, (size_t)nv, hipMemcpyDeviceToHost));
+  return FBR_OK;
 }
 
 int fbr_batch_export(fbr_ctx* c, void* device_dst) {

@@ -384,6 +384,17 @@ int fbr_batch_wait(fbr_ctx* ctx);
  * their results (fbr_batch_results, fbr_process_batch). */
 int fbr_batch_results(fbr_ctx* ctx, float* poses_out /* [n_jobs][6] */,
                       fbr_reg_stats* stats /* [n_jobs] or NULL */);
+/* Whole feature masks for batch jobs (featureExtraction.h:178-285, cloudLabel).  By default a batch
+ * resolves each segment's surf walk only within reach of its end, the only picks that reach a pose
+ * or a statistic, so its label masks are incomplete.  With on != 0, the following fbr_batch_launch
+ * calls run every walk whole (as fbr_extract_features does), at some cost in throughput; results
+ * are the same either way. */
+int fbr_batch_set_full_masks(fbr_ctx* ctx, int on);
+/* cloudLabel of job `job` of the latest launch (1 corner, -1 picked surf, 0), one entry per
+ * projected point: *n_out = the job's point count (cloud_info order).  FBR_ERR_STATE unless that
+ * launch ran with full masks; FBR_ERR_CAPACITY (with *n_out set) if cap < *n_out.  Waits for the
+ * launches in flight. */
+int fbr_batch_labels(fbr_ctx* ctx, int job, int8_t* label, int64_t cap, int64_t* n_out);
 /* Enqueue (on the ctx stream, after every launch in flight) a copy of the latest launch's per-job
  * pose records {pose[6] f32, iterations i32, status i32} = 32 B/job into `device_dst` (device
  * memory of the ctx's device, [n_jobs][8] x 4 B) — the payload of the cross-GPU pose all-gather. */

@@ -446,6 +446,42 @@ def test_process_batch_ragged_scans_match_staged_path(c2_map, h_extra):
     assert (sb["status"][:len(lens_cut)] == 0).all()
 
 
+@pytest.mark.parametrize("cfg,nj", [("C2", 10), ("C1", 4), ("C3", 2)])
+def test_batch_full_masks_match_oracle_labels(cfg, nj):
+    """The headline (batch) path reports whole feature masks on request (fbr_batch_set_full_masks):
+    every job's cloudLabel equals the oracle's bit for bit, and the poses and statistics equal the
+    default launch's, whose surf walks stop within reach of each segment end (k_features.hip)."""
+    P = synth.config_params(cfg, max_batch=nj)
+    jobs = synth.make_jobs(cfg, nj, base_seed=4100)
+    scans = [j[0] for j in jobs]
+    guesses = np.stack([j[1] for j in jobs])
+    with api.Context(P) as ctx:
+        ctx.set_map(*synth.config_map(cfg))
+        ctx.batch_stage(scans, guesses)
+        ctx.batch_launch()
+        ctx.batch_wait()
+        p0, s0 = ctx.batch_results()
+        with pytest.raises(api.FbrError):  # window masks are incomplete: not reported
+            ctx.batch_labels(0)
+        ctx.batch_set_full_masks(True)
+        ctx.batch_launch()
+        ctx.batch_wait()
+        p1, s1 = ctx.batch_results()
+        labels = [ctx.batch_labels(k) for k in range(nj)]
+        ctx.batch_set_full_masks(False)
+        ctx.batch_launch()
+        ctx.batch_wait()
+        with pytest.raises(api.FbrError):
+            ctx.batch_labels(0)
+    assert np.array_equal(p0.view(np.int32), p1.view(np.int32))
+    assert np.array_equal(s0, s1)
+    for k, pts in enumerate(scans):
+        ref = O.Stream(P).features(pts)["label"]
+        assert len(labels[k]) == len(ref) == s1["n_points"][k]
+        assert np.array_equal(labels[k], ref), (k, np.flatnonzero(labels[k] != ref)[:10])
+        assert (ref == 1).sum() > 0 and (ref == -1).sum() > 0
+
+
 def test_batch_tail_mode_matches_oracle(c2_map):
     """24 jobs = 3 sub-batches of 8: each sub-batch's last iterating job runs its final Gauss-Newton
     iterations in tail mode (fused kNN + residual launch, fbr_api.hip gn_tail_div); every pose and
