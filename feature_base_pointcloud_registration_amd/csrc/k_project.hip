@@ -28,10 +28,9 @@
 
 namespace fbr {
 
-__device__ __forceinline__ bool project_point(const fbr_point_xyzirt& q, int H, int W, int& row, int& colo) {
-  int rowIdn = q.ring;
+__device__ __forceinline__ bool project_xyzr(float x, float y, float z, int rowIdn, int H, int W, int& row, int& colo) {
   if (rowIdn < 0 || rowIdn >= H) return false;
-  float horizonAngle = (float)((double)(fd_atan2f(q.x, q.y) * 180.0f) / M_PI);
+  float horizonAngle = (float)((double)(fd_atan2f(x, y) * 180.0f) / M_PI);
   float ang_res_x = (float)(360.0 / (double)(float)W);
   int columnIdn = x86_cvt(-round(((double)horizonAngle - 90.0) / (double)ang_res_x) + (double)(W / 2));
   if (columnIdn >= W) columnIdn -= W;
@@ -40,10 +39,14 @@ __device__ __forceinline__ bool project_point(const fbr_point_xyzirt& q, int H, 
   // when its argument is (the largest float below 1 has a square root that rounds below 1; a NaN
   // is not below 1 either way), so the test needs no square root here (k_compact recomputes the
   // stored range)
-  if (q.x * q.x + q.y * q.y + q.z * q.z < 1.0f) return false;
+  if (x * x + y * y + z * z < 1.0f) return false;
   row = rowIdn;
   colo = columnIdn;
   return true;
+}
+
+__device__ __forceinline__ bool project_point(const fbr_point_xyzirt& q, int H, int W, int& row, int& colo) {
+  return project_xyzr(q.x, q.y, q.z, q.ring, H, W, row, colo);
 }
 
 // K1: a 256-thread block owns a chunk of kProjChunk consecutive input points of one job.  In the
@@ -76,11 +79,24 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
   int32_t* O = owner + (int64_t)job * H * W;
   for (int64_t base = (int64_t)blockIdx.x * kProjChunk; base < n; base += (int64_t)gridDim.x * kProjChunk) {
     int cmin = INT_MAX, cmax = -1;
-#pragma unroll 2
+    // every load of the thread's points first (x, y | z | ring: 16 of the 24 B), then the
+    // arithmetic: one memory round trip per chunk instead of two dependent ones per point
+    float px[kProjPPT], py[kProjPPT], pz[kProjPPT];
+    int pr[kProjPPT];
+#pragma unroll
     for (int k = 0; k < kProjPPT; ++k) {
       const int64_t i = base + k * kProjThreads + tid;
+      const int64_t ic = i < n ? i : n - 1;  // branch-free: every lane loads (base < n)
+      const float2 xy = *reinterpret_cast<const float2*>(&P[ic].x);
+      px[k] = xy.x;
+      py[k] = xy.y;
+      pz[k] = P[ic].z;
+      pr[k] = i < n ? (int)P[ic].ring : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < kProjPPT; ++k) {
       int row, col, v = -1;
-      if (i < n && project_point(P[i], H, W, row, col)) {
+      if (project_xyzr(px[k], py[k], pz[k], pr[k], H, W, row, col)) {
         v = (row << 16) | col;
         cmin = min(cmin, col);
         cmax = max(cmax, col);
@@ -262,16 +278,28 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, int32_t* __res
   }
   // owners, row by row (coalesced); the owner image is reset behind the read for the next scan
   // (this tile is its last reader), which replaces a separate memset launch per call
+  // Two cells per thread at a time with both loads issued before either is used (clamped to the
+  // tile's first cell instead of a branch), here and in the gather below: one memory round trip per
+  // pair instead of one per cell.
   int32_t* O = owner + job * HW;
-  for (int i = tid; i < HB * CG; i += 256) {
-    const int r = i / CG, c = i % CG;
-    int32_t o = kEmptyOwner;
-    if (r < nr && c < ncl) {
-      int32_t* a = O + (int64_t)(r0 + r) * W + c0 + c;
-      o = *a;
-      if (o != kEmptyOwner) *a = kEmptyOwner;
+  for (int i0 = tid; i0 < HB * CG; i0 += 512) {
+    int32_t o[2];
+    int32_t* a[2];
+    bool in[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = i0 + 256 * q, r = i / CG, c = i % CG;
+      in[q] = i < HB * CG && r < nr && c < ncl;
+      a[q] = O + (int64_t)(r0 + (in[q] ? r : 0)) * W + c0 + (in[q] ? c : 0);
+      o[q] = *a[q];
     }
-    own[r * PC + c] = o;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = i0 + 256 * q, r = i / CG, c = i % CG;
+      const int32_t v = in[q] ? o[q] : kEmptyOwner;
+      if (v != kEmptyOwner) *a[q] = kEmptyOwner;
+      if (i < HB * CG) own[r * PC + c] = v;
+    }
   }
   __syncthreads();
   // deskew: transStartInverse from the scan's first deskewed point (the minimum owner)
@@ -289,17 +317,31 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, int32_t* __res
     affine_inverse(rot_rpy(rx, ry, rz), Ls, ts);
   }
   // gather, column by column (consecutive threads = consecutive rings of one column)
-  for (int i = tid; i < HB * CG; i += 256) {
-    const int c = i / HB, r = i % HB, k = r * PC + c;
-    const int32_t o = own[k];
-    if (o != kEmptyOwner) {
-      const fbr_point_xyzirt q = P[o];
-      if (kDesk) {
+  if (kDesk) {
+    for (int i = tid; i < HB * CG; i += 256) {
+      const int c = i / HB, r = i % HB, k = r * PC + c;
+      const int32_t o = own[k];
+      if (o != kEmptyOwner) {
+        const fbr_point_xyzirt q = P[o];
         pxyz[k] = dsk ? deskew_point(q, *DT, Ls, ts) : make_float4(q.x, q.y, q.z, q.intensity);
         prng[k] = sqrt_rn(q.x * q.x + q.y * q.y + q.z * q.z);
-      } else {
-        pxyz[k] = make_float4(q.x, q.y, q.z, q.intensity);
       }
+    }
+  } else {
+    for (int i0 = tid; i0 < HB * CG; i0 += 512) {
+      float4 v[2];
+      int kk[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = i0 + 256 * q, c = i / HB, r = i % HB;
+        kk[q] = r * PC + (i < HB * CG ? c : CG);  // past the tile: the row's pad column (never read)
+        const int32_t o = i < HB * CG ? own[kk[q]] : kEmptyOwner;
+        v[q] = *reinterpret_cast<const float4*>(&P[o != kEmptyOwner ? o : 0].x);  // (x, y, z, intensity)
+      }
+      // stored unconditionally (an empty cell's slot is never read): no branch for the compiler to
+      // sink the loads into
+#pragma unroll
+      for (int q = 0; q < 2; ++q) pxyz[kk[q]] = v[q];
     }
   }
   __syncthreads();

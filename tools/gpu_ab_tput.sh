@@ -1,7 +1,7 @@
 #!/bin/bash
 # Throughput A/B of the in-tree library (new) against libfbr_hip_prev.so (prev), after a GPU test
 # subset: interleaved C2 B = 1024 lines, then C3 B = 256 and C5 B = 16 once each.
-# usage: tools/gpu_ab_tput.sh TAG "pytest -k expression" [reps] [kernel family to print]
+# usage: tools/gpu_ab_tput.sh TAG "pytest -k expression" [reps] [kernel families to print, comma-separated]
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/$1; SEL=$2; REPS=${3:-3}; KF=${4:-gn_knn}
@@ -14,7 +14,7 @@ for rep in $(seq 1 $REPS); do for v in new prev; do
   FBR_LIB=$(lib $v) timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --latency 0 --ingest 0 --exact-line 0 --no-cpu-baseline > $OUT/ab_${v}_$rep.json 2>/dev/null || exit 17
   python3 -c "
 import json; d=json.loads(open('$OUT/ab_${v}_$rep.json').read().strip().splitlines()[-1]); k=d['kernel_ms_per_step']
-print('B1024 $v rep $rep', d['value'], '$KF', k['$KF'])"
+print('B1024 $v rep $rep', d['value'], {f: k[f] for f in '$KF'.split(',')})"
 done; done
 for v in new prev; do
   FBR_LIB=$(lib $v) timeout -k 10 300 python3 bench.py --config C3 --batch 256 --steps 6 --warmup 2 --latency 0 --ingest 0 --exact-line 0 --no-cpu-baseline > $OUT/c3_${v}.json 2>/dev/null || exit 18
@@ -23,5 +23,5 @@ for v in new prev; do
 import json
 for c in ('c3', 'c5'):
     d=json.loads(open('$OUT/'+c+'_${v}.json').read().strip().splitlines()[-1]); k=d['kernel_ms_per_step']
-    print(c.upper(), '$v', d['value'], '$KF', k['$KF'])"
+    print(c.upper(), '$v', d['value'], {f: k[f] for f in '$KF'.split(',')})"
 done
