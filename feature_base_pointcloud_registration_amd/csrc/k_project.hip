@@ -248,27 +248,59 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, int32_t* __res
   const int nr = min(HB, H - r0), ncl = min(CG, W - c0);
   const int64_t HW = (int64_t)H * W;
   const int32_t* RC = rowcnt + job * H;
-  // prefix of the row counts: rows before r0 (block reduction), then the tile rows
+  // Every load the tile needs before its gather is issued first, branch-free: its owners (two cells
+  // per thread, clamped to the tile's first cell), the row counts before the tile, the tile rows'
+  // counts and chunk offsets.  One memory round trip for all of them and one barrier for the
+  // prefix (the owner image is reset behind the read for the next scan: this tile is its last
+  // reader, which replaces a separate memset launch per call).
+  int32_t* O = owner + job * HW;
+  int32_t o[2];
+  int32_t* a[2];
+  bool in[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int i = tid + 256 * q, r = i / CG, c = i % CG;
+    in[q] = i < HB * CG && r < nr && c < ncl;
+    a[q] = O + (int64_t)(r0 + (in[q] ? r : 0)) * W + c0 + (in[q] ? c : 0);
+    o[q] = *a[q];
+  }
+  const int tr = min(tid, nr - 1);  // wave 0 holds the tile rows (nr <= HB <= 64)
+  const int rcv = RC[r0 + tr];
+  const int cho = choff[((int64_t)job * H + r0 + tr) * nch + ch];
   int before = 0;
   for (int r = tid; r < r0; r += 256) before += RC[r];
-  scan[tid] = before;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (tid < s) scan[tid] += scan[tid + s];
-    __syncthreads();
+  for (int sh = 32; sh > 0; sh >>= 1) before += __shfl_xor(before, sh);
+  if (lane == 0) scan[tid >> 6] = before;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int i = tid + 256 * q, r = i / CG, c = i % CG;
+    const int32_t v = in[q] ? o[q] : kEmptyOwner;
+    if (v != kEmptyOwner) *a[q] = kEmptyOwner;
+    if (i < HB * CG) own[r * PC + c] = v;
   }
-  const int base = scan[0];
+  for (int i = tid + 512; i < HB * CG; i += 256) {  // tiles above 512 cells (FBR_COMPACT_CELLS)
+    const int r = i / CG, c = i % CG;
+    int32_t v = kEmptyOwner;
+    if (r < nr && c < ncl) {
+      int32_t* p = O + (int64_t)(r0 + r) * W + c0 + c;
+      v = *p;
+      if (v != kEmptyOwner) *p = kEmptyOwner;
+    }
+    own[r * PC + c] = v;
+  }
+  __syncthreads();
   if (tid < 64) {
     // inclusive prefix of the tile rows' counts (lane r of wave 0), plus this chunk's offset
-    int v = tid < nr ? RC[r0 + tid] : 0;
+    const int base = scan[0] + scan[1] + scan[2] + scan[3];
+    const int v = tid < nr ? rcv : 0;
     int inc = v;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(inc, o);
-      if (lane >= o) inc += y;
+    for (int sh = 1; sh < 64; sh <<= 1) {
+      const int y = __shfl_up(inc, sh);
+      if (lane >= sh) inc += y;
     }
     if (tid < nr) {
       const int roff = base + inc - v;
-      rowoff[tid] = roff + choff[((int64_t)job * H + r0 + tid) * nch + ch];
+      rowoff[tid] = roff + cho;
       if (ch == 0) {
         start_ring[job * H + r0 + tid] = roff - 1 + 5;   // imageProjection.cpp:650
         end_ring[job * H + r0 + tid] = roff + v - 1 - 5;  // :668
@@ -276,32 +308,6 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, int32_t* __res
       }
     }
   }
-  // owners, row by row (coalesced); the owner image is reset behind the read for the next scan
-  // (this tile is its last reader), which replaces a separate memset launch per call
-  // Two cells per thread at a time with both loads issued before either is used (clamped to the
-  // tile's first cell instead of a branch), here and in the gather below: one memory round trip per
-  // pair instead of one per cell.
-  int32_t* O = owner + job * HW;
-  for (int i0 = tid; i0 < HB * CG; i0 += 512) {
-    int32_t o[2];
-    int32_t* a[2];
-    bool in[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int i = i0 + 256 * q, r = i / CG, c = i % CG;
-      in[q] = i < HB * CG && r < nr && c < ncl;
-      a[q] = O + (int64_t)(r0 + (in[q] ? r : 0)) * W + c0 + (in[q] ? c : 0);
-      o[q] = *a[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int i = i0 + 256 * q, r = i / CG, c = i % CG;
-      const int32_t v = in[q] ? o[q] : kEmptyOwner;
-      if (v != kEmptyOwner) *a[q] = kEmptyOwner;
-      if (i < HB * CG) own[r * PC + c] = v;
-    }
-  }
-  __syncthreads();
   // deskew: transStartInverse from the scan's first deskewed point (the minimum owner)
   const fbr_point_xyzirt* P = pts + (int64_t)job * nmax;
   const bool dsk = kDesk && (desk.mode[job] & kDeskPoints);
