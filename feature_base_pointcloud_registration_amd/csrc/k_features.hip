@@ -685,10 +685,7 @@ k_features(FeatArgs a) {
       const int pb = max(psp - S.wlo - 6, 0), pl = min(pep - S.wlo + 7, S.L) - pb;
       if (pl > 64 * kCq || pep - psp + 1 > segcap) return;
 #pragma unroll
-      for (int q = 0; q < kCq; ++q) {
-        const int t = 64 * q + lane;
-        cpf[q] = t < pl ? S.gcurv[pb + t] : 0.0f;
-      }
+      for (int q = 0; q < kCq; ++q) cpf[q] = S.gcurv[pb + min(64 * q + lane, pl - 1)];  // clamped: no branch
       pf_next = jj;
       pf_len = pl;
       return;

@@ -916,6 +916,23 @@ k_voxel_ring(VgRing A) {
   for (int j = 0; j < 6; ++j) all6 = all6 && sp6[j] < ep6[j];
   bool cd[KPT];
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  // Every label and point load issued before any is used (one round trip; clamped indices, and an
+  // empty asm taking the values, or the compiler sinks each point load under its label test: a
+  // chain of 2 * KPT dependent round trips).  The exact instance keeps its round-5 loads: the
+  // hoisted form cost its partition phase's register allocation 25 % (voxel_ring 10.3 -> 12.8 ms per
+  // B = 1024 step, profiles/r06y_voxel_ring_loads_ab.txt).
+  int lbr[KPT];
+  float4 pr[KPT];
+  if constexpr (!kExact) {
+#pragma unroll
+    for (int r = 0; r < KPT; ++r) {
+      const int kc = min(s + r * T + tid, e - 1);
+      lbr[r] = LB[kc];
+      pr[r] = CL[kc - s];
+    }
+#pragma unroll
+    for (int r = 0; r < KPT; ++r) asm volatile("" ::"v"(lbr[r]), "v"(pr[r].x), "v"(pr[r].y), "v"(pr[r].z));
+  }
 #pragma unroll
   for (int r = 0; r < KPT; ++r) {
     const int k = s + r * T + tid;
@@ -926,10 +943,15 @@ k_voxel_ring(VgRing A) {
 #pragma unroll
       for (int j = 0; j < 6; ++j) in |= sp6[j] < ep6[j] && k >= sp6[j] && k <= ep6[j];
     }
-    // label and point loads issued together (one round trip; the point's line is read anyway)
-    const int8_t lab = in ? LB[k] : (int8_t)1;
-    const float4 p = in ? CL[k - s] : make_float4(0.f, 0.f, 0.f, 0.f);
-    cd[r] = lab <= 0;
+    float4 p;
+    if constexpr (kExact) {
+      const int8_t lab = in ? LB[k] : (int8_t)1;
+      p = in ? CL[k - s] : make_float4(0.f, 0.f, 0.f, 0.f);
+      cd[r] = lab <= 0;
+    } else {
+      p = pr[r];
+      cd[r] = in && lbr[r] <= 0;
+    }
     if (cd[r]) {
       const float v[3] = {p.x, p.y, p.z};
 #pragma unroll
@@ -1265,16 +1287,22 @@ k_voxel_ring_q(VgRing A) {
   // ---- pass A: this wave's quarter [q0, q1) in one round of loads, kept in registers ----
   const int qlen = (((len + NW - 1) / NW) + 63) & ~63;
   const int q0 = min(len, w * qlen), q1 = min(len, q0 + qlen);
+  // Every label and point load of the wave is issued before any is used: loads of a clamped index
+  // (no branch), then an empty asm that takes all the values.  Without it the compiler sank each
+  // point load under its label test, a chain of 2 * KQ dependent round trips per wave.
   float4 pt[KQ];
   bool cd[KQ];
+  int lb[KQ];
 #pragma unroll
   for (int u = 0; u < KQ; ++u) {
-    const int i = q0 + 64 * u + lane;
-    const bool ok = i < q1;
-    const int8_t lab = ok ? LB[i] : (int8_t)1;
-    pt[u] = ok ? CL[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    cd[u] = ok && lab <= 0;
+    const int ic = min(q0 + 64 * u + lane, len - 1);
+    lb[u] = LB[ic];
+    pt[u] = CL[ic];
   }
+#pragma unroll
+  for (int u = 0; u < KQ; ++u) asm volatile("" ::"v"(lb[u]), "v"(pt[u].x), "v"(pt[u].y), "v"(pt[u].z));
+#pragma unroll
+  for (int u = 0; u < KQ; ++u) cd[u] = q0 + 64 * u + lane < q1 && lb[u] <= 0;
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
   int nw = 0;
 #pragma unroll
