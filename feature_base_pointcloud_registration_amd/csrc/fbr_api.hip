@@ -88,7 +88,9 @@ constexpr int kMaxSub = 8;  // sub-batch streams per launch (FBR_NSUB); more tha
 struct Ingest {
   static constexpr int kChunks = 4;
   hipStream_t cstream = nullptr;
-  hipEvent_t up_ev[2] = {};          // the upload of input slot s is complete (on cstream)
+  hipStream_t xstream = nullptr;     // k_expand_scans, off the copy stream (FBR_INGEST_XSTREAM=0: on it)
+  hipEvent_t copied_ev = nullptr;    // the copies of the current upload are done (on cstream)
+  hipEvent_t up_ev[2] = {};          // the upload of input slot s is complete (on xstream / cstream)
   hipEvent_t chunk_ev[kChunks] = {};  // the copies out of chunk k are complete
   bool chunk_used[kChunks] = {};
   int next_chunk = 0;
@@ -101,7 +103,8 @@ struct Ingest {
   // (f32) and the rings (u8 below 256 rings), 13 B per point instead of 24, expanded on the device
   // by k_expand_scans (the batch returns poses and statistics, which no point's intensity or time
   // reaches).
-  uint8_t* d_stage = nullptr;        // [Bcap][ingest_region_bytes(NMAX)]
+  uint8_t* d_stage[2] = {};          // per input slot: [Bcap][ingest_region_bytes(NMAX)] (one per
+                                     // slot, so slot s's expand overlaps slot s^1's copies)
   int64_t* d_nin = nullptr;          // [2][2][Bcap] per input slot: the staged scans' point counts,
                                      // then their records' byte offsets in d_stage (copy stream)
   int64_t* h_nin = nullptr;          // [2][2][Bcap] pinned
@@ -1579,9 +1582,12 @@ int fbr_destroy(fbr_ctx* c) {
     if (h) (void)hipHostFree(h);
   if (c->d_result) (void)hipFree(c->d_result);
   if (c->ing.cstream) (void)fbr_sync(c->ing.cstream);
+  if (c->ing.xstream) (void)fbr_sync(c->ing.xstream);
   if (c->ing.h_stage) (void)hipHostFree(c->ing.h_stage);
   if (c->ing.d_pts_slot[1]) (void)hipFree(c->ing.d_pts_slot[1]);
-  if (c->ing.d_stage) (void)hipFree(c->ing.d_stage);
+  for (uint8_t* d : c->ing.d_stage)
+    if (d) (void)hipFree(d);
+  if (c->ing.copied_ev) (void)hipEventDestroy(c->ing.copied_ev);
   if (c->ing.d_nin) (void)hipFree(c->ing.d_nin);
   if (c->ing.h_nin) (void)hipHostFree(c->ing.h_nin);
   for (auto& e : c->ing.up_ev)
@@ -1589,6 +1595,7 @@ int fbr_destroy(fbr_ctx* c) {
   for (auto& e : c->ing.chunk_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ing.cstream) (void)hipStreamDestroy(c->ing.cstream);
+  if (c->ing.xstream) (void)hipStreamDestroy(c->ing.xstream);
   for (auto& kv : c->timers) {
     for (auto& pr : kv.second.pending) {
       (void)hipEventDestroy(pr.first);
@@ -2291,6 +2298,15 @@ int fbr_batch_bytes(fbr_ctx* c, double* bytes_total, double* bytes_gn) {
 
 namespace {
 
+// FBR_INGEST_XSTREAM=0: k_expand_scans on the copy stream, one device stage (A/B).
+bool ingest_expand_stream() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_INGEST_XSTREAM");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 int ingest_init(fbr_ctx* c) {
   Ingest& g = c->ing;
   if (g.cstream) return FBR_OK;
@@ -2302,12 +2318,17 @@ int ingest_init(fbr_ctx* c) {
   g.nthreads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   if (const char* e = std::getenv("FBR_STAGE_THREADS")) g.nthreads = std::max(1, std::atoi(e));
   CK(hipStreamCreateWithFlags(&g.cstream, hipStreamNonBlocking));
+  if (ingest_expand_stream()) {
+    CK(hipStreamCreateWithFlags(&g.xstream, hipStreamNonBlocking));
+    CK(hipEventCreateWithFlags(&g.copied_ev, hipEventDisableTiming));
+  }
   for (auto& e : g.up_ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto& e : g.chunk_ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   CK(hipHostMalloc((void**)&g.h_stage, (size_t)g.chunk_bytes * Ingest::kChunks, hipHostMallocDefault));
   g.d_pts_slot[0] = c->d_pts;
   if (dalloc(&g.d_pts_slot[1], (int64_t)c->Bcap * c->NMAX)) return FBR_ERR_HIP;
-  if (dalloc(&g.d_stage, (int64_t)c->Bcap * ingest_region_bytes(c->NMAX))) return FBR_ERR_HIP;
+  for (int k = 0; k < (g.xstream ? 2 : 1); ++k)
+    if (dalloc(&g.d_stage[k], (int64_t)c->Bcap * ingest_region_bytes(c->NMAX))) return FBR_ERR_HIP;
   if (dalloc(&g.d_nin, 4 * (int64_t)c->Bcap)) return FBR_ERR_HIP;
   CK(hipHostMalloc((void**)&g.h_nin, sizeof(int64_t) * 4 * c->Bcap, hipHostMallocDefault));
   return FBR_OK;
@@ -2395,7 +2416,8 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
   // k_expand_scans' counts and record offsets (the slot's half of the pinned array)
   int64_t* h_nin = g.h_nin + 2 * (int64_t)slot * c->Bcap;
   int64_t* h_off = h_nin + c->Bcap;
-  int64_t dpos = 0;  // d_stage offset of the next chunk: the chunks land back to back
+  uint8_t* dstage = g.d_stage[g.xstream ? slot : 0];
+  int64_t dpos = 0;  // dstage offset of the next chunk: the chunks land back to back
   std::vector<int64_t> off;
   for (int j = 0; j < B;) {
     const int k = g.next_chunk;
@@ -2436,7 +2458,7 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
     // compact records: the whole chunk in one copy (1.4 MB copies ran at 41 GB/s on the box, 64 MB
     // ones at 57: tools/h2d_probe.py); 24-B records straight into their scan slots
     if (compact)
-      CK(hipMemcpyAsync(g.d_stage + dpos, base, end, hipMemcpyHostToDevice, g.cstream));
+      CK(hipMemcpyAsync(dstage + dpos, base, end, hipMemcpyHostToDevice, g.cstream));
     else
       for (int jj = j; jj < j1; ++jj)
         if (n_in[jj])
@@ -2451,7 +2473,15 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
   if (compact) {  // stream order: after the copies
     int64_t* d_nin = g.d_nin + 2 * (int64_t)slot * c->Bcap;
     CK(hipMemcpyAsync(d_nin, h_nin, sizeof(int64_t) * 2 * c->Bcap, hipMemcpyHostToDevice, g.cstream));
-    launch_expand_scans(g.cstream, g.d_stage, c->NMAX, B, d_nin, d_nin + c->Bcap, rb, dst);
+    hipStream_t es = g.cstream;
+    if (g.xstream) {  // the expand off the copy stream: the next upload's copies start at once
+      CK(hipEventRecord(g.copied_ev, g.cstream));
+      CK(hipStreamWaitEvent(g.xstream, g.copied_ev, 0));
+      es = g.xstream;
+    }
+    launch_expand_scans(es, dstage, c->NMAX, B, d_nin, d_nin + c->Bcap, rb, dst);
+    CK(hipEventRecord(g.up_ev[slot], es));
+    return FBR_OK;
   }
   CK(hipEventRecord(g.up_ev[slot], g.cstream));
   return FBR_OK;
@@ -2514,6 +2544,7 @@ int fbr_process_batch(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const in
     if (!rc) rc = up_rc;
   }
   (void)fbr_sync(c->ing.cstream);
+  if (c->ing.xstream) (void)fbr_sync(c->ing.xstream);
   c->d_pts = c->ing.d_pts_slot[0];
   if (rc) (void)drop_staged_batch(c);
   return rc;
