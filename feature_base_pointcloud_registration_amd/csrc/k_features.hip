@@ -1137,7 +1137,10 @@ int feature_waves(int rings) {
 void launch_features(hipStream_t s, const FeatArgs& a) {
   const int nwv = feature_waves(a.B * a.H);
   const dim3 grid(a.B * a.H);
-  if (a.segcap <= 6 * 64 && a.kseg <= 4 * 128) {
+  if (nwv == 1 && a.segcap <= 5 * 64 && a.kseg <= 4 * 128) {
+    // Horizon_SCAN <= 1872 (C1 / C2): five mask words, twelve SGPRs of und / tak / frz less
+    fbr_launch((k_features<5, 4, 1>), grid, dim3(64), features_lds_bytes(a, 1), s, a);
+  } else if (a.segcap <= 6 * 64 && a.kseg <= 4 * 128) {
     if (nwv == 4)
       fbr_launch((k_features<6, 4, 4>), grid, dim3(256), features_lds_bytes(a, 4), s, a);
     else if (nwv == 2)
