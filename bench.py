@@ -62,13 +62,19 @@ VALU_PEAK_GINST, VALU_PEAK_SOURCE = valu_peak_ginst()
 # feature points, Q DS queries, IQ query-iterations (IQc of them corner ones).  The traffic the
 # design itself adds on top (scratch it stages, caches it keeps) is design_bytes below: reported
 # beside the algorithmic figure, never folded into the roofline fraction.
+# Batch scans are 16-B device records (x, y, z, ring; fbr_kernels.h) unless FBR_PACKED_SCANS=0 keeps
+# the 24-B fbr_point_xyzirt scans.
+SCAN_REC_B = 24.0 if os.environ.get("FBR_PACKED_SCANS", "1") == "0" else 16.0
+
+
 def kernel_bytes(name, tot):
     n_in, HW, n, C = tot["n_in"], tot["HW"], tot["n"], tot["C"]
     S, F, Q, IQ = tot["S"], tot["F"], tot["Q"], tot["IQ"]
+    R = SCAN_REC_B
     return {
-        "project": 24.0 * n_in + 4.0 * n,        # raw point (24 B AoS) read + first-wins owner claim
-        "extract": 4.0 * HW + 4.0 * n + 24.0 * n + 24.0 * n,  # owner image read + claimed cells reset, owning
-                                                             # raw point gather, xyzi+col+range write
+        "project": R * n_in + 4.0 * n,           # raw point record read + first-wins owner claim
+        "extract": 4.0 * HW + 4.0 * n + R * n + 24.0 * n,  # owner image read + claimed cells reset, owning
+                                                          # raw point gather, xyzi+col+range write
         "features": 9.0 * n + 32.0 * C,          # range + col read, label written; corner points read + written
         "voxel_ring": 17.0 * n + 16.0 * S,       # label + candidate point read, per-ring DS write
         "concat": 32.0 * F,                      # per-ring corner / surf outputs read + job clouds written
@@ -96,8 +102,9 @@ def design_bytes(name, tot):
 
 
 BYTE_MODEL = {
-    "project": "24 B per raw point + 4 B owner claim per valid point",
-    "extract": "4 B per range-image cell + 4 B owner reset + 24 B raw-point gather + 24 B written per valid point",
+    "project": "%d B per raw point record + 4 B owner claim per valid point" % SCAN_REC_B,
+    "extract": "4 B per range-image cell + 4 B owner reset + %d B raw-record gather + 24 B written per valid point"
+               % SCAN_REC_B,
     "features": "9 B per valid point (range + col read, label written) + 32 B per corner pick",
     "voxel_ring": "17 B per valid point + 16 B per per-ring DS point",
     "concat": "32 B per feature point",
@@ -618,7 +625,9 @@ def main():
             "timed_region": ("fbr_batch_launch of a staged batch, every stage on the device: projection, features, "
                              "per-ring and mapping VoxelGrids, CropBox statistics, Gauss-Newton registration, "
                              "results; excludes the host-to-device copy of the raw scans and guesses "
-                             "(fbr_batch_stage: inputs resident in HBM), reported separately as the ingest line"),
+                             "(fbr_batch_stage: inputs resident in HBM as 16-B x, y, z, ring records packed "
+                             "by host threads, as the ingest path's records are), reported separately as "
+                             "the ingest line"),
         },
         "roofline": {
             "bound": "valu" if valu_bound else "hbm",

@@ -109,6 +109,7 @@ struct Ingest {
                                      // then their records' byte offsets in d_stage (copy stream)
   int64_t* h_nin = nullptr;          // [2][2][Bcap] pinned
   bool compact_used = false;         // the last fbr_process_batch used compact records
+  bool pk_slot[2] = {};              // input slot s holds 16-B device records (launch_expand_scans pk)
 };
 
 // A contiguous sub-batch of jobs driven on one stream.  j0 is the first job of the sub-batch's
@@ -203,6 +204,11 @@ struct fbr_ctx {
   int64_t HW = 0, NMAX = 0;
   // inputs
   fbr_point_xyzirt* d_pts = nullptr;
+  // the staged batch's 16-B device records (fbr_kernels.h: x, y, z, ring bits), null = the 24-B
+  // scans in d_pts; d_pk backs them for fbr_batch_stage (fbr_process_batch expands into its slots)
+  float4* d_pk = nullptr;
+  const float4* staged_pk = nullptr;
+  bool staged_24 = false;  // d_pts holds the staged batch's 24-B scans (a deskewing launch needs them)
   int64_t* d_nin = nullptr;
   int64_t single_n = -1;  // the single-scan path's point count (k_project's argument, no copy)
   float* d_guess = nullptr;
@@ -526,15 +532,27 @@ int stage_project(fbr_ctx* c, const Sub& sb) {
   DeskArgs desk{nullptr, nullptr, nullptr};
   if (c->desk_any && !c->no_time_call)  // deskewFlag == -1 without a "time" field (:296-297, :548)
     desk = DeskArgs{c->d_desk_mode + i0, c->d_desk + i0, c->d_rowmin + j0 * c->H};
+  // batch jobs read the 16-B device records when the staged batch has them and nothing deskews
+  const float4* pk = (!sb.stream_mode && !desk.mode && c->staged_pk) ? c->staged_pk + i0 * c->NMAX : nullptr;
+  if (!sb.stream_mode && !pk && !c->staged_24) return FBR_ERR_STATE;  // deskew tables set after a 16-B upload
   int32_t* owner = c->d_owner + j0 * c->HW;  // all kEmptyOwner: set at fbr_create, reset by k_compact
   TIMED_ON(c, sb.st, "project", launch_project(sb.st, c->d_pts + i0 * c->NMAX, c->d_nin + i0, c->NMAX, sb.B, c->H,
-                                               c->W, owner, c->d_err + j0, sb.stream_mode ? c->single_n : -1));
+                                               c->W, owner, c->d_err + j0, sb.stream_mode ? c->single_n : -1, pk));
   TIMED_ON(c, sb.st, "extract",
            launch_extract(sb.st, c->d_pts + i0 * c->NMAX, c->NMAX, owner, sb.B, c->H, c->W, c->d_rowcnt + j0 * c->H,
                           c->d_choff + j0 * c->H * (c->W / 32 + 1),
                           c->d_cloud + j0 * c->HW, c->d_col + j0 * c->HW, c->d_range + j0 * c->HW,
-                          c->d_start + j0 * c->H, c->d_end + j0 * c->H, c->d_nvalid + j0, desk));
+                          c->d_start + j0 * c->H, c->d_end + j0 * c->H, c->d_nvalid + j0, desk, pk));
   return FBR_OK;
+}
+
+// Batch scans as 16-B device records (fbr_kernels.h; FBR_PACKED_SCANS=0: the 24-B scans, for A/B).
+bool packed_scans_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_PACKED_SCANS");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
 }
 
 // Batch jobs resolve the surf walk only within reach of each segment's end (FeatArgs::surf_full;
@@ -687,6 +705,8 @@ int batch_quiesce(fbr_ctx* c);
 int drop_staged_batch(fbr_ctx* c) {
   const int rc = batch_quiesce(c);
   c->staged_B = 0;
+  c->staged_pk = nullptr;
+  c->staged_24 = false;
   c->crop_cached = false;
   c->last_slot = -1;
   // launch ids only grow: every launch made so far belongs to the dropped batch (or its slot was
@@ -1570,7 +1590,7 @@ int fbr_destroy(fbr_ctx* c) {
                   c->d_ncds, c->d_nsds, c->d_vg_scratch, c->d_gn, c->d_items, c->d_nitems,
                   c->d_item_range, c->d_cropcnt, c->d_cropwork, c->d_partial, c->d_pose_out, c->d_stats, c->d_trace, c->d_nbr, c->d_fitc, c->d_fits, c->d_nsame, c->d_fb_list, c->d_bin, c->d_iter_cnt, c->d_feat_scratch, c->d_msg,
                   c->d_desk, c->d_desk_mode, c->d_rowmin, c->d_choff,
-                  c->d_kf_c, c->d_kf_s, c->d_kraw_c, c->d_kraw_s, c->d_kds_c, c->d_kds_s, c->d_kf_segs, c->d_bounds, c->d_direct_done};
+                  c->d_kf_c, c->d_kf_s, c->d_kraw_c, c->d_kraw_s, c->d_kds_c, c->d_kds_s, c->d_kf_segs, c->d_bounds, c->d_direct_done, c->d_pk};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_iter_flags) (void)hipHostFree(c->h_iter_flags);
@@ -1887,10 +1907,50 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
   auto q = [&](hipError_t e) {
     if (e != hipSuccess && !rc) rc = FBR_ERR_HIP;
   };
-  for (int j = 0; j < n_jobs && !rc; ++j)
-    if (n_in[j])
-      q(hipMemcpyAsync(c->d_pts + j * c->NMAX, scans[j], sizeof(fbr_point_xyzirt) * n_in[j], hipMemcpyHostToDevice,
-                       c->stream));
+  // Without deskew tables the scans go over as 16-B device records (x, y, z, ring bits; packed by
+  // host threads, as fbr_process_batch's compact records are); a deskewing batch keeps the 24-B
+  // scans, whose time deskewPoint reads.
+  const bool pk = packed_scans_enabled() && !c->desk_any;
+  if (pk) {
+    if (!c->d_pk && dalloc(&c->d_pk, (int64_t)c->Bcap * c->NMAX)) return FBR_ERR_HIP;
+    std::vector<float4> rec;
+    for (int j0 = 0; j0 < n_jobs && !rc; j0 += 64) {  // 64 scans per host buffer (~118 MB for C2)
+      const int j1 = std::min(n_jobs, j0 + 64);
+      std::vector<int64_t> at(j1 - j0 + 1, 0);
+      for (int j = j0; j < j1; ++j) at[j - j0 + 1] = at[j - j0] + n_in[j];
+      rec.resize((size_t)at.back());
+      const int nt = std::max(1, std::min(16, j1 - j0));
+      auto pack = [&](int t) {
+        for (int j = j0 + t; j < j1; j += nt) {
+          const fbr_point_xyzirt* P = scans[j];
+          float4* o = rec.data() + at[j - j0];
+          for (int64_t i = 0; i < n_in[j]; ++i) {
+            float4 v;
+            v.x = P[i].x;
+            v.y = P[i].y;
+            v.z = P[i].z;
+            const int32_t ring = P[i].ring;
+            std::memcpy(&v.w, &ring, 4);
+            o[i] = v;
+          }
+        }
+      };
+      std::vector<std::thread> th;
+      for (int t = 1; t < nt; ++t) th.emplace_back(pack, t);
+      pack(0);
+      for (auto& x : th) x.join();
+      for (int j = j0; j < j1 && !rc; ++j)
+        if (n_in[j])
+          q(hipMemcpyAsync(c->d_pk + j * c->NMAX, rec.data() + at[j - j0], sizeof(float4) * n_in[j],
+                           hipMemcpyHostToDevice, c->stream));
+      q(fbr_sync(c->stream));  // rec is refilled next round
+    }
+  } else {
+    for (int j = 0; j < n_jobs && !rc; ++j)
+      if (n_in[j])
+        q(hipMemcpyAsync(c->d_pts + j * c->NMAX, scans[j], sizeof(fbr_point_xyzirt) * n_in[j],
+                         hipMemcpyHostToDevice, c->stream));
+  }
   if (!rc) q(hipMemcpyAsync(c->d_nin, n_in, sizeof(int64_t) * n_jobs, hipMemcpyHostToDevice, c->stream));
   if (!rc) q(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * n_jobs, hipMemcpyHostToDevice, c->stream));
   if (!rc && c->has_map && c->map_nocrop) rc = crop_stats(c, Sub{0, n_jobs, 0, c->stream});
@@ -1900,6 +1960,8 @@ int fbr_batch_stage(fbr_ctx* c, const fbr_point_xyzirt* const* scans, const int6
   if (rc) return rc;
   c->crop_cached = c->has_map && c->map_nocrop;
   c->staged_B = n_jobs;
+  c->staged_pk = pk ? c->d_pk : nullptr;
+  c->staged_24 = !pk;
   c->staged_nin.assign(n_in, n_in + n_jobs);
   return FBR_OK;
 }
@@ -2407,6 +2469,9 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
   // compact records unless a deskew table may read the per-point time (deskewPoint, :545-580)
   const bool compact = ingest_compact_enabled() && !c->desk_any;
   g.compact_used = compact;
+  // compact records expand into 16-B device records (k_project / k_compact read those)
+  const bool pk = compact && packed_scans_enabled();
+  g.pk_slot[slot] = pk;
   // ring bytes per point: u8 for sensors of < 256 rings, where every out-of-range ring (>= H, which
   // projectPointCloud drops, imageProjection.cpp:599) is stored as 255, still out of range
   const int rb = c->H < 256 ? 1 : 2;
@@ -2479,7 +2544,7 @@ int ingest_upload(fbr_ctx* c, int slot, const fbr_point_xyzirt* const* scans, co
       CK(hipStreamWaitEvent(g.xstream, g.copied_ev, 0));
       es = g.xstream;
     }
-    launch_expand_scans(es, dstage, c->NMAX, B, d_nin, d_nin + c->Bcap, rb, dst);
+    launch_expand_scans(es, dstage, c->NMAX, B, d_nin, d_nin + c->Bcap, rb, dst, pk);
     CK(hipEventRecord(g.up_ev[slot], es));
     return FBR_OK;
   }
@@ -2494,6 +2559,8 @@ int ingest_stage(fbr_ctx* c, int slot, const int64_t* n_in, int B, const float* 
   if (rc0) return rc0;
   c->no_time_call = false;
   c->d_pts = c->ing.d_pts_slot[slot];
+  // 16-B records live in the slot's scan buffer (16 <= 24 B per point at the same NMAX stride)
+  c->staged_pk = c->ing.pk_slot[slot] ? reinterpret_cast<const float4*>(c->d_pts) : nullptr;
   CK(hipMemcpyAsync(c->d_nin, n_in, sizeof(int64_t) * B, hipMemcpyHostToDevice, c->stream));
   CK(hipMemcpyAsync(c->d_guess, poses_in, sizeof(float) * 6 * B, hipMemcpyHostToDevice, c->stream));
   CK(hipStreamWaitEvent(c->stream, c->ing.up_ev[slot], 0));
@@ -2505,6 +2572,7 @@ int ingest_stage(fbr_ctx* c, int slot, const int64_t* n_in, int B, const float* 
   CK(fbr_sync(c->stream));  // n_in / poses_in are the caller's
   c->crop_cached = c->has_map && c->map_nocrop;
   c->staged_B = B;
+  c->staged_24 = !c->staged_pk;
   c->staged_nin.assign(n_in, n_in + B);
   return FBR_OK;
 }

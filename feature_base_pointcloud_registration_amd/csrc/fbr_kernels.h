@@ -71,11 +71,16 @@ void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_
 // (rb = 1), else u16 (rb = 2).  ingest_region_bytes(nmax) bounds one record, padding included.
 __host__ __device__ inline int64_t ingest_plane(int64_t n) { return (n + 3) & ~(int64_t)3; }
 inline int64_t ingest_region_bytes(int64_t nmax) { return (14 * nmax + 48 + 15) & ~(int64_t)15; }
+// Batch scans may live on the device as 16-B records (ScanRec): float4 (x, y, z, ring as int bits
+// in w), one dwordx4 per point where the 24-B fbr_point_xyzirt costs 24 B of cache lines for the 16
+// projection and extraction read.  pk = the records (null: the 24-B scans); intensity and time are
+// not carried, so launches that deskew keep the 24-B scans.
+// out: fbr_point_xyzirt records, or with pk the 16-B ones.
 void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, const int64_t* nin,
-                         const int64_t* off, int rb, fbr_point_xyzirt* out);
+                         const int64_t* off, int rb, void* out, bool pk);
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
                     int W, int32_t* owner,
-                    int32_t* err, int64_t n_single = -1);
+                    int32_t* err, int64_t n_single = -1, const float4* pk = nullptr);
 // Optional IMU deskew of the kept points (deskewPoint, imageProjection.cpp:545-580): desk_mode
 // [B] (kDesk* bits, fbr_imu.h) and desk [B] tables, both null when no job deskews; rowmin [B][H]
 // receives each row's minimum owner (the scan's first deskewed point is the minimum over rows).
@@ -87,7 +92,8 @@ struct DeskArgs {
 // choff: [B][H][ceil(W / 32)] scratch (claimed cells of a row before each compaction tile)
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, int32_t* owner, int B, int H,
                     int W, int32_t* rowcnt, int32_t* choff, float4* cloud, int32_t* col, float* range,
-                    int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk);
+                    int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk,
+                    const float4* pk = nullptr);
 
 // ---- A6-A8 (k_features.hip) ----
 struct FeatArgs {

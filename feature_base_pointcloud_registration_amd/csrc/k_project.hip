@@ -62,8 +62,11 @@ constexpr int kProjThreads = 256, kProjPPT = 8, kProjChunk = kProjThreads * kPro
 // rather than in registers across the claim phase: the column arithmetic (fdlibm atan2f, double
 // conversions) then runs two points at a time and the kernel stays at a register count that lets
 // 8 waves per SIMD hide the atomic latency.
+// kPk: the batch's 16-B device records (ScanRec: x, y, z, ring bits in w; one dwordx4 per point)
+// instead of the 24-B fbr_point_xyzirt (read whole by the cache lines, 8 of its bytes unused here).
+template <bool kPk>
 __global__ void __launch_bounds__(kProjThreads)
-k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ nin, int64_t nmax, int H, int W,
+k_project(const void* __restrict__ src, const int64_t* __restrict__ nin, int64_t nmax, int H, int W,
           int tile_log2, int32_t* __restrict__ owner, int32_t* __restrict__ err, int64_t n_single) {
   extern __shared__ int32_t tile[];  // [H][(1 << tile_log2) + 1]: the pad puts the consecutive rings of one
                                      // column (consecutive points in firing order) in distinct banks
@@ -75,7 +78,8 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
   if (err && blockIdx.x == 0 && tid == 0) err[job] = 0;
   const int tcols = 1 << tile_log2, tcells = H << tile_log2, tpitch = tcols + 1;
   const int64_t n = n_single >= 0 ? n_single : nin[job];  // single scans: the count as an argument
-  const fbr_point_xyzirt* P = pts + (int64_t)job * nmax;
+  const fbr_point_xyzirt* P = static_cast<const fbr_point_xyzirt*>(src) + (int64_t)job * nmax;
+  const float4* PK = static_cast<const float4*>(src) + (int64_t)job * nmax;
   int32_t* O = owner + (int64_t)job * H * W;
   for (int64_t base = (int64_t)blockIdx.x * kProjChunk; base < n; base += (int64_t)gridDim.x * kProjChunk) {
     int cmin = INT_MAX, cmax = -1;
@@ -87,11 +91,19 @@ k_project(const fbr_point_xyzirt* __restrict__ pts, const int64_t* __restrict__ 
     for (int k = 0; k < kProjPPT; ++k) {
       const int64_t i = base + k * kProjThreads + tid;
       const int64_t ic = i < n ? i : n - 1;  // branch-free: every lane loads (base < n)
-      const float2 xy = *reinterpret_cast<const float2*>(&P[ic].x);
-      px[k] = xy.x;
-      py[k] = xy.y;
-      pz[k] = P[ic].z;
-      pr[k] = i < n ? (int)P[ic].ring : -1;
+      if constexpr (kPk) {
+        const float4 q = PK[ic];
+        px[k] = q.x;
+        py[k] = q.y;
+        pz[k] = q.z;
+        pr[k] = i < n ? __float_as_int(q.w) : -1;
+      } else {
+        const float2 xy = *reinterpret_cast<const float2*>(&P[ic].x);
+        px[k] = xy.x;
+        py[k] = xy.y;
+        pz[k] = P[ic].z;
+        pr[k] = i < n ? (int)P[ic].ring : -1;
+      }
     }
 #pragma unroll
     for (int k = 0; k < kProjPPT; ++k) {
@@ -218,9 +230,9 @@ __device__ __forceinline__ float4 deskew_point(const fbr_point_xyzirt& q, const 
 // LDS (dynamic): xyzi [HB*CG] float4, owners [HB*CG] int32, and with deskew the raw ranges
 // [HB*CG] float (without deskew the staged point is the raw point and the range is recomputed
 // from it at the write, same expression, same bits): 20 KB per 1024-cell tile.
-template <bool kDesk>
+template <bool kDesk, bool kPk = false>
 __global__ void __launch_bounds__(256)
-k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, int32_t* __restrict__ owner,
+k_compact(const fbr_point_xyzirt* __restrict__ pts, const float4* __restrict__ pk, int64_t nmax, int32_t* __restrict__ owner,
           const int32_t* __restrict__ rowcnt, const int32_t* __restrict__ choff, int B, int H, int W, int HB, int CG,
           float4* __restrict__ cloud, int32_t* __restrict__ col, float* __restrict__ range,
           int32_t* __restrict__ start_ring, int32_t* __restrict__ end_ring, int32_t* __restrict__ nvalid,
@@ -342,7 +354,12 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, int64_t nmax, int32_t* __res
         const int i = i0 + 256 * q, c = i / HB, r = i % HB;
         kk[q] = r * PC + (i < HB * CG ? c : CG);  // past the tile: the row's pad column (never read)
         const int32_t o = i < HB * CG ? own[kk[q]] : kEmptyOwner;
-        v[q] = *reinterpret_cast<const float4*>(&P[o != kEmptyOwner ? o : 0].x);  // (x, y, z, intensity)
+        if constexpr (kPk) {  // 16-B records: (x, y, z, ring); the batch's clouds carry no intensity
+          v[q] = pk[(int64_t)job * nmax + (o != kEmptyOwner ? o : 0)];
+          v[q].w = 0.0f;
+        } else {
+          v[q] = *reinterpret_cast<const float4*>(&P[o != kEmptyOwner ? o : 0].x);  // (x, y, z, intensity)
+        }
       }
       // stored unconditionally (an empty cell's slot is never read): no branch for the compiler to
       // sink the loads into
@@ -445,9 +462,10 @@ void launch_unpack_msg(hipStream_t s, const uint8_t* data, const MsgDev& L, fbr_
 // intensity = time = 0.  Slots
 // past n are not written (k_project reads n points).  HBM-bound: 12 + rb B read + 24 B written per
 // point.
+template <bool kPk>
 __global__ void __launch_bounds__(256)
 k_expand_scans(const uint8_t* __restrict__ stage, int64_t nmax, const int64_t* __restrict__ nin,
-               const int64_t* __restrict__ off, int rb, fbr_point_xyzirt* __restrict__ out) {
+               const int64_t* __restrict__ off, int rb, void* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t job = blockIdx.y;
   const int64_t n = min(nin[job], nmax);
@@ -456,34 +474,45 @@ k_expand_scans(const uint8_t* __restrict__ stage, int64_t nmax, const int64_t* _
   const float* pl = reinterpret_cast<const float*>(r);
   const int64_t m = ingest_plane(n);
   const uint16_t ring = rb == 1 ? (uint16_t)r[12 * m + i] : reinterpret_cast<const uint16_t*>(r + 12 * m)[i];
-  fbr_point_xyzirt q;
-  q.x = pl[i];
-  q.y = pl[m + i];
-  q.z = pl[2 * m + i];
-  q.intensity = 0.0f;
-  q.ring = ring;
-  q.pad_ = 0;
-  q.time = 0.0f;
-  out[job * nmax + i] = q;
+  if constexpr (kPk) {
+    static_cast<float4*>(dst)[job * nmax + i] = make_float4(pl[i], pl[m + i], pl[2 * m + i], __int_as_float((int)ring));
+  } else {
+    fbr_point_xyzirt q;
+    q.x = pl[i];
+    q.y = pl[m + i];
+    q.z = pl[2 * m + i];
+    q.intensity = 0.0f;
+    q.ring = ring;
+    q.pad_ = 0;
+    q.time = 0.0f;
+    static_cast<fbr_point_xyzirt*>(dst)[job * nmax + i] = q;
+  }
 }
 
 void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, const int64_t* nin,
-                         const int64_t* off, int rb, fbr_point_xyzirt* out) {
+                         const int64_t* off, int rb, void* out, bool pk) {
   if (B <= 0 || nmax <= 0) return;
-  fbr_launch(k_expand_scans, dim3((unsigned)((nmax + 255) / 256), B), dim3(256), 0, s, stage, nmax, nin, off, rb,
-             out);
+  const dim3 grid((unsigned)((nmax + 255) / 256), B);
+  if (pk)
+    fbr_launch(k_expand_scans<true>, grid, dim3(256), 0, s, stage, nmax, nin, off, rb, out);
+  else
+    fbr_launch(k_expand_scans<false>, grid, dim3(256), 0, s, stage, nmax, nin, off, rb, out);
 }
 
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
-                    int W, int32_t* owner, int32_t* err, int64_t n_single) {
+                    int W, int32_t* owner, int32_t* err, int64_t n_single, const float4* pk) {
   int blocks = (int)((nmax + kProjChunk - 1) / kProjChunk);
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
   int tile_log2 = 6;  // 64 columns, shrunk so the tile stays <= 32 KB
   while (tile_log2 > 3 && ((int64_t)H << tile_log2) > 8192) --tile_log2;
   const size_t lds = sizeof(int32_t) * (size_t)H * ((1 << tile_log2) + 1);
-  fbr_launch(k_project, dim3(blocks, B), dim3(kProjThreads), lds, s, pts, nin, nmax, H, W, tile_log2, owner, err,
-             n_single);
+  if (pk)
+    fbr_launch(k_project<true>, dim3(blocks, B), dim3(kProjThreads), lds, s, (const void*)pk, nin, nmax, H, W,
+               tile_log2, owner, err, n_single);
+  else
+    fbr_launch(k_project<false>, dim3(blocks, B), dim3(kProjThreads), lds, s, (const void*)pts, nin, nmax, H, W,
+               tile_log2, owner, err, n_single);
 }
 
 // Compaction tile size in cells (FBR_COMPACT_CELLS: 512, 1024 or 2048).  512 since round 5: 10 KB of
@@ -501,7 +530,7 @@ int compact_cells() {
 
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, int32_t* owner, int B, int H,
                     int W, int32_t* rowcnt, int32_t* choff, float4* cloud, int32_t* col, float* range,
-                    int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk) {
+                    int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk, const float4* pk) {
   const CompactTile T = compact_tile(H, compact_cells());
   fbr_launch(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, T.cg, rowcnt, desk.mode ? desk.rowmin : nullptr,
              choff);
@@ -510,11 +539,14 @@ void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, in
   const dim3 grid((unsigned)(groups * 8 * tiles));
   const size_t cells = (size_t)T.hb * (T.cg + 1);  // padded pitch (k_compact)
   if (desk.mode)
-    fbr_launch(k_compact<true>, grid, dim3(256), (uint32_t)(cells * 24), s, pts, nmax, owner, rowcnt, choff, B, H, W,
-               T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk);
+    fbr_launch(k_compact<true>, grid, dim3(256), (uint32_t)(cells * 24), s, pts, pk, nmax, owner, rowcnt, choff, B,
+               H, W, T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk);
+  else if (pk)
+    fbr_launch(k_compact<false, true>, grid, dim3(256), (uint32_t)(cells * 20), s, pts, pk, nmax, owner, rowcnt,
+               choff, B, H, W, T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk);
   else
-    fbr_launch(k_compact<false>, grid, dim3(256), (uint32_t)(cells * 20), s, pts, nmax, owner, rowcnt, choff, B, H,
-               W, T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk);
+    fbr_launch(k_compact<false>, grid, dim3(256), (uint32_t)(cells * 20), s, pts, pk, nmax, owner, rowcnt, choff, B,
+               H, W, T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk);
 }
 
 }  // namespace fbr

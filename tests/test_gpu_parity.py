@@ -1084,3 +1084,41 @@ def test_kilometre_prior_map_uses_sparse_grid_and_matches_oracle(c2_map):
             assert (sg["iterations"], sg["n_sel"], sg["status"]) == (so["iterations"], so["n_sel"], so["status"])
             assert (sg["n_corner_map"], sg["n_surf_map"]) == (so["n_corner_map"], so["n_surf_map"])
             assert np.abs(pg[3:5] - (gt[3:5] + [100.0 * i, 100.0 * j])).max() < 0.05
+
+
+_BOTH_BATCH_PATHS_CHILD = (
+    "import sys, numpy as np; sys.path.insert(0, %r); from feature_base_pointcloud_registration_amd import api, synth; "
+    "d = np.load(%r); scans = [d['arr_%%d' %% k] for k in range(%d)]; g = d['guesses']; "
+    "c = api.Context(synth.config_params(%r, max_batch=%d)); c.set_map(*synth.config_map(%r)); "
+    "p, s = c.process_batch(scans, g); c.batch_stage(scans, g); c.batch_launch(); c.batch_wait(); "
+    "p2, s2 = c.batch_results(); sys.stdout.buffer.write(p.tobytes() + s.tobytes() + p2.tobytes() + s2.tobytes())")
+
+
+def _both_batch_paths(cfg, jobs, env):
+    """Poses + stats bytes of fbr_process_batch (ingest) and fbr_batch_stage / launch (host scans
+    with their intensities) on the same jobs, in a child process with extra environment knobs."""
+    import subprocess
+    import sys
+    n = len(jobs)
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "fbr_child_both_%s.npz" % cfg)
+    np.savez(path, *[j[0] for j in jobs], guesses=np.stack([j[1] for j in jobs]).astype(np.float32))
+    code = _BOTH_BATCH_PATHS_CHILD % (REPO, path, n, cfg, n, cfg)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, env=dict(os.environ, **env), timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    half = len(r.stdout) // 2
+    return r.stdout[:half], r.stdout[half:]
+
+
+@pytest.mark.parametrize("cfg,nj,seed", [("C2", 12, 660), ("C3", 2, 661)])
+def test_packed_scan_records_are_bit_identical_to_24b_scans(cfg, nj, seed):
+    """Batch scans live on the device as 16-B records (x, y, z, ring bits; fbr_kernels.h) that
+    k_project and k_compact read with one dwordx4 per point.  Intensity and time are not carried:
+    neither reaches a batch result.  Against the 24-B fbr_point_xyzirt scans (FBR_PACKED_SCANS=0,
+    child process), through the ingest path (fbr_process_batch) and through fbr_batch_stage (whose
+    scans carry real intensities): poses and stats bit-equal, and the two entry points agree."""
+    jobs = synth.make_jobs(cfg, nj, base_seed=seed)
+    a_ingest, a_stage = _both_batch_paths(cfg, jobs, {"FBR_PACKED_SCANS": "0"})
+    b_ingest, b_stage = _both_batch_paths(cfg, jobs, {"FBR_PACKED_SCANS": "1"})
+    assert b_ingest == a_ingest
+    assert b_stage == a_stage
+    assert b_stage == b_ingest
