@@ -213,6 +213,10 @@ struct fbr_ctx {
   int64_t single_n = -1;  // the single-scan path's point count (k_project's argument, no copy)
   float* d_guess = nullptr;
   // projection
+  // owner image generations (OwnerTag, fbr_kernels.h): owner_ib index bits, owner_tmax the last
+  // generation before the image is refilled (0: untagged, reset by k_compact)
+  int owner_ib = 0;
+  uint32_t owner_gen = 0, owner_tmax = 0;
   int32_t *d_owner = nullptr, *d_rowcnt = nullptr, *d_col = nullptr, *d_start = nullptr, *d_end = nullptr,
           *d_nvalid = nullptr;
   float4* d_cloud = nullptr;
@@ -523,6 +527,34 @@ int voxel_grid_once(fbr_ctx* c, const fbr_point_xyzi* in, int64_t n, float leaf,
 // Sub-batches (struct Sub above) share the context's buffers without overlapping: the stages offset
 // every per-job work array by j0 and every input array by in0.
 
+// Generation-tagged owner images (fbr_kernels.h OwnerTag; FBR_OWNER_TAGS=0: untagged images reset
+// by k_compact, for A/B).
+bool owner_tags_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_OWNER_TAGS");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+// The next owner generation of a projection call.  When the tags run out, every owner image is
+// refilled once the device is idle (a call of the previous tag may still be running on another stream).
+int next_owner_tag(fbr_ctx* c, OwnerTag* ot) {
+  if (!c->owner_tmax) {
+    *ot = OwnerTag{0u, 0x7FFFFFFFu, true};
+    return FBR_OK;
+  }
+  if (c->owner_gen >= c->owner_tmax) {
+    CK(hipDeviceSynchronize());
+    CK(hipMemset(c->d_owner, 0x7F, sizeof(int32_t) * (int64_t)c->Bwork * c->HW));
+    CK(hipDeviceSynchronize());
+    c->owner_gen = 0;
+  }
+  const uint32_t g = ++c->owner_gen;
+  *ot = OwnerTag{(((uint32_t)kEmptyOwner >> c->owner_ib) - g) << c->owner_ib, (1u << c->owner_ib) - 1u, false};
+  return FBR_OK;
+}
+
 // The single-scan sub-batch: job slot 0 on the primary stream, stream mode (the state the
 // reference's stage objects keep between scans is carried between calls).
 Sub single_sub(fbr_ctx* c) { return Sub{0, 1, 0, c->stream, true}; }
@@ -535,14 +567,17 @@ int stage_project(fbr_ctx* c, const Sub& sb) {
   // batch jobs read the 16-B device records when the staged batch has them and nothing deskews
   const float4* pk = (!sb.stream_mode && !desk.mode && c->staged_pk) ? c->staged_pk + i0 * c->NMAX : nullptr;
   if (!sb.stream_mode && !pk && !c->staged_24) return FBR_ERR_STATE;  // deskew tables set after a 16-B upload
-  int32_t* owner = c->d_owner + j0 * c->HW;  // all kEmptyOwner: set at fbr_create, reset by k_compact
+  int32_t* owner = c->d_owner + j0 * c->HW;
+  OwnerTag ot;
+  const int trc = next_owner_tag(c, &ot);
+  if (trc) return trc;
   TIMED_ON(c, sb.st, "project", launch_project(sb.st, c->d_pts + i0 * c->NMAX, c->d_nin + i0, c->NMAX, sb.B, c->H,
-                                               c->W, owner, c->d_err + j0, sb.stream_mode ? c->single_n : -1, pk));
+                                               c->W, owner, c->d_err + j0, sb.stream_mode ? c->single_n : -1, pk, ot));
   TIMED_ON(c, sb.st, "extract",
            launch_extract(sb.st, c->d_pts + i0 * c->NMAX, c->NMAX, owner, sb.B, c->H, c->W, c->d_rowcnt + j0 * c->H,
                           c->d_choff + j0 * c->H * (c->W / 32 + 1),
                           c->d_cloud + j0 * c->HW, c->d_col + j0 * c->HW, c->d_range + j0 * c->HW,
-                          c->d_start + j0 * c->H, c->d_end + j0 * c->H, c->d_nvalid + j0, desk, pk));
+                          c->d_start + j0 * c->H, c->d_end + j0 * c->H, c->d_nvalid + j0, desk, pk, ot));
   return FBR_OK;
 }
 
@@ -1569,10 +1604,16 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
       hipMemset(c->d_label_stream, 0, HW) != hipSuccess || hipMemset(c->d_col, 0, sizeof(int32_t) * Bw * HW) != hipSuccess ||
       hipMemset(c->d_range, 0, sizeof(float) * Bw * HW) != hipSuccess ||
       hipMemset(c->d_desk_mode, 0, sizeof(int32_t) * B) != hipSuccess ||
-      hipMemset(c->d_owner, 0x7F, sizeof(int32_t) * Bw * HW) != hipSuccess) {  // k_compact resets it after use
+      hipMemset(c->d_owner, 0x7F, sizeof(int32_t) * Bw * HW) != hipSuccess) {  // OwnerTag: refilled when the tags run out
     fbr_destroy(c);
     return FBR_ERR_HIP;
   }
+  // index bits of the owner claims; tagged while at least 2^6 generations fit (scans up to 2^24 points)
+  c->owner_ib = 1;
+  while (((int64_t)1 << c->owner_ib) < c->NMAX) ++c->owner_ib;
+  c->owner_tmax = (owner_tags_enabled() && c->owner_ib <= 24) ? ((uint32_t)kEmptyOwner >> c->owner_ib) - 1 : 0;
+  if (const char* e = std::getenv("FBR_OWNER_TMAX"))  // tests: refill the images every few calls
+    if (c->owner_tmax && std::atoi(e) > 0) c->owner_tmax = std::min<uint32_t>(c->owner_tmax, (uint32_t)std::atoi(e));
   *out = c;
   return FBR_OK;
 }

@@ -78,9 +78,21 @@ inline int64_t ingest_region_bytes(int64_t nmax) { return (14 * nmax + 48 + 15) 
 // out: fbr_point_xyzirt records, or with pk the 16-B ones.
 void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int B, const int64_t* nin,
                          const int64_t* off, int rb, void* out, bool pk);
+// Generation-tagged owner image: a claim is (tag << ib) | input index, where the tag of call g is
+// (kEmptyOwner >> ib) - g, so a later call's claims win atomicMin against every stale one, and a cell
+// belongs to this call only when its tag bits equal `bits`.  The image is then never reset between
+// calls (only when the generations run out).  bits = 0, mask = 0x7FFFFFFF: untagged, k_compact
+// resets the claimed cells behind its read (owner images of > 2^24-point scans).
+struct OwnerTag {
+  uint32_t bits, mask;
+  bool reset;  // untagged: k_compact writes kEmptyOwner back
+};
+__host__ __device__ inline bool owner_valid(int32_t o, const OwnerTag& t) {
+  return o != 0x7F7F7F7F && ((uint32_t)o & ~t.mask) == t.bits;
+}
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
                     int W, int32_t* owner,
-                    int32_t* err, int64_t n_single = -1, const float4* pk = nullptr);
+                    int32_t* err, int64_t n_single, const float4* pk, const OwnerTag& ot);
 // Optional IMU deskew of the kept points (deskewPoint, imageProjection.cpp:545-580): desk_mode
 // [B] (kDesk* bits, fbr_imu.h) and desk [B] tables, both null when no job deskews; rowmin [B][H]
 // receives each row's minimum owner (the scan's first deskewed point is the minimum over rows).
@@ -93,7 +105,7 @@ struct DeskArgs {
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, int32_t* owner, int B, int H,
                     int W, int32_t* rowcnt, int32_t* choff, float4* cloud, int32_t* col, float* range,
                     int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk,
-                    const float4* pk = nullptr);
+                    const float4* pk, const OwnerTag& ot);
 
 // ---- A6-A8 (k_features.hip) ----
 struct FeatArgs {

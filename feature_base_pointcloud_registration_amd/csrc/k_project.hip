@@ -64,10 +64,12 @@ constexpr int kProjThreads = 256, kProjPPT = 8, kProjChunk = kProjThreads * kPro
 // 8 waves per SIMD hide the atomic latency.
 // kPk: the batch's 16-B device records (ScanRec: x, y, z, ring bits in w; one dwordx4 per point)
 // instead of the 24-B fbr_point_xyzirt (read whole by the cache lines, 8 of its bytes unused here).
+// Claims are tagged with the call's owner generation (OwnerTag).
+// (6 waves per SIMD: the LDS tile's limit; the 16-B record instance otherwise took 90 VGPRs, 5 waves)
 template <bool kPk>
-__global__ void __launch_bounds__(kProjThreads)
+__global__ void __launch_bounds__(kProjThreads) __attribute__((amdgpu_waves_per_eu(6, 8)))
 k_project(const void* __restrict__ src, const int64_t* __restrict__ nin, int64_t nmax, int H, int W,
-          int tile_log2, int32_t* __restrict__ owner, int32_t* __restrict__ err, int64_t n_single) {
+          int tile_log2, int32_t* __restrict__ owner, int32_t* __restrict__ err, int64_t n_single, OwnerTag ot) {
   extern __shared__ int32_t tile[];  // [H][(1 << tile_log2) + 1]: the pad puts the consecutive rings of one
                                      // column (consecutive points in firing order) in distinct banks
   __shared__ int32_t cellk[kProjChunk];
@@ -141,12 +143,12 @@ k_project(const void* __restrict__ src, const int64_t* __restrict__ nin, int64_t
       __syncthreads();
       for (int e = tid; e < tcells; e += kProjThreads) {
         const int32_t v = tile[(e >> tile_log2) * tpitch + (e & (tcols - 1))];
-        if (v != kEmptyOwner) atomicMin(&O[(e >> tile_log2) * W + cmin + (e & (tcols - 1))], v);
+        if (v != kEmptyOwner) atomicMin(&O[(e >> tile_log2) * W + cmin + (e & (tcols - 1))], (int32_t)(ot.bits | (uint32_t)v));
       }
     } else {
       for (int k = 0; k < kProjPPT; ++k) {
         const int v = cellk[k * kProjThreads + tid];
-        if (v >= 0) atomicMin(&O[(v >> 16) * W + (v & 0xFFFF)], (int32_t)(base + k * kProjThreads + tid));
+        if (v >= 0) atomicMin(&O[(v >> 16) * W + (v & 0xFFFF)], (int32_t)(ot.bits | (uint32_t)(base + k * kProjThreads + tid)));
       }
     }
     __syncthreads();
@@ -170,7 +172,7 @@ __host__ __device__ inline int compact_nchunk(int cg, int W) { return (W + cg - 
 // One wave per (job, row): number of claimed cells in the row, the claimed cells of the row before
 // each CG-column chunk (choff [job][row][chunk]), and, for deskew, the row's minimum owner.
 __global__ void k_rowcount(const int32_t* __restrict__ owner, int H, int W, int cg, int32_t* __restrict__ rowcnt,
-                           int32_t* __restrict__ rowmin, int32_t* __restrict__ choff) {
+                           int32_t* __restrict__ rowmin, int32_t* __restrict__ choff, OwnerTag ot) {
   const int row = blockIdx.x, job = blockIdx.y, lane = threadIdx.x;
   const int32_t* O = owner + ((int64_t)job * H + row) * W;
   const int nch = compact_nchunk(cg, W);
@@ -189,9 +191,10 @@ __global__ void k_rowcount(const int32_t* __restrict__ owner, int H, int W, int 
     for (int q = 0; q < 4; ++q) {
       const int c0 = c00 + 64 * q;
       if (c0 >= W) break;  // wave-uniform
-      const int32_t o = o4[q];
+      const bool ok = owner_valid(o4[q], ot);
+      const int32_t o = ok ? (int32_t)((uint32_t)o4[q] & ot.mask) : kEmptyOwner;
       mn = min(mn, o);
-      const uint64_t m = __ballot(o != kEmptyOwner);
+      const uint64_t m = __ballot(ok);
       // chunk starts inside this 64-column step (cg is a multiple of 32)
       if (lane == 0) {
         if (c0 % cg == 0) CH[c0 / cg] = run;
@@ -236,7 +239,7 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, const float4* __restrict__ p
           const int32_t* __restrict__ rowcnt, const int32_t* __restrict__ choff, int B, int H, int W, int HB, int CG,
           float4* __restrict__ cloud, int32_t* __restrict__ col, float* __restrict__ range,
           int32_t* __restrict__ start_ring, int32_t* __restrict__ end_ring, int32_t* __restrict__ nvalid,
-          DeskArgs desk) {
+          DeskArgs desk, OwnerTag ot) {
   // [HB][CG + 1] arrays: the column-by-column gather has consecutive lanes on consecutive rows, and
   // the pad puts those in distinct banks (a CG-word pitch put a whole wave on one bank group:
   // 13.8 conflict cycles per LDS instruction, profiles/r05a_sq_decomp.txt)
@@ -286,8 +289,8 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, const float4* __restrict__ p
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int i = tid + 256 * q, r = i / CG, c = i % CG;
-    const int32_t v = in[q] ? o[q] : kEmptyOwner;
-    if (v != kEmptyOwner) *a[q] = kEmptyOwner;
+    const int32_t v = in[q] && owner_valid(o[q], ot) ? (int32_t)((uint32_t)o[q] & ot.mask) : kEmptyOwner;
+    if (ot.reset && v != kEmptyOwner) *a[q] = kEmptyOwner;
     if (i < HB * CG) own[r * PC + c] = v;
   }
   for (int i = tid + 512; i < HB * CG; i += 256) {  // tiles above 512 cells (FBR_COMPACT_CELLS)
@@ -296,7 +299,8 @@ k_compact(const fbr_point_xyzirt* __restrict__ pts, const float4* __restrict__ p
     if (r < nr && c < ncl) {
       int32_t* p = O + (int64_t)(r0 + r) * W + c0 + c;
       v = *p;
-      if (v != kEmptyOwner) *p = kEmptyOwner;
+      v = owner_valid(v, ot) ? (int32_t)((uint32_t)v & ot.mask) : kEmptyOwner;
+      if (ot.reset && v != kEmptyOwner) *p = kEmptyOwner;
     }
     own[r * PC + c] = v;
   }
@@ -500,7 +504,7 @@ void launch_expand_scans(hipStream_t s, const uint8_t* stage, int64_t nmax, int 
 }
 
 void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* nin, int64_t nmax, int B, int H,
-                    int W, int32_t* owner, int32_t* err, int64_t n_single, const float4* pk) {
+                    int W, int32_t* owner, int32_t* err, int64_t n_single, const float4* pk, const OwnerTag& ot) {
   int blocks = (int)((nmax + kProjChunk - 1) / kProjChunk);
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
@@ -509,10 +513,10 @@ void launch_project(hipStream_t s, const fbr_point_xyzirt* pts, const int64_t* n
   const size_t lds = sizeof(int32_t) * (size_t)H * ((1 << tile_log2) + 1);
   if (pk)
     fbr_launch(k_project<true>, dim3(blocks, B), dim3(kProjThreads), lds, s, (const void*)pk, nin, nmax, H, W,
-               tile_log2, owner, err, n_single);
+               tile_log2, owner, err, n_single, ot);
   else
     fbr_launch(k_project<false>, dim3(blocks, B), dim3(kProjThreads), lds, s, (const void*)pts, nin, nmax, H, W,
-               tile_log2, owner, err, n_single);
+               tile_log2, owner, err, n_single, ot);
 }
 
 // Compaction tile size in cells (FBR_COMPACT_CELLS: 512, 1024 or 2048).  512 since round 5: 10 KB of
@@ -530,23 +534,24 @@ int compact_cells() {
 
 void launch_extract(hipStream_t s, const fbr_point_xyzirt* pts, int64_t nmax, int32_t* owner, int B, int H,
                     int W, int32_t* rowcnt, int32_t* choff, float4* cloud, int32_t* col, float* range,
-                    int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk, const float4* pk) {
+                    int32_t* start_ring, int32_t* end_ring, int32_t* nvalid, const DeskArgs& desk, const float4* pk,
+                    const OwnerTag& ot) {
   const CompactTile T = compact_tile(H, compact_cells());
   fbr_launch(k_rowcount, dim3(H, B), dim3(64), 0, s, owner, H, W, T.cg, rowcnt, desk.mode ? desk.rowmin : nullptr,
-             choff);
+             choff, ot);
   const int tiles = ((H + T.hb - 1) / T.hb) * compact_nchunk(T.cg, W);
   const int groups = (B + 7) / 8;
   const dim3 grid((unsigned)(groups * 8 * tiles));
   const size_t cells = (size_t)T.hb * (T.cg + 1);  // padded pitch (k_compact)
   if (desk.mode)
     fbr_launch(k_compact<true>, grid, dim3(256), (uint32_t)(cells * 24), s, pts, pk, nmax, owner, rowcnt, choff, B,
-               H, W, T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk);
+               H, W, T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk, ot);
   else if (pk)
     fbr_launch(k_compact<false, true>, grid, dim3(256), (uint32_t)(cells * 20), s, pts, pk, nmax, owner, rowcnt,
-               choff, B, H, W, T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk);
+               choff, B, H, W, T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk, ot);
   else
     fbr_launch(k_compact<false>, grid, dim3(256), (uint32_t)(cells * 20), s, pts, pk, nmax, owner, rowcnt, choff, B,
-               H, W, T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk);
+               H, W, T.hb, T.cg, cloud, col, range, start_ring, end_ring, nvalid, desk, ot);
 }
 
 }  // namespace fbr
