@@ -815,6 +815,16 @@ int gn_grid_cap() {
 }
 
 
+// One work item per workgroup in the batch kNN / residual launches (GnArgs::one_item;
+// FBR_GN_ONE_ITEM=0: grid-stride loops, for A/B).
+bool gn_one_item() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_GN_ONE_ITEM");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 // Tail mode: once at most 1/FBR_GN_TAIL of a sub-batch's jobs are still iterating (default 8),
 // its iterations run fused (kNN + residual in one launch) on a smaller grid: the few remaining
 // jobs' work is latency-bound, so one launch less per iteration and fewer idle workgroups
@@ -936,8 +946,12 @@ int gn_run_pass(fbr_ctx* c, GnRun& r, bool block, bool* progress) {
     if (tail) {  // kNN and residual in one launch (whole runs fused: 4 % slower at round 6, r06b)
       TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, r.a[k], grid, it, true));
     } else {
-      TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, r.a[k], grid, it, false));
-      TIMED_ON(c, sb.st, "gn_residual", launch_gn_residual(sb.st, r.a[k], grid));
+      // batch sub-batches: one work item per workgroup (GnArgs::one_item); single scans keep the
+      // loop over a grid sized by the previous scan's items (no second launch on the critical path)
+      GnArgs a1 = r.a[k];
+      a1.one_item = (!sb.stream_mode && gn_one_item()) ? 1 : 0;
+      TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a1, grid, it, false));
+      TIMED_ON(c, sb.st, "gn_residual", launch_gn_residual(sb.st, a1, grid));
     }
     TIMED_ON(c, sb.st, "gn_solve", launch_gn_solve(sb.st, r.a[k], it, r.gen));
     r.it[k] = it + 1;

@@ -4,7 +4,9 @@
 // parallel; one file holding all of them took ~8 minutes).  See k_register.hip for the design
 // notes and reference citations (mapOptmization.h:1002-1243, :1403-1442).
 #pragma once
+#include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "fbr_common.h"
 #include "fbr_imu.h"
@@ -624,15 +626,36 @@ __device__ __forceinline__ void gn_knn_block(const GnArgs& a, int v, int use_pre
   if (kFused) res_reduce(red, tid, row, b, rok, a.partial + (int64_t)it * kPartial);
 }
 
-template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ = 1>
+// kLoop = false: virtual workgroup base + blockIdx.x only (one_item launches); true: a grid-stride
+// loop from base.
+template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ = 1, bool kLoop = true>
 __global__ void __launch_bounds__(kResThreads)
-k_gn_knn(GnArgs a, int use_prev) {
+k_gn_knn(GnArgs a, int use_prev, int base) {
   static_assert(LPQ == 1 || (!kFused && !kFlat), "wide mode is the plain kNN pass");
   __shared__ double red[kFused ? kResThreads / 64 : 1][28];
   __shared__ int2 rows[kFlat ? (2 * R + 1) * (2 * R + 1) : 1][kResThreads];
   const int nitems = a.nitems[0];
-  for (int v = blockIdx.x; v < nitems * LPQ; v += gridDim.x)
-    gn_knn_block<R, RX, kFused, kFlat, kSparse, LPQ>(a, v, use_prev, red, &rows[0][threadIdx.x]);
+  if constexpr (kLoop) {
+    for (int v = base + blockIdx.x; v < nitems * LPQ; v += gridDim.x)
+      gn_knn_block<R, RX, kFused, kFlat, kSparse, LPQ>(a, v, use_prev, red, &rows[0][threadIdx.x]);
+  } else {
+    const int v = base + (int)blockIdx.x;
+    if (v < nitems * LPQ) gn_knn_block<R, RX, kFused, kFlat, kSparse, LPQ>(a, v, use_prev, red, &rows[0][threadIdx.x]);
+  }
+}
+
+// Items past a one-item launch's grid: a loop launch of at most this many workgroups from `grid`
+// (its workgroups return at once when the grid covered every item).
+constexpr int kRestGrid = 2048;
+template <typename Kmain, typename Krest, typename... Args>
+void launch_one_item(hipStream_t s, const GnArgs& a, int grid, int total, size_t lds, Kmain kmain, Krest krest,
+                     Args... args) {
+  if (a.one_item && grid < total) {
+    fbr_launch(kmain, dim3(grid), dim3(kResThreads), lds, s, args..., 0);
+    fbr_launch(krest, dim3(std::min(kRestGrid, total - grid)), dim3(kResThreads), lds, s, args..., grid);
+  } else {
+    fbr_launch(a.one_item ? kmain : krest, dim3(grid), dim3(kResThreads), lds, s, args..., 0);
+  }
 }
 
 // pcl::getTransformation (x,y,z,roll,pitch,yaw) in float with glibc's sinf / cosf
@@ -824,10 +847,21 @@ template <int R, bool F, bool L, bool S, int LPQ = 1>
 void launch_gn_knn_rls(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
   const float invx = a.mc.g.inv_x;  // == a.ms.g.inv_x
   grid *= LPQ;
-  if (invx > 4.0f) fbr_launch((k_gn_knn<R, 8, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);       // 0.125 m
-  else if (invx > 2.0f) fbr_launch((k_gn_knn<R, 4, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.25 m
-  else if (invx > 1.0f) fbr_launch((k_gn_knn<R, 2, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);  // 0.5 m
-  else fbr_launch((k_gn_knn<R, 1, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev);                  // >= 1 m
+  const int total = a.max_items * LPQ;
+  // one-item launches for the plain pass at one lane per query (the fused tail and wide mode loop)
+  constexpr bool kOne = !F && LPQ == 1;
+  auto go = [&](auto rx) {
+    constexpr int RX = decltype(rx)::value;
+    if constexpr (kOne)
+      launch_one_item(s, a, grid, total, 0, k_gn_knn<R, RX, F, L, S, LPQ, false>, k_gn_knn<R, RX, F, L, S, LPQ, true>, a,
+                      use_prev);
+    else
+      fbr_launch((k_gn_knn<R, RX, F, L, S, LPQ, true>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev, 0);
+  };
+  if (invx > 4.0f) go(std::integral_constant<int, 8>{});       // 0.125 m
+  else if (invx > 2.0f) go(std::integral_constant<int, 4>{});  // 0.25 m
+  else if (invx > 1.0f) go(std::integral_constant<int, 2>{});  // 0.5 m
+  else go(std::integral_constant<int, 1>{});                  // >= 1 m
 }
 // Dense or hashed-chunk map grids (one flag for both maps: fbr_set_map builds them alike).
 template <int R, bool F, bool L, int LPQ = 1>

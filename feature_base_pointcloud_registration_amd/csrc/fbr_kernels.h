@@ -283,6 +283,10 @@ int grid_build_device(hipStream_t s, DevArena& ar, const float4* pts, int64_t n,
 struct JobResult;
 struct GnArgs {
   int B, max_iter;
+  // one_item: the plain kNN / residual launches run one work item per workgroup over
+  // [0, grid) (no grid-stride loop: the loop's carried state took k_gn_residual from 64 to 108
+  // VGPRs, the flat kNN from 54 to 68), and a loop launch picks up items past the grid
+  int one_item;
   const float4* cornerDS;
   int64_t capc;
   const int32_t* ncds;

@@ -104,11 +104,17 @@ __global__ void k_gn_init(GnArgs a) {
   if (tid == 0) a.nitems[0] = min(base, a.max_items);
 }
 
+template <bool kLoop>  // as k_gn_knn: one item per workgroup from base, or a grid-stride loop from base
 __global__ void __launch_bounds__(kResThreads)
-k_gn_residual(GnArgs a) {
+k_gn_residual(GnArgs a, int base) {
   __shared__ double red[kResThreads / 64][28];
   const int nitems = a.nitems[0];
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x) gn_residual_item(a, it, red);
+  if constexpr (kLoop) {
+    for (int it = base + blockIdx.x; it < nitems; it += gridDim.x) gn_residual_item(a, it, red);
+  } else {
+    const int it = base + (int)blockIdx.x;
+    if (it < nitems) gn_residual_item(a, it, red);
+  }
 }
 
 
@@ -308,7 +314,7 @@ void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fuse
   else launch_gn_knn_f<false>(s, a, grid, use_prev);
 }
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
-  fbr_launch(k_gn_residual, dim3(grid), dim3(kResThreads), 0, s, a);
+  launch_one_item(s, a, grid, a.max_items, 0, k_gn_residual<false>, k_gn_residual<true>, a);
 }
 void launch_gn_solve(hipStream_t s, const GnArgs& a, int iter_idx, unsigned long long gen) {
   fbr_launch(k_gn_solve, dim3(a.B), dim3(kSolveThreads), 0, s, a, iter_idx, gen);
