@@ -825,6 +825,14 @@ bool gn_one_item() {
   return v;
 }
 
+bool gn_tail_one_item() {
+  static const bool v = [] {
+    const char* e = std::getenv("FBR_GN_TAIL_ONE_ITEM");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 // Tail mode: once at most 1/FBR_GN_TAIL of a sub-batch's jobs are still iterating (default 8),
 // its iterations run fused (kNN + residual in one launch) on a smaller grid: the few remaining
 // jobs' work is latency-bound, so one launch less per iteration and fewer idle workgroups
@@ -941,10 +949,15 @@ int gn_run_pass(fbr_ctx* c, GnRun& r, bool block, bool* progress) {
     }
     all_done = false;
     const bool tail = gn_tail_div() > 0 && (int64_t)r.active[k] * gn_tail_div() <= sb.B;
-    int grid = std::max(1, std::min(r.a[k].max_items, tail ? std::min(gn_grid_cap(), 1024) : gn_grid_cap()));
+    // the batch tail also one item per workgroup (the grid then covers the items of the jobs that
+    // stopped too, which return at once); FBR_GN_TAIL_ONE_ITEM=0: a 1,024-workgroup loop
+    const bool tail_one = tail && !sb.stream_mode && gn_one_item() && gn_tail_one_item();
+    int grid = std::max(1, std::min(r.a[k].max_items, tail && !tail_one ? std::min(gn_grid_cap(), 1024) : gn_grid_cap()));
     if (sb.stream_mode && c->items_hint > 0) grid = std::min(grid, std::max(16, 2 * c->items_hint));
     if (tail) {  // kNN and residual in one launch (whole runs fused: 4 % slower at round 6, r06b)
-      TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, r.a[k], grid, it, true));
+      GnArgs a1 = r.a[k];
+      a1.one_item = tail_one ? 1 : 0;
+      TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a1, grid, it, true));
     } else {
       // batch sub-batches: one work item per workgroup (GnArgs::one_item); single scans keep the
       // loop over a grid sized by the previous scan's items (no second launch on the critical path)

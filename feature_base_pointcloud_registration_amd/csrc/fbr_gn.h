@@ -848,8 +848,8 @@ void launch_gn_knn_rls(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
   const float invx = a.mc.g.inv_x;  // == a.ms.g.inv_x
   grid *= LPQ;
   const int total = a.max_items * LPQ;
-  // one-item launches for the plain pass at one lane per query (the fused tail and wide mode loop)
-  constexpr bool kOne = !F && LPQ == 1;
+  // one-item launches at one lane per query (wide mode loops)
+  constexpr bool kOne = LPQ == 1;
   auto go = [&](auto rx) {
     constexpr int RX = decltype(rx)::value;
     if constexpr (kOne)
