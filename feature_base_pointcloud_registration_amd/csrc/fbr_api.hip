@@ -706,6 +706,7 @@ GnArgs gn_args(fbr_ctx* c, const Sub& sb, bool trace) {
   }();
   a.fit_cache = fit_cache;
   a.iter_flags = c->d_iter_flags + (int64_t)sb.k * mi;
+  a.items_flag = c->d_iter_flags + (int64_t)kMaxSub * mi + sb.k;  // after every sub-batch's iteration flags
   a.iter_cnt = c->d_iter_cnt + (int64_t)sb.k * 4 * mi;  // [2 * mi] solve, [mi] queued, [mi] blocks
   if (c->d_bin) {
     const int64_t slots = (int64_t)c->max_items * 256;
@@ -875,6 +876,25 @@ void gn_run_start(fbr_ctx* c, GnRun& r, const Sub* subs, int nsub, bool trace) {
   }
 }
 
+// The run's work-item count once iteration 0's solve has published it (GnArgs::items_flag), else -1.
+int items_known(fbr_ctx* c, const GnRun& r, int k) {
+  if (!c->h_iter_flags) return -1;
+  const int mi = std::max(1, c->P.max_iterations);
+  const volatile unsigned long long* f = c->h_iter_flags + (int64_t)kMaxSub * mi + r.subs[k].k;
+  const unsigned long long v = *f;
+  return (v >> 32) == (r.gen & 0xFFFFFFFFull) ? (int)(uint32_t)v : -1;
+}
+
+// Workgroups of a one-item launch before the run's item count is known (FBR_GN_ONE_GRID; a C2
+// launch of 1,024 jobs has ~25.6k items); the loop launch behind it takes any items past them.
+int gn_one_grid() {
+  static const int v = [] {
+    const char* e = std::getenv("FBR_GN_ONE_GRID");
+    return e ? std::max(1, std::atoi(e)) : 32768;
+  }();
+  return v;
+}
+
 // One pass over the run's sub-batches: each enqueues its next iteration if the flag it needs is
 // visible (block: wait for it).  A sub-batch whose jobs all stopped, or that reached
 // max_iterations, gets its transformUpdate.  *progress: something was enqueued.
@@ -954,15 +974,24 @@ int gn_run_pass(fbr_ctx* c, GnRun& r, bool block, bool* progress) {
     const bool tail_one = tail && !sb.stream_mode && gn_one_item() && gn_tail_one_item();
     int grid = std::max(1, std::min(r.a[k].max_items, tail && !tail_one ? std::min(gn_grid_cap(), 1024) : gn_grid_cap()));
     if (sb.stream_mode && c->items_hint > 0) grid = std::min(grid, std::max(16, 2 * c->items_hint));
+    // one-item launches: one workgroup per item once the count is known (no loop launch), before
+    // that a grid of gn_one_grid() workgroups and the loop launch behind it
+    const bool one = !sb.stream_mode && gn_one_item() && (!tail || tail_one);
+    int one_mode = 0;
+    if (one) {
+      const int nk = items_known(c, r, k);
+      grid = nk >= 0 ? std::max(1, nk) : std::max(1, std::min(r.a[k].max_items, gn_one_grid()));
+      one_mode = nk >= 0 ? 2 : 1;
+    }
     if (tail) {  // kNN and residual in one launch (whole runs fused: 4 % slower at round 6, r06b)
       GnArgs a1 = r.a[k];
-      a1.one_item = tail_one ? 1 : 0;
+      a1.one_item = one_mode;
       TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a1, grid, it, true));
     } else {
       // batch sub-batches: one work item per workgroup (GnArgs::one_item); single scans keep the
       // loop over a grid sized by the previous scan's items (no second launch on the critical path)
       GnArgs a1 = r.a[k];
-      a1.one_item = (!sb.stream_mode && gn_one_item()) ? 1 : 0;
+      a1.one_item = one_mode;
       TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a1, grid, it, false));
       TIMED_ON(c, sb.st, "gn_residual", launch_gn_residual(sb.st, a1, grid));
     }
@@ -1606,7 +1635,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
               dalloc(&c->d_nsame, (int64_t)c->max_items * 256) ||
               dalloc(&c->d_iter_cnt, kMaxSub * 4 * std::max(1, p->max_iterations)) ||
               dalloc(&c->d_feat_scratch, Bw * H * feat_slot_bytes(c->W)) ||
-              hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * kMaxSub * std::max(1, p->max_iterations),
+              hipHostMalloc((void**)&c->h_iter_flags, sizeof(unsigned long long) * kMaxSub * (std::max(1, p->max_iterations) + 1),
                             hipHostMallocMapped) != hipSuccess ||
               hipHostGetDevicePointer((void**)&c->d_iter_flags, c->h_iter_flags, 0) != hipSuccess || dalloc(&c->d_pose_out, Bw * 6) ||
               dalloc(&c->d_stats, Bw) || dalloc(&c->d_trace, Bw * p->max_iterations * 6) ||
@@ -1625,7 +1654,7 @@ int fbr_create(fbr_ctx** out, const fbr_params* p, int hip_device) {
     fbr_destroy(c);
     return FBR_ERR_HIP;
   }
-  std::memset(c->h_iter_flags, 0, sizeof(unsigned long long) * kMaxSub * std::max(1, p->max_iterations));
+  std::memset(c->h_iter_flags, 0, sizeof(unsigned long long) * kMaxSub * (std::max(1, p->max_iterations) + 1));
   std::memset(c->h_direct, 0, sizeof(JobResult));
   if (hipMemset(c->d_sstream, 0, sizeof(StreamState)) != hipSuccess ||
       hipMemset(c->d_label_stream, 0, HW) != hipSuccess || hipMemset(c->d_col, 0, sizeof(int32_t) * Bw * HW) != hipSuccess ||

@@ -650,7 +650,7 @@ constexpr int kRestGrid = 2048;
 template <typename Kmain, typename Krest, typename... Args>
 void launch_one_item(hipStream_t s, const GnArgs& a, int grid, int total, size_t lds, Kmain kmain, Krest krest,
                      Args... args) {
-  if (a.one_item && grid < total) {
+  if (a.one_item == 1 && grid < total) {
     fbr_launch(kmain, dim3(grid), dim3(kResThreads), lds, s, args..., 0);
     fbr_launch(krest, dim3(std::min(kRestGrid, total - grid)), dim3(kResThreads), lds, s, args..., grid);
   } else {

@@ -286,6 +286,7 @@ struct GnArgs {
   // one_item: the plain kNN / residual launches run one work item per workgroup over
   // [0, grid) (no grid-stride loop: the loop's carried state took k_gn_residual from 64 to 108
   // VGPRs, the flat kNN from 54 to 68), and a loop launch picks up items past the grid
+  // (one_item = 2: the host has seen the run's item count fit the grid, no loop launch)
   int one_item;
   const float4* cornerDS;
   int64_t capc;
@@ -313,6 +314,7 @@ struct GnArgs {
   int8_t* nsame;             // [max_items][256] 1: this iteration's neighbours equal the previous ones
   int fit_cache;             // reuse cached fits (FBR_FIT_CACHE, default 1)
   unsigned long long* iter_flags;  // host-mapped [max_iter]: (generation << 32) | jobs still active
+  unsigned long long* items_flag;  // host-mapped: (generation << 32) | work items (k_gn_solve, iteration 0)
   int32_t* iter_cnt;         // [max_iter][2] active-job count / finished workgroups, then [max_iter]
                              // queued-query and [max_iter] non-empty-block counts of the block
                              // tiles (k_knn_tile.hip; all zeroed by k_gn_init)

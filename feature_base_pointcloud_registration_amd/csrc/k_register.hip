@@ -211,6 +211,9 @@ __global__ void __launch_bounds__(kSolveThreads) k_gn_solve(GnArgs a, int iter_i
         }
         __threadfence_system();
       }
+      if (a.items_flag && iter_idx == 0)  // the run's item count, for the host's launch grids
+        __hip_atomic_store(a.items_flag, (gen << 32) | (unsigned long long)(uint32_t)a.nitems[0], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       if (a.iter_flags)
         __hip_atomic_store(&a.iter_flags[iter_idx], (gen << 32) | (unsigned long long)cnt, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);

@@ -1161,11 +1161,13 @@ def test_owner_generations_are_bit_identical_to_reset_images():
 
 def test_one_item_gn_launches_are_bit_identical_to_grid_stride_loops():
     """Batch kNN / residual launches run one work item per workgroup (GnArgs::one_item: without
-    the grid-stride loop the residual kernel takes 64 VGPRs instead of 108), and a loop launch picks
-    up the items past the grid.  Against grid-stride loops everywhere (FBR_GN_ONE_ITEM=0) and with a
-    37-workgroup grid that leaves most items to the loop launch (FBR_GN_GRID=37), child processes,
-    C2 jobs through the ingest and staged paths: poses and stats bit-equal."""
+    the grid-stride loop the residual kernel takes 64 VGPRs instead of 108): one workgroup per item
+    once iteration 0's solve has published the run's item count, before that a fixed grid and a loop
+    launch for the items past it.  Against grid-stride loops everywhere (FBR_GN_ONE_ITEM=0) and with
+    a 37-workgroup first grid that leaves most items of iterations 0-1 to the loop launch
+    (FBR_GN_ONE_GRID=37), child processes, C2 jobs through the ingest and staged paths: poses and
+    stats bit-equal."""
     jobs = synth.make_jobs("C2", 24, base_seed=700)
     ref = _both_batch_paths("C2", jobs, {"FBR_GN_ONE_ITEM": "0"})
     assert _both_batch_paths("C2", jobs, {}) == ref
-    assert _both_batch_paths("C2", jobs, {"FBR_GN_GRID": "37"}) == ref
+    assert _both_batch_paths("C2", jobs, {"FBR_GN_ONE_GRID": "37"}) == ref
