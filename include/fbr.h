@@ -372,7 +372,11 @@ int fbr_debug_counters(long long* launches, long long* host_syncs, long long* fl
  * to the next launch / flush / wait call.  So launch n's projection and features run beside launch
  * n-1's last iterations.  The single-scan entry points (fbr_project, fbr_register*,
  * fbr_process_scan) share the device buffers and drop a staged batch (after enqueueing every
- * launch in flight): fbr_batch_launch then returns FBR_ERR_STATE until the next fbr_batch_stage. */
+ * launch in flight): fbr_batch_launch then returns FBR_ERR_STATE until the next fbr_batch_stage.
+ * Without deskew tables the staged scans live on the device as 16-B records (x, y, z, ring):
+ * intensity and time reach no batch result (poses, statistics, feature masks) and are not copied;
+ * a batch staged that way and then given deskew tables (fbr_set_deskew) is reported FBR_ERR_STATE
+ * at launch (stage it again). */
 int fbr_batch_stage(fbr_ctx* ctx, const fbr_point_xyzirt* const* scans, const int64_t* n_in,
                     int n_jobs, const float* poses_in /* [n_jobs][6] */);
 int fbr_batch_launch(fbr_ctx* ctx);
