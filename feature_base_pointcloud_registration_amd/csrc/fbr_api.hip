@@ -2088,6 +2088,8 @@ int fbr_batch_launch(fbr_ctx* c) {
   if (!c) return FBR_ERR_INVALID_ARG;
   if (c->staged_B <= 0) return FBR_ERR_STATE;
   if (!c->has_map) return FBR_ERR_NO_MAP;
+  // deskew tables set after the batch was staged as 16-B records (no time field): stage it again
+  if (c->desk_any && !c->no_time_call && !c->staged_24) return FBR_ERR_STATE;
   CK(enter(c));
   const auto t0 = std::chrono::steady_clock::now();
   // Sub-batches on separate streams: one sub-batch's low-occupancy phases (the features' ring-0

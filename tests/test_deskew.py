@@ -262,3 +262,28 @@ def test_deskew_skipped_without_time_field():
         b = O.project(P, pts)
     assert a["msg_flags"] & 1
     assert np.array_equal(a["cloud"].view(np.uint8), b["cloud"].view(np.uint8))
+
+
+@pytest.mark.gpu
+def test_deskew_tables_after_a_record_stage_require_restaging():
+    """A batch staged without deskew tables lives on the device as 16-B records (no time field);
+    giving it deskew tables afterwards makes fbr_batch_launch report FBR_ERR_STATE, and staging it
+    again (24-B scans, with time) deskews it like fbr_process_batch with the same tables."""
+    H, W = synth.CONFIGS["C2"][:2]
+    cmap, smap = synth.config_map("C2")
+    jobs = synth.make_jobs("C2", 2, base_seed=310)
+    scans, guesses = [j[0] for j in jobs], np.stack([j[1] for j in jobs])
+    tabs = np.zeros(2, DESKEW_TABLE)
+    tabs[0] = scan_table(41.0, gyro=(0.02, 0.03, 0.6), seed=0)
+    with api.Context(default_params(H, W, max_batch=2)) as ctx:
+        ctx.set_map(cmap, smap)
+        ctx.batch_stage(scans, guesses)
+        ctx.set_deskew(tabs)
+        with pytest.raises(Exception):
+            ctx.batch_launch()
+        ctx.batch_stage(scans, guesses)
+        ctx.batch_launch()
+        ctx.batch_wait()
+        p1, s1 = ctx.batch_results()
+        p2, s2 = ctx.process_batch(scans, guesses)
+    assert np.array_equal(p1.view(np.int32), p2.view(np.int32)) and s1.tobytes() == s2.tobytes()
