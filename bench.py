@@ -122,6 +122,7 @@ DESIGN_MODEL = {
 KERNEL_SYMBOLS = {"project": ["k_project"], "extract": ["k_rowcount", "k_compact"], "features": ["k_features"],
                   "voxel_ring": ["k_voxel_ring"], "concat": ["k_concat"], "voxel_scan": ["k_voxel_grid"],
                   "gn_knn": ["k_gn_knn"], "gn_residual": ["k_gn_residual"], "gn_solve": ["k_gn_solve"],
+                  "gn_loop": ["k_gn_loop_knn", "k_gn_loop_residual"],
                   "gn_init": ["k_gn_init"], "gn_finalize": ["k_gn_finalize"], "crop": ["k_crop_count"]}
 
 
@@ -444,7 +445,7 @@ def main():
         gather_rest()
     ctx.batch_wait()
     kernels = ["gn_knn", "gn_residual", "gn_solve", "project", "extract", "features", "voxel_ring", "concat",
-               "voxel_scan", "gn_init", "crop", "gn_finalize"]
+               "voxel_scan", "gn_init", "crop", "gn_finalize", "gn_loop"]
     # one untimed profiled step: per-kernel device times (HIP events) and the dominant kernel
     ctx.set_profiling(True)
     step()

@@ -216,6 +216,7 @@ struct fbr_ctx {
   // owner image generations (OwnerTag, fbr_kernels.h): owner_ib index bits, owner_tmax the last
   // generation before the image is refilled (0: untagged, reset by k_compact)
   int owner_ib = 0;
+  int gn_items_hint = 0, gn_items_hint_B = 0;  // the last batch run's work items and its job count
   uint32_t owner_gen = 0, owner_tmax = 0;
   int32_t *d_owner = nullptr, *d_rowcnt = nullptr, *d_col = nullptr, *d_start = nullptr, *d_end = nullptr,
           *d_nvalid = nullptr;
@@ -976,24 +977,54 @@ int gn_run_pass(fbr_ctx* c, GnRun& r, bool block, bool* progress) {
     if (sb.stream_mode && c->items_hint > 0) grid = std::min(grid, std::max(16, 2 * c->items_hint));
     // one-item launches: one workgroup per item once the count is known (no loop launch), before
     // that a grid of gn_one_grid() workgroups and the loop launch behind it
-    const bool one = !sb.stream_mode && gn_one_item() && (!tail || tail_one);
-    int one_mode = 0;
+    // (single scans: once the count is known, iteration 2 on; before that the loop over the
+    // previous scan's grid, so no second launch sits on their critical path)
+    const int nk = gn_one_item() && (!tail || tail_one || sb.stream_mode) ? items_known(c, r, k) : -1;
+    const bool one = gn_one_item() && (!tail || tail_one) && (!sb.stream_mode || nk >= 0);
+    int one_mode = 0, rest_grid = 0;
     if (one) {
-      const int nk = items_known(c, r, k);
-      grid = nk >= 0 ? std::max(1, nk) : std::max(1, std::min(r.a[k].max_items, gn_one_grid()));
-      one_mode = nk >= 0 ? 2 : 1;
+      if (nk >= 0) {
+        grid = std::max(1, nk);
+        one_mode = 2;
+        c->gn_items_hint = nk;  // the next run's first grids
+        c->gn_items_hint_B = sb.B;
+      } else if (c->gn_items_hint > 0 && c->gn_items_hint_B == sb.B) {
+        // a previous run of this many jobs: its count + 25 % + 256, and a small loop launch behind
+        grid = std::max(1, std::min(r.a[k].max_items, c->gn_items_hint + c->gn_items_hint / 4 + 256));
+        one_mode = 1;
+        rest_grid = 64;
+      } else {
+        grid = std::max(1, std::min(r.a[k].max_items, gn_one_grid()));
+        one_mode = 1;
+      }
     }
     if (tail) {  // kNN and residual in one launch (whole runs fused: 4 % slower at round 6, r06b)
       GnArgs a1 = r.a[k];
       a1.one_item = one_mode;
+      a1.rest_grid = rest_grid;
+      // the one-item launch and the loop launch behind it timed apart (rocprof: k_gn_knn / k_gn_loop_*)
+      a1.one_part = one_mode == 1 ? 1 : 0;
       TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a1, grid, it, true));
+      if (one_mode == 1) {
+        a1.one_part = 2;
+        TIMED_ON(c, sb.st, "gn_loop", launch_gn_knn(sb.st, a1, grid, it, true));
+      }
     } else {
-      // batch sub-batches: one work item per workgroup (GnArgs::one_item); single scans keep the
-      // loop over a grid sized by the previous scan's items (no second launch on the critical path)
       GnArgs a1 = r.a[k];
       a1.one_item = one_mode;
+      a1.rest_grid = rest_grid;
+      a1.one_part = one_mode == 1 ? 1 : 0;
       TIMED_ON(c, sb.st, "gn_knn", launch_gn_knn(sb.st, a1, grid, it, false));
+      if (one_mode == 1) {
+        a1.one_part = 2;
+        TIMED_ON(c, sb.st, "gn_loop", launch_gn_knn(sb.st, a1, grid, it, false));
+        a1.one_part = 1;
+      }
       TIMED_ON(c, sb.st, "gn_residual", launch_gn_residual(sb.st, a1, grid));
+      if (one_mode == 1) {
+        a1.one_part = 2;
+        TIMED_ON(c, sb.st, "gn_loop", launch_gn_residual(sb.st, a1, grid));
+      }
     }
     TIMED_ON(c, sb.st, "gn_solve", launch_gn_solve(sb.st, r.a[k], it, r.gen));
     r.it[k] = it + 1;

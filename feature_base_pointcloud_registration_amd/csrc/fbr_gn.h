@@ -626,11 +626,10 @@ __device__ __forceinline__ void gn_knn_block(const GnArgs& a, int v, int use_pre
   if (kFused) res_reduce(red, tid, row, b, rok, a.partial + (int64_t)it * kPartial);
 }
 
-// kLoop = false: virtual workgroup base + blockIdx.x only (one_item launches); true: a grid-stride
-// loop from base.
-template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ = 1, bool kLoop = true>
-__global__ void __launch_bounds__(kResThreads)
-k_gn_knn(GnArgs a, int use_prev, int base) {
+// kLoop = false: virtual workgroup base + blockIdx.x only (one_item launches, k_gn_knn); true: a
+// grid-stride loop from base (k_gn_loop_knn: single scans, wide mode, the items past a one-item grid).
+template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ, bool kLoop>
+__device__ __forceinline__ void gn_knn_kernel(const GnArgs& a, int use_prev, int base) {
   static_assert(LPQ == 1 || (!kFused && !kFlat), "wide mode is the plain kNN pass");
   __shared__ double red[kFused ? kResThreads / 64 : 1][28];
   __shared__ int2 rows[kFlat ? (2 * R + 1) * (2 * R + 1) : 1][kResThreads];
@@ -643,17 +642,29 @@ k_gn_knn(GnArgs a, int use_prev, int base) {
     if (v < nitems * LPQ) gn_knn_block<R, RX, kFused, kFlat, kSparse, LPQ>(a, v, use_prev, red, &rows[0][threadIdx.x]);
   }
 }
+template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ = 1>
+__global__ void __launch_bounds__(kResThreads) k_gn_knn(GnArgs a, int use_prev, int base) {
+  gn_knn_kernel<R, RX, kFused, kFlat, kSparse, LPQ, false>(a, use_prev, base);
+}
+template <int R, int RX, bool kFused, bool kFlat, bool kSparse, int LPQ = 1>
+__global__ void __launch_bounds__(kResThreads) k_gn_loop_knn(GnArgs a, int use_prev, int base) {
+  gn_knn_kernel<R, RX, kFused, kFlat, kSparse, LPQ, true>(a, use_prev, base);
+}
 
-// Items past a one-item launch's grid: a loop launch of at most this many workgroups from `grid`
-// (its workgroups return at once when the grid covered every item).
+// Items past a one-item launch's grid: a loop launch of at most GnArgs::rest_grid (default 2048)
+// workgroups from `grid` (they return at once when the grid covered every item; while other
+// streams' kernels hold the CUs, even returning workgroups wait for slots, so the host keeps the
+// loop launch small when it sized the grid from a previous run's count).
 constexpr int kRestGrid = 2048;
 template <typename Kmain, typename Krest, typename... Args>
 void launch_one_item(hipStream_t s, const GnArgs& a, int grid, int total, size_t lds, Kmain kmain, Krest krest,
                      Args... args) {
   if (a.one_item == 1 && grid < total) {
-    fbr_launch(kmain, dim3(grid), dim3(kResThreads), lds, s, args..., 0);
-    fbr_launch(krest, dim3(std::min(kRestGrid, total - grid)), dim3(kResThreads), lds, s, args..., grid);
-  } else {
+    if (a.one_part != 2) fbr_launch(kmain, dim3(grid), dim3(kResThreads), lds, s, args..., 0);
+    if (a.one_part != 1)
+      fbr_launch(krest, dim3(std::min(a.rest_grid > 0 ? a.rest_grid : kRestGrid, total - grid)), dim3(kResThreads), lds,
+                 s, args..., grid);
+  } else if (a.one_part != 2) {
     fbr_launch(a.one_item ? kmain : krest, dim3(grid), dim3(kResThreads), lds, s, args..., 0);
   }
 }
@@ -853,10 +864,10 @@ void launch_gn_knn_rls(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
   auto go = [&](auto rx) {
     constexpr int RX = decltype(rx)::value;
     if constexpr (kOne)
-      launch_one_item(s, a, grid, total, 0, k_gn_knn<R, RX, F, L, S, LPQ, false>, k_gn_knn<R, RX, F, L, S, LPQ, true>, a,
+      launch_one_item(s, a, grid, total, 0, k_gn_knn<R, RX, F, L, S, LPQ>, k_gn_loop_knn<R, RX, F, L, S, LPQ>, a,
                       use_prev);
-    else
-      fbr_launch((k_gn_knn<R, RX, F, L, S, LPQ, true>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev, 0);
+    else if (a.one_part != 2)
+      fbr_launch((k_gn_loop_knn<R, RX, F, L, S, LPQ>), dim3(grid), dim3(kResThreads), 0, s, a, use_prev, 0);
   };
   if (invx > 4.0f) go(std::integral_constant<int, 8>{});       // 0.125 m
   else if (invx > 2.0f) go(std::integral_constant<int, 4>{});  // 0.25 m

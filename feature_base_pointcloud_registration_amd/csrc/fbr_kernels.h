@@ -288,6 +288,8 @@ struct GnArgs {
   // VGPRs, the flat kNN from 54 to 68), and a loop launch picks up items past the grid
   // (one_item = 2: the host has seen the run's item count fit the grid, no loop launch)
   int one_item;
+  int rest_grid;  // workgroups of that loop launch (few when the grid was sized from a previous count)
+  int one_part;   // 0: both launches; 1: the one-item launch only; 2: the loop launch only (timed apart)
   const float4* cornerDS;
   int64_t capc;
   const int32_t* ncds;

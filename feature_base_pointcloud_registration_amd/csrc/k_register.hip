@@ -104,17 +104,18 @@ __global__ void k_gn_init(GnArgs a) {
   if (tid == 0) a.nitems[0] = min(base, a.max_items);
 }
 
-template <bool kLoop>  // as k_gn_knn: one item per workgroup from base, or a grid-stride loop from base
+// As k_gn_knn / k_gn_loop_knn: one item per workgroup from base, or a grid-stride loop from base.
 __global__ void __launch_bounds__(kResThreads)
 k_gn_residual(GnArgs a, int base) {
   __shared__ double red[kResThreads / 64][28];
+  const int it = base + (int)blockIdx.x;
+  if (it < a.nitems[0]) gn_residual_item(a, it, red);
+}
+__global__ void __launch_bounds__(kResThreads)
+k_gn_loop_residual(GnArgs a, int base) {
+  __shared__ double red[kResThreads / 64][28];
   const int nitems = a.nitems[0];
-  if constexpr (kLoop) {
-    for (int it = base + blockIdx.x; it < nitems; it += gridDim.x) gn_residual_item(a, it, red);
-  } else {
-    const int it = base + (int)blockIdx.x;
-    if (it < nitems) gn_residual_item(a, it, red);
-  }
+  for (int it = base + blockIdx.x; it < nitems; it += gridDim.x) gn_residual_item(a, it, red);
 }
 
 
@@ -312,12 +313,13 @@ void launch_gn_knn_f(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
 
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fused) {
   const int use_prev = iter > 0;  // nbr holds this launch's previous iteration
+  if (a.one_part == 2 && a.one_item != 1) return;  // no loop launch after this one
   if (!fused && launch_gn_knn_tile(s, a, grid, iter)) return;  // dense maps: LDS tiles (k_knn_tile.hip)
   if (fused) launch_gn_knn_f<true>(s, a, grid, use_prev);
   else launch_gn_knn_f<false>(s, a, grid, use_prev);
 }
 void launch_gn_residual(hipStream_t s, const GnArgs& a, int grid) {
-  launch_one_item(s, a, grid, a.max_items, 0, k_gn_residual<false>, k_gn_residual<true>, a);
+  launch_one_item(s, a, grid, a.max_items, 0, k_gn_residual, k_gn_loop_residual, a);
 }
 void launch_gn_solve(hipStream_t s, const GnArgs& a, int iter_idx, unsigned long long gen) {
   fbr_launch(k_gn_solve, dim3(a.B), dim3(kSolveThreads), 0, s, a, iter_idx, gen);

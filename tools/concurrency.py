@@ -18,7 +18,7 @@ from collections import defaultdict
 FAM = [("project", r"k_project\b"), ("extract", r"k_compact|k_rowcount"), ("features", r"k_features"),
        ("voxel_ring", r"k_voxel_ring"), ("concat", r"k_concat"), ("voxel_scan", r"k_voxel_grid"),
        ("gn_knn", r"k_gn_knn"), ("gn_residual", r"k_gn_residual"), ("gn_solve", r"k_gn_solve"),
-       ("gn_init", r"k_gn_init"), ("gn_finalize", r"k_gn_finalize"), ("crop", r"k_crop"),
+       ("gn_loop", r"k_gn_loop"), ("gn_init", r"k_gn_init"), ("gn_finalize", r"k_gn_finalize"), ("crop", r"k_crop"),
        ("pack", r"k_pack|k_export")]
 
 
