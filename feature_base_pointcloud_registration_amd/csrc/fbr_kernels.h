@@ -349,6 +349,7 @@ unsigned long long* knn_stats_buffer();
 #endif
 // iterations >= 1 on dense maps: the wave-tile search (k_knn_tile.hip); false = not applicable
 bool launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int iter);
+bool gn_knn_tile_applies(const GnArgs& a, int iter);
 bool knn_tile_applies(const GridDesc& gc, const GridDesc& gs);
 int64_t knn_tile_blocks(const GridDesc& g);
 void launch_gn_init(hipStream_t s, const GnArgs& a);

@@ -418,8 +418,12 @@ int64_t knn_tile_blocks(const GridDesc& g) { return (int64_t)((g.dims[0] + 3) / 
 
 unsigned long long* knn_tile_stats_buffer();
 
+bool gn_knn_tile_applies(const GnArgs& a, int iter) {
+  return iter > 0 && a.bin && knn_tile_applies(a.mc.g, a.ms.g);
+}
+
 bool launch_gn_knn_tile(hipStream_t s, const GnArgs& a, int grid, int iter) {
-  if (iter <= 0 || !a.bin || !knn_tile_applies(a.mc.g, a.ms.g)) return false;
+  if (!gn_knn_tile_applies(a, iter)) return false;
   const float rmax2 = 1.0f / (kFineInv * kFineInv);  // bounds up to one fine cell
   const int gq = std::max(1, std::min(grid, 16384));
   unsigned long long* st = knn_tile_stats_buffer();

@@ -313,7 +313,8 @@ void launch_gn_knn_f(hipStream_t s, const GnArgs& a, int grid, int use_prev) {
 
 void launch_gn_knn(hipStream_t s, const GnArgs& a, int grid, int iter, bool fused) {
   const int use_prev = iter > 0;  // nbr holds this launch's previous iteration
-  if (a.one_part == 2 && a.one_item != 1) return;  // no loop launch after this one
+  // no loop launch after this one (or the LDS-tile path, which covers every item itself)
+  if (a.one_part == 2 && (a.one_item != 1 || (!fused && gn_knn_tile_applies(a, iter)))) return;
   if (!fused && launch_gn_knn_tile(s, a, grid, iter)) return;  // dense maps: LDS tiles (k_knn_tile.hip)
   if (fused) launch_gn_knn_f<true>(s, a, grid, use_prev);
   else launch_gn_knn_f<false>(s, a, grid, use_prev);
